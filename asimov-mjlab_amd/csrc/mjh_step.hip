@@ -1,0 +1,1700 @@
+// mjh_step.hip — batched mj_step / mj_forward for gfx950 (MI355X).
+//
+// One workgroup per world. Every per-world intermediate (poses, com inertias,
+// mass matrix and its factor, contacts, constraint Jacobian, solver state)
+// lives in LDS for the whole step; HBM is touched once to read the state and
+// once to write the outputs (world-outermost arrays, see mjh_fields.h).
+// Lanes are spread over the world's inner dimensions: bodies (kinematic chains
+// are walked per lane, no per-level barriers), dofs, geom pairs, constraint
+// rows and lower-triangle matrix entries. Per-world reductions are wave
+// butterflies (__shfl_xor) + an LDS combine across waves; compaction of
+// contacts / constraint rows uses a block exclusive scan, so contact and row
+// order is deterministic (pair-table order, as MuJoCo's collision driver).
+//
+// Pipeline (MuJoCo's mj_step; reference call sites sim.py:138-147,186-199):
+//   kinematics -> com_pos -> crb -> LDL^T(M) -> collision -> make_constraint
+//   -> com_vel/rne -> passive/actuation -> qacc_smooth -> Newton solve
+//   -> post-constraint acc -> sensors -> implicitfast / Euler integration.
+// Solver options follow mjlab's MujocoCfg (sim.py:42-76): Newton, pyramidal
+// cones, exact line search, tolerance scaled by meaninertia.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/mjh_abi.h"
+#include "mjh_math.h"
+
+using namespace mjh;
+
+namespace {
+
+// Per-world LDS layout, offsets in 4-byte words from the world's base.
+struct Layout {
+  int qpos, qvel, qacc, qacc_smooth, qfrc_smooth, qfrc_bias, qfrc_con, qfrc_passive, qfrc_act;
+  int grad, search, Ma, Mv, tmp, tmp2;
+  int xpos, xquat, xmat, xipos, ximat, subtree_com, cinert, crb, cvel, cacc, cfrc;
+  int xanchor, xaxis, cdof, cdof_dot;
+  int cgpos, cgmat, sxpos, sxmat;
+  int M, L, ldm;
+  int act_force;
+  int con_pos, con_frame, con_dist, con_fric, con_solref, con_solimp, con_imargin, con_dim, con_geom, con_efcadr;
+  int J, ldj, efc_D, efc_R, efc_aref, efc_jaref, efc_jv, efc_force, efc_fl, efc_pos, efc_type, efc_id, efc_mask;
+  int red, ints;
+  int total;
+  int ncap, rcap;
+};
+
+enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
+
+thread_local std::string g_err;
+
+__device__ __forceinline__ const float* wf(const float* p, long long stride, int w) { return p + (long long)w * stride; }
+
+// ---- block-level primitives -------------------------------------------------
+template <int NT>
+__device__ __forceinline__ float bsum(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if constexpr (NT == 64) {
+    return v;
+  } else {
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) s += red[i];
+    return s;
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void bsum2(float& a, float& b, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  if constexpr (NT != 64) {
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+      red[2 * (threadIdx.x >> 6)] = a;
+      red[2 * (threadIdx.x >> 6) + 1] = b;
+    }
+    __syncthreads();
+    a = 0.f;
+    b = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
+      a += red[2 * i];
+      b += red[2 * i + 1];
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ int bscan(int v, int* total, int* redi) {
+  const int lane = threadIdx.x & 63;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if constexpr (NT == 64) {
+    *total = __shfl(x, 63, 64);
+    return x - v;
+  } else {
+    const int wv = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 63) redi[wv] = x;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
+      int t = redi[i];
+      off += (i < wv) ? t : 0;
+      tot += t;
+    }
+    *total = tot;
+    return off + x - v;
+  }
+}
+
+// index q of the "reversed" triangle -> (i, j) with i >= j, both in [n-m, n).
+// Pairs with i, j >= n-m are exactly q < m(m+1)/2 (a prefix), which lets the
+// factorisation walk a shrinking trailing block with one flat loop.
+__device__ __forceinline__ void tri_rev(int q, int n, int& i, int& j) {
+  int b = (int)((sqrtf(8.f * (float)q + 1.f) - 1.f) * 0.5f);
+  while ((b + 1) * (b + 2) / 2 <= q) b++;
+  while (b * (b + 1) / 2 > q) b--;
+  int a = q - b * (b + 1) / 2;  // a <= b
+  i = n - 1 - a;
+  j = n - 1 - b;
+}
+
+// In-place LDL^T of the symmetric matrix in A (lower triangle used).
+// On exit: strict lower = unit L, diagonal = D. One barrier per column: the
+// scaling of column k-1 is deferred into pass k (disjoint addresses).
+template <int NT>
+__device__ void ldl_factor(float* A, int n, int ld) {
+  const int tid = threadIdx.x;
+  float prev_inv = 0.f;
+  for (int k = 0; k < n; k++) {
+    __syncthreads();
+    float piv = A[k * ld + k];
+    if (piv < MJH_MINVAL) piv = MJH_MINVAL;
+    const float inv = 1.f / piv;
+    const int mrem = n - 1 - k;  // trailing block size
+    const int nitems = mrem * (mrem + 1) / 2;
+    for (int q = tid; q < nitems; q += NT) {
+      int i, j;
+      tri_rev(q, n, i, j);
+      A[i * ld + j] -= A[i * ld + k] * A[j * ld + k] * inv;
+    }
+    if (k > 0)
+      for (int i = k + tid; i < n; i += NT) A[i * ld + (k - 1)] *= prev_inv;
+    if (tid == 0) A[k * ld + k] = piv;
+    prev_inv = inv;
+  }
+  __syncthreads();
+  (void)prev_inv;
+}
+
+// Solve (L D L^T) x = x in place.
+template <int NT>
+__device__ void ldl_solve(const float* A, int n, int ld, float* x) {
+  const int tid = threadIdx.x;
+  for (int k = 0; k < n; k++) {
+    __syncthreads();
+    const float xk = x[k];
+    for (int i = k + 1 + tid; i < n; i += NT) x[i] -= A[i * ld + k] * xk;
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += NT) x[i] /= A[i * ld + i];
+  for (int k = n - 1; k > 0; k--) {
+    __syncthreads();
+    const float xk = x[k];
+    for (int i = tid; i < k; i += NT) x[i] -= A[k * ld + i] * xk;
+  }
+  __syncthreads();
+}
+
+// y = A x for a full symmetric n x n matrix stored in the lower triangle.
+template <int NT>
+__device__ void symv(const float* A, int n, int ld, const float* x, float* y) {
+  for (int i = threadIdx.x; i < n; i += NT) {
+    float s = 0.f;
+    for (int j = 0; j < n; j++) s += (j <= i ? A[i * ld + j] : A[j * ld + i]) * x[j];
+    y[i] = s;
+  }
+}
+
+// ---- contact primitives ----------------------------------------------------
+struct Con {
+  float dist, pos[3], frame[6];  // frame: normal + tangent hint
+};
+
+__device__ __forceinline__ int sphere_sphere(Con* c, float margin, const float* p1, float r1, const float* p2, float r2) {
+  float dif[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  float cd = sqrtf(dot3(dif, dif));
+  if (cd > margin + r1 + r2) return 0;
+  float n[3];
+  if (cd < MJH_MINVAL) {
+    n[0] = 1.f; n[1] = 0.f; n[2] = 0.f;
+  } else {
+    float inv = 1.f / cd;
+    n[0] = dif[0] * inv; n[1] = dif[1] * inv; n[2] = dif[2] * inv;
+  }
+  c->dist = cd - r1 - r2;
+  float s = r1 + 0.5f * c->dist;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    c->pos[k] = p1[k] + n[k] * s;
+    c->frame[k] = n[k];
+    c->frame[3 + k] = 0.f;
+  }
+  return 1;
+}
+
+__device__ __forceinline__ int plane_sphere(Con* c, float margin, const float* pp, const float* pm, const float* sp, float r) {
+  float n[3] = {pm[2], pm[5], pm[8]};
+  float dif[3] = {sp[0] - pp[0], sp[1] - pp[1], sp[2] - pp[2]};
+  float cd = dot3(dif, n);
+  if (cd > margin + r) return 0;
+  c->dist = cd - r;
+  float s = r + 0.5f * c->dist;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    c->pos[k] = sp[k] - n[k] * s;
+    c->frame[k] = n[k];
+    c->frame[3 + k] = 0.f;
+  }
+  return 1;
+}
+
+// Narrowphase for one pair (types ascending). Up to 4 contacts.
+__device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, const float* s1, const float* p2,
+                           const float* m2, const float* s2, float margin, Con* out) {
+  if (t1 == 0 && t2 == 2) return plane_sphere(out, margin, p1, m1, p2, s2[0]);
+  if (t1 == 0 && t2 == 3) {
+    float ax[3] = {m2[2], m2[5], m2[8]};
+    float a[3], b[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      a[k] = p2[k] + ax[k] * s2[1];
+      b[k] = p2[k] - ax[k] * s2[1];
+    }
+    int n1 = plane_sphere(out, margin, p1, m1, a, s2[0]);
+    int n2 = plane_sphere(out + n1, margin, p1, m1, b, s2[0]);
+    if (n1) { out[0].frame[3] = ax[0]; out[0].frame[4] = ax[1]; out[0].frame[5] = ax[2]; }
+    if (n2) { out[n1].frame[3] = ax[0]; out[n1].frame[4] = ax[1]; out[n1].frame[5] = ax[2]; }
+    return n1 + n2;
+  }
+  if (t1 == 0 && t2 == 6) {
+    float n[3] = {m1[2], m1[5], m1[8]};
+    float dif[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+    float dist = dot3(dif, n);
+    int cnt = 0;
+    for (int i = 0; i < 8 && cnt < 4; i++) {
+      float v[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        float s = (i & (1 << k)) ? s2[k] : -s2[k];
+        v[0] += m2[k] * s;
+        v[1] += m2[3 + k] * s;
+        v[2] += m2[6 + k] * s;
+      }
+      float ld = dot3(n, v);
+      if (dist + ld > margin) continue;
+      Con* c = out + cnt++;
+      c->dist = dist + ld;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        c->pos[k] = p2[k] + v[k] - n[k] * 0.5f * c->dist;
+        c->frame[k] = n[k];
+        c->frame[3 + k] = 0.f;
+      }
+    }
+    return cnt;
+  }
+  if (t1 == 2 && t2 == 2) return sphere_sphere(out, margin, p1, s1[0], p2, s2[0]);
+  if (t1 == 2 && t2 == 3) {
+    float ax[3] = {m2[2], m2[5], m2[8]};
+    float dif[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+    float x = clampf(dot3(dif, ax), -s2[1], s2[1]);
+    float v[3] = {p2[0] + ax[0] * x, p2[1] + ax[1] * x, p2[2] + ax[2] * x};
+    return sphere_sphere(out, margin, p1, s1[0], v, s2[0]);
+  }
+  if (t1 == 3 && t2 == 3) {
+    float a1[3] = {m1[2] * s1[1], m1[5] * s1[1], m1[8] * s1[1]};
+    float a2[3] = {m2[2] * s2[1], m2[5] * s2[1], m2[8] * s2[1]};
+    float dif[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+    float ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2);
+    float u = -dot3(a1, dif), v = dot3(a2, dif), det = ma * mc - mb * mb;
+    float v1[3], v2[3];
+    if (fabsf(det) >= MJH_MINVAL) {
+      float x1 = (mc * u - mb * v) / det, x2 = (ma * v - mb * u) / det;
+      if (x1 > 1.f) { x1 = 1.f; x2 = (v - mb) / mc; }
+      else if (x1 < -1.f) { x1 = -1.f; x2 = (v + mb) / mc; }
+      if (x2 > 1.f) { x2 = 1.f; x1 = clampf((u - mb) / ma, -1.f, 1.f); }
+      else if (x2 < -1.f) { x2 = -1.f; x1 = clampf((u + mb) / ma, -1.f, 1.f); }
+#pragma unroll
+      for (int k = 0; k < 3; k++) { v1[k] = p1[k] + a1[k] * x1; v2[k] = p2[k] + a2[k] * x2; }
+      return sphere_sphere(out, margin, v1, s1[0], v2, s2[0]);
+    }
+    int n = 0;
+    for (int e = 0; e < 2 && n < 2; e++) {
+      float x1 = e ? -1.f : 1.f;
+      float x2 = clampf((v - mb * x1) / mc, -1.f, 1.f);
+      for (int k = 0; k < 3; k++) { v1[k] = p1[k] + a1[k] * x1; v2[k] = p2[k] + a2[k] * x2; }
+      n += sphere_sphere(out + n, margin, v1, s1[0], v2, s2[0]);
+    }
+    for (int e = 0; e < 2 && n < 2; e++) {
+      float x2 = e ? -1.f : 1.f;
+      float x1 = clampf((u - mb * x2) / ma, -1.f, 1.f);
+      for (int k = 0; k < 3; k++) { v1[k] = p1[k] + a1[k] * x1; v2[k] = p2[k] + a2[k] * x2; }
+      n += sphere_sphere(out + n, margin, v1, s1[0], v2, s2[0]);
+    }
+    return n;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ void make_frame(float f[9]) {
+  normalize3(f);
+  if (sqrtf(dot3(f + 3, f + 3)) < 0.5f) {
+    f[3] = f[4] = f[5] = 0.f;
+    if (f[1] < 0.5f && f[1] > -0.5f) f[4] = 1.f; else f[5] = 1.f;
+  }
+  float d = dot3(f, f + 3);
+  f[3] -= d * f[0]; f[4] -= d * f[1]; f[5] -= d * f[2];
+  normalize3(f + 3);
+  cross3(f + 6, f, f + 3);
+}
+
+// ---- constraint row parameters (solref/solimp -> D, aref) -------------------
+__device__ __forceinline__ void row_params(float timestep, float pos_aref, float pos_imp, float invweight,
+                                           const float* solref, const float* solimp, float jqvel, float* D,
+                                           float* R, float* aref) {
+  float timeconst = solref[0], dampratio = solref[1];
+  if (solref[0] > 0.f && timeconst < 2.f * timestep) timeconst = 2.f * timestep;
+  float dmin = clampf(solimp[0], MJH_MINIMP, MJH_MAXIMP);
+  float dmax = clampf(solimp[1], MJH_MINIMP, MJH_MAXIMP);
+  float width = fmaxf(solimp[2], MJH_MINVAL);
+  float mid = clampf(solimp[3], MJH_MINIMP, MJH_MAXIMP);
+  float power = fmaxf(solimp[4], 1.f);
+  float k = 1.f / (dmax * dmax * timeconst * timeconst * dampratio * dampratio);
+  float b = 2.f / (dmax * timeconst);
+  if (solref[0] <= 0.f) k = -solref[0] / (dmax * dmax);
+  if (solref[1] <= 0.f) b = -solref[1] / dmax;
+  float x = fabsf(pos_imp) / width, imp;
+  if (x > 1.f) {
+    imp = dmax;
+  } else {
+    float y = x < mid ? powf(x, power) / powf(mid, power - 1.f)
+                      : 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
+    imp = clampf(dmin + y * (dmax - dmin), dmin, dmax);
+  }
+  float r = fmaxf(invweight * (1.f - imp) / imp, MJH_MINVAL);
+  *R = r;
+  *D = 1.f / r;
+  *aref = -k * imp * pos_aref - b * jqvel;
+}
+
+// constraint state at jaref: writes force, returns Hessian weight (0 if inactive/linear)
+__device__ __forceinline__ float row_state(int type, float D, float R, float fl, float jaref, float* force, float* cost) {
+  if (type == MJH_CNSTR_FRICTION_DOF) {
+    if (jaref >= R * fl) { *force = -fl; *cost = fl * jaref - 0.5f * R * fl * fl; return 0.f; }
+    if (jaref <= -R * fl) { *force = fl; *cost = -fl * jaref - 0.5f * R * fl * fl; return 0.f; }
+    *force = -D * jaref; *cost = 0.5f * D * jaref * jaref; return D;
+  }
+  if (jaref < 0.f) { *force = -D * jaref; *cost = 0.5f * D * jaref * jaref; return D; }
+  *force = 0.f; *cost = 0.f; return 0.f;
+}
+
+// ---- the step kernel --------------------------------------------------------
+template <int NT, bool STEP>
+__global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo) {
+  extern __shared__ float smem[];
+  const int w = blockIdx.x;
+  if (w >= d.nworld) return;
+  const int tid = threadIdx.x;
+  float* S = smem;
+  int* SI = reinterpret_cast<int*>(smem);
+  const int nq = m.nq, nv = m.nv, nb = m.nbody, nu = m.nu, nj = m.njnt;
+  const int ldm = Lo.ldm, ldj = Lo.ldj;
+
+  float* qpos = S + Lo.qpos;
+  float* qvel = S + Lo.qvel;
+  float* qacc = S + Lo.qacc;
+  float* qacc_smooth = S + Lo.qacc_smooth;
+  float* qfrc_smooth = S + Lo.qfrc_smooth;
+  float* qfrc_bias = S + Lo.qfrc_bias;
+  float* qfrc_con = S + Lo.qfrc_con;
+  float* qfrc_passive = S + Lo.qfrc_passive;
+  float* qfrc_act = S + Lo.qfrc_act;
+  float* grad = S + Lo.grad;
+  float* search = S + Lo.search;
+  float* Ma = S + Lo.Ma;
+  float* Mv = S + Lo.Mv;
+  float* tmp = S + Lo.tmp;
+  float* tmp2 = S + Lo.tmp2;
+  float* xpos = S + Lo.xpos;
+  float* xquat = S + Lo.xquat;
+  float* xmat = S + Lo.xmat;
+  float* xipos = S + Lo.xipos;
+  float* ximat = S + Lo.ximat;
+  float* subtree_com = S + Lo.subtree_com;
+  float* cinert = S + Lo.cinert;
+  float* crb = S + Lo.crb;
+  float* cvel = S + Lo.cvel;
+  float* cacc = S + Lo.cacc;
+  float* cfrc = S + Lo.cfrc;
+  float* xanchor = S + Lo.xanchor;
+  float* xaxis = S + Lo.xaxis;
+  float* cdof = S + Lo.cdof;
+  float* cdof_dot = S + Lo.cdof_dot;
+  float* cgpos = S + Lo.cgpos;
+  float* cgmat = S + Lo.cgmat;
+  float* sxpos = S + Lo.sxpos;
+  float* sxmat = S + Lo.sxmat;
+  float* Mm = S + Lo.M;
+  float* Lm = S + Lo.L;
+  float* act_force = S + Lo.act_force;
+  float* con_pos = S + Lo.con_pos;
+  float* con_frame = S + Lo.con_frame;
+  float* con_dist = S + Lo.con_dist;
+  float* con_fric = S + Lo.con_fric;
+  float* con_solref = S + Lo.con_solref;
+  float* con_solimp = S + Lo.con_solimp;
+  float* con_imargin = S + Lo.con_imargin;
+  int* con_dim = SI + Lo.con_dim;
+  int* con_geom = SI + Lo.con_geom;
+  int* con_efcadr = SI + Lo.con_efcadr;
+  float* J = S + Lo.J;
+  float* efc_D = S + Lo.efc_D;
+  float* efc_R = S + Lo.efc_R;
+  float* efc_aref = S + Lo.efc_aref;
+  float* jaref = S + Lo.efc_jaref;
+  float* jv = S + Lo.efc_jv;
+  float* efc_force = S + Lo.efc_force;
+  float* efc_fl = S + Lo.efc_fl;
+  float* efc_pos = S + Lo.efc_pos;
+  int* efc_type = SI + Lo.efc_type;
+  int* efc_id = SI + Lo.efc_id;
+  unsigned long long* efc_mask = reinterpret_cast<unsigned long long*>(S + Lo.efc_mask);
+  float* red = S + Lo.red;
+  int* redi = SI + Lo.red + 2 * (NT / 64) + 2;
+  int* ints = SI + Lo.ints;
+
+  // per-world model fields (stride 0 = shared)
+  const float* body_pos = wf(m.body_pos, m.body_pos_wstride, w);
+  const float* body_quat = wf(m.body_quat, m.body_quat_wstride, w);
+  const float* body_ipos = wf(m.body_ipos, m.body_ipos_wstride, w);
+  const float* body_iquat = wf(m.body_iquat, m.body_iquat_wstride, w);
+  const float* body_mass = wf(m.body_mass, m.body_mass_wstride, w);
+  const float* body_inertia = wf(m.body_inertia, m.body_inertia_wstride, w);
+  const float* jnt_range = wf(m.jnt_range, m.jnt_range_wstride, w);
+  const float* jnt_stiffness = wf(m.jnt_stiffness, m.jnt_stiffness_wstride, w);
+  const float* dof_armature = wf(m.dof_armature, m.dof_armature_wstride, w);
+  const float* dof_damping = wf(m.dof_damping, m.dof_damping_wstride, w);
+  const float* dof_frictionloss = wf(m.dof_frictionloss, m.dof_frictionloss_wstride, w);
+  const float* geom_pos = wf(m.geom_pos, m.geom_pos_wstride, w);
+  const float* geom_quat = wf(m.geom_quat, m.geom_quat_wstride, w);
+  const float* geom_friction = wf(m.geom_friction, m.geom_friction_wstride, w);
+  const float* site_pos = wf(m.site_pos, m.site_pos_wstride, w);
+  const float* site_quat = wf(m.site_quat, m.site_quat_wstride, w);
+  const float* qpos0 = wf(m.qpos0, m.qpos0_wstride, w);
+
+  const long long W = w;
+
+  // ---------------------------------------------------------------- load state
+  for (int i = tid; i < nq; i += NT) qpos[i] = d.qpos[W * nq + i];
+  for (int i = tid; i < nv; i += NT) qvel[i] = d.qvel[W * nv + i];
+  if (tid < I_COUNT) ints[tid] = (tid == I_MISC) ? 0x7fffffff : 0;
+  __syncthreads();
+
+  // ---------------------------------------------------------------- kinematics
+  // Each lane walks its body's chain root->body (no per-level barriers). The
+  // per-body normalisation matches a level-by-level sweep exactly.
+  for (int b = tid; b < nb; b += NT) {
+    float p[3] = {0.f, 0.f, 0.f}, q[4] = {1.f, 0.f, 0.f, 0.f};
+    const int ca = m.body_chainadr[b], cn = (b == 0) ? 0 : m.body_chainnum[b];
+    for (int c = 0; c < cn; c++) {
+      const int k = m.body_chain[ca + c];
+      const int ja = m.body_jntadr[k], jn = m.body_jntnum[k];
+      if (jn == 1 && m.jnt_type[ja] == 0) {
+        const int qa = m.jnt_qposadr[ja];
+        p[0] = qpos[qa]; p[1] = qpos[qa + 1]; p[2] = qpos[qa + 2];
+        q[0] = qpos[qa + 3]; q[1] = qpos[qa + 4]; q[2] = qpos[qa + 5]; q[3] = qpos[qa + 6];
+        quat_normalize(q);
+        if (k == b) {
+          float R[9];
+          quat2mat(R, q);
+          xanchor[3 * ja] = p[0]; xanchor[3 * ja + 1] = p[1]; xanchor[3 * ja + 2] = p[2];
+          xaxis[3 * ja] = R[2]; xaxis[3 * ja + 1] = R[5]; xaxis[3 * ja + 2] = R[8];
+        }
+        continue;
+      }
+      float R[9], t[3];
+      quat2mat(R, q);
+      mat_vec(t, R, body_pos + 3 * k);
+      p[0] += t[0]; p[1] += t[1]; p[2] += t[2];
+      quat_mul(q, q, body_quat + 4 * k);
+      for (int j = ja; j < ja + jn; j++) {
+        float Rq[9], ax[3], anc[3];
+        quat2mat(Rq, q);
+        mat_vec(ax, Rq, m.jnt_axis + 3 * j);
+        mat_vec(anc, Rq, m.jnt_pos + 3 * j);
+        anc[0] += p[0]; anc[1] += p[1]; anc[2] += p[2];
+        const int qa = m.jnt_qposadr[j];
+        if (m.jnt_type[j] == 2) {
+          const float dd = qpos[qa] - qpos0[qa];
+          p[0] += ax[0] * dd; p[1] += ax[1] * dd; p[2] += ax[2] * dd;
+        } else if (m.jnt_type[j] == 3) {
+          float ql[4], v[3];
+          axis_angle(ql, m.jnt_axis + 3 * j, qpos[qa] - qpos0[qa]);
+          quat_mul(q, q, ql);
+          quat2mat(Rq, q);
+          mat_vec(v, Rq, m.jnt_pos + 3 * j);
+          p[0] = anc[0] - v[0]; p[1] = anc[1] - v[1]; p[2] = anc[2] - v[2];
+        }
+        if (k == b) {
+          xanchor[3 * j] = anc[0]; xanchor[3 * j + 1] = anc[1]; xanchor[3 * j + 2] = anc[2];
+          xaxis[3 * j] = ax[0]; xaxis[3 * j + 1] = ax[1]; xaxis[3 * j + 2] = ax[2];
+        }
+      }
+      quat_normalize(q);
+    }
+    float R[9];
+    quat2mat(R, q);
+    xpos[3 * b] = p[0]; xpos[3 * b + 1] = p[1]; xpos[3 * b + 2] = p[2];
+    xquat[4 * b] = q[0]; xquat[4 * b + 1] = q[1]; xquat[4 * b + 2] = q[2]; xquat[4 * b + 3] = q[3];
+#pragma unroll
+    for (int k = 0; k < 9; k++) xmat[9 * b + k] = R[k];
+    float t[3], IR[9], IM[9];
+    mat_vec(t, R, body_ipos + 3 * b);
+    xipos[3 * b] = p[0] + t[0]; xipos[3 * b + 1] = p[1] + t[1]; xipos[3 * b + 2] = p[2] + t[2];
+    quat2mat(IR, body_iquat + 4 * b);
+    mat_mul(IM, R, IR);
+#pragma unroll
+    for (int k = 0; k < 9; k++) ximat[9 * b + k] = IM[k];
+  }
+  __syncthreads();
+
+  // geoms (all written out; collision geoms kept in LDS) and sites
+  for (int g = tid; g < m.ngeom; g += NT) {
+    const int b = m.geom_bodyid[g];
+    float t[3], GR[9], GM[9];
+    mat_vec(t, xmat + 9 * b, geom_pos + 3 * g);
+    float gp[3] = {xpos[3 * b] + t[0], xpos[3 * b + 1] + t[1], xpos[3 * b + 2] + t[2]};
+    quat2mat(GR, geom_quat + 4 * g);
+    mat_mul(GM, xmat + 9 * b, GR);
+    float* og = d.geom_xpos + W * m.ngeom * 3 + 3 * g;
+    og[0] = gp[0]; og[1] = gp[1]; og[2] = gp[2];
+    float* om = d.geom_xmat + W * m.ngeom * 9 + 9 * g;
+#pragma unroll
+    for (int k = 0; k < 9; k++) om[k] = GM[k];
+    const int slot = m.geom_colslot[g];
+    if (slot >= 0) {
+      cgpos[3 * slot] = gp[0]; cgpos[3 * slot + 1] = gp[1]; cgpos[3 * slot + 2] = gp[2];
+#pragma unroll
+      for (int k = 0; k < 9; k++) cgmat[9 * slot + k] = GM[k];
+    }
+  }
+  for (int s = tid; s < m.nsite; s += NT) {
+    const int b = m.site_bodyid[s];
+    float t[3], SR[9], SM[9];
+    mat_vec(t, xmat + 9 * b, site_pos + 3 * s);
+    quat2mat(SR, site_quat + 4 * s);
+    mat_mul(SM, xmat + 9 * b, SR);
+    sxpos[3 * s] = xpos[3 * b] + t[0]; sxpos[3 * s + 1] = xpos[3 * b + 1] + t[1]; sxpos[3 * s + 2] = xpos[3 * b + 2] + t[2];
+#pragma unroll
+    for (int k = 0; k < 9; k++) sxmat[9 * s + k] = SM[k];
+  }
+
+  // ---------------------------------------------------------------- com_pos
+  // subtree com: lane b sums the bodies whose chain contains b
+  for (int b = tid; b < nb; b += NT) {
+    float ms = 0.f, mp[3] = {0.f, 0.f, 0.f};
+    for (int k = 0; k < nb; k++) {
+      const bool in = (b == 0) || ((unsigned long long)m.body_treemask[k] >> b) & 1ull;
+      if (!in) continue;
+      const float mk = body_mass[k];
+      ms += mk;
+      mp[0] += mk * xipos[3 * k]; mp[1] += mk * xipos[3 * k + 1]; mp[2] += mk * xipos[3 * k + 2];
+    }
+    if (ms < MJH_MINVAL) {
+      subtree_com[3 * b] = xipos[3 * b]; subtree_com[3 * b + 1] = xipos[3 * b + 1]; subtree_com[3 * b + 2] = xipos[3 * b + 2];
+    } else {
+      const float inv = 1.f / ms;
+      subtree_com[3 * b] = mp[0] * inv; subtree_com[3 * b + 1] = mp[1] * inv; subtree_com[3 * b + 2] = mp[2] * inv;
+    }
+  }
+  __syncthreads();
+  for (int b = tid; b < nb; b += NT) {
+    float* ci = cinert + 10 * b;
+    const float* R = ximat + 9 * b;
+    const float* c = subtree_com + 3 * m.body_rootid[b];
+    const float dd0 = xipos[3 * b] - c[0], dd1 = xipos[3 * b + 1] - c[1], dd2 = xipos[3 * b + 2] - c[2];
+    const float* in = body_inertia + 3 * b;
+    float I[6];  // xx yy zz xy xz yz of R diag(in) R^T
+    I[0] = R[0] * in[0] * R[0] + R[1] * in[1] * R[1] + R[2] * in[2] * R[2];
+    I[1] = R[3] * in[0] * R[3] + R[4] * in[1] * R[4] + R[5] * in[2] * R[5];
+    I[2] = R[6] * in[0] * R[6] + R[7] * in[1] * R[7] + R[8] * in[2] * R[8];
+    I[3] = R[0] * in[0] * R[3] + R[1] * in[1] * R[4] + R[2] * in[2] * R[5];
+    I[4] = R[0] * in[0] * R[6] + R[1] * in[1] * R[7] + R[2] * in[2] * R[8];
+    I[5] = R[3] * in[0] * R[6] + R[4] * in[1] * R[7] + R[5] * in[2] * R[8];
+    const float mm = body_mass[b], dsq = dd0 * dd0 + dd1 * dd1 + dd2 * dd2;
+    ci[0] = I[0] + mm * (dsq - dd0 * dd0);
+    ci[1] = I[1] + mm * (dsq - dd1 * dd1);
+    ci[2] = I[2] + mm * (dsq - dd2 * dd2);
+    ci[3] = I[3] - mm * dd0 * dd1;
+    ci[4] = I[4] - mm * dd0 * dd2;
+    ci[5] = I[5] - mm * dd1 * dd2;
+    ci[6] = mm * dd0; ci[7] = mm * dd1; ci[8] = mm * dd2; ci[9] = mm;
+  }
+  for (int j = tid; j < nj; j += NT) {
+    const int b = m.jnt_bodyid[j], da = m.jnt_dofadr[j];
+    const float* c = subtree_com + 3 * m.body_rootid[b];
+    float off[3] = {c[0] - xanchor[3 * j], c[1] - xanchor[3 * j + 1], c[2] - xanchor[3 * j + 2]};
+    const int t = m.jnt_type[j];
+    if (t == 0) {
+      for (int k = 0; k < 3; k++) {
+        float* cd = cdof + 6 * (da + k);
+        cd[0] = cd[1] = cd[2] = cd[3] = cd[4] = cd[5] = 0.f;
+        cd[3 + k] = 1.f;
+        float* cr = cdof + 6 * (da + 3 + k);
+        float ax[3] = {xmat[9 * b + k], xmat[9 * b + 3 + k], xmat[9 * b + 6 + k]};
+        cr[0] = ax[0]; cr[1] = ax[1]; cr[2] = ax[2];
+        cross3(cr + 3, ax, off);
+      }
+    } else if (t == 2) {
+      float* cd = cdof + 6 * da;
+      cd[0] = cd[1] = cd[2] = 0.f;
+      cd[3] = xaxis[3 * j]; cd[4] = xaxis[3 * j + 1]; cd[5] = xaxis[3 * j + 2];
+    } else {
+      float* cd = cdof + 6 * da;
+      cd[0] = xaxis[3 * j]; cd[1] = xaxis[3 * j + 1]; cd[2] = xaxis[3 * j + 2];
+      cross3(cd + 3, xaxis + 3 * j, off);
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- crb + M
+  for (int b = tid; b < nb; b += NT) {
+    float acc[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (b > 0)
+      for (int k = b; k < nb; k++) {
+        if (!(((unsigned long long)m.body_treemask[k] >> b) & 1ull)) continue;
+#pragma unroll
+        for (int c = 0; c < 10; c++) acc[c] += cinert[10 * k + c];
+      }
+#pragma unroll
+    for (int c = 0; c < 10; c++) crb[10 * b + c] = acc[c];
+  }
+  for (int i = tid; i < nv * ldm; i += NT) Mm[i] = 0.f;
+  __syncthreads();
+  for (int i = tid; i < nv; i += NT) {
+    float buf[6];
+    inert_vec(buf, crb + 10 * m.dof_bodyid[i], cdof + 6 * i);
+    unsigned long long mask = (unsigned long long)m.body_dofmask[m.dof_bodyid[i]];
+    mask &= (i == 63) ? ~0ull : ((2ull << i) - 1ull);
+    while (mask) {
+      const int j = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const float* cj = cdof + 6 * j;
+      float s = cj[0] * buf[0] + cj[1] * buf[1] + cj[2] * buf[2] + cj[3] * buf[3] + cj[4] * buf[4] + cj[5] * buf[5];
+      if (j == i) s += dof_armature[i];
+      Mm[i * ldm + j] = s;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < nv * ldm; i += NT) Lm[i] = Mm[i];
+  ldl_factor<NT>(Lm, nv, ldm);
+
+  // ---------------------------------------------------------------- com_vel / rne (bias)
+  for (int b = tid; b < nb; b += NT) {
+    float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    unsigned long long mask = (unsigned long long)m.body_dofmask[b];
+    while (mask) {
+      const int j = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const float qv = qvel[j];
+#pragma unroll
+      for (int c = 0; c < 6; c++) v[c] += cdof[6 * j + c] * qv;
+    }
+#pragma unroll
+    for (int c = 0; c < 6; c++) cvel[6 * b + c] = v[c];
+  }
+  __syncthreads();
+  for (int i = tid; i < nv; i += NT) {
+    const int b = m.dof_bodyid[i], jnt = m.dof_jntid[i], da = m.jnt_dofadr[jnt];
+    const bool freej = m.jnt_type[jnt] == 0;
+    if (freej && i - da < 3) {
+      for (int c = 0; c < 6; c++) cdof_dot[6 * i + c] = 0.f;
+      continue;
+    }
+    float v[6];
+    const int p = m.body_parentid[b];
+#pragma unroll
+    for (int c = 0; c < 6; c++) v[c] = cvel[6 * p + c];
+    // earlier dofs of this body: other joints fully, own free joint translations only
+    for (int k = m.body_dofadr[b]; k < i; k++) {
+      const int jk = m.dof_jntid[k];
+      if (jk == jnt && !(freej && k - da < 3)) continue;
+#pragma unroll
+      for (int c = 0; c < 6; c++) v[c] += cdof[6 * k + c] * qvel[k];
+    }
+    cross_motion(cdof_dot + 6 * i, v, cdof + 6 * i);
+  }
+  __syncthreads();
+  {
+    const float g0 = -m.gravity_x, g1 = -m.gravity_y, g2 = -m.gravity_z;
+    for (int b = tid; b < nb; b += NT) {
+      float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
+      unsigned long long mask = (unsigned long long)m.body_dofmask[b];
+      while (mask) {
+        const int j = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const float qv = qvel[j];
+#pragma unroll
+        for (int c = 0; c < 6; c++) a[c] += cdof_dot[6 * j + c] * qv;
+      }
+      float f1[6], f2[6], f3[6];
+      inert_vec(f1, cinert + 10 * b, a);
+      inert_vec(f2, cinert + 10 * b, cvel + 6 * b);
+      cross_force(f3, cvel + 6 * b, f2);
+#pragma unroll
+      for (int c = 0; c < 6; c++) cfrc[6 * b + c] = (b == 0) ? 0.f : f1[c] + f3[c];
+    }
+  }
+  __syncthreads();
+  // subtree sums of cfrc into crb (crb no longer needed)
+  for (int b = tid; b < nb; b += NT) {
+    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (b > 0)
+      for (int k = b; k < nb; k++) {
+        if (!(((unsigned long long)m.body_treemask[k] >> b) & 1ull)) continue;
+#pragma unroll
+        for (int c = 0; c < 6; c++) acc[c] += cfrc[6 * k + c];
+      }
+#pragma unroll
+    for (int c = 0; c < 6; c++) crb[6 * b + c] = acc[c];
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- passive, actuation, smooth force
+  for (int i = tid; i < nv; i += NT) {
+    const float* cd = cdof + 6 * i;
+    const float* f = crb + 6 * m.dof_bodyid[i];
+    qfrc_bias[i] = cd[0] * f[0] + cd[1] * f[1] + cd[2] * f[2] + cd[3] * f[3] + cd[4] * f[4] + cd[5] * f[5];
+    float pas = -dof_damping[i] * qvel[i];
+    const int jnt = m.dof_jntid[i];
+    const int t = m.jnt_type[jnt];
+    if ((t == 2 || t == 3) && jnt_stiffness[jnt] != 0.f) {
+      const int qa = m.jnt_qposadr[jnt];
+      pas -= jnt_stiffness[jnt] * (qpos[qa] - m.qpos_spring[qa]);
+    }
+    qfrc_passive[i] = pas;
+    qfrc_act[i] = 0.f;
+  }
+  __syncthreads();
+  for (int i = tid; i < nu; i += NT) {
+    const int j = m.actuator_trnid[i];
+    const float gear = m.actuator_gear[i];
+    const float len = gear * qpos[m.jnt_qposadr[j]];
+    const float vel = gear * qvel[m.jnt_dofadr[j]];
+    float c = d.ctrl[W * nu + i];
+    if (m.actuator_ctrllimited[i]) c = clampf(c, m.actuator_ctrlrange[2 * i], m.actuator_ctrlrange[2 * i + 1]);
+    const float* gp = m.actuator_gainprm + 10 * i;
+    const float* bp = m.actuator_biasprm + 10 * i;
+    float f = gp[0] * c + bp[0] + bp[1] * len + bp[2] * vel;
+    if (m.actuator_forcelimited[i]) f = clampf(f, m.actuator_forcerange[2 * i], m.actuator_forcerange[2 * i + 1]);
+    act_force[i] = f;
+    d.actuator_force[W * nu + i] = f;
+    d.actuator_length[W * nu + i] = len;
+    d.actuator_velocity[W * nu + i] = vel;
+    // one actuator per dof in mjlab models; atomic keeps it correct otherwise
+    atomicAdd(&qfrc_act[m.jnt_dofadr[j]], gear * f);
+  }
+  __syncthreads();
+  {
+    const float* xfrc = d.xfrc_applied + W * nb * 6;
+    for (int i = tid; i < nv; i += NT) {
+      float s = qfrc_passive[i] - qfrc_bias[i] + d.qfrc_applied[W * nv + i] + qfrc_act[i];
+      // J^T xfrc_applied at each body com
+      const float* cd = cdof + 6 * i;
+      for (int b = 1; b < nb; b++) {
+        if (!(((unsigned long long)m.body_dofmask[b] >> i) & 1ull)) continue;
+        const float* f = xfrc + 6 * b;
+        if (f[0] == 0.f && f[1] == 0.f && f[2] == 0.f && f[3] == 0.f && f[4] == 0.f && f[5] == 0.f) continue;
+        const float* c = subtree_com + 3 * m.body_rootid[b];
+        float off[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
+        cross3(t, cd, off);
+        s += (cd[3] + t[0]) * f[0] + (cd[4] + t[1]) * f[1] + (cd[5] + t[2]) * f[2] + cd[0] * f[3] + cd[1] * f[4] + cd[2] * f[5];
+      }
+      qfrc_smooth[i] = s;
+      qacc_smooth[i] = s;
+    }
+  }
+  ldl_solve<NT>(Lm, nv, ldm, qacc_smooth);
+
+  // ---------------------------------------------------------------- collision
+  {
+    const int npair = m.npair;
+    for (int base = 0; base < npair; base += NT) {
+      const int p = base + tid;
+      Con cc[4];
+      int n = 0, g1 = 0, g2 = 0;
+      if (p < npair) {
+        g1 = m.pair_geom1[p];
+        g2 = m.pair_geom2[p];
+        const int s1 = m.geom_colslot[g1], s2 = m.geom_colslot[g2];
+        const float* p1 = cgpos + 3 * s1;
+        const float* p2 = cgpos + 3 * s2;
+        const float* m1 = cgmat + 9 * s1;
+        const float* m2 = cgmat + 9 * s2;
+        const float margin = fmaxf(m.geom_margin[g1], m.geom_margin[g2]);
+        const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+        float dif[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+        bool near;
+        if (t1 == 0) {
+          float nrm[3] = {m1[2], m1[5], m1[8]};
+          near = dot3(dif, nrm) <= margin + m.geom_rbound[g2];
+        } else {
+          near = sqrtf(dot3(dif, dif)) <= margin + m.geom_rbound[g1] + m.geom_rbound[g2];
+        }
+        if (near) n = narrowphase(t1, t2, p1, m1, m.geom_size + 3 * g1, p2, m2, m.geom_size + 3 * g2, margin, cc);
+      }
+      int total;
+      const int off = bscan<NT>(n, &total, redi);
+      const int base_con = ints[I_NCON];
+      if (n > 0) {
+        // contact parameters (mj_contactParam semantics)
+        int condim;
+        float fri[3], solref[2], solimp[5];
+        const int pr1 = m.geom_priority[g1], pr2 = m.geom_priority[g2];
+        if (pr1 != pr2) {
+          const int g = pr1 > pr2 ? g1 : g2;
+          condim = m.geom_condim[g];
+          for (int k = 0; k < 3; k++) fri[k] = geom_friction[3 * g + k];
+          for (int k = 0; k < 2; k++) solref[k] = m.geom_solref[2 * g + k];
+          for (int k = 0; k < 5; k++) solimp[k] = m.geom_solimp[5 * g + k];
+        } else {
+          condim = max(m.geom_condim[g1], m.geom_condim[g2]);
+          for (int k = 0; k < 3; k++) fri[k] = fmaxf(geom_friction[3 * g1 + k], geom_friction[3 * g2 + k]);
+          const float sm1 = m.geom_solmix[g1], sm2 = m.geom_solmix[g2];
+          float mix;
+          if (sm1 >= MJH_MINVAL && sm2 >= MJH_MINVAL) mix = sm1 / (sm1 + sm2);
+          else if (sm1 < MJH_MINVAL && sm2 < MJH_MINVAL) mix = 0.5f;
+          else mix = sm1 < MJH_MINVAL ? 0.f : 1.f;
+          const float* r1 = m.geom_solref + 2 * g1;
+          const float* r2 = m.geom_solref + 2 * g2;
+          if (r1[0] > 0.f && r2[0] > 0.f)
+            for (int k = 0; k < 2; k++) solref[k] = mix * r1[k] + (1.f - mix) * r2[k];
+          else
+            for (int k = 0; k < 2; k++) solref[k] = fminf(r1[k], r2[k]);
+          for (int k = 0; k < 5; k++) solimp[k] = mix * m.geom_solimp[5 * g1 + k] + (1.f - mix) * m.geom_solimp[5 * g2 + k];
+        }
+        const float imargin = fmaxf(m.geom_margin[g1], m.geom_margin[g2]) - fmaxf(m.geom_gap[g1], m.geom_gap[g2]);
+        for (int e = 0; e < n; e++) {
+          const int ci = base_con + off + e;
+          if (ci >= Lo.ncap) {
+            ints[I_FLAGS] |= MJH_FLAG_CONTACT_OVERFLOW;  // benign race: all writers set the same bit
+            break;
+          }
+          float fr[9] = {cc[e].frame[0], cc[e].frame[1], cc[e].frame[2], cc[e].frame[3], cc[e].frame[4], cc[e].frame[5], 0.f, 0.f, 0.f};
+          make_frame(fr);
+          con_dist[ci] = cc[e].dist;
+          for (int k = 0; k < 3; k++) con_pos[3 * ci + k] = cc[e].pos[k];
+          for (int k = 0; k < 9; k++) con_frame[9 * ci + k] = fr[k];
+          con_fric[5 * ci] = fri[0]; con_fric[5 * ci + 1] = fri[0]; con_fric[5 * ci + 2] = fri[1];
+          con_fric[5 * ci + 3] = fri[2]; con_fric[5 * ci + 4] = fri[2];
+          con_solref[2 * ci] = solref[0]; con_solref[2 * ci + 1] = solref[1];
+          for (int k = 0; k < 5; k++) con_solimp[5 * ci + k] = solimp[k];
+          con_imargin[ci] = imargin;
+          con_dim[ci] = condim;
+          con_geom[2 * ci] = g1;
+          con_geom[2 * ci + 1] = g2;
+          con_efcadr[ci] = -1;
+        }
+      }
+      __syncthreads();
+      if (tid == 0) ints[I_NCON] = min(base_con + total, Lo.ncap);
+      __syncthreads();
+    }
+  }
+  const int ncon = ints[I_NCON];
+
+  // ---------------------------------------------------------------- make_constraint
+  {
+    int nefc = 0;
+    const int rcap = Lo.rcap;
+    // dof friction loss rows
+    for (int base = 0; base < nv; base += NT) {
+      const int i = base + tid;
+      const int f = (i < nv && dof_frictionloss[i] > 0.f) ? 1 : 0;
+      int total;
+      const int off = bscan<NT>(f, &total, redi);
+      if (f) {
+        const int r = nefc + off;
+        if (r < rcap) {
+          efc_type[r] = MJH_CNSTR_FRICTION_DOF;
+          efc_id[r] = i;
+          efc_fl[r] = dof_frictionloss[i];
+          efc_mask[r] = 1ull << i;
+          efc_pos[r] = 0.f;
+          row_params(m.timestep, 0.f, 0.f, m.dof_invweight0[i], m.dof_solref + 2 * i, m.dof_solimp + 5 * i, qvel[i],
+                     efc_D + r, efc_R + r, efc_aref + r);
+        }
+      }
+      nefc += total;
+    }
+    // joint limits
+    for (int base = 0; base < nj; base += NT) {
+      const int j = base + tid;
+      int f = 0;
+      float pos = 0.f, sgn = 0.f;
+      if (j < nj && m.jnt_limited[j] && (m.jnt_type[j] == 2 || m.jnt_type[j] == 3)) {
+        const float q = qpos[m.jnt_qposadr[j]];
+        const float dlo = q - jnt_range[2 * j], dhi = jnt_range[2 * j + 1] - q;
+        pos = fminf(dlo, dhi) - m.jnt_margin[j];
+        sgn = dlo < dhi ? 1.f : -1.f;
+        f = pos < 0.f ? 1 : 0;
+      }
+      int total;
+      const int off = bscan<NT>(f, &total, redi);
+      if (f) {
+        const int r = nefc + off;
+        if (r < rcap) {
+          const int dof = m.jnt_dofadr[j];
+          efc_type[r] = MJH_CNSTR_LIMIT_JOINT;
+          efc_id[r] = j;
+          efc_fl[r] = 0.f;
+          efc_mask[r] = 1ull << dof;
+          efc_pos[r] = pos + m.jnt_margin[j];
+          jv[r] = sgn;  // temporarily hold the Jacobian sign
+          row_params(m.timestep, pos, pos, m.dof_invweight0[dof], m.jnt_solref + 2 * j, m.jnt_solimp + 5 * j,
+                     sgn * qvel[dof], efc_D + r, efc_R + r, efc_aref + r);
+        }
+      }
+      nefc += total;
+    }
+    const int nsimple = min(nefc, rcap);
+    // contact rows
+    for (int base = 0; base < ncon; base += NT) {
+      const int ci = base + tid;
+      int nr = 0;
+      if (ci < ncon && con_dist[ci] - con_imargin[ci] < 0.f) nr = con_dim[ci] == 1 ? 1 : 2 * (con_dim[ci] - 1);
+      int total;
+      const int off = bscan<NT>(nr, &total, redi);
+      if (nr) {
+        const int r0 = nefc + off;
+        if (r0 + nr <= rcap) {
+          con_efcadr[ci] = r0;
+        } else {
+          con_efcadr[ci] = -1;
+          atomicMin(&ints[I_MISC], r0);  // rows of this and later contacts are dropped
+        }
+      }
+      nefc += total;
+    }
+    __syncthreads();
+    if (nefc > rcap) {
+      if (tid == 0) ints[I_FLAGS] |= MJH_FLAG_EFC_OVERFLOW;
+      nefc = max(nsimple, min(rcap, ints[I_MISC]));
+    }
+    __syncthreads();
+    // zero J rows, write the single-dof rows
+    for (int i = tid; i < nefc * ldj; i += NT) J[i] = 0.f;
+    __syncthreads();
+    for (int r = tid; r < nsimple; r += NT) {
+      const int t = efc_type[r];
+      if (t == MJH_CNSTR_FRICTION_DOF) J[r * ldj + efc_id[r]] = 1.f;
+      else J[r * ldj + m.jnt_dofadr[efc_id[r]]] = jv[r];
+    }
+    // contact Jacobian rows: flat over (contact, dof)
+    for (int item = tid; item < ncon * nv; item += NT) {
+      const int ci = item / nv, dof = item - ci * nv;
+      const int r0 = con_efcadr[ci];
+      if (r0 < 0) continue;
+      const int b1 = m.geom_bodyid[con_geom[2 * ci]], b2 = m.geom_bodyid[con_geom[2 * ci + 1]];
+      const bool in1 = ((unsigned long long)m.body_dofmask[b1] >> dof) & 1ull;
+      const bool in2 = ((unsigned long long)m.body_dofmask[b2] >> dof) & 1ull;
+      const int dim = con_dim[ci];
+      const int nr = dim == 1 ? 1 : 2 * (dim - 1);
+      if (in1 == in2) {  // not in either chain, or in both (relative motion cancels)
+        continue;
+      }
+      const float sg = in2 ? 1.f : -1.f;
+      const int bb = in2 ? b2 : b1;
+      const float* cd = cdof + 6 * dof;
+      const float* c = subtree_com + 3 * m.body_rootid[bb];
+      const float* cp = con_pos + 3 * ci;
+      float off[3] = {cp[0] - c[0], cp[1] - c[1], cp[2] - c[2]}, t[3];
+      cross3(t, cd, off);
+      float jp[3] = {sg * (cd[3] + t[0]), sg * (cd[4] + t[1]), sg * (cd[5] + t[2])};
+      float jr[3] = {sg * cd[0], sg * cd[1], sg * cd[2]};
+      const float* fr = con_frame + 9 * ci;
+      float jf[6];
+      jf[0] = dot3(fr, jp); jf[1] = dot3(fr + 3, jp); jf[2] = dot3(fr + 6, jp);
+      jf[3] = dot3(fr, jr); jf[4] = dot3(fr + 3, jr); jf[5] = dot3(fr + 6, jr);
+      if (dim == 1) {
+        J[r0 * ldj + dof] = jf[0];
+      } else {
+        for (int e = 0; e < nr; e++) {
+          const int k = e / 2 + 1;
+          const float fk = con_fric[5 * ci + k - 1];
+          J[(r0 + e) * ldj + dof] = jf[0] + ((e & 1) ? -fk : fk) * jf[k];
+        }
+      }
+    }
+    // contact row parameters
+    for (int ci = tid; ci < ncon; ci += NT) {
+      const int r0 = con_efcadr[ci];
+      if (r0 < 0) continue;
+      const int b1 = m.geom_bodyid[con_geom[2 * ci]], b2 = m.geom_bodyid[con_geom[2 * ci + 1]];
+      const int dim = con_dim[ci];
+      const int nr = dim == 1 ? 1 : 2 * (dim - 1);
+      const unsigned long long msk =
+          (unsigned long long)m.body_dofmask[b1] ^ (unsigned long long)m.body_dofmask[b2];
+      for (int e = 0; e < nr; e++) {
+        const int r = r0 + e;
+        efc_type[r] = dim == 1 ? MJH_CNSTR_CONTACT_FRICTIONLESS : MJH_CNSTR_CONTACT_PYRAMIDAL;
+        efc_id[r] = ci;
+        efc_fl[r] = 0.f;
+        efc_mask[r] = msk;
+        efc_pos[r] = con_dist[ci];
+      }
+    }
+    __syncthreads();
+    for (int r = tid; r < nefc; r += NT) {
+      if (efc_type[r] != MJH_CNSTR_CONTACT_FRICTIONLESS && efc_type[r] != MJH_CNSTR_CONTACT_PYRAMIDAL) continue;
+      const int ci = efc_id[r];
+      const int b1 = m.geom_bodyid[con_geom[2 * ci]], b2 = m.geom_bodyid[con_geom[2 * ci + 1]];
+      float invw = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+      if (con_dim[ci] > 1) {
+        const float f0 = con_fric[5 * ci];
+        invw = invw + f0 * f0 * invw;
+        invw = invw * 2.f * f0 * f0 / m.impratio;
+      }
+      float jq = 0.f;
+      for (int k = 0; k < nv; k++) jq += J[r * ldj + k] * qvel[k];
+      const float pos = con_dist[ci] - con_imargin[ci];
+      row_params(m.timestep, pos, pos, invw, con_solref + 2 * ci, con_solimp + 5 * ci, jq, efc_D + r, efc_R + r,
+                 efc_aref + r);
+    }
+    if (tid == 0) ints[I_NEFC] = nefc;
+    __syncthreads();
+  }
+  const int nefc = ints[I_NEFC];
+
+  // ---------------------------------------------------------------- Newton solver
+  const float scale = 1.f / (m.meaninertia * (float)(nv > 1 ? nv : 1));
+  int niter = 0;
+  if (nefc == 0) {
+    for (int i = tid; i < nv; i += NT) {
+      qacc[i] = qacc_smooth[i];
+      qfrc_con[i] = 0.f;
+    }
+    __syncthreads();
+  } else {
+    // jaref = J x - aref ; Ma = M x ; forces, qfrc_constraint, cost
+    auto eval_point = [&](const float* x) {
+      symv<NT>(Mm, nv, ldm, x, Ma);
+      for (int r = tid; r < nefc; r += NT) {
+        float s = 0.f;
+        for (int k = 0; k < nv; k++) s += J[r * ldj + k] * x[k];
+        jaref[r] = s - efc_aref[r];
+      }
+      __syncthreads();
+    };
+    auto update_constraint = [&]() -> float {
+      float c = 0.f;
+      for (int r = tid; r < nefc; r += NT) {
+        float f, cr;
+        row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], jaref[r], &f, &cr);
+        efc_force[r] = f;
+        c += cr;
+      }
+      for (int i = tid; i < nv; i += NT) c += 0.5f * (Ma[i] - qfrc_smooth[i]) * (qacc[i] - qacc_smooth[i]);
+      __syncthreads();
+      for (int i = tid; i < nv; i += NT) {
+        float s = 0.f;
+        for (int r = 0; r < nefc; r++) {
+          const float f = efc_force[r];
+          if (f != 0.f && ((efc_mask[r] >> i) & 1ull)) s += J[r * ldj + i] * f;
+        }
+        qfrc_con[i] = s;
+      }
+      return bsum<NT>(c, red);
+    };
+    auto newton_direction = [&]() {
+      for (int i = tid; i < nv; i += NT) grad[i] = Ma[i] - qfrc_smooth[i] - qfrc_con[i];
+      // H = M + J' diag(h) J  (lower triangle), stored in Lm
+      const int ntri = nv * (nv + 1) / 2;
+      for (int q = tid; q < ntri; q += NT) {
+        int i, j;
+        tri_rev(q, nv, i, j);
+        float s = Mm[i * ldm + j];
+        for (int r = 0; r < nefc; r++) {
+          const unsigned long long mk = efc_mask[r];
+          if (!((mk >> i) & 1ull) || !((mk >> j) & 1ull)) continue;
+          float f, cr;
+          const float h = row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], jaref[r], &f, &cr);
+          if (h == 0.f) continue;
+          s += h * J[r * ldj + i] * J[r * ldj + j];
+        }
+        Lm[i * ldm + j] = s;
+      }
+      ldl_factor<NT>(Lm, nv, ldm);
+      for (int i = tid; i < nv; i += NT) search[i] = grad[i];
+      ldl_solve<NT>(Lm, nv, ldm, search);
+      for (int i = tid; i < nv; i += NT) search[i] = -search[i];
+      __syncthreads();
+    };
+
+    // warm start: the cheaper of qacc_warmstart and qacc_smooth
+    for (int i = tid; i < nv; i += NT) qacc[i] = d.qacc_warmstart[W * nv + i];
+    __syncthreads();
+    eval_point(qacc);
+    float cost = update_constraint();
+    float cs = 0.f;
+    for (int r = tid; r < nefc; r += NT) {
+      float s = 0.f;
+      for (int k = 0; k < nv; k++) s += J[r * ldj + k] * qacc_smooth[k];
+      float f, cr;
+      row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], s - efc_aref[r], &f, &cr);
+      cs += cr;
+    }
+    const float cost_smooth = bsum<NT>(cs, red);
+    if (cost > cost_smooth) {
+      for (int i = tid; i < nv; i += NT) qacc[i] = qacc_smooth[i];
+      __syncthreads();
+      eval_point(qacc);
+      cost = update_constraint();
+    }
+    __syncthreads();
+    newton_direction();
+
+    for (int it = 0; it < m.iterations; it++) {
+      // ---- exact line search along `search`
+      symv<NT>(Mm, nv, ldm, search, Mv);
+      for (int r = tid; r < nefc; r += NT) {
+        float s = 0.f;
+        for (int k = 0; k < nv; k++) s += J[r * ldj + k] * search[k];
+        jv[r] = s;
+      }
+      __syncthreads();
+      float g1 = 0.f, g2 = 0.f;
+      for (int i = tid; i < nv; i += NT) {
+        g1 += search[i] * (Ma[i] - qfrc_smooth[i]);
+        g2 += search[i] * Mv[i];
+      }
+      bsum2<NT>(g1, g2, red);
+      auto derivs = [&](float alpha, float& d1, float& d2) {
+        float a = 0.f, b = 0.f;
+        for (int r = tid; r < nefc; r += NT) {
+          float f, cr;
+          const float h = row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], jaref[r] + alpha * jv[r], &f, &cr);
+          a -= f * jv[r];
+          b += h * jv[r] * jv[r];
+        }
+        bsum2<NT>(a, b, red);
+        d1 = g1 + alpha * g2 + a;
+        d2 = g2 + b;
+      };
+      float d10, d20;
+      derivs(0.f, d10, d20);
+      float alpha = 0.f;
+      if (d10 < 0.f) {
+        const float gtol = m.ls_tolerance * fabsf(d10);
+        float lo = 0.f, hi = -1.f;
+        alpha = -d10 / d20;
+        for (int li = 0; li < m.ls_iterations; li++) {
+          float d1, d2;
+          derivs(alpha, d1, d2);
+          if (fabsf(d1) <= gtol) break;
+          if (d1 < 0.f) lo = alpha; else hi = alpha;
+          float an = alpha - d1 / d2;
+          if (an <= lo || (hi >= 0.f && an >= hi)) an = hi >= 0.f ? 0.5f * (lo + hi) : 2.f * alpha;
+          alpha = an;
+        }
+      }
+      if (alpha == 0.f) break;
+      for (int i = tid; i < nv; i += NT) {
+        qacc[i] += alpha * search[i];
+        Ma[i] += alpha * Mv[i];
+      }
+      for (int r = tid; r < nefc; r += NT) jaref[r] += alpha * jv[r];
+      __syncthreads();
+      const float old = cost;
+      cost = update_constraint();
+      __syncthreads();
+      newton_direction();
+      niter++;
+      float gn = 0.f;
+      for (int i = tid; i < nv; i += NT) gn += grad[i] * grad[i];
+      gn = bsum<NT>(gn, red);
+      const float improvement = scale * (old - cost), gradient = scale * sqrtf(gn);
+      if (improvement < m.tolerance || gradient < m.tolerance) break;
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- post-constraint acceleration (cacc)
+  {
+    const float g0 = -m.gravity_x, g1 = -m.gravity_y, g2 = -m.gravity_z;
+    for (int b = tid; b < nb; b += NT) {
+      float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
+      unsigned long long mask = (unsigned long long)m.body_dofmask[b];
+      while (mask) {
+        const int j = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const float qv = qvel[j], qa = qacc[j];
+#pragma unroll
+        for (int c = 0; c < 6; c++) a[c] += cdof_dot[6 * j + c] * qv + cdof[6 * j + c] * qa;
+      }
+#pragma unroll
+      for (int c = 0; c < 6; c++) cacc[6 * b + c] = a[c];
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- sensors
+  {
+    float* sd = d.sensordata + W * m.nsensordata;
+    for (int s = 0; s < m.nsensor; s++) {
+      const int type = m.sensor_type[s], id = m.sensor_objid[s], adr = m.sensor_adr[s];
+      if (type == 40) {
+        // contact sensor: lanes over contacts
+        const int bits = m.sensor_intprm[3 * s], reduce = m.sensor_intprm[3 * s + 1], nslot = m.sensor_intprm[3 * s + 2];
+        const int otype = m.sensor_objtype[s], rtype = m.sensor_reftype[s], rid = m.sensor_refid[s];
+        const int dim = m.sensor_dim[s];
+        for (int k = tid; k < dim; k += NT) sd[adr + k] = 0.f;
+        __syncthreads();
+        // match flags
+        float cnt = 0.f, fx = 0.f, fy = 0.f, fz = 0.f;
+        for (int base = 0; base < ncon; base += NT) {
+          const int ci = base + tid;
+          int match = 0;
+          float Fw[3] = {0.f, 0.f, 0.f};
+          if (ci < ncon) {
+            const int g1 = con_geom[2 * ci], g2 = con_geom[2 * ci + 1];
+            auto om = [&](int ty, int oid, int g) -> bool {
+              if (oid < 0) return true;
+              const int gb = m.geom_bodyid[g];
+              if (ty == 5) return g == oid;
+              if (ty == 1) return gb == oid;
+              if (ty == 2) return oid == 0 || (((unsigned long long)m.body_treemask[gb] >> oid) & 1ull);
+              return false;
+            };
+            int flip = 0;
+            if (om(otype, id, g1) && om(rtype, rid, g2)) match = 1;
+            else if (om(otype, id, g2) && om(rtype, rid, g1)) { match = 1; flip = 1; }
+            if (match) {
+              const int r0 = con_efcadr[ci];
+              float F[3] = {0.f, 0.f, 0.f};
+              if (r0 >= 0) {
+                const int cdm = con_dim[ci];
+                if (cdm == 1) {
+                  F[0] = efc_force[r0];
+                } else {
+                  for (int e = 0; e < 2 * (cdm - 1); e++) F[0] += efc_force[r0 + e];
+                  for (int k = 1; k < 3 && k < cdm; k++) F[k] = con_fric[5 * ci + k - 1] * (efc_force[r0 + 2 * k - 2] - efc_force[r0 + 2 * k - 1]);
+                }
+              }
+              const float* fr = con_frame + 9 * ci;
+              const float sgn = flip ? 1.f : -1.f;
+              for (int a = 0; a < 3; a++) Fw[a] = sgn * (F[0] * fr[a] + F[1] * fr[3 + a] + F[2] * fr[6 + a]);
+              // non-netforce, single slot, reduce none: first match in contact order
+              if (reduce != 3) {
+                // slot fill handled below by the first matching lane (serialised)
+              }
+            }
+          }
+          int total;
+          const int off = bscan<NT>(match, &total, redi);
+          if (reduce != 3 && match && off < nslot) {
+            // "none"/"mindist"/"maxforce" with the first nslot matches in contact order
+            // (mindist/maxforce reordering applied below for nslot == 1)
+            const int slot = (int)cnt + off;
+            if (slot < nslot) {
+              const int width = dim / nslot;
+              float* o = sd + adr + slot * width;
+              const int r0 = con_efcadr[ci];
+              float F[3] = {0.f, 0.f, 0.f};
+              if (r0 >= 0) {
+                const int cdm = con_dim[ci];
+                if (cdm == 1) F[0] = efc_force[r0];
+                else {
+                  for (int e = 0; e < 2 * (cdm - 1); e++) F[0] += efc_force[r0 + e];
+                  for (int k = 1; k < 3 && k < cdm; k++) F[k] = con_fric[5 * ci + k - 1] * (efc_force[r0 + 2 * k - 2] - efc_force[r0 + 2 * k - 1]);
+                }
+              }
+              int q = 0;
+              if (bits & 1) o[q++] = -1.f;  // patched with the total below
+              if (bits & 2) { o[q++] = F[0]; o[q++] = F[1]; o[q++] = F[2]; }
+              if (bits & 4) { o[q++] = 0.f; o[q++] = 0.f; o[q++] = 0.f; }
+              if (bits & 8) o[q++] = con_dist[ci];
+              if (bits & 16) { o[q++] = con_pos[3 * ci]; o[q++] = con_pos[3 * ci + 1]; o[q++] = con_pos[3 * ci + 2]; }
+              const float* fr = con_frame + 9 * ci;
+              const int g1 = con_geom[2 * ci];
+              const bool flipped = !(otype == 5 ? g1 == id : (otype == 1 ? m.geom_bodyid[g1] == id
+                                        : (id == 0 || (((unsigned long long)m.body_treemask[m.geom_bodyid[g1]] >> id) & 1ull))));
+              const float sg = flipped ? -1.f : 1.f;
+              if (bits & 32) { o[q++] = sg * fr[0]; o[q++] = sg * fr[1]; o[q++] = sg * fr[2]; }
+              if (bits & 64) { o[q++] = sg * fr[3]; o[q++] = sg * fr[4]; o[q++] = sg * fr[5]; }
+            }
+          }
+          cnt += (float)total;
+          fx += Fw[0]; fy += Fw[1]; fz += Fw[2];
+          __syncthreads();
+        }
+        float sx = fx, sy = fy;
+        bsum2<NT>(sx, sy, red);
+        const float sz = bsum<NT>(fz, red);
+        const float found = fminf(cnt, (float)m.contact_sensor_maxmatch);
+        if (tid == 0 && cnt > 0.f) {
+          if (reduce == 3) {
+            int q = 0;
+            float* o = sd + adr;
+            if (bits & 1) o[q++] = found;
+            if (bits & 2) { o[q++] = sx; o[q++] = sy; o[q++] = sz; }
+          } else if (bits & 1) {
+            const int width = dim / nslot;
+            for (int sl = 0; sl < nslot && sl < (int)cnt; sl++) sd[adr + sl * width] = found;
+          }
+        }
+        __syncthreads();
+        continue;
+      }
+      if (tid != 0) continue;
+      float* out = sd + adr;
+      switch (type) {
+        case 3: {  // gyro
+          const int b = m.site_bodyid[id];
+          float r[3];
+          matT_vec(r, sxmat + 9 * id, cvel + 6 * b);
+          out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
+          break;
+        }
+        case 2:
+        case 1: {  // velocimeter / accelerometer
+          const int b = m.site_bodyid[id];
+          const float* c = subtree_com + 3 * m.body_rootid[b];
+          const float* sp = sxpos + 3 * id;
+          float dif[3] = {sp[0] - c[0], sp[1] - c[1], sp[2] - c[2]}, t[3], lin[3], r[3];
+          const float* v = cvel + 6 * b;
+          cross3(t, dif, v);
+          lin[0] = v[3] - t[0]; lin[1] = v[4] - t[1]; lin[2] = v[5] - t[2];
+          matT_vec(r, sxmat + 9 * id, lin);
+          if (type == 2) {
+            out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
+          } else {
+            const float* a = cacc + 6 * b;
+            float al[3], ar[3], wl[3], cor[3];
+            cross3(t, dif, a);
+            al[0] = a[3] - t[0]; al[1] = a[4] - t[1]; al[2] = a[5] - t[2];
+            matT_vec(ar, sxmat + 9 * id, al);
+            matT_vec(wl, sxmat + 9 * id, v);
+            cross3(cor, wl, r);
+            out[0] = ar[0] + cor[0]; out[1] = ar[1] + cor[1]; out[2] = ar[2] + cor[2];
+          }
+          break;
+        }
+        case 30: out[0] = sxpos[3 * id]; out[1] = sxpos[3 * id + 1]; out[2] = sxpos[3 * id + 2]; break;
+        case 9: out[0] = qpos[m.jnt_qposadr[id]]; break;
+        case 10: out[0] = qvel[m.jnt_dofadr[id]]; break;
+        case 34: out[0] = subtree_com[3 * id]; out[1] = subtree_com[3 * id + 1]; out[2] = subtree_com[3 * id + 2]; break;
+        case 31: {
+          const float* R = sxmat + 9 * id;
+          float q[4], tr = R[0] + R[4] + R[8];
+          if (tr > 0.f) {
+            float sq = sqrtf(tr + 1.f) * 2.f;
+            q[0] = 0.25f * sq; q[1] = (R[7] - R[5]) / sq; q[2] = (R[2] - R[6]) / sq; q[3] = (R[3] - R[1]) / sq;
+          } else if (R[0] > R[4] && R[0] > R[8]) {
+            float sq = sqrtf(1.f + R[0] - R[4] - R[8]) * 2.f;
+            q[0] = (R[7] - R[5]) / sq; q[1] = 0.25f * sq; q[2] = (R[1] + R[3]) / sq; q[3] = (R[2] + R[6]) / sq;
+          } else if (R[4] > R[8]) {
+            float sq = sqrtf(1.f + R[4] - R[0] - R[8]) * 2.f;
+            q[0] = (R[2] - R[6]) / sq; q[1] = (R[1] + R[3]) / sq; q[2] = 0.25f * sq; q[3] = (R[5] + R[7]) / sq;
+          } else {
+            float sq = sqrtf(1.f + R[8] - R[0] - R[4]) * 2.f;
+            q[0] = (R[3] - R[1]) / sq; q[1] = (R[2] + R[6]) / sq; q[2] = (R[5] + R[7]) / sq; q[3] = 0.25f * sq;
+          }
+          if (q[0] < 0.f) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+          quat_normalize(q);
+          out[0] = q[0]; out[1] = q[1]; out[2] = q[2]; out[3] = q[3];
+          break;
+        }
+        case 35:
+        case 36: {
+          float msum = 0.f, lin[3] = {0.f, 0.f, 0.f};
+          for (int b = 1; b < nb; b++) {
+            if (!(id == 0 || (((unsigned long long)m.body_treemask[b] >> id) & 1ull))) continue;
+            const float bm = cinert[10 * b + 9];
+            const float* c = subtree_com + 3 * m.body_rootid[b];
+            const float* v = cvel + 6 * b;
+            float dif[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
+            cross3(t, dif, v);
+            msum += bm;
+            lin[0] += bm * (v[3] - t[0]); lin[1] += bm * (v[4] - t[1]); lin[2] += bm * (v[5] - t[2]);
+          }
+          float vc[3] = {0.f, 0.f, 0.f};
+          if (msum > MJH_MINVAL) { vc[0] = lin[0] / msum; vc[1] = lin[1] / msum; vc[2] = lin[2] / msum; }
+          if (type == 35) { out[0] = vc[0]; out[1] = vc[1]; out[2] = vc[2]; break; }
+          float L[3] = {0.f, 0.f, 0.f};
+          const float* sc = subtree_com + 3 * id;
+          for (int b = 1; b < nb; b++) {
+            if (!(id == 0 || (((unsigned long long)m.body_treemask[b] >> id) & 1ull))) continue;
+            const float bm = cinert[10 * b + 9];
+            const float* c = subtree_com + 3 * m.body_rootid[b];
+            const float* v = cvel + 6 * b;
+            float dd[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
+            cross3(t, dd, v);
+            float vb[3] = {v[3] - t[0], v[4] - t[1], v[5] - t[2]};
+            const float* ci = cinert + 10 * b;
+            const float dsq = dot3(dd, dd);
+            float I[9] = {ci[0] - bm * (dsq - dd[0] * dd[0]), ci[3] + bm * dd[0] * dd[1], ci[4] + bm * dd[0] * dd[2],
+                          ci[3] + bm * dd[0] * dd[1], ci[1] - bm * (dsq - dd[1] * dd[1]), ci[5] + bm * dd[1] * dd[2],
+                          ci[4] + bm * dd[0] * dd[2], ci[5] + bm * dd[1] * dd[2], ci[2] - bm * (dsq - dd[2] * dd[2])};
+            float Iw[3], dx[3], dv[3];
+            mat_vec(Iw, I, v);
+            for (int k = 0; k < 3; k++) { dx[k] = xipos[3 * b + k] - sc[k]; dv[k] = (vb[k] - vc[k]) * bm; }
+            cross3(t, dx, dv);
+            L[0] += Iw[0] + t[0]; L[1] += Iw[1] + t[1]; L[2] += Iw[2] + t[2];
+          }
+          out[0] = L[0]; out[1] = L[1]; out[2] = L[2];
+          break;
+        }
+        default:
+          break;
+      }
+      const float cut = m.sensor_cutoff[s];
+      if (cut > 0.f && type != 31)
+        for (int k = 0; k < m.sensor_dim[s]; k++) out[k] = clampf(out[k], -cut, cut);
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- forward outputs
+  for (int i = tid; i < nb * 3; i += NT) {
+    d.xpos[W * nb * 3 + i] = xpos[i];
+    d.xipos[W * nb * 3 + i] = xipos[i];
+    d.subtree_com[W * nb * 3 + i] = subtree_com[i];
+  }
+  for (int i = tid; i < nb * 4; i += NT) d.xquat[W * nb * 4 + i] = xquat[i];
+  for (int i = tid; i < nb * 9; i += NT) {
+    d.xmat[W * nb * 9 + i] = xmat[i];
+    d.ximat[W * nb * 9 + i] = ximat[i];
+  }
+  for (int i = tid; i < nb * 6; i += NT) {
+    d.cvel[W * nb * 6 + i] = cvel[i];
+    d.cacc[W * nb * 6 + i] = cacc[i];
+  }
+  for (int i = tid; i < nj * 3; i += NT) {
+    d.xanchor[W * nj * 3 + i] = xanchor[i];
+    d.xaxis[W * nj * 3 + i] = xaxis[i];
+  }
+  for (int i = tid; i < m.nsite * 3; i += NT) d.site_xpos[W * m.nsite * 3 + i] = sxpos[i];
+  for (int i = tid; i < m.nsite * 9; i += NT) d.site_xmat[W * m.nsite * 9 + i] = sxmat[i];
+  for (int i = tid; i < nv; i += NT) {
+    d.qfrc_bias[W * nv + i] = qfrc_bias[i];
+    d.qfrc_passive[W * nv + i] = qfrc_passive[i];
+    d.qfrc_actuator[W * nv + i] = qfrc_act[i];
+    d.qfrc_smooth[W * nv + i] = qfrc_smooth[i];
+    d.qfrc_constraint[W * nv + i] = qfrc_con[i];
+    d.qacc_smooth[W * nv + i] = qacc_smooth[i];
+    d.qacc[W * nv + i] = qacc[i];
+    d.qacc_warmstart[W * nv + i] = qacc[i];
+  }
+  for (int ci = tid; ci < ncon; ci += NT) {
+    const long long o = W * m.nconmax + ci;
+    d.contact_dist[o] = con_dist[ci];
+    for (int k = 0; k < 3; k++) d.contact_pos[3 * o + k] = con_pos[3 * ci + k];
+    for (int k = 0; k < 9; k++) d.contact_frame[9 * o + k] = con_frame[9 * ci + k];
+    for (int k = 0; k < 5; k++) d.contact_friction[5 * o + k] = con_fric[5 * ci + k];
+    d.contact_includemargin[o] = con_imargin[ci];
+    d.contact_dim[o] = con_dim[ci];
+    d.contact_geom[2 * o] = con_geom[2 * ci];
+    d.contact_geom[2 * o + 1] = con_geom[2 * ci + 1];
+    d.contact_efc_address[o] = con_efcadr[ci];
+  }
+  for (int r = tid; r < nefc; r += NT) {
+    const long long o = W * m.njmax + r;
+    d.efc_type[o] = efc_type[r];
+    d.efc_id[o] = efc_id[r];
+    d.efc_pos[o] = efc_pos[r];
+    d.efc_D[o] = efc_D[r];
+    d.efc_aref[o] = efc_aref[r];
+    d.efc_force[o] = efc_force[r];
+  }
+  if (tid == 0) {
+    d.ncon[W] = ncon;
+    d.nefc[W] = nefc;
+    d.solver_niter[W] = niter;
+  }
+
+  // ---------------------------------------------------------------- integration
+  if constexpr (STEP) {
+    const float dt = m.timestep;
+    float* qa_int = tmp;
+    if (m.integrator == MJH_INT_IMPLICITFAST) {
+      for (int i = tid; i < nv * ldm; i += NT) Lm[i] = Mm[i];
+      __syncthreads();
+      for (int i = tid; i < nv; i += NT) Lm[i * ldm + i] += dt * dof_damping[i];
+      __syncthreads();
+      for (int i = tid; i < nu; i += NT) {
+        if (m.actuator_forcelimited[i]) {
+          const float f = act_force[i];
+          if (f <= m.actuator_forcerange[2 * i] || f >= m.actuator_forcerange[2 * i + 1]) continue;
+        }
+        const int dof = m.jnt_dofadr[m.actuator_trnid[i]];
+        const float g = m.actuator_gear[i];
+        atomicAdd(&Lm[dof * ldm + dof], -dt * g * g * m.actuator_biasprm[10 * i + 2]);
+      }
+      for (int i = tid; i < nv; i += NT) qa_int[i] = qfrc_smooth[i] + qfrc_con[i];
+      ldl_factor<NT>(Lm, nv, ldm);
+      ldl_solve<NT>(Lm, nv, ldm, qa_int);
+    } else {
+      float anyd = 0.f;
+      for (int i = tid; i < nv; i += NT) anyd += dof_damping[i] > 0.f ? 1.f : 0.f;
+      anyd = bsum<NT>(anyd, red);
+      if (anyd > 0.f) {
+        for (int i = tid; i < nv * ldm; i += NT) Lm[i] = Mm[i];
+        __syncthreads();
+        for (int i = tid; i < nv; i += NT) Lm[i * ldm + i] += dt * dof_damping[i];
+        symv<NT>(Mm, nv, ldm, qacc, qa_int);
+        ldl_factor<NT>(Lm, nv, ldm);
+        ldl_solve<NT>(Lm, nv, ldm, qa_int);
+      } else {
+        for (int i = tid; i < nv; i += NT) qa_int[i] = qacc[i];
+        __syncthreads();
+      }
+    }
+    for (int i = tid; i < nv; i += NT) qvel[i] += dt * qa_int[i];
+    __syncthreads();
+    for (int j = tid; j < nj; j += NT) {
+      const int q0 = m.jnt_qposadr[j], v0 = m.jnt_dofadr[j];
+      if (m.jnt_type[j] == 0) {
+        qpos[q0] += dt * qvel[v0];
+        qpos[q0 + 1] += dt * qvel[v0 + 1];
+        qpos[q0 + 2] += dt * qvel[v0 + 2];
+        float q[4] = {qpos[q0 + 3], qpos[q0 + 4], qpos[q0 + 5], qpos[q0 + 6]};
+        float om[3] = {qvel[v0 + 3], qvel[v0 + 4], qvel[v0 + 5]};
+        const float ang = dt * normalize3(om);
+        float qr[4];
+        axis_angle(qr, om, ang);
+        quat_normalize(q);
+        quat_mul(q, q, qr);
+        quat_normalize(q);
+        qpos[q0 + 3] = q[0]; qpos[q0 + 4] = q[1]; qpos[q0 + 5] = q[2]; qpos[q0 + 6] = q[3];
+      } else {
+        qpos[q0] += dt * qvel[v0];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < nq; i += NT) d.qpos[W * nq + i] = qpos[i];
+    for (int i = tid; i < nv; i += NT) d.qvel[W * nv + i] = qvel[i];
+    if (tid == 0) d.time[W] += dt;
+  }
+
+  // non-finite check on the new state
+  {
+    float bad = 0.f;
+    for (int i = tid; i < nq; i += NT) bad += isfinite(qpos[i]) ? 0.f : 1.f;
+    for (int i = tid; i < nv; i += NT) bad += (isfinite(qvel[i]) && isfinite(qacc[i])) ? 0.f : 1.f;
+    bad = bsum<NT>(bad, red);
+    if (tid == 0) d.flags[W] = ints[I_FLAGS] | (bad > 0.f ? MJH_FLAG_NONFINITE : 0);
+  }
+}
+
+__global__ void repeat_kernel(float* dst, const float* src, long long nelem, long long total) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+    dst[i] = src[i % nelem];
+}
+
+// ---- host side ---------------------------------------------------------------
+Layout make_layout(const mjh_model* m, int nt) {
+  Layout L;
+  std::memset(&L, 0, sizeof(L));
+  int off = 0;
+  auto take = [&](int n) {
+    int o = off;
+    off += (n + 1) & ~1;  // keep 8-byte alignment for the int64 masks
+    return o;
+  };
+  const int nv = m->nv, nb = m->nbody, nj = m->njnt;
+  L.ldm = nv | 1;
+  L.ldj = nv | 1;
+  L.qpos = take(m->nq);
+  L.qvel = take(nv); L.qacc = take(nv); L.qacc_smooth = take(nv); L.qfrc_smooth = take(nv);
+  L.qfrc_bias = take(nv); L.qfrc_con = take(nv); L.qfrc_passive = take(nv); L.qfrc_act = take(nv);
+  L.grad = take(nv); L.search = take(nv); L.Ma = take(nv); L.Mv = take(nv); L.tmp = take(nv); L.tmp2 = take(nv);
+  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
+  L.ximat = take(9 * nb); L.subtree_com = take(3 * nb); L.cinert = take(10 * nb); L.crb = take(10 * nb);
+  L.cvel = take(6 * nb); L.cacc = take(6 * nb); L.cfrc = take(6 * nb);
+  L.xanchor = take(3 * nj); L.xaxis = take(3 * nj); L.cdof = take(6 * nv); L.cdof_dot = take(6 * nv);
+  L.cgpos = take(3 * m->ncolgeom); L.cgmat = take(9 * m->ncolgeom);
+  L.sxpos = take(3 * m->nsite); L.sxmat = take(9 * m->nsite);
+  L.M = take(nv * L.ldm); L.L = take(nv * L.ldm);
+  L.act_force = take(m->nu);
+  const int C = m->nconmax;
+  L.ncap = C;
+  L.con_pos = take(3 * C); L.con_frame = take(9 * C); L.con_dist = take(C); L.con_fric = take(5 * C);
+  L.con_solref = take(2 * C); L.con_solimp = take(5 * C); L.con_imargin = take(C); L.con_dim = take(C);
+  L.con_geom = take(2 * C); L.con_efcadr = take(C);
+  L.red = take(4 * (nt / 64) + 8);
+  L.ints = take(8);
+  // constraint rows: as many as fit in the LDS budget, up to njmax
+  const int fixed = off;
+  const int per_row = L.ldj + 10 + 2;  // J row + 10 scalars + 64-bit mask
+  const int budget_words = (160 * 1024 / 4) / 2;  // two worlds per CU
+  int rcap = (budget_words - fixed - 8) / per_row;
+  if (rcap > m->njmax) rcap = m->njmax;
+  if (rcap < 1) rcap = 1;
+  L.rcap = rcap;
+  L.J = take(rcap * L.ldj);
+  L.efc_D = take(rcap); L.efc_R = take(rcap); L.efc_aref = take(rcap); L.efc_jaref = take(rcap);
+  L.efc_jv = take(rcap); L.efc_force = take(rcap); L.efc_fl = take(rcap); L.efc_pos = take(rcap);
+  L.efc_type = take(rcap); L.efc_id = take(rcap);
+  L.efc_mask = take(2 * rcap);
+  L.total = off;
+  return L;
+}
+
+constexpr int kThreads = 64;
+
+template <bool STEP>
+int launch(const mjh_model* m, const mjh_data* d, void* stream) {
+  if (mjh_model_check(m) != 0) return 1;
+  if (d->nworld <= 0) return 0;
+  Layout L = make_layout(m, kThreads);
+  size_t shmem = (size_t)L.total * 4;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  static bool attr_set[2] = {false, false};
+  auto kern = step_kernel<kThreads, STEP>;
+  if (!attr_set[STEP]) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set[STEP] = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(d->nworld), dim3(kThreads), shmem, s, *m, *d, L);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string("step launch failed: ") + hipGetErrorString(e);
+    return 2;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mjh_abi_version(void) { return MJH_ABI_VERSION; }
+
+const char* mjh_last_error(void) { return g_err.c_str(); }
+
+size_t mjh_sizeof_model(void) { return sizeof(mjh_model); }
+size_t mjh_sizeof_data(void) { return sizeof(mjh_data); }
+
+int mjh_model_check(const mjh_model* m) {
+  if (!m) { g_err = "null model"; return 1; }
+  if (m->nv > 63 || m->nbody > 63) { g_err = "device path supports nv <= 63 and nbody <= 63"; return 1; }
+  if (m->nconmax <= 0 || m->njmax <= 0) { g_err = "nconmax and njmax must be positive"; return 1; }
+  Layout L = make_layout(m, kThreads);
+  if ((size_t)L.total * 4 > 160 * 1024) { g_err = "per-world scratch exceeds LDS"; return 1; }
+  if (L.rcap < 8) { g_err = "too little LDS left for constraint rows"; return 1; }
+  for (int p = 0; p < m->npair; p++) {
+    (void)p;  // pair type support is validated by the compiler (host arrays)
+  }
+  g_err.clear();
+  return 0;
+}
+
+int mjh_scratch_bytes(const mjh_model* m) { return make_layout(m, kThreads).total * 4; }
+
+int mjh_efc_capacity(const mjh_model* m) { return make_layout(m, kThreads).rcap; }
+
+int mjh_step(const mjh_model* m, const mjh_data* d, void* stream) { return launch<true>(m, d, stream); }
+
+int mjh_forward(const mjh_model* m, const mjh_data* d, void* stream) { return launch<false>(m, d, stream); }
+
+int mjh_repeat(float* dst, const float* src, long long nelem, int nworld, void* stream) {
+  if (nelem <= 0 || nworld <= 0) return 0;
+  long long total = nelem * (long long)nworld;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(repeat_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dst, src, nelem, total);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { g_err = hipGetErrorString(e); return 2; }
+  return 0;
+}
+
+}  // extern "C"

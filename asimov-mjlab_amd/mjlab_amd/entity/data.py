@@ -1,0 +1,298 @@
+"""EntityData: state writes and derived reads on the batched sim data.
+
+Restates ``src/mjlab/entity/data.py``. Writes index ``sim.data.<field>`` torch
+views in place (``data.py:75-198``); reads derive poses and velocities from the
+kinematics outputs of the last forward pass (``data.py:212-528``), including
+``compute_velocity_from_cvel`` (``data.py:20-31``) and the convention that body,
+geom and site velocities use the *root* subtree com (``data.py:264,282,306,325``).
+
+Writes of a subset of envs use a boolean mask + ``torch.where`` when ``env_ids``
+is a bool tensor, so the env loop stays capturable (no ``nonzero`` syncs).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Any
+
+import torch
+
+from mjlab_amd.utils.math import quat_apply, quat_apply_inverse, quat_from_matrix, quat_mul
+
+
+def compute_velocity_from_cvel(pos: torch.Tensor, subtree_com: torch.Tensor, cvel: torch.Tensor) -> torch.Tensor:
+  lin_vel_c = cvel[..., 3:6]
+  ang_vel_c = cvel[..., 0:3]
+  offset = subtree_com - pos
+  lin_vel_w = lin_vel_c - torch.cross(ang_vel_c, offset, dim=-1)
+  return torch.cat([lin_vel_w, ang_vel_c], dim=-1)
+
+
+def _masked_write(dst: torch.Tensor, cols: torch.Tensor | slice, value: torch.Tensor, env_ids) -> None:
+  """dst[env_ids, cols] = value, for env_ids None/slice/index tensor/bool mask."""
+  if env_ids is None or isinstance(env_ids, slice):
+    rows = env_ids if env_ids is not None else slice(None)
+    if isinstance(cols, slice):
+      dst[rows, cols] = value
+    else:
+      dst[rows, cols.long()] = value
+    return
+  if env_ids.dtype == torch.bool:
+    cols_l = torch.arange(dst.shape[1], device=dst.device)[cols] if isinstance(cols, slice) else cols.long()
+    cur = dst[:, cols_l]
+    value = value.expand_as(cur) if value.dim() <= cur.dim() else value
+    dst[:, cols_l] = torch.where(env_ids.view(-1, *([1] * (cur.dim() - 1))), value, cur)
+    return
+  idx = env_ids.long()[:, None]
+  cols_l = torch.arange(dst.shape[1], device=dst.device)[cols] if isinstance(cols, slice) else cols.long()
+  dst[idx, cols_l] = value
+
+
+@dataclass
+class EntityData:
+  indexing: Any
+  data: Any
+  model: Any
+  device: str
+  default_root_state: torch.Tensor
+  default_joint_pos: torch.Tensor
+  default_joint_vel: torch.Tensor
+  default_joint_stiffness: torch.Tensor
+  default_joint_damping: torch.Tensor
+  default_joint_pos_limits: torch.Tensor
+  joint_pos_limits: torch.Tensor
+  soft_joint_pos_limits: torch.Tensor
+  gravity_vec_w: torch.Tensor
+  forward_vec_b: torch.Tensor
+  is_fixed_base: bool
+  is_articulated: bool
+  is_actuated: bool
+
+  ROOT_POSE_DIM = 7
+  ROOT_VEL_DIM = 6
+  ROOT_STATE_DIM = 13
+
+  # ---- writes ----
+  def write_root_state(self, root_state: torch.Tensor, env_ids=None) -> None:
+    if self.is_fixed_base:
+      raise ValueError("Cannot write root state for fixed-base entity.")
+    assert root_state.shape[-1] == self.ROOT_STATE_DIM
+    self.write_root_pose(root_state[:, :7], env_ids)
+    self.write_root_velocity(root_state[:, 7:], env_ids)
+
+  def write_root_pose(self, pose: torch.Tensor, env_ids=None) -> None:
+    if self.is_fixed_base:
+      raise ValueError("Cannot write root pose for fixed-base entity.")
+    assert pose.shape[-1] == self.ROOT_POSE_DIM
+    _masked_write(self.data.qpos, self.indexing.free_joint_q_adr, pose, env_ids)
+
+  def write_root_velocity(self, velocity: torch.Tensor, env_ids=None) -> None:
+    if self.is_fixed_base:
+      raise ValueError("Cannot write root velocity for fixed-base entity.")
+    assert velocity.shape[-1] == self.ROOT_VEL_DIM
+    qadr = self.indexing.free_joint_q_adr[3:7].long()
+    if env_ids is None or isinstance(env_ids, slice) or env_ids.dtype == torch.bool:
+      quat_w = self.data.qpos[:, qadr] if not isinstance(env_ids, slice) else self.data.qpos[env_ids][:, qadr]
+    else:
+      quat_w = self.data.qpos[env_ids.long()][:, qadr]
+    if velocity.shape[0] != quat_w.shape[0]:
+      velocity = velocity.expand(quat_w.shape[0], -1)
+    ang_b = quat_apply_inverse(quat_w, velocity[:, 3:])
+    qv = torch.cat([velocity[:, :3], ang_b], dim=-1)
+    _masked_write(self.data.qvel, self.indexing.free_joint_v_adr, qv, env_ids)
+
+  def write_joint_state(self, position, velocity, joint_ids=None, env_ids=None) -> None:
+    if not self.is_articulated:
+      raise ValueError("Cannot write joint state for non-articulated entity.")
+    self.write_joint_position(position, joint_ids, env_ids)
+    self.write_joint_velocity(velocity, joint_ids, env_ids)
+
+  def write_joint_position(self, position, joint_ids=None, env_ids=None) -> None:
+    if not self.is_articulated:
+      raise ValueError("Cannot write joint position for non-articulated entity.")
+    cols = self.indexing.joint_q_adr[joint_ids if joint_ids is not None else slice(None)]
+    _masked_write(self.data.qpos, cols, position, env_ids)
+
+  def write_joint_velocity(self, velocity, joint_ids=None, env_ids=None) -> None:
+    if not self.is_articulated:
+      raise ValueError("Cannot write joint velocity for non-articulated entity.")
+    cols = self.indexing.joint_v_adr[joint_ids if joint_ids is not None else slice(None)]
+    _masked_write(self.data.qvel, cols, velocity, env_ids)
+
+  def write_external_wrench(self, force, torque, body_ids=None, env_ids=None) -> None:
+    gb = self.indexing.body_ids[body_ids if body_ids is not None else slice(None)].long()
+    xf = self.data.xfrc_applied
+    if force is not None:
+      cols = (gb[:, None] * 6 + torch.arange(3, device=gb.device)).reshape(-1)
+      _masked_write(xf.view(xf.shape[0], -1), cols, force.reshape(force.shape[0], -1), env_ids)
+    if torque is not None:
+      cols = (gb[:, None] * 6 + 3 + torch.arange(3, device=gb.device)).reshape(-1)
+      _masked_write(xf.view(xf.shape[0], -1), cols, torque.reshape(torque.shape[0], -1), env_ids)
+
+  def write_ctrl(self, ctrl: torch.Tensor, ctrl_ids=None, env_ids=None) -> None:
+    if not self.is_actuated:
+      raise ValueError("Cannot write control for non-actuated entity.")
+    cols = self.indexing.ctrl_ids[ctrl_ids if ctrl_ids is not None else slice(None)]
+    _masked_write(self.data.ctrl, cols, ctrl, env_ids)
+
+  def clear_state(self, env_ids=None) -> None:
+    n = self.data.qpos.shape[0]
+    v = self.indexing.free_joint_v_adr
+    if v.numel():
+      _masked_write(self.data.qfrc_applied, v, torch.zeros(n if env_ids is None or isinstance(env_ids, slice) or env_ids.dtype == torch.bool else env_ids.numel(), v.numel(), device=self.data.qpos.device), env_ids)
+    gb = self.indexing.body_ids.long()
+    xf = self.data.xfrc_applied.view(n, -1)
+    cols = (gb[:, None] * 6 + torch.arange(6, device=gb.device)).reshape(-1)
+    rows = n if env_ids is None or isinstance(env_ids, slice) or env_ids.dtype == torch.bool else env_ids.numel()
+    _masked_write(xf, cols, torch.zeros(rows, cols.numel(), device=xf.device), env_ids)
+    if self.is_actuated:
+      c = self.indexing.ctrl_ids
+      _masked_write(self.data.ctrl, c, torch.zeros(rows, c.numel(), device=xf.device), env_ids)
+
+  # ---- reads ----
+  @property
+  def _root(self) -> int:
+    return self.indexing.root_body_id
+
+  @property
+  def root_link_pose_w(self) -> torch.Tensor:
+    return torch.cat([self.data.xpos[:, self._root], self.data.xquat[:, self._root]], dim=-1)
+
+  @property
+  def root_link_vel_w(self) -> torch.Tensor:
+    r = self._root
+    return compute_velocity_from_cvel(self.data.xpos[:, r], self.data.subtree_com[:, r], self.data.cvel[:, r])
+
+  @property
+  def root_com_pose_w(self) -> torch.Tensor:
+    r = self._root
+    q = quat_mul(self.data.xquat[:, r], self.model.body_iquat[:, r].expand(self.data.xquat.shape[0], -1))
+    return torch.cat([self.data.xipos[:, r], q], dim=-1)
+
+  @property
+  def root_com_vel_w(self) -> torch.Tensor:
+    r = self._root
+    return compute_velocity_from_cvel(self.data.xipos[:, r], self.data.subtree_com[:, r], self.data.cvel[:, r])
+
+  @property
+  def body_link_pose_w(self) -> torch.Tensor:
+    ids = self.indexing.body_ids.long()
+    return torch.cat([self.data.xpos[:, ids], self.data.xquat[:, ids]], dim=-1)
+
+  @property
+  def body_link_vel_w(self) -> torch.Tensor:
+    ids = self.indexing.body_ids.long()
+    com = self.data.subtree_com[:, self._root].unsqueeze(1)
+    return compute_velocity_from_cvel(self.data.xpos[:, ids], com, self.data.cvel[:, ids])
+
+  @property
+  def body_com_pose_w(self) -> torch.Tensor:
+    ids = self.indexing.body_ids.long()
+    iq = self.model.body_iquat[:, ids].expand(self.data.xquat.shape[0], -1, -1)
+    return torch.cat([self.data.xipos[:, ids], quat_mul(self.data.xquat[:, ids], iq)], dim=-1)
+
+  @property
+  def body_com_vel_w(self) -> torch.Tensor:
+    ids = self.indexing.body_ids.long()
+    com = self.data.subtree_com[:, self._root].unsqueeze(1)
+    return compute_velocity_from_cvel(self.data.xipos[:, ids], com, self.data.cvel[:, ids])
+
+  @property
+  def body_external_wrench(self) -> torch.Tensor:
+    return self.data.xfrc_applied[:, self.indexing.body_ids.long()]
+
+  @property
+  def geom_pose_w(self) -> torch.Tensor:
+    ids = self.indexing.geom_ids.long()
+    return torch.cat([self.data.geom_xpos[:, ids], quat_from_matrix(self.data.geom_xmat[:, ids])], dim=-1)
+
+  @property
+  def geom_vel_w(self) -> torch.Tensor:
+    ids = self.indexing.geom_ids.long()
+    bids = self.model.geom_bodyid[ids].long()
+    com = self.data.subtree_com[:, self._root].unsqueeze(1)
+    return compute_velocity_from_cvel(self.data.geom_xpos[:, ids], com, self.data.cvel[:, bids])
+
+  @property
+  def site_pose_w(self) -> torch.Tensor:
+    ids = self.indexing.site_ids.long()
+    return torch.cat([self.data.site_xpos[:, ids], quat_from_matrix(self.data.site_xmat[:, ids])], dim=-1)
+
+  @property
+  def site_vel_w(self) -> torch.Tensor:
+    ids = self.indexing.site_ids.long()
+    bids = self.model.site_bodyid[ids].long()
+    com = self.data.subtree_com[:, self._root].unsqueeze(1)
+    return compute_velocity_from_cvel(self.data.site_xpos[:, ids], com, self.data.cvel[:, bids])
+
+  @property
+  def joint_pos(self) -> torch.Tensor:
+    return self.data.qpos[:, self.indexing.joint_q_adr.long()]
+
+  @property
+  def joint_vel(self) -> torch.Tensor:
+    return self.data.qvel[:, self.indexing.joint_v_adr.long()]
+
+  @property
+  def joint_acc(self) -> torch.Tensor:
+    return self.data.qacc[:, self.indexing.joint_v_adr.long()]
+
+  @property
+  def actuator_force(self) -> torch.Tensor:
+    return self.data.actuator_force[:, self.indexing.ctrl_ids.long()]
+
+  @property
+  def generalized_force(self) -> torch.Tensor:
+    return self.data.qfrc_applied[:, self.indexing.free_joint_v_adr.long()]
+
+  root_link_pos_w = property(lambda s: s.root_link_pose_w[:, 0:3])
+  root_link_quat_w = property(lambda s: s.root_link_pose_w[:, 3:7])
+  root_link_lin_vel_w = property(lambda s: s.root_link_vel_w[:, 0:3])
+  root_link_ang_vel_w = property(lambda s: s.root_link_vel_w[:, 3:6])
+  root_com_pos_w = property(lambda s: s.root_com_pose_w[:, 0:3])
+  root_com_quat_w = property(lambda s: s.root_com_pose_w[:, 3:7])
+  root_com_lin_vel_w = property(lambda s: s.root_com_vel_w[:, 0:3])
+  root_com_ang_vel_w = property(lambda s: s.root_com_vel_w[:, 3:6])
+  body_link_pos_w = property(lambda s: s.body_link_pose_w[..., 0:3])
+  body_link_quat_w = property(lambda s: s.body_link_pose_w[..., 3:7])
+  body_link_lin_vel_w = property(lambda s: s.body_link_vel_w[..., 0:3])
+  body_link_ang_vel_w = property(lambda s: s.body_link_vel_w[..., 3:6])
+  body_com_pos_w = property(lambda s: s.body_com_pose_w[..., 0:3])
+  body_com_quat_w = property(lambda s: s.body_com_pose_w[..., 3:7])
+  body_com_lin_vel_w = property(lambda s: s.body_com_vel_w[..., 0:3])
+  body_com_ang_vel_w = property(lambda s: s.body_com_vel_w[..., 3:6])
+  body_external_force = property(lambda s: s.body_external_wrench[..., 0:3])
+  body_external_torque = property(lambda s: s.body_external_wrench[..., 3:6])
+  geom_pos_w = property(lambda s: s.geom_pose_w[..., 0:3])
+  geom_quat_w = property(lambda s: s.geom_pose_w[..., 3:7])
+  geom_lin_vel_w = property(lambda s: s.geom_vel_w[..., 0:3])
+  geom_ang_vel_w = property(lambda s: s.geom_vel_w[..., 3:6])
+  site_pos_w = property(lambda s: s.site_pose_w[..., 0:3])
+  site_quat_w = property(lambda s: s.site_pose_w[..., 3:7])
+  site_lin_vel_w = property(lambda s: s.site_vel_w[..., 0:3])
+  site_ang_vel_w = property(lambda s: s.site_vel_w[..., 3:6])
+
+  @property
+  def projected_gravity_b(self) -> torch.Tensor:
+    return quat_apply_inverse(self.root_link_quat_w, self.gravity_vec_w)
+
+  @property
+  def heading_w(self) -> torch.Tensor:
+    f = quat_apply(self.root_link_quat_w, self.forward_vec_b)
+    return torch.atan2(f[:, 1], f[:, 0])
+
+  @property
+  def root_link_lin_vel_b(self) -> torch.Tensor:
+    return quat_apply_inverse(self.root_link_quat_w, self.root_link_lin_vel_w)
+
+  @property
+  def root_link_ang_vel_b(self) -> torch.Tensor:
+    return quat_apply_inverse(self.root_link_quat_w, self.root_link_ang_vel_w)
+
+  @property
+  def root_com_lin_vel_b(self) -> torch.Tensor:
+    return quat_apply_inverse(self.root_link_quat_w, self.root_com_lin_vel_w)
+
+  @property
+  def root_com_ang_vel_b(self) -> torch.Tensor:
+    return quat_apply_inverse(self.root_link_quat_w, self.root_com_ang_vel_w)

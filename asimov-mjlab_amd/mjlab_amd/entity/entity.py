@@ -1,0 +1,323 @@
+"""Entity: one robot/prop in the scene, and its indexing into the batched data.
+
+Restates ``src/mjlab/entity/entity.py`` on top of mjlab_amd's own spec and
+compiled model: spec editors and the ``init_state`` keyframe
+(``entity.py:116-166``), global indexing (``_compute_indexing``,
+``entity.py:601-660``), default states / PD gains / soft joint limits
+(``initialize``, ``entity.py:321-420``), and the write API (``:428-599``).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Sequence
+
+import numpy as np
+import torch
+
+from mjlab_amd.entity.data import EntityData
+from mjlab_amd.spec.spec import KeySpec, Spec
+from mjlab_amd.utils import spec_config as spec_cfg
+from mjlab_amd.utils.string import resolve_expr, resolve_matching_names
+
+
+@dataclass(frozen=True)
+class EntityIndexing:
+  body_names: tuple[str, ...]
+  body_ids: torch.Tensor
+  geom_ids: torch.Tensor
+  site_ids: torch.Tensor
+  ctrl_ids: torch.Tensor
+  joint_ids: torch.Tensor
+  mocap_id: int | None
+  joint_q_adr: torch.Tensor
+  joint_v_adr: torch.Tensor
+  free_joint_q_adr: torch.Tensor
+  free_joint_v_adr: torch.Tensor
+  root_body_id: int
+
+
+@dataclass
+class EntityArticulationInfoCfg:
+  actuators: tuple[spec_cfg.ActuatorCfg, ...] = field(default_factory=tuple)
+  soft_joint_pos_limit_factor: float = 1.0
+
+
+@dataclass
+class EntityCfg:
+  @dataclass
+  class InitialStateCfg:
+    pos: tuple[float, float, float] = (0.0, 0.0, 0.0)
+    rot: tuple[float, float, float, float] = (1.0, 0.0, 0.0, 0.0)
+    lin_vel: tuple[float, float, float] = (0.0, 0.0, 0.0)
+    ang_vel: tuple[float, float, float] = (0.0, 0.0, 0.0)
+    joint_pos: dict[str, float] = field(default_factory=lambda: {".*": 0.0})
+    joint_vel: dict[str, float] = field(default_factory=lambda: {".*": 0.0})
+
+  init_state: InitialStateCfg = field(default_factory=InitialStateCfg)
+  spec_fn: Callable[[], Spec] = field(default_factory=lambda: (lambda: Spec()))
+  articulation: EntityArticulationInfoCfg | None = None
+  collisions: tuple[spec_cfg.CollisionCfg, ...] = field(default_factory=tuple)
+  debug_vis: bool = False
+
+
+class Entity:
+  def __init__(self, cfg: EntityCfg) -> None:
+    self.cfg = cfg
+    self._spec = cfg.spec_fn()
+    joints = self._spec.joints
+    self._free_joint = joints[0] if joints and joints[0].type == "free" else None
+    self._non_free_joints = tuple(j for j in joints if j.type != "free")
+    for c in cfg.collisions:
+      c.edit_spec(self._spec)
+    if cfg.articulation:
+      spec_cfg.ActuatorSetCfg(cfg.articulation.actuators).edit_spec(self._spec)
+    self._add_initial_state_keyframe()
+    self.prefix = ""
+
+  def _add_initial_state_keyframe(self) -> None:
+    comps: list[np.ndarray] = []
+    if self._free_joint is not None:
+      comps += [np.array(self.cfg.init_state.pos), np.array(self.cfg.init_state.rot)]
+    jp = None
+    if self._non_free_joints:
+      jp = resolve_expr(self.cfg.init_state.joint_pos, self.joint_names)
+      comps.append(np.array(jp))
+    key = KeySpec(name="init_state", qpos=list(np.hstack(comps)) if comps else [])
+    if self.is_actuated and jp is not None:
+      n2p = dict(zip(self.joint_names, jp))
+      key.ctrl = [n2p.get(a.name, 0.0) for a in self._spec.actuators]
+    self._spec.keys = [key]
+    if self.is_fixed_base:
+      root = self.root_body
+      root.pos = list(self.cfg.init_state.pos)
+      root.quat = list(self.cfg.init_state.rot)
+
+  # --- attributes ---
+  @property
+  def spec(self) -> Spec:
+    return self._spec
+
+  @property
+  def data(self) -> EntityData:
+    return self._data
+
+  @property
+  def is_fixed_base(self) -> bool:
+    return self._free_joint is None
+
+  @property
+  def is_articulated(self) -> bool:
+    return len(self._non_free_joints) > 0
+
+  @property
+  def is_actuated(self) -> bool:
+    return self.num_actuators > 0
+
+  @property
+  def is_mocap(self) -> bool:
+    return bool(self.root_body.mocap) if self.is_fixed_base else False
+
+  @property
+  def root_body(self):
+    return self._spec.bodies[1]
+
+  @property
+  def joint_names(self) -> tuple[str, ...]:
+    return tuple(j.name.split("/")[-1] for j in self._non_free_joints)
+
+  @property
+  def body_names(self) -> tuple[str, ...]:
+    return tuple(b.name.split("/")[-1] for b in self._spec.bodies[1:])
+
+  @property
+  def geom_names(self) -> tuple[str, ...]:
+    return tuple(g.name.split("/")[-1] for g in self._spec.geoms)
+
+  @property
+  def site_names(self) -> tuple[str, ...]:
+    return tuple(s.name.split("/")[-1] for s in self._spec.sites)
+
+  @property
+  def actuator_names(self) -> tuple[str, ...]:
+    return tuple(a.name.split("/")[-1] for a in self._spec.actuators)
+
+  @property
+  def num_joints(self) -> int:
+    return len(self.joint_names)
+
+  @property
+  def num_bodies(self) -> int:
+    return len(self.body_names)
+
+  @property
+  def num_geoms(self) -> int:
+    return len(self.geom_names)
+
+  @property
+  def num_sites(self) -> int:
+    return len(self.site_names)
+
+  @property
+  def num_actuators(self) -> int:
+    return len(self._spec.actuators)
+
+  def find_bodies(self, name_keys, preserve_order: bool = False):
+    return resolve_matching_names(name_keys, self.body_names, preserve_order)
+
+  def find_joints(self, name_keys, joint_subset=None, preserve_order: bool = False):
+    return resolve_matching_names(
+      name_keys, joint_subset if joint_subset is not None else self.joint_names, preserve_order
+    )
+
+  def find_actuators(self, name_keys, actuator_subset=None, preserve_order: bool = False):
+    return resolve_matching_names(
+      name_keys,
+      actuator_subset if actuator_subset is not None else self.actuator_names,
+      preserve_order,
+    )
+
+  def find_geoms(self, name_keys, geom_subset=None, preserve_order: bool = False):
+    return resolve_matching_names(
+      name_keys, geom_subset if geom_subset is not None else self.geom_names, preserve_order
+    )
+
+  def find_sites(self, name_keys, site_subset=None, preserve_order: bool = False):
+    return resolve_matching_names(
+      name_keys, site_subset if site_subset is not None else self.site_names, preserve_order
+    )
+
+  # --- init ---
+  def initialize(self, model, sim_model, data, device: str) -> None:
+    """``model`` is the compiled host model, ``sim_model``/``data`` the bridges."""
+    self.indexing = self._compute_indexing(model, device)
+    nworld = data.nworld
+    init = self.cfg.init_state
+    root = list(init.pos) + list(init.rot)
+    if not self.is_fixed_base:
+      root += list(init.lin_vel) + list(init.ang_vel)
+    default_root_state = torch.tensor(root, dtype=torch.float, device=device).repeat(nworld, 1)
+    if self.is_articulated:
+      djp = torch.tensor(resolve_expr(init.joint_pos, self.joint_names), device=device)[None].repeat(nworld, 1).float()
+      djv = torch.tensor(resolve_expr(init.joint_vel, self.joint_names), device=device)[None].repeat(nworld, 1).float()
+      if self.is_actuated:
+        kp = sim_model.actuator_gainprm[:, self.indexing.ctrl_ids, 0]
+        kd = -sim_model.actuator_biasprm[:, self.indexing.ctrl_ids, 2]
+        if kp.shape[0] != nworld:
+          kp = kp.expand(nworld, -1)
+          kd = kd.expand(nworld, -1)
+        kp, kd = kp.clone(), kd.clone()
+      else:
+        kp = torch.empty(nworld, 0, device=device)
+        kd = torch.empty(nworld, 0, device=device)
+      lim = sim_model.jnt_range[:, self.indexing.joint_ids]
+      if lim.shape[0] != nworld:
+        lim = lim.expand(nworld, -1, -1)
+      default_lim = lim.clone()
+      mean = (default_lim[..., 0] + default_lim[..., 1]) / 2
+      rng = default_lim[..., 1] - default_lim[..., 0]
+      f = self.cfg.articulation.soft_joint_pos_limit_factor if self.cfg.articulation else 1.0
+      soft = torch.stack([mean - 0.5 * rng * f, mean + 0.5 * rng * f], dim=-1)
+    else:
+      djp = torch.empty(nworld, 0, device=device)
+      djv = torch.empty(nworld, 0, device=device)
+      kp = torch.empty(nworld, 0, device=device)
+      kd = torch.empty(nworld, 0, device=device)
+      default_lim = torch.empty(nworld, 0, 2, device=device)
+      soft = torch.empty(nworld, 0, 2, device=device)
+    self._data = EntityData(
+      indexing=self.indexing,
+      data=data,
+      model=sim_model,
+      device=device,
+      default_root_state=default_root_state,
+      default_joint_pos=djp,
+      default_joint_vel=djv,
+      default_joint_stiffness=kp,
+      default_joint_damping=kd,
+      default_joint_pos_limits=default_lim,
+      joint_pos_limits=default_lim.clone(),
+      soft_joint_pos_limits=soft,
+      gravity_vec_w=torch.tensor([0.0, 0.0, -1.0], device=device).repeat(nworld, 1),
+      forward_vec_b=torch.tensor([1.0, 0.0, 0.0], device=device).repeat(nworld, 1),
+      is_fixed_base=self.is_fixed_base,
+      is_articulated=self.is_articulated,
+      is_actuated=self.is_actuated,
+    )
+
+  def _compute_indexing(self, model, device: str) -> EntityIndexing:
+    p = self.prefix
+    bnames = [p + n for n in self.body_names]
+    body_ids = [model.names["body"].index(n) for n in bnames]
+    geom_ids = [model.names["geom"].index(p + n) for n in self.geom_names]
+    site_ids = [model.names["site"].index(p + n) for n in self.site_names]
+    joint_ids = [model.names["joint"].index(p + n) for n in self.joint_names]
+    ctrl_ids = [model.names["actuator"].index(p + n) for n in self.actuator_names]
+    jq, jv, fq, fv = [], [], [], []
+    all_joints = ([self._free_joint] if self._free_joint is not None else []) + list(self._non_free_joints)
+    for j in all_joints:
+      jid = model.names["joint"].index(j.name if j.name.startswith(p) else p + j.name)
+      t = int(model.jnt_type[jid])
+      va, qa = int(model.jnt_dofadr[jid]), int(model.jnt_qposadr[jid])
+      if t == 0:
+        fv += list(range(va, va + 6))
+        fq += list(range(qa, qa + 7))
+      else:
+        jv.append(va)
+        jq.append(qa)
+
+    def T(x):
+      return torch.tensor(x, dtype=torch.int, device=device)
+
+    return EntityIndexing(
+      body_names=tuple(self.body_names),
+      body_ids=T(body_ids),
+      geom_ids=T(geom_ids),
+      site_ids=T(site_ids),
+      ctrl_ids=T(ctrl_ids),
+      joint_ids=T(joint_ids),
+      mocap_id=None,
+      joint_q_adr=T(jq),
+      joint_v_adr=T(jv),
+      free_joint_q_adr=T(fq),
+      free_joint_v_adr=T(fv),
+      root_body_id=body_ids[0],
+    )
+
+  # --- per-step hooks ---
+  def update(self, dt: float) -> None:
+    del dt
+
+  def reset(self, env_ids=None) -> None:
+    self.clear_state(env_ids)
+
+  def write_data_to_sim(self) -> None:
+    pass
+
+  def clear_state(self, env_ids=None) -> None:
+    self._data.clear_state(env_ids)
+
+  # --- write API (entity.py:431-599) ---
+  def write_root_state_to_sim(self, root_state, env_ids=None) -> None:
+    self._data.write_root_state(root_state, env_ids)
+
+  def write_root_link_pose_to_sim(self, root_pose, env_ids=None) -> None:
+    self._data.write_root_pose(root_pose, env_ids)
+
+  def write_root_link_velocity_to_sim(self, root_velocity, env_ids=None) -> None:
+    self._data.write_root_velocity(root_velocity, env_ids)
+
+  def write_joint_state_to_sim(self, position, velocity, joint_ids=None, env_ids=None) -> None:
+    self._data.write_joint_state(position, velocity, joint_ids, env_ids)
+
+  def write_joint_position_to_sim(self, position, joint_ids=None, env_ids=None) -> None:
+    self._data.write_joint_position(position, joint_ids, env_ids)
+
+  def write_joint_velocity_to_sim(self, velocity, joint_ids=None, env_ids=None) -> None:
+    self._data.write_joint_velocity(velocity, joint_ids, env_ids)
+
+  def write_joint_position_target_to_sim(self, position_target, joint_ids=None, env_ids=None) -> None:
+    self._data.write_ctrl(position_target, joint_ids, env_ids)
+
+  def write_external_wrench_to_sim(self, forces, torques, env_ids=None, body_ids: Sequence[int] | slice | None = None) -> None:
+    self._data.write_external_wrench(forces, torques, body_ids, env_ids)

@@ -1,0 +1,72 @@
+"""Loader for the HIP library ``libmjh.so`` (the C ABI in include/mjh_abi.h).
+
+There is no CPU fallback: if the library is missing or was built for another
+ABI version, every physics call raises. Build it with
+``python -c "import __graft_entry__ as g; g.build()"`` (hipcc, gfx950).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from functools import lru_cache
+from pathlib import Path
+
+from mjlab_amd.sim import abi
+
+PKG = Path(__file__).resolve().parents[1]
+LIB_PATH = PKG / "libmjh.so"
+ABI_VERSION = 1
+
+EXPORTS = (
+  "mjh_abi_version",
+  "mjh_last_error",
+  "mjh_sizeof_model",
+  "mjh_sizeof_data",
+  "mjh_model_check",
+  "mjh_scratch_bytes",
+  "mjh_efc_capacity",
+  "mjh_step",
+  "mjh_forward",
+  "mjh_repeat",
+)
+
+
+class NativeLibraryError(RuntimeError):
+  pass
+
+
+@lru_cache(maxsize=1)
+def lib() -> ctypes.CDLL:
+  if not LIB_PATH.exists():
+    raise NativeLibraryError(
+      f"{LIB_PATH} not found: the HIP step library is required (no CPU fallback). "
+      "Build it with __graft_entry__.build()."
+    )
+  L = ctypes.CDLL(str(LIB_PATH))
+  for name in EXPORTS:
+    if not hasattr(L, name):
+      raise NativeLibraryError(f"{LIB_PATH} does not export {name}")
+  L.mjh_abi_version.restype = ctypes.c_int
+  L.mjh_last_error.restype = ctypes.c_char_p
+  L.mjh_sizeof_model.restype = ctypes.c_size_t
+  L.mjh_sizeof_data.restype = ctypes.c_size_t
+  L.mjh_model_check.argtypes = [ctypes.c_void_p]
+  L.mjh_scratch_bytes.argtypes = [ctypes.c_void_p]
+  L.mjh_efc_capacity.argtypes = [ctypes.c_void_p]
+  for f in (L.mjh_step, L.mjh_forward):
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+  L.mjh_repeat.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p]
+  if L.mjh_abi_version() != ABI_VERSION:
+    raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
+  if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):
+    raise NativeLibraryError("mjh_model layout mismatch between header parse and library")
+  if L.mjh_sizeof_data() != ctypes.sizeof(abi.data_struct()):
+    raise NativeLibraryError("mjh_data layout mismatch between header parse and library")
+  return L
+
+
+def check(rc: int, what: str) -> None:
+  if rc != 0:
+    msg = lib().mjh_last_error().decode()
+    raise RuntimeError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,330 @@
+"""Simulation: the drop-in replacement for mjlab's MuJoCo-Warp boundary.
+
+Same surface as ``src/mjlab/sim/sim.py:97-199``: ``Simulation(num_envs, cfg,
+model, device)`` with ``.mj_model``, ``.model``/``.data`` bridges,
+``expand_model_fields``, ``forward``, ``step``, ``create_graph`` and a
+``nan_guard``. ``MujocoCfg`` / ``SimulationCfg`` mirror ``sim.py:42-94``.
+
+Differences by construction (MI355X-first):
+* torch allocates every buffer; the HIP library only receives raw pointers
+  through the ``mjh_model``/``mjh_data`` descriptors (include/mjh_abi.h);
+* ``step``/``forward`` launch one kernel each on torch's current stream, and
+  are replayed from ``torch.cuda.CUDAGraph`` (hipGraph) captures;
+* there is no CPU physics fallback: on a non-GPU device the bridges work (host
+  logic, indexing, writes) but ``step``/``forward`` raise.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from contextlib import contextmanager
+from dataclasses import dataclass, field
+from typing import Literal
+
+import numpy as np
+import torch
+
+from mjlab_amd.sim import abi, native
+from mjlab_amd.sim.sim_data import BATCHED_STATIC, DATA_SHAPES, MODEL_SHAPES, Bridge, make_opt, shape_of
+from mjlab_amd.spec.compiler import Model
+
+_INTEGRATORS = {"euler": 0, "implicitfast": 3}
+_SOLVERS = {"pgs": 0, "cg": 1, "newton": 2}
+_CONES = {"pyramidal": 0, "elliptic": 1}
+
+
+@dataclass
+class MujocoCfg:
+  timestep: float = 0.002
+  integrator: Literal["euler", "implicitfast"] = "implicitfast"
+  impratio: float = 1.0
+  cone: Literal["pyramidal", "elliptic"] = "pyramidal"
+  jacobian: Literal["auto", "dense", "sparse"] = "auto"
+  solver: Literal["newton", "cg", "pgs"] = "newton"
+  iterations: int = 100
+  tolerance: float = 1e-8
+  ls_iterations: int = 50
+  ls_tolerance: float = 0.01
+  gravity: tuple[float, float, float] = (0, 0, -9.81)
+
+  def apply(self, model: Model) -> None:
+    if self.cone != "pyramidal":
+      raise NotImplementedError("only pyramidal friction cones are implemented")
+    if self.solver != "newton":
+      raise NotImplementedError("only the Newton solver is implemented")
+    model.cone = _CONES[self.cone]
+    model.solver = _SOLVERS[self.solver]
+    model.jacobian = {"dense": 0, "sparse": 1, "auto": 2}[self.jacobian]
+    model.integrator = _INTEGRATORS[self.integrator]
+    model.timestep = self.timestep
+    model.impratio = self.impratio
+    model.gravity = np.array(self.gravity, dtype=np.float64)
+    model.iterations = self.iterations
+    model.tolerance = self.tolerance
+    model.ls_iterations = self.ls_iterations
+    model.ls_tolerance = self.ls_tolerance
+
+
+@dataclass
+class NanGuardCfg:
+  enabled: bool = False
+  buffer_size: int = 100
+  output_dir: str = "/tmp/mjlab/nan_dumps"
+  max_envs_to_dump: int = 5
+
+
+class NanGuard:
+  """Disabled-by-default NaN watcher (``src/mjlab/utils/nan_guard.py:16-104``).
+
+  Enabled, it reads the per-world ``flags`` word the kernel sets on
+  non-finite state after each step (one host sync per step, debug only).
+  """
+
+  def __init__(self, cfg: NanGuardCfg, num_envs: int, model) -> None:
+    self.cfg = cfg
+    self.num_envs = num_envs
+    self.tripped: torch.Tensor | None = None
+
+  @contextmanager
+  def watch(self, data):
+    yield
+    if self.cfg.enabled:
+      bad = (data.flags & 4) != 0
+      if bool(bad.any()):
+        self.tripped = bad.nonzero().flatten()
+
+
+@dataclass(kw_only=True)
+class SimulationCfg:
+  nconmax: int | None = None
+  njmax: int | None = None
+  ls_parallel: bool = True
+  contact_sensor_maxmatch: int = 64
+  mujoco: MujocoCfg = field(default_factory=MujocoCfg)
+  nan_guard: NanGuardCfg = field(default_factory=NanGuardCfg)
+
+
+_TORCH_DT = {"float": torch.float32, "int": torch.int32, "mjh_i64": torch.int64}
+
+
+class Simulation:
+  def __init__(self, num_envs: int, cfg: SimulationCfg, model: Model, device: str) -> None:
+    self.cfg = cfg
+    self.device = device
+    self.num_envs = num_envs
+    self._mj_model = model
+    cfg.mujoco.apply(model)
+    if cfg.nconmax is not None:
+      model.nconmax = int(cfg.nconmax)
+    if cfg.njmax is not None:
+      model.njmax = int(cfg.njmax)
+    model.contact_sensor_maxmatch = cfg.contact_sensor_maxmatch
+    self.sizes = abi.model_sizes(model)
+
+    # ---- model buffers (torch-owned) ----
+    host = abi.model_host_arrays(model)
+    self._model_flat: dict[str, torch.Tensor] = {}
+    self._wstride: dict[str, int] = {}
+    self._fields = {f.name: f for f in abi.model_array_fields()}
+    for f in abi.model_array_fields():
+      self._model_flat[f.name] = torch.as_tensor(host[f.name], dtype=_TORCH_DT[f.ctype], device=device).contiguous()
+      if f.kind == "MW":
+        self._wstride[f.name] = 0
+    model_views = {n: self._model_view(n) for n in self._model_flat}
+    self._model_bridge = Bridge(model_views, extra={"opt": make_opt(model, cfg)}, nworld=num_envs)
+
+    # ---- data buffers ----
+    self._data_flat: dict[str, torch.Tensor] = {}
+    for f in abi.data_array_fields():
+      n = max(1, abi.count(f, self.sizes))
+      self._data_flat[f.name] = torch.zeros((num_envs, n), dtype=_TORCH_DT[f.ctype], device=device)
+    self._data_flat["qpos"][:] = torch.as_tensor(model.qpos0, dtype=torch.float32, device=device)
+    data_views = {n: self._data_view(n) for n in self._data_flat}
+    self._data_bridge = Bridge(data_views, nworld=num_envs)
+
+    self._build_structs()
+    self.use_cuda_graph = str(device).startswith("cuda") and torch.cuda.is_available()
+    self.step_graph = None
+    self.forward_graph = None
+    self.nan_guard = NanGuard(cfg.nan_guard, num_envs, model)
+    if self.use_cuda_graph:
+      native.check(native.lib().mjh_model_check(ctypes.addressof(self._mstruct)), "mjh_model_check")
+      self.forward()
+      self.create_graph()
+
+  # ---- descriptors ----
+  def _model_view(self, name: str) -> torch.Tensor:
+    flat = self._model_flat[name]
+    if name in MODEL_SHAPES:
+      shp = shape_of(MODEL_SHAPES[name], self.sizes)
+      if name in self._wstride or name in BATCHED_STATIC:
+        return flat.view(-1, *shp)
+      return flat.view(*shp)
+    return flat
+
+  def _data_view(self, name: str) -> torch.Tensor:
+    flat = self._data_flat[name]
+    shp = shape_of(DATA_SHAPES.get(name, (flat.shape[1],)), self.sizes)
+    if shp == ():
+      return flat.view(-1)
+    if 0 in shp:
+      return flat[:, :0].reshape(flat.shape[0], *shp)
+    return flat.view(flat.shape[0], *shp)
+
+  def _build_structs(self) -> None:
+    MS = abi.model_struct()
+    DS = abi.data_struct()
+    ms = MS()
+    for k, v in self.sizes.items():
+      setattr(ms, k, v)
+    for k, v in abi.model_options(self._mj_model).items():
+      setattr(ms, k, v)
+    for name, t in self._model_flat.items():
+      setattr(ms, name, t.data_ptr())
+      if name in self._wstride:
+        setattr(ms, name + "_wstride", self._wstride[name])
+    ds = DS()
+    ds.nworld = self.num_envs
+    for name, t in self._data_flat.items():
+      setattr(ds, name, t.data_ptr())
+    self._mstruct, self._dstruct = ms, ds
+
+  def set_option(self, **kw) -> None:
+    """Change solver/integrator options after construction (re-captures graphs)."""
+    for k, v in kw.items():
+      setattr(self._mj_model, k, v)
+    self._build_structs()
+    if self.use_cuda_graph:
+      self.create_graph()
+
+  # ---- reference API ----
+  @property
+  def mj_model(self) -> Model:
+    return self._mj_model
+
+  @property
+  def mj_data(self):
+    return None
+
+  @property
+  def wp_model(self) -> Bridge:
+    return self._model_bridge
+
+  @property
+  def wp_data(self) -> Bridge:
+    return self._data_bridge
+
+  @property
+  def data(self) -> Bridge:
+    return self._data_bridge
+
+  @property
+  def model(self) -> Bridge:
+    return self._model_bridge
+
+  def expand_model_fields(self, fields: tuple[str, ...]) -> None:
+    invalid = [f for f in fields if not hasattr(self._mj_model, f)]
+    if invalid:
+      raise ValueError(f"Fields not found in model: {invalid}")
+    not_expandable = [f for f in fields if f not in self._wstride]
+    if not_expandable:
+      raise ValueError(f"Fields cannot be expanded per world: {not_expandable}")
+    for name in fields:
+      if self._wstride[name] != 0:
+        continue
+      src = self._model_flat[name]
+      n = src.numel()
+      dst = torch.empty(self.num_envs * n, dtype=src.dtype, device=src.device)
+      if self.use_cuda_graph:
+        native.check(
+          native.lib().mjh_repeat(
+            ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()), n, self.num_envs,
+            ctypes.c_void_p(torch.cuda.current_stream().cuda_stream),
+          ),
+          "mjh_repeat",
+        )
+      else:
+        dst.copy_(src.repeat(self.num_envs))
+      self._model_flat[name] = dst
+      self._wstride[name] = n
+      self._model_bridge._rebind(name, self._model_view(name))
+    self._build_structs()
+
+  def create_graph(self) -> None:
+    self.step_graph = None
+    self.forward_graph = None
+    if not self.use_cuda_graph:
+      return
+    # warm-up launches outside capture (attribute setup), then capture
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+      self._launch_forward()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+      self._launch_step()
+    self.step_graph = g
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2):
+      self._launch_forward()
+    self.forward_graph = g2
+
+  def _stream(self) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+  def _launch_step(self) -> None:
+    native.check(
+      native.lib().mjh_step(ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), self._stream()), "mjh_step"
+    )
+
+  def _launch_forward(self) -> None:
+    native.check(
+      native.lib().mjh_forward(ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), self._stream()),
+      "mjh_forward",
+    )
+
+  def _require_gpu(self) -> None:
+    if not self.use_cuda_graph:
+      raise native.NativeLibraryError(
+        f"Simulation on device '{self.device}': the physics step runs only on the HIP path (no CPU fallback)"
+      )
+
+  def forward(self) -> None:
+    self._require_gpu()
+    if self.forward_graph is not None:
+      self.forward_graph.replay()
+    else:
+      self._launch_forward()
+
+  def step(self) -> None:
+    self._require_gpu()
+    with self.nan_guard.watch(self.data):
+      if self.step_graph is not None:
+        self.step_graph.replay()
+      else:
+        self._launch_step()
+
+  # ---- utilities ----
+  def efc_capacity(self) -> int:
+    return int(native.lib().mjh_efc_capacity(ctypes.addressof(self._mstruct)))
+
+  def scratch_bytes(self) -> int:
+    return int(native.lib().mjh_scratch_bytes(ctypes.addressof(self._mstruct)))
+
+  def state_dict(self) -> dict[str, torch.Tensor]:
+    """Physics state (qpos, qvel, act, ctrl, qacc_warmstart, time) for checkpoint/resume."""
+    return {k: self._data_flat[k].clone() for k in ("qpos", "qvel", "act", "ctrl", "qacc_warmstart", "time")}
+
+  def load_state_dict(self, state: dict[str, torch.Tensor]) -> None:
+    for k, v in state.items():
+      self._data_flat[k].copy_(v)
+
+
+def detect_nans(data) -> torch.Tensor:
+  """Per-world bool: non-finite qpos/qvel/qacc (``utils/nan_guard.py`` semantics)."""
+  return (
+    ~torch.isfinite(data.qpos).all(dim=-1)
+    | ~torch.isfinite(data.qvel).all(dim=-1)
+    | ~torch.isfinite(data.qacc).all(dim=-1)
+  )

@@ -1,0 +1,335 @@
+"""MJCF (MuJoCo XML) reader producing a :class:`~mjlab_amd.spec.spec.Spec`.
+
+Handles the MJCF subset mjlab's robots and tests use: ``<compiler>``,
+``<option>``, nested ``<default>`` classes with ``childclass`` inheritance,
+``<body>``/``<inertial>``/``<joint>``/``<freejoint>``/``<geom>``/``<site>``,
+``<contact><exclude>``, ``<actuator><position|motor|general>``, ``<sensor>`` and
+``<keyframe>``. Orientation via ``quat``, ``axisangle``, ``euler``, ``xyaxes`` or
+``zaxis`` (MuJoCo XML reference, "Frame orientations").
+
+Unsupported elements that carry physics (tendons, equality constraints, meshes
+used as collision geometry) raise ``NotImplementedError`` instead of being
+silently dropped; purely visual ones (lights, cameras, materials) are skipped.
+"""
+
+from __future__ import annotations
+
+import math
+import xml.etree.ElementTree as ET
+from pathlib import Path
+
+import numpy as np
+
+from mjlab_amd.spec.spec import (
+  ActuatorSpec,
+  BodySpec,
+  GeomSpec,
+  InertialSpec,
+  JointSpec,
+  KeySpec,
+  SensorSpec,
+  SiteSpec,
+  Spec,
+)
+from mjlab_amd.utils import rot
+
+_VISUAL_ONLY = {"light", "camera", "frame_visual"}
+
+
+def _floats(s: str | None, n: int | None = None) -> list[float] | None:
+  if s is None:
+    return None
+  v = [float(x) for x in s.split()]
+  if n is not None and len(v) < n:
+    v = v + [0.0] * (n - len(v))
+  return v
+
+
+def _orientation(attrs: dict[str, str], angle_deg: bool, eulerseq: str) -> list[float] | None:
+  """Resolve the alternative orientation specifiers to a unit quaternion."""
+  if "quat" in attrs:
+    q = np.array(_floats(attrs["quat"]), dtype=np.float64)
+    return list(q / np.linalg.norm(q))
+  scale = math.pi / 180.0 if angle_deg else 1.0
+  if "axisangle" in attrs:
+    a = _floats(attrs["axisangle"])
+    return list(rot.axis_angle_to_quat(np.array(a[:3]), a[3] * scale))
+  if "euler" in attrs:
+    e = np.array(_floats(attrs["euler"])) * scale
+    q = np.array([1.0, 0.0, 0.0, 0.0])
+    for ang, ax in zip(e, eulerseq):
+      axis = {"x": [1, 0, 0], "y": [0, 1, 0], "z": [0, 0, 1]}[ax.lower()]
+      qa = rot.axis_angle_to_quat(np.array(axis, float), ang)
+      # Lower case: axes rotate with the frame (post-multiply); upper: fixed.
+      q = rot.quat_mul(q, qa) if ax.islower() else rot.quat_mul(qa, q)
+    return list(q / np.linalg.norm(q))
+  if "xyaxes" in attrs:
+    v = np.array(_floats(attrs["xyaxes"]))
+    x = v[:3] / np.linalg.norm(v[:3])
+    y = v[3:] - x * np.dot(x, v[3:])
+    y /= np.linalg.norm(y)
+    z = np.cross(x, y)
+    return list(rot.mat_to_quat(np.stack([x, y, z], axis=1)))
+  if "zaxis" in attrs:
+    return list(rot.quat_z2vec(np.array(_floats(attrs["zaxis"]))))
+  return None
+
+
+class _Defaults:
+  """Flattened default classes: class name -> element tag -> attribute dict."""
+
+  def __init__(self) -> None:
+    self.classes: dict[str, dict[str, dict[str, str]]] = {"main": {}}
+
+  def parse(self, node: ET.Element, parent: str | None) -> None:
+    name = node.get("class", "main")
+    base = {} if parent is None else {k: dict(v) for k, v in self.classes[parent].items()}
+    for child in node:
+      if child.tag == "default":
+        continue
+      base.setdefault(child.tag, {}).update(child.attrib)
+    self.classes[name] = base
+    for child in node:
+      if child.tag == "default":
+        self.parse(child, name)
+
+  def resolve(self, tag: str, cls: str, attrs: dict[str, str]) -> dict[str, str]:
+    out = dict(self.classes.get(cls, {}).get(tag, {}))
+    out.update(attrs)
+    return out
+
+
+class MjcfReader:
+  def __init__(self, path: str | Path) -> None:
+    self.path = Path(path)
+    self.root = ET.parse(self.path).getroot()
+    comp = self.root.find("compiler")
+    comp_attr = comp.attrib if comp is not None else {}
+    self.angle_deg = comp_attr.get("angle", "degree") == "degree"
+    self.eulerseq = comp_attr.get("eulerseq", "xyz")
+    self.autolimits = comp_attr.get("autolimits", "true") == "true"
+    self.defaults = _Defaults()
+    dnode = self.root.find("default")
+    if dnode is not None:
+      self.defaults.parse(dnode, None)
+
+  def read(self) -> Spec:
+    spec = Spec(model=self.root.get("model", ""), autolimits=self.autolimits)
+    opt = self.root.find("option")
+    if opt is not None:
+      for k, v in opt.attrib.items():
+        if k in ("timestep", "impratio", "tolerance", "ls_tolerance"):
+          setattr(spec.option, k, float(v))
+        elif k in ("iterations", "ls_iterations"):
+          setattr(spec.option, k, int(v))
+        elif k == "gravity":
+          spec.option.gravity = _floats(v)
+        elif k in ("integrator", "cone", "solver", "jacobian"):
+          setattr(spec.option, k, v.lower())
+    for tag in ("tendon", "equality"):
+      node = self.root.find(tag)
+      if node is not None and len(node):
+        raise NotImplementedError(f"MJCF <{tag}> is not supported by mjlab_amd")
+    wb = self.root.find("worldbody")
+    if wb is not None:
+      self._read_body_contents(wb, spec.worldbody, "main")
+    contact = self.root.find("contact")
+    if contact is not None:
+      for ex in contact.findall("exclude"):
+        spec.excludes.append((ex.get("body1"), ex.get("body2")))
+      if contact.findall("pair"):
+        raise NotImplementedError("explicit <contact><pair> is not supported")
+    act = self.root.find("actuator")
+    if act is not None:
+      for a in act:
+        spec.actuators.append(self._read_actuator(a))
+    sens = self.root.find("sensor")
+    if sens is not None:
+      for s in sens:
+        spec.sensors.append(self._read_sensor(s))
+    kf = self.root.find("keyframe")
+    if kf is not None:
+      for k in kf.findall("key"):
+        spec.keys.append(
+          KeySpec(name=k.get("name", ""), qpos=_floats(k.get("qpos")), ctrl=_floats(k.get("ctrl")))
+        )
+    return spec
+
+  # ------------------------------------------------------------------
+  def _read_body_contents(self, node: ET.Element, body: BodySpec, childclass: str) -> None:
+    for child in node:
+      tag = child.tag
+      if tag == "body":
+        body.children.append(self._read_body(child, childclass))
+      elif tag == "geom":
+        body.geoms.append(self._read_geom(child, childclass))
+      elif tag == "site":
+        body.sites.append(self._read_site(child, childclass))
+      elif tag in ("joint", "freejoint"):
+        body.joints.append(self._read_joint(child, childclass))
+      elif tag == "inertial":
+        a = child.attrib
+        q = _orientation(a, self.angle_deg, self.eulerseq) or [1.0, 0.0, 0.0, 0.0]
+        if "fullinertia" in a:
+          full = _floats(a["fullinertia"])
+          I = np.array(
+            [[full[0], full[3], full[4]], [full[3], full[1], full[5]], [full[4], full[5], full[2]]]
+          )
+          w, V = np.linalg.eigh(I)
+          if np.linalg.det(V) < 0:
+            V[:, 0] = -V[:, 0]
+          q = list(rot.quat_mul(np.array(q), rot.mat_to_quat(V)))
+          diag = list(w)
+        else:
+          diag = _floats(a.get("diaginertia"), 3)
+        body.inertial = InertialSpec(
+          pos=_floats(a.get("pos", "0 0 0")), quat=q, mass=float(a["mass"]), diaginertia=diag
+        )
+      elif tag in _VISUAL_ONLY:
+        continue
+      elif tag == "frame":
+        raise NotImplementedError("MJCF <frame> is not supported")
+      else:
+        raise NotImplementedError(f"unsupported body child <{tag}>")
+
+  def _read_body(self, node: ET.Element, parent_class: str) -> BodySpec:
+    a = node.attrib
+    childclass = a.get("childclass", parent_class)
+    b = BodySpec(name=a.get("name", ""))
+    b.pos = _floats(a.get("pos", "0 0 0"))
+    b.quat = _orientation(a, self.angle_deg, self.eulerseq) or [1.0, 0.0, 0.0, 0.0]
+    b.mocap = a.get("mocap", "false") == "true"
+    self._read_body_contents(node, b, childclass)
+    return b
+
+  def _attrs(self, node: ET.Element, tag: str, childclass: str) -> dict[str, str]:
+    cls = node.get("class", childclass)
+    return self.defaults.resolve(tag, cls, node.attrib)
+
+  def _read_joint(self, node: ET.Element, childclass: str) -> JointSpec:
+    if node.tag == "freejoint":
+      return JointSpec(name=node.get("name", ""), type="free", limited="false")
+    a = self._attrs(node, "joint", childclass)
+    j = JointSpec(name=a.get("name", ""), type=a.get("type", "hinge"))
+    j.pos = _floats(a.get("pos", "0 0 0"))
+    ax = np.array(_floats(a.get("axis", "0 0 1")))
+    j.axis = list(ax / np.linalg.norm(ax))
+    scale = math.pi / 180.0 if (self.angle_deg and j.type in ("hinge", "ball")) else 1.0
+    if "range" in a:
+      j.range = [x * scale for x in _floats(a["range"])]
+    j.limited = a.get("limited", "auto")
+    j.ref = float(a.get("ref", 0.0)) * scale
+    j.springref = float(a.get("springref", 0.0)) * scale
+    for k in ("armature", "damping", "stiffness", "frictionloss", "margin"):
+      if k in a:
+        setattr(j, k, float(a[k]))
+    if "solreflimit" in a:
+      j.solref_limit = _floats(a["solreflimit"])
+    if "solimplimit" in a:
+      j.solimp_limit = _floats(a["solimplimit"], 5)
+    if "solreffriction" in a:
+      j.solref_friction = _floats(a["solreffriction"])
+    if "solimpfriction" in a:
+      j.solimp_friction = _floats(a["solimpfriction"], 5)
+    return j
+
+  def _read_geom(self, node: ET.Element, childclass: str) -> GeomSpec:
+    a = self._attrs(node, "geom", childclass)
+    g = GeomSpec(name=a.get("name", ""), type=a.get("type", "sphere"))
+    if "size" in a:
+      g.size = _floats(a["size"], 3)
+    g.pos = _floats(a.get("pos", "0 0 0"))
+    g.quat = _orientation(a, self.angle_deg, self.eulerseq) or [1.0, 0.0, 0.0, 0.0]
+    if "fromto" in a:
+      g.fromto = _floats(a["fromto"])
+    for k in ("contype", "conaffinity", "condim", "priority", "group"):
+      if k in a:
+        setattr(g, k, int(a[k]))
+    for k in ("solmix", "margin", "gap", "density"):
+      if k in a:
+        setattr(g, k, float(a[k]))
+    if "mass" in a:
+      g.mass = float(a["mass"])
+    if "friction" in a:
+      f = _floats(a["friction"])
+      g.friction = f + [1.0, 0.005, 0.0001][len(f):]
+    if "solref" in a:
+      g.solref = _floats(a["solref"])
+    if "solimp" in a:
+      g.solimp = _floats(a["solimp"], 5)
+    if "rgba" in a:
+      g.rgba = _floats(a["rgba"])
+    g.mesh = a.get("mesh")
+    g.material = a.get("material")
+    if g.type in ("hfield", "sdf"):
+      raise NotImplementedError(f"geom type {g.type} is not supported")
+    return g
+
+  def _read_site(self, node: ET.Element, childclass: str) -> SiteSpec:
+    a = self._attrs(node, "site", childclass)
+    s = SiteSpec(name=a.get("name", ""), type=a.get("type", "sphere"))
+    s.pos = _floats(a.get("pos", "0 0 0"))
+    s.quat = _orientation(a, self.angle_deg, self.eulerseq) or [1.0, 0.0, 0.0, 0.0]
+    if "size" in a:
+      s.size = _floats(a["size"], 3)
+    if "group" in a:
+      s.group = int(a["group"])
+    return s
+
+  def _read_actuator(self, node: ET.Element) -> ActuatorSpec:
+    a = self._attrs(node, node.tag, "main")
+    if "joint" not in a:
+      raise NotImplementedError("only joint transmissions are supported")
+    act = ActuatorSpec(name=a.get("name", ""), joint=a["joint"])
+    act.gear = _floats(a.get("gear", "1"))[0]
+    if node.tag == "motor":
+      act.gainprm = [1.0, 0.0, 0.0]
+      act.biasprm = [0.0, 0.0, 0.0]
+    elif node.tag == "position":
+      kp = float(a.get("kp", 1.0))
+      kv = float(a.get("kv", 0.0))
+      act.gainprm = [kp, 0.0, 0.0]
+      act.biasprm = [0.0, -kp, -kv]
+    elif node.tag == "general":
+      act.gainprm = _floats(a.get("gainprm", "1 0 0"), 3)[:3]
+      act.biasprm = _floats(a.get("biasprm", "0 0 0"), 3)[:3]
+    else:
+      raise NotImplementedError(f"actuator <{node.tag}> not supported")
+    if "ctrlrange" in a:
+      act.ctrlrange = _floats(a["ctrlrange"])
+    if "forcerange" in a:
+      act.forcerange = _floats(a["forcerange"])
+    act.ctrllimited = a.get("ctrllimited", "auto")
+    act.forcelimited = a.get("forcelimited", "auto")
+    act.inheritrange = float(a.get("inheritrange", 0.0))
+    return act
+
+  def _read_sensor(self, node: ET.Element) -> SensorSpec:
+    a = node.attrib
+    s = SensorSpec(name=a.get("name", ""), type=node.tag)
+    if node.tag in ("gyro", "velocimeter", "accelerometer", "framequat", "framepos"):
+      s.objtype, s.objname = "site", a["site"]
+    elif node.tag in ("subtreeangmom", "subtreecom", "subtreelinvel"):
+      s.objtype, s.objname = "body", a["body"]
+    elif node.tag in ("jointpos", "jointvel"):
+      s.objtype, s.objname = "joint", a["joint"]
+    else:
+      raise NotImplementedError(f"sensor <{node.tag}> not supported")
+    s.cutoff = float(a.get("cutoff", 0.0))
+    return s
+
+
+def read_mjcf(path: str | Path) -> Spec:
+  return MjcfReader(path).read()
+
+
+def read_mjcf_string(text: str, name: str = "inline.xml") -> Spec:
+  import tempfile
+
+  with tempfile.NamedTemporaryFile("w", suffix=".xml", delete=False) as f:
+    f.write(text)
+    p = f.name
+  try:
+    return read_mjcf(p)
+  finally:
+    Path(p).unlink(missing_ok=True)

@@ -1,0 +1,110 @@
+/* mjh_abi.h — C ABI of the MI355X batched MuJoCo step (libmjh.so).
+ *
+ * Drop-in boundary for mjlab's physics backend. The reference binds
+ *   mujoco_warp.put_model / put_data   (src/mjlab/sim/sim.py:116-126)
+ *   mujoco_warp.step / forward         (src/mjlab/sim/sim.py:138-147,186-199)
+ *   warp repeat_array_kernel           (src/mjlab/sim/randomization.py:9-54)
+ * through Warp's Python FFI. This library replaces those four entry points with
+ * plain C functions on raw device pointers:
+ *
+ *   - Ownership: the caller (torch) allocates every buffer; the library never
+ *     allocates or frees device memory and keeps no global mutable state, so
+ *     all launches are capturable into a hipGraph (torch.cuda.CUDAGraph).
+ *   - Layout: world-outermost, (nworld, COUNT) contiguous float32/int32 arrays
+ *     with the mjData field names listed in mjh_fields.h.
+ *   - Stream: every call takes the hipStream_t to launch on (as void*), normally
+ *     torch.cuda.current_stream().cuda_stream. No call synchronises the host.
+ *   - Errors: functions return 0 on success, nonzero on failure, and
+ *     mjh_last_error() returns a thread-local message. Runtime overflow of the
+ *     per-world contact/constraint capacity (nconmax/njmax) is reported through
+ *     the per-world `flags` array (bit 0: contacts dropped, bit 1: constraint
+ *     rows dropped, bit 2: non-finite state), never by a host sync.
+ */
+#ifndef MJH_ABI_H_
+#define MJH_ABI_H_
+
+#include <stddef.h>
+#include "mjh_fields.h"
+
+typedef long long mjh_i64;
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MJH_ABI_VERSION 1
+
+/* efc_type codes (mjtConstraint) */
+#define MJH_CNSTR_FRICTION_DOF 1
+#define MJH_CNSTR_LIMIT_JOINT 3
+#define MJH_CNSTR_CONTACT_FRICTIONLESS 5
+#define MJH_CNSTR_CONTACT_PYRAMIDAL 6
+
+/* flags bits */
+#define MJH_FLAG_CONTACT_OVERFLOW 1
+#define MJH_FLAG_EFC_OVERFLOW 2
+#define MJH_FLAG_NONFINITE 4
+
+/* integrator codes (mjtIntegrator) */
+#define MJH_INT_EULER 0
+#define MJH_INT_IMPLICITFAST 3
+
+/* Model descriptor: sizes, options, device pointers. */
+typedef struct mjh_model {
+#define MJH_X_SIZE(name) int name;
+  MJH_MODEL_SIZES(MJH_X_SIZE)
+#undef MJH_X_SIZE
+#define MJH_X_OPT(type, name) type name;
+  MJH_MODEL_OPTIONS(MJH_X_OPT)
+#undef MJH_X_OPT
+#define MJH_X_ARR(type, name, count) const type* name;
+  MJH_MODEL_ARRAYS(MJH_X_ARR)
+#undef MJH_X_ARR
+#define MJH_X_WARR(type, name, count) const type* name; long long name##_wstride;
+  MJH_MODEL_WARRAYS(MJH_X_WARR)
+#undef MJH_X_WARR
+} mjh_model;
+
+/* Data descriptor: one pointer per per-world array, (nworld, COUNT). */
+typedef struct mjh_data {
+  int nworld;
+  int _pad;
+#define MJH_X_DATA(type, name, count) type* name;
+  MJH_DATA_ARRAYS(MJH_X_DATA)
+#undef MJH_X_DATA
+} mjh_data;
+
+/* Version of this ABI (MJH_ABI_VERSION). */
+int mjh_abi_version(void);
+
+/* Thread-local message describing the last failure ("" if none). */
+const char* mjh_last_error(void);
+
+/* sizeof the descriptors, so a binding can check its struct layout. */
+size_t mjh_sizeof_model(void);
+size_t mjh_sizeof_data(void);
+
+/* Host-side validation of a model descriptor against the kernel limits
+ * (nv <= 64, nbody <= 64, capacity of per-world scratch). Returns 0 if the
+ * model can be stepped. Replaces put_model's checks (sim.py:116). */
+int mjh_model_check(const mjh_model* m);
+
+/* Bytes of per-world on-chip scratch the step kernel uses for this model. */
+int mjh_scratch_bytes(const mjh_model* m);
+
+/* One physics step (mj_step: forward + implicitfast/Euler integration) for all
+ * nworld worlds. Replaces mjwarp.step (sim.py:193-199). */
+int mjh_step(const mjh_model* m, const mjh_data* d, void* stream);
+
+/* Forward dynamics only (no integration, time unchanged). Replaces
+ * mjwarp.forward (sim.py:186-191). */
+int mjh_forward(const mjh_model* m, const mjh_data* d, void* stream);
+
+/* Tile src[0:nelem] into dst[w*nelem:(w+1)*nelem] for w < nworld.
+ * Replaces repeat_array_kernel (randomization.py:9-17). */
+int mjh_repeat(float* dst, const float* src, long long nelem, int nworld, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MJH_ABI_H_ */

@@ -1,0 +1,1411 @@
+/* oracle.c — serial CPU restatement of mj_step for the parity oracle.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h). One world at a time, in the order of
+ * MuJoCo's published pipeline (mj_step = mj_forward + integration):
+ *   kinematics -> com_pos -> crb -> tree LDL^T factor (mj_factorI) -> collision
+ *   -> make_constraint -> com_vel -> passive -> rne -> actuation ->
+ *   acceleration -> Newton solver -> sensors -> implicitfast/Euler integration.
+ * Reference anchors: mjlab's solver/integrator options sim.py:42-76 and
+ * velocity_env_cfg.py:53-61; actuator semantics spec_config.py:402-414;
+ * contact sensor semantics contact_sensor.py:16-47,472-533.
+ * Deliberately written differently from the HIP kernel (tree-sparse LDL^T,
+ * level-order recursions, dense serial loops) so that agreement is evidence.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define MINVAL 1e-15
+#define MINIMP 0.0001
+#define MAXIMP 0.9999
+
+#define WF(m, f, w) ((m)->f + (long long)(w) * (m)->f##_wstride)
+
+/* ---------------------------------------------------------------- math */
+static void mul_quat(real r[4], const real a[4], const real b[4]) {
+  real t[4];
+  t[0] = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  t[1] = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  t[2] = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  t[3] = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  memcpy(r, t, sizeof(t));
+}
+static real norm3(const real v[3]) { return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+static real dot3(const real a[3], const real b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void cross3(real r[3], const real a[3], const real b[3]) {
+  real t[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+  memcpy(r, t, sizeof(t));
+}
+static void normalize4(real q[4]) {
+  real n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) {
+    q[0] = 1; q[1] = q[2] = q[3] = 0;
+  } else {
+    for (int i = 0; i < 4; i++) q[i] /= n;
+  }
+}
+static real normalize3(real v[3]) {
+  real n = norm3(v);
+  if (n < MINVAL) {
+    v[0] = 1; v[1] = v[2] = 0;
+  } else {
+    v[0] /= n; v[1] /= n; v[2] /= n;
+  }
+  return n;
+}
+static void quat2mat(real m[9], const real q[4]) {
+  real w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
+}
+static void mat_vec(real r[3], const real m[9], const real v[3]) {
+  real t[3] = {m[0] * v[0] + m[1] * v[1] + m[2] * v[2], m[3] * v[0] + m[4] * v[1] + m[5] * v[2],
+               m[6] * v[0] + m[7] * v[1] + m[8] * v[2]};
+  memcpy(r, t, sizeof(t));
+}
+static void matT_vec(real r[3], const real m[9], const real v[3]) {
+  real t[3] = {m[0] * v[0] + m[3] * v[1] + m[6] * v[2], m[1] * v[0] + m[4] * v[1] + m[7] * v[2],
+               m[2] * v[0] + m[5] * v[1] + m[8] * v[2]};
+  memcpy(r, t, sizeof(t));
+}
+static void mat_mul(real r[9], const real a[9], const real b[9]) {
+  real t[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) t[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+  memcpy(r, t, sizeof(t));
+}
+static void rot_quat(real r[3], const real v[3], const real q[4]) {
+  real m[9];
+  quat2mat(m, q);
+  mat_vec(r, m, v);
+}
+static void axis_angle(real q[4], const real axis[3], real ang) {
+  real s = sin(ang * 0.5);
+  q[0] = cos(ang * 0.5); q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
+}
+/* spatial motion cross product  res = v x m  (v, m: [ang; lin]) */
+static void cross_motion(real r[6], const real v[6], const real m[6]) {
+  real t[6];
+  t[0] = -v[2] * m[1] + v[1] * m[2];
+  t[1] = v[2] * m[0] - v[0] * m[2];
+  t[2] = -v[1] * m[0] + v[0] * m[1];
+  t[3] = -v[2] * m[4] + v[1] * m[5] - v[5] * m[1] + v[4] * m[2];
+  t[4] = v[2] * m[3] - v[0] * m[5] + v[5] * m[0] - v[3] * m[2];
+  t[5] = -v[1] * m[3] + v[0] * m[4] - v[4] * m[0] + v[3] * m[1];
+  memcpy(r, t, sizeof(t));
+}
+/* spatial force cross product  res = v x* f */
+static void cross_force(real r[6], const real v[6], const real f[6]) {
+  real t[6];
+  t[0] = -v[2] * f[1] + v[1] * f[2] - v[5] * f[4] + v[4] * f[5];
+  t[1] = v[2] * f[0] - v[0] * f[2] + v[5] * f[3] - v[3] * f[5];
+  t[2] = -v[1] * f[0] + v[0] * f[1] - v[4] * f[3] + v[3] * f[4];
+  t[3] = -v[2] * f[4] + v[1] * f[5];
+  t[4] = v[2] * f[3] - v[0] * f[5];
+  t[5] = -v[1] * f[3] + v[0] * f[4];
+  memcpy(r, t, sizeof(t));
+}
+/* 10-vector inertia (I about com frame origin, h = m*c, m) times motion */
+static void inert_vec(real r[6], const real in[10], const real v[6]) {
+  r[0] = in[0] * v[0] + in[3] * v[1] + in[4] * v[2] - in[8] * v[4] + in[7] * v[5];
+  r[1] = in[3] * v[0] + in[1] * v[1] + in[5] * v[2] + in[8] * v[3] - in[6] * v[5];
+  r[2] = in[4] * v[0] + in[5] * v[1] + in[2] * v[2] - in[7] * v[3] + in[6] * v[4];
+  r[3] = in[8] * v[1] - in[7] * v[2] + in[9] * v[3];
+  r[4] = in[6] * v[2] - in[8] * v[0] + in[9] * v[4];
+  r[5] = in[7] * v[0] - in[6] * v[1] + in[9] * v[5];
+}
+/* velocity/acceleration of a spatial vector at point p, rotated into frame rot (if given) */
+static void transform_motion(real res[6], const real vec[6], const real p[3], const real c[3], const real* rot) {
+  real dif[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]}, t[3], out[6];
+  cross3(t, dif, vec);
+  out[0] = vec[0]; out[1] = vec[1]; out[2] = vec[2];
+  out[3] = vec[3] - t[0]; out[4] = vec[4] - t[1]; out[5] = vec[5] - t[2];
+  if (rot) {
+    matT_vec(res, rot, out);
+    matT_vec(res + 3, rot, out + 3);
+  } else {
+    memcpy(res, out, sizeof(out));
+  }
+}
+
+/* ---------------------------------------------------------------- workspace */
+typedef struct {
+  real dist, pos[3], frame[9], friction[5], solref[2], solimp[5], includemargin;
+  int dim, geom[2], efc_address;
+} contact_t;
+
+typedef struct {
+  real *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis, *subtree_com;
+  real *cinert, *crb, *cdof, *cdof_dot, *cvel, *cacc, *cfrc;
+  real *gxpos, *gxmat, *sxpos, *sxmat;
+  real *M, *LD, *H, *qvel, *qpos, *qacc, *qacc_smooth, *qfrc_smooth, *qfrc_bias, *qfrc_passive,
+      *qfrc_actuator, *qfrc_constraint, *act_force, *act_length, *act_vel, *tmpv, *tmpv2, *grad, *search,
+      *Ma, *Mv, *Mgrad, *qacc_int;
+  real *J, *efc_pos, *efc_margin, *efc_D, *efc_R, *efc_aref, *efc_fl, *jaref, *jv, *efc_force;
+  int *efc_type, *efc_id;
+  int nefc, ncon, flags, niter;
+  contact_t* con;
+} ws_t;
+
+static void* xcalloc(size_t n, size_t s) { return calloc(n ? n : 1, s); }
+
+static void ws_alloc(ws_t* w, const or_model* m) {
+  int nb = m->nbody, nv = m->nv, nj = m->njnt;
+  memset(w, 0, sizeof(*w));
+#define AR(p, n) w->p = (real*)xcalloc((size_t)(n), sizeof(real))
+  AR(xpos, 3 * nb); AR(xquat, 4 * nb); AR(xmat, 9 * nb); AR(xipos, 3 * nb); AR(ximat, 9 * nb);
+  AR(xanchor, 3 * nj); AR(xaxis, 3 * nj); AR(subtree_com, 3 * nb); AR(cinert, 10 * nb); AR(crb, 10 * nb);
+  AR(cdof, 6 * nv); AR(cdof_dot, 6 * nv); AR(cvel, 6 * nb); AR(cacc, 6 * nb); AR(cfrc, 6 * nb);
+  AR(gxpos, 3 * m->ngeom); AR(gxmat, 9 * m->ngeom); AR(sxpos, 3 * m->nsite); AR(sxmat, 9 * m->nsite);
+  AR(M, nv * nv); AR(LD, nv * nv); AR(H, nv * nv); AR(qvel, nv); AR(qpos, m->nq); AR(qacc, nv);
+  AR(qacc_smooth, nv); AR(qfrc_smooth, nv); AR(qfrc_bias, nv); AR(qfrc_passive, nv); AR(qfrc_actuator, nv);
+  AR(qfrc_constraint, nv); AR(act_force, m->nu); AR(act_length, m->nu); AR(act_vel, m->nu);
+  AR(tmpv, nv); AR(tmpv2, nv); AR(grad, nv); AR(search, nv); AR(Ma, nv); AR(Mv, nv); AR(Mgrad, nv);
+  AR(qacc_int, nv);
+  AR(J, (size_t)m->njmax * nv); AR(efc_pos, m->njmax); AR(efc_margin, m->njmax); AR(efc_D, m->njmax);
+  AR(efc_R, m->njmax); AR(efc_aref, m->njmax); AR(efc_fl, m->njmax); AR(jaref, m->njmax); AR(jv, m->njmax);
+  AR(efc_force, m->njmax);
+#undef AR
+  w->efc_type = (int*)xcalloc(m->njmax, sizeof(int));
+  w->efc_id = (int*)xcalloc(m->njmax, sizeof(int));
+  w->con = (contact_t*)xcalloc(m->nconmax, sizeof(contact_t));
+}
+
+static void ws_free(ws_t* w) {
+  real** ptrs[] = {&w->xpos, &w->xquat, &w->xmat, &w->xipos, &w->ximat, &w->xanchor, &w->xaxis, &w->subtree_com,
+                   &w->cinert, &w->crb, &w->cdof, &w->cdof_dot, &w->cvel, &w->cacc, &w->cfrc, &w->gxpos, &w->gxmat,
+                   &w->sxpos, &w->sxmat, &w->M, &w->LD, &w->H, &w->qvel, &w->qpos, &w->qacc, &w->qacc_smooth,
+                   &w->qfrc_smooth, &w->qfrc_bias, &w->qfrc_passive, &w->qfrc_actuator, &w->qfrc_constraint,
+                   &w->act_force, &w->act_length, &w->act_vel, &w->tmpv, &w->tmpv2, &w->grad, &w->search, &w->Ma,
+                   &w->Mv, &w->Mgrad, &w->qacc_int, &w->J, &w->efc_pos, &w->efc_margin, &w->efc_D, &w->efc_R,
+                   &w->efc_aref, &w->efc_fl, &w->jaref, &w->jv, &w->efc_force};
+  for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); i++) free(*ptrs[i]);
+  free(w->efc_type);
+  free(w->efc_id);
+  free(w->con);
+}
+
+/* ---------------------------------------------------------------- smooth dynamics */
+static void kinematics(const or_model* m, int wi, ws_t* w) {
+  const real* bpos = WF(m, body_pos, wi);
+  const real* bquat = WF(m, body_quat, wi);
+  const real* qpos0 = WF(m, qpos0, wi);
+  w->xquat[0] = 1;
+  quat2mat(w->xmat, w->xquat);
+  for (int b = 1; b < m->nbody; b++) {
+    int p = m->body_parentid[b];
+    real* xp = w->xpos + 3 * b;
+    real* xq = w->xquat + 4 * b;
+    int ja = m->body_jntadr[b], jn = m->body_jntnum[b];
+    if (jn == 1 && m->jnt_type[ja] == 0) {
+      const real* q = w->qpos + m->jnt_qposadr[ja];
+      xp[0] = q[0]; xp[1] = q[1]; xp[2] = q[2];
+      xq[0] = q[3]; xq[1] = q[4]; xq[2] = q[5]; xq[3] = q[6];
+      normalize4(xq);
+      memcpy(w->xanchor + 3 * ja, xp, 3 * sizeof(real));
+      quat2mat(w->xmat + 9 * b, xq);
+      real* ax = w->xaxis + 3 * ja;
+      ax[0] = w->xmat[9 * b + 2]; ax[1] = w->xmat[9 * b + 5]; ax[2] = w->xmat[9 * b + 8];
+      continue;
+    }
+    real t[3];
+    mat_vec(t, w->xmat + 9 * p, bpos + 3 * b);
+    for (int k = 0; k < 3; k++) xp[k] = w->xpos[3 * p + k] + t[k];
+    mul_quat(xq, w->xquat + 4 * p, bquat + 4 * b);
+    for (int j = ja; j < ja + jn; j++) {
+      real* anc = w->xanchor + 3 * j;
+      real* ax = w->xaxis + 3 * j;
+      rot_quat(ax, m->jnt_axis + 3 * j, xq);
+      rot_quat(anc, m->jnt_pos + 3 * j, xq);
+      for (int k = 0; k < 3; k++) anc[k] += xp[k];
+      int qa = m->jnt_qposadr[j];
+      if (m->jnt_type[j] == 2) { /* slide */
+        real d = w->qpos[qa] - qpos0[qa];
+        for (int k = 0; k < 3; k++) xp[k] += ax[k] * d;
+      } else if (m->jnt_type[j] == 3) { /* hinge */
+        real ql[4], v[3];
+        axis_angle(ql, m->jnt_axis + 3 * j, w->qpos[qa] - qpos0[qa]);
+        mul_quat(xq, xq, ql);
+        rot_quat(v, m->jnt_pos + 3 * j, xq);
+        for (int k = 0; k < 3; k++) xp[k] = anc[k] - v[k];
+      }
+    }
+    normalize4(xq);
+    quat2mat(w->xmat + 9 * b, xq);
+  }
+  /* inertial frames, geoms, sites */
+  const real* ipos = WF(m, body_ipos, wi);
+  const real* iquat = WF(m, body_iquat, wi);
+  for (int b = 0; b < m->nbody; b++) {
+    real t[3], im[9];
+    mat_vec(t, w->xmat + 9 * b, ipos + 3 * b);
+    for (int k = 0; k < 3; k++) w->xipos[3 * b + k] = w->xpos[3 * b + k] + t[k];
+    quat2mat(im, iquat + 4 * b);
+    mat_mul(w->ximat + 9 * b, w->xmat + 9 * b, im);
+  }
+  const real* gpos = WF(m, geom_pos, wi);
+  const real* gquat = WF(m, geom_quat, wi);
+  for (int g = 0; g < m->ngeom; g++) {
+    int b = m->geom_bodyid[g];
+    real t[3], gm[9];
+    mat_vec(t, w->xmat + 9 * b, gpos + 3 * g);
+    for (int k = 0; k < 3; k++) w->gxpos[3 * g + k] = w->xpos[3 * b + k] + t[k];
+    quat2mat(gm, gquat + 4 * g);
+    mat_mul(w->gxmat + 9 * g, w->xmat + 9 * b, gm);
+  }
+  const real* spos = WF(m, site_pos, wi);
+  const real* squat = WF(m, site_quat, wi);
+  for (int s = 0; s < m->nsite; s++) {
+    int b = m->site_bodyid[s];
+    real t[3], sm[9];
+    mat_vec(t, w->xmat + 9 * b, spos + 3 * s);
+    for (int k = 0; k < 3; k++) w->sxpos[3 * s + k] = w->xpos[3 * b + k] + t[k];
+    quat2mat(sm, squat + 4 * s);
+    mat_mul(w->sxmat + 9 * s, w->xmat + 9 * b, sm);
+  }
+}
+
+static void com_pos(const or_model* m, int wi, ws_t* w) {
+  const real* mass = WF(m, body_mass, wi);
+  const real* inertia = WF(m, body_inertia, wi);
+  int nb = m->nbody;
+  real* msum = w->tmpv;  /* nv may be < nbody; use a local buffer instead */
+  real* mb = (real*)calloc((size_t)nb * 4, sizeof(real));
+  (void)msum;
+  for (int b = 0; b < nb; b++) {
+    mb[4 * b + 3] = mass[b];
+    for (int k = 0; k < 3; k++) mb[4 * b + k] = mass[b] * w->xipos[3 * b + k];
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    for (int k = 0; k < 4; k++) mb[4 * p + k] += mb[4 * b + k];
+  }
+  for (int b = 0; b < nb; b++) {
+    for (int k = 0; k < 3; k++)
+      w->subtree_com[3 * b + k] = mb[4 * b + 3] < MINVAL ? w->xipos[3 * b + k] : mb[4 * b + k] / mb[4 * b + 3];
+  }
+  free(mb);
+  /* cinert: inertia about subtree_com[root] in world orientation */
+  for (int b = 0; b < nb; b++) {
+    real* ci = w->cinert + 10 * b;
+    const real* R = w->ximat + 9 * b;
+    const real* c = w->subtree_com + 3 * m->body_rootid[b];
+    real d[3] = {w->xipos[3 * b] - c[0], w->xipos[3 * b + 1] - c[1], w->xipos[3 * b + 2] - c[2]};
+    real I[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        real s = 0;
+        for (int k = 0; k < 3; k++) s += R[3 * i + k] * inertia[3 * b + k] * R[3 * j + k];
+        I[3 * i + j] = s;
+      }
+    real mm = mass[b], dd = dot3(d, d);
+    ci[0] = I[0] + mm * (dd - d[0] * d[0]);
+    ci[1] = I[4] + mm * (dd - d[1] * d[1]);
+    ci[2] = I[8] + mm * (dd - d[2] * d[2]);
+    ci[3] = I[1] - mm * d[0] * d[1];
+    ci[4] = I[2] - mm * d[0] * d[2];
+    ci[5] = I[5] - mm * d[1] * d[2];
+    ci[6] = mm * d[0]; ci[7] = mm * d[1]; ci[8] = mm * d[2]; ci[9] = mm;
+  }
+  /* cdof */
+  for (int j = 0; j < m->njnt; j++) {
+    int b = m->jnt_bodyid[j], da = m->jnt_dofadr[j];
+    const real* c = w->subtree_com + 3 * m->body_rootid[b];
+    real off[3] = {c[0] - w->xanchor[3 * j], c[1] - w->xanchor[3 * j + 1], c[2] - w->xanchor[3 * j + 2]};
+    switch (m->jnt_type[j]) {
+      case 0:
+        for (int k = 0; k < 3; k++) {
+          real* cd = w->cdof + 6 * (da + k);
+          memset(cd, 0, 6 * sizeof(real));
+          cd[3 + k] = 1;
+        }
+        for (int k = 0; k < 3; k++) {
+          real* cd = w->cdof + 6 * (da + 3 + k);
+          real ax[3] = {w->xmat[9 * b + k], w->xmat[9 * b + 3 + k], w->xmat[9 * b + 6 + k]};
+          memcpy(cd, ax, 3 * sizeof(real));
+          cross3(cd + 3, ax, off);
+        }
+        break;
+      case 2: {
+        real* cd = w->cdof + 6 * da;
+        memset(cd, 0, 3 * sizeof(real));
+        memcpy(cd + 3, w->xaxis + 3 * j, 3 * sizeof(real));
+        break;
+      }
+      case 3: {
+        real* cd = w->cdof + 6 * da;
+        memcpy(cd, w->xaxis + 3 * j, 3 * sizeof(real));
+        cross3(cd + 3, w->xaxis + 3 * j, off);
+        break;
+      }
+    }
+  }
+}
+
+static void crb(const or_model* m, int wi, ws_t* w) {
+  int nv = m->nv;
+  memcpy(w->crb, w->cinert, sizeof(real) * 10 * m->nbody);
+  for (int b = m->nbody - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    if (p > 0)
+      for (int k = 0; k < 10; k++) w->crb[10 * p + k] += w->crb[10 * b + k];
+  }
+  memset(w->M, 0, sizeof(real) * nv * nv);
+  const real* arm = WF(m, dof_armature, wi);
+  for (int i = 0; i < nv; i++) {
+    real buf[6];
+    inert_vec(buf, w->crb + 10 * m->dof_bodyid[i], w->cdof + 6 * i);
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+      real s = 0;
+      for (int k = 0; k < 6; k++) s += w->cdof[6 * j + k] * buf[k];
+      w->M[i * nv + j] = s;
+      w->M[j * nv + i] = s;
+    }
+    w->M[i * nv + i] += arm[i];
+  }
+}
+
+/* tree LDL^T (mj_factorI): LD holds L (strict lower, tree pattern) and D on the diagonal */
+static void factor_tree(const or_model* m, const real* A, real* LD) {
+  int nv = m->nv;
+  memcpy(LD, A, sizeof(real) * nv * nv);
+  for (int k = nv - 1; k >= 0; k--) {
+    if (LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
+    real invD = 1.0 / LD[k * nv + k];
+    for (int i = m->dof_parentid[k]; i >= 0; i = m->dof_parentid[i]) {
+      real t = LD[k * nv + i];
+      for (int j = i; j >= 0; j = m->dof_parentid[j]) LD[i * nv + j] -= t * invD * LD[k * nv + j];
+      LD[k * nv + i] = t * invD;
+    }
+  }
+}
+static void solve_tree(const or_model* m, const real* LD, real* x) {
+  int nv = m->nv;
+  for (int k = nv - 1; k >= 0; k--)
+    for (int i = m->dof_parentid[k]; i >= 0; i = m->dof_parentid[i]) x[i] -= LD[k * nv + i] * x[k];
+  for (int k = 0; k < nv; k++) x[k] /= LD[k * nv + k];
+  for (int k = 0; k < nv; k++)
+    for (int i = m->dof_parentid[k]; i >= 0; i = m->dof_parentid[i]) x[k] -= LD[k * nv + i] * x[i];
+}
+
+static void com_vel(const or_model* m, ws_t* w) {
+  memset(w->cvel, 0, 6 * sizeof(real));
+  for (int b = 1; b < m->nbody; b++) {
+    real cv[6];
+    memcpy(cv, w->cvel + 6 * m->body_parentid[b], sizeof(cv));
+    for (int j = m->body_jntadr[b]; j < m->body_jntadr[b] + m->body_jntnum[b] && m->body_jntnum[b] > 0; j++) {
+      int da = m->jnt_dofadr[j];
+      if (m->jnt_type[j] == 0) {
+        for (int k = 0; k < 3; k++) {
+          memset(w->cdof_dot + 6 * (da + k), 0, 6 * sizeof(real));
+          for (int c = 0; c < 6; c++) cv[c] += w->cdof[6 * (da + k) + c] * w->qvel[da + k];
+        }
+        for (int k = 3; k < 6; k++) cross_motion(w->cdof_dot + 6 * (da + k), cv, w->cdof + 6 * (da + k));
+        for (int k = 3; k < 6; k++)
+          for (int c = 0; c < 6; c++) cv[c] += w->cdof[6 * (da + k) + c] * w->qvel[da + k];
+      } else {
+        cross_motion(w->cdof_dot + 6 * da, cv, w->cdof + 6 * da);
+        for (int c = 0; c < 6; c++) cv[c] += w->cdof[6 * da + c] * w->qvel[da];
+      }
+    }
+    memcpy(w->cvel + 6 * b, cv, sizeof(cv));
+  }
+}
+
+/* RNE: cacc from qacc (NULL: bias only), cfrc_body, returns generalized force in out */
+static void rne(const or_model* m, ws_t* w, const real* qacc, real* out) {
+  real g[3] = {m->gravity_x, m->gravity_y, m->gravity_z};
+  real* cacc = w->cacc;
+  memset(cacc, 0, 6 * sizeof(real));
+  cacc[3] = -g[0]; cacc[4] = -g[1]; cacc[5] = -g[2];
+  for (int b = 1; b < m->nbody; b++) {
+    real* a = cacc + 6 * b;
+    memcpy(a, cacc + 6 * m->body_parentid[b], 6 * sizeof(real));
+    for (int d = m->body_dofadr[b]; d < m->body_dofadr[b] + m->body_dofnum[b] && m->body_dofnum[b] > 0; d++) {
+      for (int c = 0; c < 6; c++) {
+        a[c] += w->cdof_dot[6 * d + c] * w->qvel[d];
+        if (qacc) a[c] += w->cdof[6 * d + c] * qacc[d];
+      }
+    }
+    real f1[6], f2[6], f3[6];
+    inert_vec(f1, w->cinert + 10 * b, a);
+    inert_vec(f2, w->cinert + 10 * b, w->cvel + 6 * b);
+    cross_force(f3, w->cvel + 6 * b, f2);
+    for (int c = 0; c < 6; c++) w->cfrc[6 * b + c] = f1[c] + f3[c];
+  }
+  for (int b = m->nbody - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    if (p > 0)
+      for (int c = 0; c < 6; c++) w->cfrc[6 * p + c] += w->cfrc[6 * b + c];
+  }
+  if (out)
+    for (int d = 0; d < m->nv; d++) {
+      real s = 0;
+      for (int c = 0; c < 6; c++) s += w->cdof[6 * d + c] * w->cfrc[6 * m->dof_bodyid[d] + c];
+      out[d] = s;
+    }
+}
+
+/* translational/rotational jacobian column of dof d at point p for body b (0 if d not in chain) */
+static int in_chain(const or_model* m, int b, int d) {
+  int db = m->dof_bodyid[d];
+  for (int k = b; k > 0; k = m->body_parentid[k])
+    if (k == db) return 1;
+  return 0;
+}
+static void jac_col(const or_model* m, ws_t* w, int b, const real p[3], int d, real jp[3], real jr[3]) {
+  if (!in_chain(m, b, d)) {
+    jp[0] = jp[1] = jp[2] = jr[0] = jr[1] = jr[2] = 0;
+    return;
+  }
+  const real* cd = w->cdof + 6 * d;
+  const real* c = w->subtree_com + 3 * m->body_rootid[b];
+  real off[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]}, t[3];
+  cross3(t, cd, off);
+  for (int k = 0; k < 3; k++) {
+    jp[k] = cd[3 + k] + t[k];
+    jr[k] = cd[k];
+  }
+}
+
+static void passive_actuation(const or_model* m, int wi, ws_t* w, const real* ctrl, const real* qfrc_applied,
+                              const real* xfrc) {
+  int nv = m->nv;
+  const real* damping = WF(m, dof_damping, wi);
+  const real* stiff = WF(m, jnt_stiffness, wi);
+  memset(w->qfrc_passive, 0, sizeof(real) * nv);
+  for (int j = 0; j < m->njnt; j++) {
+    int t = m->jnt_type[j];
+    if ((t == 2 || t == 3) && stiff[j] != 0) {
+      int qa = m->jnt_qposadr[j];
+      w->qfrc_passive[m->jnt_dofadr[j]] -= stiff[j] * (w->qpos[qa] - m->qpos_spring[qa]);
+    }
+  }
+  for (int d = 0; d < nv; d++) w->qfrc_passive[d] -= damping[d] * w->qvel[d];
+  memset(w->qfrc_actuator, 0, sizeof(real) * nv);
+  for (int i = 0; i < m->nu; i++) {
+    int j = m->actuator_trnid[i];
+    real gear = m->actuator_gear[i];
+    real len = gear * w->qpos[m->jnt_qposadr[j]];
+    real vel = gear * w->qvel[m->jnt_dofadr[j]];
+    real c = ctrl[i];
+    if (m->actuator_ctrllimited[i]) {
+      real lo = m->actuator_ctrlrange[2 * i], hi = m->actuator_ctrlrange[2 * i + 1];
+      c = c < lo ? lo : (c > hi ? hi : c);
+    }
+    const real* gp = m->actuator_gainprm + 10 * i;
+    const real* bp = m->actuator_biasprm + 10 * i;
+    real f = gp[0] * c + bp[0] + bp[1] * len + bp[2] * vel;
+    if (m->actuator_forcelimited[i]) {
+      real lo = m->actuator_forcerange[2 * i], hi = m->actuator_forcerange[2 * i + 1];
+      f = f < lo ? lo : (f > hi ? hi : f);
+    }
+    w->act_force[i] = f;
+    w->act_length[i] = len;
+    w->act_vel[i] = vel;
+    w->qfrc_actuator[m->jnt_dofadr[j]] += gear * f;
+  }
+  /* smooth force */
+  for (int d = 0; d < nv; d++)
+    w->qfrc_smooth[d] = w->qfrc_passive[d] - w->qfrc_bias[d] + qfrc_applied[d] + w->qfrc_actuator[d];
+  /* xfrc_applied at body com */
+  for (int b = 1; b < m->nbody; b++) {
+    const real* f = xfrc + 6 * b;
+    if (!(f[0] || f[1] || f[2] || f[3] || f[4] || f[5])) continue;
+    for (int d = 0; d < nv; d++) {
+      real jp[3], jr[3];
+      jac_col(m, w, b, w->xipos + 3 * b, d, jp, jr);
+      w->qfrc_smooth[d] += dot3(jp, f) + dot3(jr, f + 3);
+    }
+  }
+}
+
+/* ---------------------------------------------------------------- collision */
+static void make_frame(real f[9]) {
+  normalize3(f);
+  if (norm3(f + 3) < 0.5) {
+    f[3] = f[4] = f[5] = 0;
+    if (f[1] < 0.5 && f[1] > -0.5) f[4] = 1; else f[5] = 1;
+  }
+  real d = dot3(f, f + 3);
+  for (int k = 0; k < 3; k++) f[3 + k] -= d * f[k];
+  normalize3(f + 3);
+  cross3(f + 6, f, f + 3);
+}
+
+static int raw_sphere_sphere(contact_t* c, real margin, const real p1[3], real r1, const real p2[3], real r2) {
+  real dif[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  real cd = norm3(dif);
+  if (cd > margin + r1 + r2) return 0;
+  real n[3];
+  if (cd < MINVAL) { n[0] = 1; n[1] = n[2] = 0; }
+  else { n[0] = dif[0] / cd; n[1] = dif[1] / cd; n[2] = dif[2] / cd; }
+  c->dist = cd - r1 - r2;
+  for (int k = 0; k < 3; k++) {
+    c->pos[k] = p1[k] + n[k] * (r1 + 0.5 * c->dist);
+    c->frame[k] = n[k];
+    c->frame[3 + k] = 0;
+  }
+  return 1;
+}
+static int raw_plane_sphere(contact_t* c, real margin, const real pp[3], const real pm[9], const real sp[3], real r) {
+  real n[3] = {pm[2], pm[5], pm[8]};
+  real dif[3] = {sp[0] - pp[0], sp[1] - pp[1], sp[2] - pp[2]};
+  real cd = dot3(dif, n);
+  if (cd > margin + r) return 0;
+  c->dist = cd - r;
+  for (int k = 0; k < 3; k++) {
+    c->pos[k] = sp[k] - n[k] * (r + 0.5 * c->dist);
+    c->frame[k] = n[k];
+    c->frame[3 + k] = 0;
+  }
+  return 1;
+}
+
+static int collide(const or_model* m, ws_t* w, int g1, int g2, real margin, contact_t* out) {
+  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  const real *p1 = w->gxpos + 3 * g1, *m1 = w->gxmat + 9 * g1, *s1 = m->geom_size + 3 * g1;
+  const real *p2 = w->gxpos + 3 * g2, *m2 = w->gxmat + 9 * g2, *s2 = m->geom_size + 3 * g2;
+  if (t1 == 0 && t2 == 2) return raw_plane_sphere(out, margin, p1, m1, p2, s2[0]);
+  if (t1 == 0 && t2 == 3) {
+    real ax[3] = {m2[2], m2[5], m2[8]}, a[3], b[3];
+    for (int k = 0; k < 3; k++) { a[k] = p2[k] + ax[k] * s2[1]; b[k] = p2[k] - ax[k] * s2[1]; }
+    int n1 = raw_plane_sphere(out, margin, p1, m1, a, s2[0]);
+    int n2 = raw_plane_sphere(out + n1, margin, p1, m1, b, s2[0]);
+    if (n1) memcpy(out[0].frame + 3, ax, 3 * sizeof(real));
+    if (n2) memcpy(out[n1].frame + 3, ax, 3 * sizeof(real));
+    return n1 + n2;
+  }
+  if (t1 == 0 && t2 == 6) {
+    real n[3] = {m1[2], m1[5], m1[8]};
+    real dif[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+    real dist = dot3(dif, n);
+    int cnt = 0;
+    for (int i = 0; i < 8 && cnt < 4; i++) {
+      real v[3] = {0, 0, 0};
+      for (int k = 0; k < 3; k++) {
+        real s = (i & (1 << k)) ? s2[k] : -s2[k];
+        v[0] += m2[k] * s; v[1] += m2[3 + k] * s; v[2] += m2[6 + k] * s;
+      }
+      real ld = dot3(n, v);
+      if (dist + ld > margin) continue;
+      contact_t* c = out + cnt++;
+      c->dist = dist + ld;
+      for (int k = 0; k < 3; k++) {
+        c->pos[k] = p2[k] + v[k] - n[k] * 0.5 * c->dist;
+        c->frame[k] = n[k];
+        c->frame[3 + k] = 0;
+      }
+    }
+    return cnt;
+  }
+  if (t1 == 2 && t2 == 2) return raw_sphere_sphere(out, margin, p1, s1[0], p2, s2[0]);
+  if (t1 == 2 && t2 == 3) {
+    real ax[3] = {m2[2], m2[5], m2[8]};
+    real dif[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+    real x = dot3(dif, ax);
+    x = x < -s2[1] ? -s2[1] : (x > s2[1] ? s2[1] : x);
+    real v[3] = {p2[0] + ax[0] * x, p2[1] + ax[1] * x, p2[2] + ax[2] * x};
+    return raw_sphere_sphere(out, margin, p1, s1[0], v, s2[0]);
+  }
+  if (t1 == 3 && t2 == 3) {
+    real a1[3] = {m1[2] * s1[1], m1[5] * s1[1], m1[8] * s1[1]};
+    real a2[3] = {m2[2] * s2[1], m2[5] * s2[1], m2[8] * s2[1]};
+    real dif[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+    real ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2);
+    real u = -dot3(a1, dif), v = dot3(a2, dif), det = ma * mc - mb * mb;
+    real v1[3], v2[3];
+    if (fabs(det) >= MINVAL) {
+      real x1 = (mc * u - mb * v) / det, x2 = (ma * v - mb * u) / det;
+      if (x1 > 1) { x1 = 1; x2 = (v - mb) / mc; }
+      else if (x1 < -1) { x1 = -1; x2 = (v + mb) / mc; }
+      if (x2 > 1) { x2 = 1; x1 = (u - mb) / ma; x1 = x1 < -1 ? -1 : (x1 > 1 ? 1 : x1); }
+      else if (x2 < -1) { x2 = -1; x1 = (u + mb) / ma; x1 = x1 < -1 ? -1 : (x1 > 1 ? 1 : x1); }
+      for (int k = 0; k < 3; k++) { v1[k] = p1[k] + a1[k] * x1; v2[k] = p2[k] + a2[k] * x2; }
+      return raw_sphere_sphere(out, margin, v1, s1[0], v2, s2[0]);
+    }
+    /* parallel axes: test segment end points */
+    int n = 0;
+    for (int e = 0; e < 2 && n < 2; e++) {
+      real x1 = e ? -1 : 1;
+      real x2 = (v - mb * x1) / mc;
+      x2 = x2 < -1 ? -1 : (x2 > 1 ? 1 : x2);
+      for (int k = 0; k < 3; k++) { v1[k] = p1[k] + a1[k] * x1; v2[k] = p2[k] + a2[k] * x2; }
+      n += raw_sphere_sphere(out + n, margin, v1, s1[0], v2, s2[0]);
+    }
+    for (int e = 0; e < 2 && n < 2; e++) {
+      real x2 = e ? -1 : 1;
+      real x1 = (u - mb * x2) / ma;
+      x1 = x1 < -1 ? -1 : (x1 > 1 ? 1 : x1);
+      for (int k = 0; k < 3; k++) { v1[k] = p1[k] + a1[k] * x1; v2[k] = p2[k] + a2[k] * x2; }
+      n += raw_sphere_sphere(out + n, margin, v1, s1[0], v2, s2[0]);
+    }
+    return n;
+  }
+  return 0; /* unsupported pairs are rejected by the compiler */
+}
+
+static void collision(const or_model* m, int wi, ws_t* w) {
+  const real* fr = WF(m, geom_friction, wi);
+  w->ncon = 0;
+  for (int p = 0; p < m->npair; p++) {
+    int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
+    real margin = m->geom_margin[g1] > m->geom_margin[g2] ? m->geom_margin[g1] : m->geom_margin[g2];
+    real gap = m->geom_gap[g1] > m->geom_gap[g2] ? m->geom_gap[g1] : m->geom_gap[g2];
+    /* bounding-sphere broadphase */
+    if (m->geom_type[g1] == 0) {
+      const real* pm = w->gxmat + 9 * g1;
+      real n[3] = {pm[2], pm[5], pm[8]};
+      real dif[3] = {w->gxpos[3 * g2] - w->gxpos[3 * g1], w->gxpos[3 * g2 + 1] - w->gxpos[3 * g1 + 1],
+                     w->gxpos[3 * g2 + 2] - w->gxpos[3 * g1 + 2]};
+      if (dot3(dif, n) > margin + m->geom_rbound[g2]) continue;
+    } else {
+      real dif[3] = {w->gxpos[3 * g2] - w->gxpos[3 * g1], w->gxpos[3 * g2 + 1] - w->gxpos[3 * g1 + 1],
+                     w->gxpos[3 * g2 + 2] - w->gxpos[3 * g1 + 2]};
+      if (norm3(dif) > margin + m->geom_rbound[g1] + m->geom_rbound[g2]) continue;
+    }
+    contact_t tmp[4];
+    memset(tmp, 0, sizeof(tmp));
+    int n = collide(m, w, g1, g2, margin, tmp);
+    /* contact parameters */
+    int condim;
+    real fri[3], solref[2], solimp[5];
+    int pr1 = m->geom_priority[g1], pr2 = m->geom_priority[g2];
+    if (pr1 != pr2) {
+      int g = pr1 > pr2 ? g1 : g2;
+      condim = m->geom_condim[g];
+      for (int k = 0; k < 3; k++) fri[k] = fr[3 * g + k];
+      for (int k = 0; k < 2; k++) solref[k] = m->geom_solref[2 * g + k];
+      for (int k = 0; k < 5; k++) solimp[k] = m->geom_solimp[5 * g + k];
+    } else {
+      condim = m->geom_condim[g1] > m->geom_condim[g2] ? m->geom_condim[g1] : m->geom_condim[g2];
+      for (int k = 0; k < 3; k++) fri[k] = fr[3 * g1 + k] > fr[3 * g2 + k] ? fr[3 * g1 + k] : fr[3 * g2 + k];
+      real s1 = m->geom_solmix[g1], s2 = m->geom_solmix[g2], mix;
+      if (s1 >= MINVAL && s2 >= MINVAL) mix = s1 / (s1 + s2);
+      else if (s1 < MINVAL && s2 < MINVAL) mix = 0.5;
+      else mix = s1 < MINVAL ? 0.0 : 1.0;
+      const real *r1 = m->geom_solref + 2 * g1, *r2 = m->geom_solref + 2 * g2;
+      if (r1[0] > 0 && r2[0] > 0)
+        for (int k = 0; k < 2; k++) solref[k] = mix * r1[k] + (1 - mix) * r2[k];
+      else
+        for (int k = 0; k < 2; k++) solref[k] = r1[k] < r2[k] ? r1[k] : r2[k];
+      for (int k = 0; k < 5; k++) solimp[k] = mix * m->geom_solimp[5 * g1 + k] + (1 - mix) * m->geom_solimp[5 * g2 + k];
+    }
+    for (int i = 0; i < n; i++) {
+      if (w->ncon >= m->nconmax) {
+        w->flags |= 1;
+        break;
+      }
+      contact_t* c = w->con + w->ncon++;
+      *c = tmp[i];
+      make_frame(c->frame);
+      c->dim = condim;
+      c->geom[0] = g1;
+      c->geom[1] = g2;
+      c->friction[0] = fri[0]; c->friction[1] = fri[0]; c->friction[2] = fri[1];
+      c->friction[3] = fri[2]; c->friction[4] = fri[2];
+      memcpy(c->solref, solref, sizeof(solref));
+      memcpy(c->solimp, solimp, sizeof(solimp));
+      c->includemargin = margin - gap;
+      c->efc_address = -1;
+    }
+  }
+}
+
+/* ---------------------------------------------------------------- constraints */
+static void efc_row_params(const or_model* m, ws_t* w, int r, real pos_aref, real pos_imp, real invweight,
+                           const real* solref, const real* solimp, real margin, real jqvel) {
+  real timeconst = solref[0], dampratio = solref[1];
+  real dmin = solimp[0], dmax = solimp[1], width = solimp[2], mid = solimp[3], power = solimp[4];
+  if (timeconst < 2 * m->timestep && solref[0] > 0) timeconst = 2 * m->timestep;
+  dmin = dmin < MINIMP ? MINIMP : (dmin > MAXIMP ? MAXIMP : dmin);
+  dmax = dmax < MINIMP ? MINIMP : (dmax > MAXIMP ? MAXIMP : dmax);
+  width = width < MINVAL ? MINVAL : width;
+  mid = mid < MINIMP ? MINIMP : (mid > MAXIMP ? MAXIMP : mid);
+  power = power < 1 ? 1 : power;
+  real k = 1.0 / (dmax * dmax * timeconst * timeconst * dampratio * dampratio);
+  real b = 2.0 / (dmax * timeconst);
+  if (solref[0] <= 0) k = -solref[0] / (dmax * dmax);
+  if (solref[1] <= 0) b = -solref[1] / dmax;
+  real x = fabs(pos_imp) / width, imp;
+  if (x > 1) {
+    imp = dmax;
+  } else {
+    real y;
+    if (x < mid) y = pow(x, power) / pow(mid, power - 1);
+    else y = 1 - pow(1 - x, power) / pow(1 - mid, power - 1);
+    imp = dmin + y * (dmax - dmin);
+    imp = imp < dmin ? dmin : (imp > dmax ? dmax : imp);
+  }
+  real R = invweight * (1 - imp) / imp;
+  if (R < MINVAL) R = MINVAL;
+  w->efc_R[r] = R;
+  w->efc_D[r] = 1.0 / R;
+  w->efc_aref[r] = -k * imp * pos_aref - b * jqvel;
+  w->efc_pos[r] = pos_aref + margin;
+  w->efc_margin[r] = margin;
+}
+
+static int new_row(const or_model* m, ws_t* w) {
+  if (w->nefc >= m->njmax) {
+    w->flags |= 2;
+    return -1;
+  }
+  int r = w->nefc++;
+  memset(w->J + (size_t)r * m->nv, 0, sizeof(real) * m->nv);
+  w->efc_fl[r] = 0;
+  return r;
+}
+
+static void make_constraint(const or_model* m, int wi, ws_t* w) {
+  int nv = m->nv;
+  w->nefc = 0;
+  const real* fl = WF(m, dof_frictionloss, wi);
+  const real* rng = WF(m, jnt_range, wi);
+  /* dof friction loss */
+  for (int d = 0; d < nv; d++) {
+    if (fl[d] <= 0) continue;
+    int r = new_row(m, w);
+    if (r < 0) return;
+    w->J[r * nv + d] = 1;
+    w->efc_type[r] = 1;
+    w->efc_id[r] = d;
+    w->efc_fl[r] = fl[d];
+    efc_row_params(m, w, r, 0, 0, m->dof_invweight0[d], m->dof_solref + 2 * d, m->dof_solimp + 5 * d, 0,
+                   w->qvel[d]);
+  }
+  /* joint limits */
+  for (int j = 0; j < m->njnt; j++) {
+    int t = m->jnt_type[j];
+    if (!m->jnt_limited[j] || (t != 2 && t != 3)) continue;
+    real q = w->qpos[m->jnt_qposadr[j]];
+    real dlo = q - rng[2 * j], dhi = rng[2 * j + 1] - q;
+    real pos = (dlo < dhi ? dlo : dhi) - m->jnt_margin[j];
+    if (pos >= 0) continue;
+    int r = new_row(m, w);
+    if (r < 0) return;
+    int d = m->jnt_dofadr[j];
+    real jj = dlo < dhi ? 1 : -1;
+    w->J[r * nv + d] = jj;
+    w->efc_type[r] = 3;
+    w->efc_id[r] = j;
+    efc_row_params(m, w, r, pos, pos, m->dof_invweight0[d], m->jnt_solref + 2 * j, m->jnt_solimp + 5 * j,
+                   m->jnt_margin[j], jj * w->qvel[d]);
+  }
+  /* contacts */
+  for (int ci = 0; ci < w->ncon; ci++) {
+    contact_t* c = w->con + ci;
+    real pos = c->dist - c->includemargin;
+    if (pos >= 0) continue;
+    int b1 = m->geom_bodyid[c->geom[0]], b2 = m->geom_bodyid[c->geom[1]];
+    int nrow = c->dim == 1 ? 1 : 2 * (c->dim - 1);
+    real invw = m->body_invweight0[2 * b1] + m->body_invweight0[2 * b2];
+    if (c->dim > 1) {
+      real f0 = c->friction[0];
+      invw = invw + f0 * f0 * invw;
+      invw = invw * 2 * f0 * f0 / m->impratio;
+    }
+    /* relative translational / rotational jacobians (b2 minus b1), projected on frame */
+    real* jf = (real*)calloc((size_t)6 * nv, sizeof(real)); /* rows: n, t1, t2 (trans), n, t1, t2 (rot) */
+    for (int d = 0; d < nv; d++) {
+      real jp1[3], jr1[3], jp2[3], jr2[3];
+      jac_col(m, w, b1, c->pos, d, jp1, jr1);
+      jac_col(m, w, b2, c->pos, d, jp2, jr2);
+      real dp[3] = {jp2[0] - jp1[0], jp2[1] - jp1[1], jp2[2] - jp1[2]};
+      real dr[3] = {jr2[0] - jr1[0], jr2[1] - jr1[1], jr2[2] - jr1[2]};
+      for (int a = 0; a < 3; a++) {
+        jf[a * nv + d] = dot3(c->frame + 3 * a, dp);
+        jf[(3 + a) * nv + d] = dot3(c->frame + 3 * a, dr);
+      }
+    }
+    c->efc_address = w->nefc;
+    for (int e = 0; e < nrow; e++) {
+      int r = new_row(m, w);
+      if (r < 0) {
+        free(jf);
+        return;
+      }
+      real* Jr = w->J + (size_t)r * nv;
+      if (c->dim == 1) {
+        for (int d = 0; d < nv; d++) Jr[d] = jf[d];
+        w->efc_type[r] = 5;
+      } else {
+        int k = e / 2 + 1;                           /* friction direction 1..dim-1 */
+        const real* jt = k < 3 ? jf + k * nv : jf + (3 + k - 3) * nv; /* tangent (trans) or torsion/roll (rot) */
+        real fk = c->friction[k - 1];
+        real sgn = (e % 2 == 0) ? 1 : -1;
+        for (int d = 0; d < nv; d++) Jr[d] = jf[d] + sgn * fk * jt[d];
+        w->efc_type[r] = 6;
+      }
+      w->efc_id[r] = ci;
+      real jq = 0;
+      for (int d = 0; d < nv; d++) jq += Jr[d] * w->qvel[d];
+      efc_row_params(m, w, r, pos, pos, invw, c->solref, c->solimp, c->includemargin, jq);
+    }
+    free(jf);
+  }
+}
+
+/* ---------------------------------------------------------------- solver */
+static void mat_vec_n(const real* A, const real* x, real* y, int n) {
+  for (int i = 0; i < n; i++) {
+    real s = 0;
+    for (int j = 0; j < n; j++) s += A[i * n + j] * x[j];
+    y[i] = s;
+  }
+}
+
+/* constraint state at jaref: force, cost; returns hessian weight (D if quadratic else 0) */
+static real row_eval(const ws_t* w, int r, real jaref, real* force, real* cost) {
+  real D = w->efc_D[r];
+  if (w->efc_type[r] == 1) {
+    real f = w->efc_fl[r], R = w->efc_R[r];
+    if (jaref >= R * f) { *force = -f; *cost = f * jaref - 0.5 * R * f * f; return 0; }
+    if (jaref <= -R * f) { *force = f; *cost = -f * jaref - 0.5 * R * f * f; return 0; }
+    *force = -D * jaref; *cost = 0.5 * D * jaref * jaref; return D;
+  }
+  if (jaref < 0) { *force = -D * jaref; *cost = 0.5 * D * jaref * jaref; return D; }
+  *force = 0; *cost = 0; return 0;
+}
+
+/* update forces/cost/qfrc_constraint at current jaref; returns total cost */
+static real update_constraint(const or_model* m, ws_t* w, const real* qacc_smooth) {
+  int nv = m->nv;
+  real cost = 0;
+  memset(w->qfrc_constraint, 0, sizeof(real) * nv);
+  for (int r = 0; r < w->nefc; r++) {
+    real f, c;
+    row_eval(w, r, w->jaref[r], &f, &c);
+    w->efc_force[r] = f;
+    cost += c;
+    for (int d = 0; d < nv; d++) w->qfrc_constraint[d] += w->J[(size_t)r * nv + d] * f;
+  }
+  real gauss = 0;
+  for (int d = 0; d < nv; d++) gauss += 0.5 * (w->Ma[d] - w->qfrc_smooth[d]) * (w->qacc[d] - qacc_smooth[d]);
+  return cost + gauss;
+}
+
+static int chol_dense(real* A, int n) {
+  for (int j = 0; j < n; j++) {
+    real s = A[j * n + j];
+    for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
+    if (s < MINVAL) s = MINVAL;
+    real d = sqrt(s);
+    A[j * n + j] = d;
+    for (int i = j + 1; i < n; i++) {
+      real t = A[i * n + j];
+      for (int k = 0; k < j; k++) t -= A[i * n + k] * A[j * n + k];
+      A[i * n + j] = t / d;
+    }
+  }
+  return 0;
+}
+static void chol_solve(const real* L, real* x, int n) {
+  for (int i = 0; i < n; i++) {
+    real s = x[i];
+    for (int k = 0; k < i; k++) s -= L[i * n + k] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    real s = x[i];
+    for (int k = i + 1; k < n; k++) s -= L[k * n + i] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+}
+
+static void newton_direction(const or_model* m, ws_t* w) {
+  int nv = m->nv;
+  for (int d = 0; d < nv; d++) w->grad[d] = w->Ma[d] - w->qfrc_smooth[d] - w->qfrc_constraint[d];
+  memcpy(w->H, w->M, sizeof(real) * nv * nv);
+  for (int r = 0; r < w->nefc; r++) {
+    real f, c, h = row_eval(w, r, w->jaref[r], &f, &c);
+    if (h == 0) continue;
+    const real* Jr = w->J + (size_t)r * nv;
+    for (int i = 0; i < nv; i++) {
+      if (Jr[i] == 0) continue;
+      for (int j = 0; j <= i; j++) w->H[i * nv + j] += h * Jr[i] * Jr[j];
+    }
+  }
+  chol_dense(w->H, nv);
+  memcpy(w->Mgrad, w->grad, sizeof(real) * nv);
+  chol_solve(w->H, w->Mgrad, nv);
+  for (int d = 0; d < nv; d++) w->search[d] = -w->Mgrad[d];
+}
+
+/* exact line search on the convex piecewise-quadratic cost along search */
+static real linesearch(const or_model* m, ws_t* w) {
+  int nv = m->nv;
+  mat_vec_n(w->M, w->search, w->Mv, nv);
+  for (int r = 0; r < w->nefc; r++) {
+    real s = 0;
+    for (int d = 0; d < nv; d++) s += w->J[(size_t)r * nv + d] * w->search[d];
+    w->jv[r] = s;
+  }
+  real g1 = 0, g2 = 0;
+  for (int d = 0; d < nv; d++) {
+    g1 += w->search[d] * (w->Ma[d] - w->qfrc_smooth[d]);
+    g2 += w->search[d] * w->Mv[d];
+  }
+  /* derivative of cost(alpha) */
+#define DERIVS(alpha, d1, d2)                                         \
+  do {                                                                \
+    d1 = g1 + (alpha) * g2;                                           \
+    d2 = g2;                                                          \
+    for (int r = 0; r < w->nefc; r++) {                               \
+      real ja = w->jaref[r] + (alpha) * w->jv[r], f, c;               \
+      real h = row_eval(w, r, ja, &f, &c);                            \
+      d1 -= f * w->jv[r];                                             \
+      d2 += h * w->jv[r] * w->jv[r];                                  \
+    }                                                                 \
+  } while (0)
+  real d10, d20;
+  DERIVS(0.0, d10, d20);
+  if (!(d10 < 0)) return 0;
+  real gtol = m->ls_tolerance * fabs(d10);
+  real lo = 0, hi = -1, alpha = -d10 / d20;
+  for (int it = 0; it < m->ls_iterations; it++) {
+    real d1, d2;
+    DERIVS(alpha, d1, d2);
+    if (fabs(d1) <= gtol) break;
+    if (d1 < 0) lo = alpha; else hi = alpha;
+    real an = alpha - d1 / d2;
+    if (an <= lo || (hi >= 0 && an >= hi)) an = hi >= 0 ? 0.5 * (lo + hi) : 2 * alpha;
+    alpha = an;
+  }
+#undef DERIVS
+  return alpha;
+}
+
+static void solve(const or_model* m, ws_t* w, const real* warm) {
+  int nv = m->nv;
+  real scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+  w->niter = 0;
+  if (w->nefc == 0) {
+    memcpy(w->qacc, w->qacc_smooth, sizeof(real) * nv);
+    memset(w->qfrc_constraint, 0, sizeof(real) * nv);
+    return;
+  }
+  /* warmstart: keep the lower-cost of qacc_warmstart and qacc_smooth */
+  memcpy(w->qacc, warm, sizeof(real) * nv);
+  mat_vec_n(w->M, w->qacc, w->Ma, nv);
+  for (int r = 0; r < w->nefc; r++) {
+    real s = 0;
+    for (int d = 0; d < nv; d++) s += w->J[(size_t)r * nv + d] * w->qacc[d];
+    w->jaref[r] = s - w->efc_aref[r];
+  }
+  real cost = update_constraint(m, w, w->qacc_smooth);
+  real cost_smooth = 0;
+  for (int r = 0; r < w->nefc; r++) {
+    real s = 0, f, c;
+    for (int d = 0; d < nv; d++) s += w->J[(size_t)r * nv + d] * w->qacc_smooth[d];
+    row_eval(w, r, s - w->efc_aref[r], &f, &c);
+    cost_smooth += c;
+  }
+  if (cost > cost_smooth) {
+    memcpy(w->qacc, w->qacc_smooth, sizeof(real) * nv);
+    memcpy(w->Ma, w->qfrc_smooth, sizeof(real) * nv);
+    mat_vec_n(w->M, w->qacc, w->Ma, nv);
+    for (int r = 0; r < w->nefc; r++) {
+      real s = 0;
+      for (int d = 0; d < nv; d++) s += w->J[(size_t)r * nv + d] * w->qacc[d];
+      w->jaref[r] = s - w->efc_aref[r];
+    }
+    cost = update_constraint(m, w, w->qacc_smooth);
+  }
+  newton_direction(m, w);
+  for (int it = 0; it < m->iterations; it++) {
+    real alpha = linesearch(m, w);
+    if (alpha == 0) break;
+    for (int d = 0; d < nv; d++) {
+      w->qacc[d] += alpha * w->search[d];
+      w->Ma[d] += alpha * w->Mv[d];
+    }
+    for (int r = 0; r < w->nefc; r++) w->jaref[r] += alpha * w->jv[r];
+    real old = cost;
+    cost = update_constraint(m, w, w->qacc_smooth);
+    newton_direction(m, w);
+    w->niter++;
+    real gn = 0;
+    for (int d = 0; d < nv; d++) gn += w->grad[d] * w->grad[d];
+    real improvement = scale * (old - cost), gradient = scale * sqrt(gn);
+    if (improvement < m->tolerance || gradient < m->tolerance) break;
+  }
+}
+
+/* ---------------------------------------------------------------- sensors */
+static int subtree_has(const or_model* m, int root, int b) {
+  for (int k = b; k >= 0; k = k ? m->body_parentid[k] : -1) {
+    if (k == root) return 1;
+    if (k == 0) break;
+  }
+  return 0;
+}
+static int obj_match(const or_model* m, int type, int id, int g) {
+  if (id < 0) return 1;
+  int b = m->geom_bodyid[g];
+  if (type == 5) return g == id;
+  if (type == 1) return b == id;
+  if (type == 2) return subtree_has(m, id, b);
+  return 0;
+}
+
+static void contact_force(const or_model* m, ws_t* w, int ci, real f[6]) {
+  contact_t* c = w->con + ci;
+  memset(f, 0, 6 * sizeof(real));
+  if (c->efc_address < 0) return;
+  const real* ef = w->efc_force + c->efc_address;
+  (void)m;
+  if (c->dim == 1) { f[0] = ef[0]; return; }
+  for (int e = 0; e < 2 * (c->dim - 1); e++) f[0] += ef[e];
+  for (int k = 1; k < c->dim; k++) f[k] = c->friction[k - 1] * (ef[2 * k - 2] - ef[2 * k - 1]);
+}
+
+static void sensors(const or_model* m, ws_t* w, real* sd) {
+  for (int s = 0; s < m->nsensor; s++) {
+    int type = m->sensor_type[s], id = m->sensor_objid[s];
+    real* out = sd + m->sensor_adr[s];
+    switch (type) {
+      case 3: { /* gyro */
+        int b = m->site_bodyid[id];
+        matT_vec(out, w->sxmat + 9 * id, w->cvel + 6 * b);
+        break;
+      }
+      case 2: { /* velocimeter */
+        int b = m->site_bodyid[id];
+        real v[6];
+        transform_motion(v, w->cvel + 6 * b, w->sxpos + 3 * id, w->subtree_com + 3 * m->body_rootid[b],
+                         w->sxmat + 9 * id);
+        memcpy(out, v + 3, 3 * sizeof(real));
+        break;
+      }
+      case 1: { /* accelerometer */
+        int b = m->site_bodyid[id];
+        const real* c = w->subtree_com + 3 * m->body_rootid[b];
+        real a[6], v[6], t[3];
+        transform_motion(a, w->cacc + 6 * b, w->sxpos + 3 * id, c, w->sxmat + 9 * id);
+        transform_motion(v, w->cvel + 6 * b, w->sxpos + 3 * id, c, w->sxmat + 9 * id);
+        cross3(t, v, v + 3);
+        for (int k = 0; k < 3; k++) out[k] = a[3 + k] + t[k];
+        break;
+      }
+      case 30: memcpy(out, w->sxpos + 3 * id, 3 * sizeof(real)); break;
+      case 31: { /* framequat of site from its xmat */
+        const real* R = w->sxmat + 9 * id;
+        real q[4], tr = R[0] + R[4] + R[8];
+        if (tr > 0) {
+          real sq = sqrt(tr + 1) * 2;
+          q[0] = 0.25 * sq; q[1] = (R[7] - R[5]) / sq; q[2] = (R[2] - R[6]) / sq; q[3] = (R[3] - R[1]) / sq;
+        } else if (R[0] > R[4] && R[0] > R[8]) {
+          real sq = sqrt(1 + R[0] - R[4] - R[8]) * 2;
+          q[0] = (R[7] - R[5]) / sq; q[1] = 0.25 * sq; q[2] = (R[1] + R[3]) / sq; q[3] = (R[2] + R[6]) / sq;
+        } else if (R[4] > R[8]) {
+          real sq = sqrt(1 + R[4] - R[0] - R[8]) * 2;
+          q[0] = (R[2] - R[6]) / sq; q[1] = (R[1] + R[3]) / sq; q[2] = 0.25 * sq; q[3] = (R[5] + R[7]) / sq;
+        } else {
+          real sq = sqrt(1 + R[8] - R[0] - R[4]) * 2;
+          q[0] = (R[3] - R[1]) / sq; q[1] = (R[2] + R[6]) / sq; q[2] = (R[5] + R[7]) / sq; q[3] = 0.25 * sq;
+        }
+        if (q[0] < 0) for (int k = 0; k < 4; k++) q[k] = -q[k];
+        normalize4(q);
+        memcpy(out, q, sizeof(q));
+        break;
+      }
+      case 9: out[0] = w->qpos[m->jnt_qposadr[id]]; break;
+      case 10: out[0] = w->qvel[m->jnt_dofadr[id]]; break;
+      case 34: memcpy(out, w->subtree_com + 3 * id, 3 * sizeof(real)); break;
+      case 35:
+      case 36: { /* subtree linear velocity / angular momentum about subtree com */
+        real msum = 0, lin[3] = {0, 0, 0}, L[3] = {0, 0, 0};
+        const real* mass = m->body_mass; /* world 0 copy is fine only if not expanded; use per-world below */
+        (void)mass;
+        const real* c = w->subtree_com + 3 * id;
+        /* per-body com velocity */
+        for (int b = 1; b < m->nbody; b++) {
+          if (!subtree_has(m, id, b)) continue;
+          real bm = w->cinert[10 * b + 9];
+          real v[6];
+          transform_motion(v, w->cvel + 6 * b, w->xipos + 3 * b, w->subtree_com + 3 * m->body_rootid[b], NULL);
+          msum += bm;
+          for (int k = 0; k < 3; k++) lin[k] += bm * v[3 + k];
+        }
+        real vc[3] = {0, 0, 0};
+        if (msum > MINVAL) for (int k = 0; k < 3; k++) vc[k] = lin[k] / msum;
+        if (type == 35) { memcpy(out, vc, sizeof(vc)); break; }
+        for (int b = 1; b < m->nbody; b++) {
+          if (!subtree_has(m, id, b)) continue;
+          real bm = w->cinert[10 * b + 9];
+          real v[6], Iw[3], dv[3], dx[3], t[3];
+          transform_motion(v, w->cvel + 6 * b, w->xipos + 3 * b, w->subtree_com + 3 * m->body_rootid[b], NULL);
+          /* I_b * omega in world: R diag(I) R' omega; use cinert-independent body inertia via ximat */
+          const real* R = w->ximat + 9 * b;
+          real wl[3];
+          matT_vec(wl, R, v);
+          /* inertia diag recovered from crb is not available; cinert holds I about root com.
+             Use the rotational inertia about the body com: I_com = I_root - m(|d|^2 - dd') */
+          real d[3] = {w->xipos[3 * b] - w->subtree_com[3 * m->body_rootid[b]],
+                       w->xipos[3 * b + 1] - w->subtree_com[3 * m->body_rootid[b] + 1],
+                       w->xipos[3 * b + 2] - w->subtree_com[3 * m->body_rootid[b] + 2]};
+          const real* ci = w->cinert + 10 * b;
+          real dd = dot3(d, d);
+          real I[9] = {ci[0] - bm * (dd - d[0] * d[0]), ci[3] + bm * d[0] * d[1], ci[4] + bm * d[0] * d[2],
+                       ci[3] + bm * d[0] * d[1], ci[1] - bm * (dd - d[1] * d[1]), ci[5] + bm * d[1] * d[2],
+                       ci[4] + bm * d[0] * d[2], ci[5] + bm * d[1] * d[2], ci[2] - bm * (dd - d[2] * d[2])};
+          (void)wl;
+          mat_vec(Iw, I, v);
+          for (int k = 0; k < 3; k++) { dx[k] = w->xipos[3 * b + k] - c[k]; dv[k] = (v[3 + k] - vc[k]) * bm; }
+          cross3(t, dx, dv);
+          for (int k = 0; k < 3; k++) L[k] += Iw[k] + t[k];
+        }
+        memcpy(out, L, sizeof(L));
+        break;
+      }
+      case 40: { /* contact sensor */
+        int bits = m->sensor_intprm[3 * s], reduce = m->sensor_intprm[3 * s + 1], nslot = m->sensor_intprm[3 * s + 2];
+        int rtype = m->sensor_reftype[s], rid = m->sensor_refid[s], otype = m->sensor_objtype[s];
+        int dim = m->sensor_dim[s];
+        memset(out, 0, sizeof(real) * dim);
+        int match[64], flip[64], nmatch = 0;
+        for (int ci = 0; ci < w->ncon && nmatch < m->contact_sensor_maxmatch && nmatch < 64; ci++) {
+          int g1 = w->con[ci].geom[0], g2 = w->con[ci].geom[1];
+          if (obj_match(m, otype, id, g1) && obj_match(m, rtype, rid, g2)) { match[nmatch] = ci; flip[nmatch++] = 0; }
+          else if (obj_match(m, otype, id, g2) && obj_match(m, rtype, rid, g1)) { match[nmatch] = ci; flip[nmatch++] = 1; }
+        }
+        if (nmatch == 0) break;
+        /* per-match data */
+        real F[64][6], Fw[64][3], Tw[64][3];
+        for (int k = 0; k < nmatch; k++) {
+          contact_t* c = w->con + match[k];
+          contact_force(m, w, match[k], F[k]);
+          real sgn = flip[k] ? 1 : -1; /* force on primary = +F if primary is geom2 */
+          for (int a = 0; a < 3; a++) {
+            Fw[k][a] = sgn * (F[k][0] * c->frame[a] + F[k][1] * c->frame[3 + a] + F[k][2] * c->frame[6 + a]);
+            Tw[k][a] = sgn * (F[k][3] * c->frame[a] + F[k][4] * c->frame[3 + a] + F[k][5] * c->frame[6 + a]);
+          }
+        }
+        int order[64], nfill;
+        for (int k = 0; k < nmatch; k++) order[k] = k;
+        if (reduce == 1 || reduce == 2) { /* selection sort by dist asc / force norm desc */
+          for (int a = 0; a < nmatch; a++)
+            for (int b2 = a + 1; b2 < nmatch; b2++) {
+              real ka, kb;
+              if (reduce == 1) { ka = w->con[match[order[a]]].dist; kb = w->con[match[order[b2]]].dist; }
+              else { ka = -norm3(F[order[a]]); kb = -norm3(F[order[b2]]); }
+              if (kb < ka) { int t = order[a]; order[a] = order[b2]; order[b2] = t; }
+            }
+        }
+        real* o = out;
+        if (reduce == 3) {
+          real net[3] = {0, 0, 0}, tq[3] = {0, 0, 0}, cen[3] = {0, 0, 0}, wsum = 0, mind = 1e30;
+          for (int k = 0; k < nmatch; k++) {
+            real fn = norm3(Fw[k]);
+            for (int a = 0; a < 3; a++) { net[a] += Fw[k][a]; cen[a] += fn * w->con[match[k]].pos[a]; }
+            wsum += fn;
+            if (w->con[match[k]].dist < mind) mind = w->con[match[k]].dist;
+          }
+          for (int a = 0; a < 3; a++) cen[a] = wsum > MINVAL ? cen[a] / wsum : w->con[match[0]].pos[a];
+          for (int k = 0; k < nmatch; k++) {
+            real r[3], t[3];
+            for (int a = 0; a < 3; a++) r[a] = w->con[match[k]].pos[a] - cen[a];
+            cross3(t, r, Fw[k]);
+            for (int a = 0; a < 3; a++) tq[a] += t[a] + Tw[k][a];
+          }
+          if (bits & 1) *o++ = nmatch;
+          if (bits & 2) { memcpy(o, net, 3 * sizeof(real)); o += 3; }
+          if (bits & 4) { memcpy(o, tq, 3 * sizeof(real)); o += 3; }
+          if (bits & 8) *o++ = mind;
+          if (bits & 16) { memcpy(o, cen, 3 * sizeof(real)); o += 3; }
+          if (bits & 32) { real z[3] = {0, 0, 0}; memcpy(o, z, sizeof(z)); o += 3; }
+          if (bits & 64) { real z[3] = {0, 0, 0}; memcpy(o, z, sizeof(z)); o += 3; }
+          break;
+        }
+        nfill = nmatch < nslot ? nmatch : nslot;
+        for (int sl = 0; sl < nfill; sl++) {
+          int k = order[sl];
+          contact_t* c = w->con + match[k];
+          real sg = flip[k] ? -1 : 1;
+          if (bits & 1) *o++ = nmatch;
+          if (bits & 2) { memcpy(o, F[k], 3 * sizeof(real)); o += 3; }
+          if (bits & 4) { memcpy(o, F[k] + 3, 3 * sizeof(real)); o += 3; }
+          if (bits & 8) *o++ = c->dist;
+          if (bits & 16) { memcpy(o, c->pos, 3 * sizeof(real)); o += 3; }
+          if (bits & 32) { for (int a = 0; a < 3; a++) *o++ = sg * c->frame[a]; }
+          if (bits & 64) { for (int a = 0; a < 3; a++) *o++ = sg * c->frame[3 + a]; }
+        }
+        break;
+      }
+    }
+    if (m->sensor_cutoff[s] > 0 && type != 31 && type != 40)
+      for (int k = 0; k < m->sensor_dim[s]; k++) {
+        real cut = m->sensor_cutoff[s];
+        out[k] = out[k] < -cut ? -cut : (out[k] > cut ? cut : out[k]);
+      }
+  }
+}
+
+/* ---------------------------------------------------------------- driver */
+static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_t* w) {
+  int nq = m->nq, nv = m->nv, nu = m->nu, nb = m->nbody;
+  const real* qpos_in = d->qpos + (size_t)wi * nq;
+  memcpy(w->qpos, qpos_in, sizeof(real) * nq);
+  memcpy(w->qvel, d->qvel + (size_t)wi * nv, sizeof(real) * nv);
+  const real* ctrl = d->ctrl + (size_t)wi * nu;
+  const real* qfrc_applied = d->qfrc_applied + (size_t)wi * nv;
+  const real* xfrc = d->xfrc_applied + (size_t)wi * nb * 6;
+  w->flags = 0;
+
+  kinematics(m, wi, w);
+  com_pos(m, wi, w);
+  crb(m, wi, w);
+  factor_tree(m, w->M, w->LD);
+  collision(m, wi, w);
+  com_vel(m, w);
+  rne(m, w, NULL, w->qfrc_bias);
+  passive_actuation(m, wi, w, ctrl, qfrc_applied, xfrc);
+  make_constraint(m, wi, w);
+  memcpy(w->qacc_smooth, w->qfrc_smooth, sizeof(real) * nv);
+  solve_tree(m, w->LD, w->qacc_smooth);
+  solve(m, w, d->qacc_warmstart + (size_t)wi * nv);
+  rne(m, w, w->qacc, NULL); /* cacc with constraint accelerations (accelerometer) */
+  real* sd = d->sensordata + (size_t)wi * m->nsensordata;
+  sensors(m, w, sd);
+
+  /* outputs of the forward pass */
+  memcpy(d->xpos + (size_t)wi * nb * 3, w->xpos, sizeof(real) * nb * 3);
+  memcpy(d->xquat + (size_t)wi * nb * 4, w->xquat, sizeof(real) * nb * 4);
+  memcpy(d->xmat + (size_t)wi * nb * 9, w->xmat, sizeof(real) * nb * 9);
+  memcpy(d->xipos + (size_t)wi * nb * 3, w->xipos, sizeof(real) * nb * 3);
+  memcpy(d->ximat + (size_t)wi * nb * 9, w->ximat, sizeof(real) * nb * 9);
+  memcpy(d->xanchor + (size_t)wi * m->njnt * 3, w->xanchor, sizeof(real) * m->njnt * 3);
+  memcpy(d->xaxis + (size_t)wi * m->njnt * 3, w->xaxis, sizeof(real) * m->njnt * 3);
+  memcpy(d->geom_xpos + (size_t)wi * m->ngeom * 3, w->gxpos, sizeof(real) * m->ngeom * 3);
+  memcpy(d->geom_xmat + (size_t)wi * m->ngeom * 9, w->gxmat, sizeof(real) * m->ngeom * 9);
+  memcpy(d->site_xpos + (size_t)wi * m->nsite * 3, w->sxpos, sizeof(real) * m->nsite * 3);
+  memcpy(d->site_xmat + (size_t)wi * m->nsite * 9, w->sxmat, sizeof(real) * m->nsite * 9);
+  memcpy(d->subtree_com + (size_t)wi * nb * 3, w->subtree_com, sizeof(real) * nb * 3);
+  memcpy(d->cvel + (size_t)wi * nb * 6, w->cvel, sizeof(real) * nb * 6);
+  memcpy(d->cacc + (size_t)wi * nb * 6, w->cacc, sizeof(real) * nb * 6);
+  memcpy(d->actuator_force + (size_t)wi * nu, w->act_force, sizeof(real) * nu);
+  memcpy(d->actuator_length + (size_t)wi * nu, w->act_length, sizeof(real) * nu);
+  memcpy(d->actuator_velocity + (size_t)wi * nu, w->act_vel, sizeof(real) * nu);
+  memcpy(d->qfrc_bias + (size_t)wi * nv, w->qfrc_bias, sizeof(real) * nv);
+  memcpy(d->qfrc_passive + (size_t)wi * nv, w->qfrc_passive, sizeof(real) * nv);
+  memcpy(d->qfrc_actuator + (size_t)wi * nv, w->qfrc_actuator, sizeof(real) * nv);
+  memcpy(d->qfrc_smooth + (size_t)wi * nv, w->qfrc_smooth, sizeof(real) * nv);
+  memcpy(d->qfrc_constraint + (size_t)wi * nv, w->qfrc_constraint, sizeof(real) * nv);
+  memcpy(d->qacc_smooth + (size_t)wi * nv, w->qacc_smooth, sizeof(real) * nv);
+  memcpy(d->qacc + (size_t)wi * nv, w->qacc, sizeof(real) * nv);
+  d->ncon[wi] = w->ncon;
+  for (int ci = 0; ci < w->ncon; ci++) {
+    contact_t* c = w->con + ci;
+    size_t o = (size_t)wi * m->nconmax + ci;
+    d->contact_dist[o] = c->dist;
+    memcpy(d->contact_pos + 3 * o, c->pos, 3 * sizeof(real));
+    memcpy(d->contact_frame + 9 * o, c->frame, 9 * sizeof(real));
+    memcpy(d->contact_friction + 5 * o, c->friction, 5 * sizeof(real));
+    d->contact_includemargin[o] = c->includemargin;
+    d->contact_dim[o] = c->dim;
+    d->contact_geom[2 * o] = c->geom[0];
+    d->contact_geom[2 * o + 1] = c->geom[1];
+    d->contact_efc_address[o] = c->efc_address;
+  }
+  d->nefc[wi] = w->nefc;
+  for (int r = 0; r < w->nefc; r++) {
+    size_t o = (size_t)wi * m->njmax + r;
+    d->efc_type[o] = w->efc_type[r];
+    d->efc_id[o] = w->efc_id[r];
+    d->efc_pos[o] = w->efc_pos[r];
+    d->efc_D[o] = w->efc_D[r];
+    d->efc_aref[o] = w->efc_aref[r];
+    d->efc_force[o] = w->efc_force[r];
+  }
+  d->solver_niter[wi] = w->niter;
+
+  if (integrate) {
+    real dt = m->timestep;
+    const real* damping = WF(m, dof_damping, wi);
+    real* qa = w->qacc_int;
+    if (m->integrator == 3) {
+      /* implicitfast: (M - dt*qDeriv) qacc = qfrc_smooth + qfrc_constraint,
+         qDeriv = actuator velocity gains (skipped when force-clamped) - dof damping */
+      memcpy(w->H, w->M, sizeof(real) * nv * nv);
+      for (int dd = 0; dd < nv; dd++) w->H[dd * nv + dd] += dt * damping[dd];
+      for (int i = 0; i < nu; i++) {
+        if (m->actuator_forcelimited[i]) {
+          real f = w->act_force[i];
+          if (f <= m->actuator_forcerange[2 * i] || f >= m->actuator_forcerange[2 * i + 1]) continue;
+        }
+        int dof = m->jnt_dofadr[m->actuator_trnid[i]];
+        real g = m->actuator_gear[i];
+        w->H[dof * nv + dof] -= dt * g * g * m->actuator_biasprm[10 * i + 2];
+      }
+      factor_tree(m, w->H, w->LD);
+      for (int dd = 0; dd < nv; dd++) qa[dd] = w->qfrc_smooth[dd] + w->qfrc_constraint[dd];
+      solve_tree(m, w->LD, qa);
+    } else {
+      int anyd = 0;
+      for (int dd = 0; dd < nv; dd++) anyd |= damping[dd] > 0;
+      if (anyd) {
+        memcpy(w->H, w->M, sizeof(real) * nv * nv);
+        for (int dd = 0; dd < nv; dd++) w->H[dd * nv + dd] += dt * damping[dd];
+        factor_tree(m, w->H, w->LD);
+        mat_vec_n(w->M, w->qacc, qa, nv);
+        solve_tree(m, w->LD, qa);
+      } else {
+        memcpy(qa, w->qacc, sizeof(real) * nv);
+      }
+    }
+    real* qvel = d->qvel + (size_t)wi * nv;
+    real* qpos = d->qpos + (size_t)wi * nq;
+    for (int dd = 0; dd < nv; dd++) w->qvel[dd] += dt * qa[dd];
+    for (int j = 0; j < m->njnt; j++) {
+      int q0 = m->jnt_qposadr[j], v0 = m->jnt_dofadr[j];
+      if (m->jnt_type[j] == 0) {
+        for (int k = 0; k < 3; k++) w->qpos[q0 + k] += dt * w->qvel[v0 + k];
+        real* q = w->qpos + q0 + 3;
+        real om[3] = {w->qvel[v0 + 3], w->qvel[v0 + 4], w->qvel[v0 + 5]};
+        real ang = dt * normalize3(om), qr[4];
+        axis_angle(qr, om, ang);
+        normalize4(q);
+        mul_quat(q, q, qr);
+        normalize4(q);
+      } else {
+        w->qpos[q0] += dt * w->qvel[v0];
+      }
+    }
+    memcpy(qvel, w->qvel, sizeof(real) * nv);
+    memcpy(qpos, w->qpos, sizeof(real) * nq);
+    d->time[wi] += dt;
+  }
+  memcpy(d->qacc_warmstart + (size_t)wi * nv, w->qacc, sizeof(real) * nv);
+  for (int k = 0; k < nq; k++) if (!isfinite(d->qpos[(size_t)wi * nq + k])) w->flags |= 4;
+  for (int k = 0; k < nv; k++) if (!isfinite(d->qvel[(size_t)wi * nv + k]) || !isfinite(w->qacc[k])) w->flags |= 4;
+  d->flags[wi] = w->flags;
+}
+
+int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int nthreads) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+  {
+    ws_t w;
+    ws_alloc(&w, m);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+    for (int wi = w0; wi < w1; wi++) world_step(m, d, wi, integrate, &w);
+    ws_free(&w);
+  }
+  (void)nthreads;
+  return 0;
+}
+
+size_t oracle_sizeof_model(void) { return sizeof(or_model); }
+size_t oracle_sizeof_data(void) { return sizeof(or_data); }
+int oracle_real_bytes(void) { return (int)sizeof(real); }

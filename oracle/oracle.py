@@ -1,0 +1,92 @@
+"""ctypes driver for the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Loaded only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg. Builds the oracle's model/data structs from the same X-macro field list as
+the product ABI (mjlab_amd.sim.abi), with float64 (or float32) reals.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+REPO = ORACLE_DIR.parent
+sys.path.insert(0, str(REPO / "asimov-mjlab_amd"))
+
+from mjlab_amd.sim import abi  # noqa: E402
+
+# Data fields the caller provides (the step's inputs); the rest are outputs.
+INPUTS = ("qpos", "qvel", "act", "qacc_warmstart", "ctrl", "qfrc_applied", "xfrc_applied", "mocap_pos", "mocap_quat", "time")
+
+
+def build(force: bool = False) -> None:
+  libs = [ORACLE_DIR / "liboracle_f64.so", ORACLE_DIR / "liboracle_f32.so"]
+  if force or not all(p.exists() for p in libs):
+    subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
+
+
+class Oracle:
+  def __init__(self, model, precision: str = "f64", overrides: dict | None = None) -> None:
+    build()
+    self.model = model
+    self.real = ctypes.c_double if precision == "f64" else ctypes.c_float
+    self.dtype = np.float64 if precision == "f64" else np.float32
+    self.lib = ctypes.CDLL(str(ORACLE_DIR / f"liboracle_{precision}.so"))
+    self.lib.oracle_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    self.lib.oracle_sizeof_model.restype = ctypes.c_size_t
+    self.lib.oracle_sizeof_data.restype = ctypes.c_size_t
+    MS = abi.model_struct(self.real)
+    DS = abi.data_struct(self.real)
+    assert ctypes.sizeof(MS) == self.lib.oracle_sizeof_model(), "oracle model struct layout mismatch"
+    assert ctypes.sizeof(DS) == self.lib.oracle_sizeof_data(), "oracle data struct layout mismatch"
+    self.sizes = abi.model_sizes(model)
+    self._keep = []
+    ms = MS()
+    for k, v in self.sizes.items():
+      setattr(ms, k, v)
+    for k, v in abi.model_options(model).items():
+      setattr(ms, k, v)
+    arrays = abi.model_host_arrays(model)
+    overrides = overrides or {}
+    for f in abi.model_array_fields():
+      a = arrays[f.name]
+      stride = 0
+      if f.name in overrides:
+        a = np.asarray(overrides[f.name]).reshape(-1)
+        stride = abi.count(f, self.sizes)
+      if f.ctype == "float":
+        a = a.astype(self.dtype)
+      a = np.ascontiguousarray(a)
+      self._keep.append(a)
+      setattr(ms, f.name, a.ctypes.data)
+      if f.kind == "MW":
+        setattr(ms, f.name + "_wstride", stride)
+    self.ms = ms
+
+  def run(self, nworld: int, state: dict, integrate: bool = True, nthreads: int = 1) -> dict:
+    DS = abi.data_struct(self.real)
+    ds = DS()
+    ds.nworld = nworld
+    out = {}
+    for f in abi.data_array_fields():
+      n = max(1, abi.count(f, self.sizes))
+      dt = self.dtype if f.ctype == "float" else np.int32
+      if f.name in state:
+        a = np.ascontiguousarray(np.asarray(state[f.name], dtype=dt).reshape(nworld, -1)).copy()
+        if a.shape[1] != n and abi.count(f, self.sizes) != 0:
+          raise ValueError(f"{f.name}: got {a.shape[1]} per world, expected {n}")
+        if a.shape[1] == 0:
+          a = np.zeros((nworld, 1), dt)
+      else:
+        a = np.zeros((nworld, n), dt)
+      out[f.name] = a
+      setattr(ds, f.name, a.ctypes.data)
+    rc = self.lib.oracle_run(ctypes.addressof(self.ms), ctypes.addressof(ds), 0, nworld, int(integrate), nthreads)
+    if rc != 0:
+      raise RuntimeError(f"oracle_run failed: {rc}")
+    return out
