@@ -42,6 +42,7 @@ struct Layout {
   int act_force;
   int con_pos, con_frame, con_dist, con_fric, con_solref, con_solimp, con_imargin, con_dim, con_geom, con_efcadr;
   int J, ldj, efc_D, efc_R, efc_aref, efc_jaref, efc_jv, efc_force, efc_fl, efc_pos, efc_type, efc_id, efc_mask;
+  int efc_h, arow, ash, arow_prev;
   int red, ints;
   int total;
   int ncap, rcap;
@@ -51,7 +52,50 @@ enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
 
 thread_local std::string g_err;
 
-__device__ __forceinline__ const float* wf(const float* p, long long stride, int w) { return p + (long long)w * stride; }
+#ifdef MJH_PROFILE
+__device__ unsigned long long* g_prof;
+#define PROF(k)                                                           \
+  do {                                                                    \
+    wsync();                                                              \
+    if (tid == 0 && g_prof) g_prof[(long long)w * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define PROF_ACC(k, t0)                                                   \
+  do {                                                                    \
+    wsync();                                                              \
+    if (tid == 0 && g_prof) g_prof[(long long)w * 32 + (k)] += __builtin_amdgcn_s_memtime() - (t0); \
+  } while (0)
+#define PROF_NOW() __builtin_amdgcn_s_memtime()
+#else
+#define PROF(k) do {} while (0)
+#define PROF_ACC(k, t0) do {} while (0)
+#define PROF_NOW() 0ull
+#endif
+
+// Wave-level synchronisation: one world = one wave. DS instructions of a wave
+// execute in issue order, so lanes exchanging data through LDS only need the
+// compiler not to move LDS accesses across this point (memory clobber) and the
+// outstanding LDS ops drained; no s_barrier, so waves of a workgroup that run
+// different worlds never wait for each other.
+__device__ __forceinline__ void wsync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Word offsets of every model array inside the LDS model image, and of the
+// per-world copies of expanded (domain-randomised) fields (-1: shared).
+struct ImgOff {
+#define X_IO(type, name, count) int name;
+  MJH_MODEL_ARRAYS(X_IO)
+  MJH_MODEL_WARRAYS(X_IO)
+#undef X_IO
+#define X_IOW(type, name, count) int w_##name;
+  MJH_MODEL_WARRAYS(X_IOW)
+#undef X_IOW
+  int img_words;
+  int nfields;
+};
+
+#define IMG_I(name) (reinterpret_cast<const int*>(smem + Io.name))
+#define IMG_F(name) (reinterpret_cast<const float*>(smem + Io.name))
+#define IMG_L(name) (reinterpret_cast<const long long*>(smem + Io.name))
+#define WFIELD(name) (Io.w_##name >= 0 ? (const float*)(S + Io.w_##name) : (const float*)(smem + Io.name))
 
 // ---- block-level primitives -------------------------------------------------
 template <int NT>
@@ -61,9 +105,9 @@ __device__ __forceinline__ float bsum(float v, float* red) {
   if constexpr (NT == 64) {
     return v;
   } else {
-    __syncthreads();
+    wsync();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
+    wsync();
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NT / 64; i++) s += red[i];
@@ -79,12 +123,12 @@ __device__ __forceinline__ void bsum2(float& a, float& b, float* red) {
     b += __shfl_xor(b, o, 64);
   }
   if constexpr (NT != 64) {
-    __syncthreads();
+    wsync();
     if ((threadIdx.x & 63) == 0) {
       red[2 * (threadIdx.x >> 6)] = a;
       red[2 * (threadIdx.x >> 6) + 1] = b;
     }
-    __syncthreads();
+    wsync();
     a = 0.f;
     b = 0.f;
 #pragma unroll
@@ -109,9 +153,9 @@ __device__ __forceinline__ int bscan(int v, int* total, int* redi) {
     return x - v;
   } else {
     const int wv = threadIdx.x >> 6;
-    __syncthreads();
+    wsync();
     if (lane == 63) redi[wv] = x;
-    __syncthreads();
+    wsync();
     int off = 0, tot = 0;
 #pragma unroll
     for (int i = 0; i < NT / 64; i++) {
@@ -141,10 +185,10 @@ __device__ __forceinline__ void tri_rev(int q, int n, int& i, int& j) {
 // scaling of column k-1 is deferred into pass k (disjoint addresses).
 template <int NT>
 __device__ void ldl_factor(float* A, int n, int ld) {
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x & 63;
   float prev_inv = 0.f;
   for (int k = 0; k < n; k++) {
-    __syncthreads();
+    wsync();
     float piv = A[k * ld + k];
     if (piv < MJH_MINVAL) piv = MJH_MINVAL;
     const float inv = 1.f / piv;
@@ -160,36 +204,256 @@ __device__ void ldl_factor(float* A, int n, int ld) {
     if (tid == 0) A[k * ld + k] = piv;
     prev_inv = inv;
   }
-  __syncthreads();
+  wsync();
   (void)prev_inv;
+}
+
+// Left-looking (Crout) LDL^T for a single wave: lane i owns row i; column j is
+// a dot product over the finished columns, pivots D[k] stay in registers and
+// are broadcast with readlane. One wave barrier per column; all loads in the
+// inner loop are independent (pipelined), unlike the right-looking update.
+__device__ __forceinline__ float rdlane_f(float v, int k) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+template <int NT>
+__device__ void ldl_factor_fast(float* A, int n, int ld) {
+  if constexpr (NT != 64) {
+    ldl_factor<NT>(A, n, ld);
+  } else {
+    const int lane = threadIdx.x & 63;
+    float dreg = 0.f;
+    const float* ri = A + lane * ld;
+    for (int j = 0; j < n; j++) {
+      wsync();
+      float s = 0.f;
+      if (lane >= j && lane < n) {
+        const float* rj = A + j * ld;
+        float acc0 = 0.f, acc1 = 0.f;
+        int k = 0;
+        for (; k + 4 <= j; k += 4) {
+          const float4 a = *reinterpret_cast<const float4*>(ri + k);
+          const float4 b = *reinterpret_cast<const float4*>(rj + k);
+          acc0 += a.x * b.x * rdlane_f(dreg, k) + a.y * b.y * rdlane_f(dreg, k + 1);
+          acc1 += a.z * b.z * rdlane_f(dreg, k + 2) + a.w * b.w * rdlane_f(dreg, k + 3);
+        }
+        for (; k < j; k++) acc0 += ri[k] * rj[k] * rdlane_f(dreg, k);
+        s = ri[j] - (acc0 + acc1);
+      }
+      float dj = rdlane_f(s, j);
+      if (dj < MJH_MINVAL) dj = MJH_MINVAL;
+      if (lane == j) {
+        dreg = dj;
+        A[j * ld + j] = dj;
+      } else if (lane > j && lane < n) {
+        A[lane * ld + j] = s / dj;
+      }
+    }
+    wsync();
+  }
 }
 
 // Solve (L D L^T) x = x in place.
 template <int NT>
 __device__ void ldl_solve(const float* A, int n, int ld, float* x) {
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x & 63;
   for (int k = 0; k < n; k++) {
-    __syncthreads();
+    wsync();
     const float xk = x[k];
     for (int i = k + 1 + tid; i < n; i += NT) x[i] -= A[i * ld + k] * xk;
   }
-  __syncthreads();
+  wsync();
   for (int i = tid; i < n; i += NT) x[i] /= A[i * ld + i];
   for (int k = n - 1; k > 0; k--) {
-    __syncthreads();
+    wsync();
     const float xk = x[k];
     for (int i = tid; i < k; i += NT) x[i] -= A[k * ld + i] * xk;
   }
-  __syncthreads();
+  wsync();
 }
 
-// y = A x for a full symmetric n x n matrix stored in the lower triangle.
+// Single-wave solve (n <= 64): x lives in one register per lane, the pivots of
+// the forward/backward sweeps are broadcast with readlane (no LDS round trip,
+// no barriers). Same arithmetic order as ldl_solve.
+__device__ __forceinline__ float rdlane(float v, int k) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+template <int NT>
+__device__ void ldl_solve_fast(const float* A, int n, int ld, float* x) {
+  if constexpr (NT != 64) {
+    ldl_solve<NT>(A, n, ld, x);
+  } else {
+    const int lane = threadIdx.x & 63;
+    wsync();
+    float xi = lane < n ? x[lane] : 0.f;
+    const float* row = A + lane * ld;
+    for (int k = 0; k < n - 1; k++) {
+      const float xk = rdlane(xi, k);
+      const float a = (lane > k && lane < n) ? row[k] : 0.f;
+      xi -= a * xk;
+    }
+    if (lane < n) xi /= row[lane];
+    for (int k = n - 1; k > 0; k--) {
+      const float xk = rdlane(xi, k);
+      const float a = lane < k ? A[k * ld + lane] : 0.f;
+      xi -= a * xk;
+    }
+    if (lane < n) x[lane] = xi;
+    wsync();
+  }
+}
+
+// H (lower triangle of Hout) = M + sum_k ash[k]^2 J[arow[k]] J[arow[k]]^T over the
+// nact compacted active rows, on the f32 matrix cores (v_mfma_f32_16x16x4_f32:
+// exact fp32 FMA chains). Tiles of 16x16 on the lower block triangle.
+template <int NT>
+__device__ void hessian_mfma(const float* M, int ldm, const float* J, int ldj, const int* arow, const float* ash,
+                             int nact, int n, float* Hout) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int nb = (n + 15) >> 4;  // <= 4 (n <= 63)
+  const int ci = lane & 15, kq = lane >> 4;
+  v4f acc[10];
+#pragma unroll
+  for (int t = 0; t < 10; t++) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+  int kk = kq;
+  int r = kk < nact ? arow[kk] : 0;
+  float sc = kk < nact ? ash[kk] : 0.f;
+  for (int k0 = 0; k0 < nact; k0 += 4) {
+    // this k-step's 4 rows (one per lane quarter), all column blocks at once
+    float v[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int c = b * 16 + ci;
+      v[b] = (b < nb && c < n) ? J[r * ldj + c] * sc : 0.f;
+    }
+    // prefetch the next k-step's row id / scale
+    const int kn = k0 + 4 + kq;
+    r = kn < nact ? arow[kn] : 0;
+    sc = kn < nact ? ash[kn] : 0.f;
+    int t = 0;
+#pragma unroll
+    for (int I = 0; I < 4; I++)
+#pragma unroll
+      for (int Jb = 0; Jb <= I; Jb++, t++)
+        if (I < nb) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[I], v[Jb], acc[t], 0, 0, 0);
+  }
+  int t = 0;
+#pragma unroll
+  for (int I = 0; I < 4; I++)
+#pragma unroll
+    for (int Jb = 0; Jb <= I; Jb++, t++) {
+      if (I >= nb) continue;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int i = I * 16 + kq * 4 + q, j = Jb * 16 + ci;
+        if (i < n && j <= i) Hout[i * ldm + j] = M[i * ldm + j] + acc[t][q];
+      }
+    }
+}
+
+// dot of an aligned row with an aligned vector (float4 loads, 2 accumulators)
+__device__ __forceinline__ float rowdot(const float* r, const float* x, int n) {
+  float s0 = 0.f, s1 = 0.f;
+  int j = 0;
+  for (; j + 4 <= n; j += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(r + j);
+    const float4 b = *reinterpret_cast<const float4*>(x + j);
+    s0 += a.x * b.x + a.y * b.y;
+    s1 += a.z * b.z + a.w * b.w;
+  }
+  for (; j < n; j++) s0 += r[j] * x[j];
+  return s0 + s1;
+}
+
+// ---- register-resident LDL^T (lane i owns row i; NVP = padded size) ---------
+// Right-looking LDL^T fully unrolled over compile-time column indices: the
+// entries of other rows come from v_readlane, so the factorisation never
+// touches LDS between columns. Rows >= n are inert identity rows.
+template <int NVP>
+__device__ __forceinline__ void load_row_lower(const float* A, int n, int ld, float (&a)[NVP]) {
+  const int lane = threadIdx.x & 63;
+  const float* r = A + (lane < n ? lane : 0) * ld;
+#pragma unroll
+  for (int k = 0; k < NVP; k += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(r + k);
+    a[k] = v.x; a[k + 1] = v.y; a[k + 2] = v.z; a[k + 3] = v.w;
+  }
+  if (lane >= n) {
+#pragma unroll
+    for (int k = 0; k < NVP; k++) a[k] = (k == lane) ? 1.f : 0.f;
+  }
+}
+
+template <int NVP>
+__device__ void ldl_factor_reg(float* A, int n, int ld) {
+  // Branch-free: lane i updates its whole row each step; entries right of the
+  // diagonal are scratch never read back (only rdlane(a[k], j) with k < j, i.e.
+  // lower-triangle values, crosses lanes), and rows >= n are identity rows, so
+  // the padded steps k >= n are exact no-ops for rows < n.
+  const int lane = threadIdx.x & 63;
+  float a[NVP];
+  wsync();
+  load_row_lower<NVP>(A, n, ld, a);
+#pragma unroll
+  for (int k = 0; k < NVP; k++) {
+    float piv = rdlane_f(a[k], k);
+    piv = piv < MJH_MINVAL ? MJH_MINVAL : piv;
+    const float lik = a[k] * (1.f / piv);
+#pragma unroll
+    for (int j = k + 1; j < NVP; j++) a[j] -= lik * rdlane_f(a[k], j);
+    a[k] = lane > k ? lik : (lane == k ? piv : a[k]);
+  }
+  if (lane < n) {
+    float* r = A + lane * ld;
+#pragma unroll
+    for (int k = 0; k < NVP; k += 4) *reinterpret_cast<float4*>(r + k) = make_float4(a[k], a[k + 1], a[k + 2], a[k + 3]);
+  }
+  wsync();
+}
+
+// (L D L^T) x = b with the factor from ldl_factor_reg; x in LDS (in place).
+template <int NVP>
+__device__ void ldl_solve_reg(const float* A, int n, int ld, float* x) {
+  const int lane = threadIdx.x & 63;
+  float a[NVP], c[NVP];
+  wsync();
+  load_row_lower<NVP>(A, n, ld, a);  // L[i][k<i], D[i] at k == i
+  const int cl = lane < n ? lane : 0;
+#pragma unroll
+  for (int k = 0; k < NVP; k++) c[k] = A[(k < n ? k : 0) * ld + cl];  // column i: L[k][i] (used for k > i)
+  float xi = lane < n ? x[lane] : 0.f;
+  float di = 1.f;
+#pragma unroll
+  for (int k = 0; k < NVP; k++) {
+    const float xk = rdlane_f(xi, k);
+    xi -= (lane > k ? a[k] : 0.f) * xk;
+    di = lane == k ? a[k] : di;
+  }
+  xi = lane < n ? xi / di : 0.f;
+#pragma unroll
+  for (int k = NVP - 1; k > 0; k--) {
+    const float xk = rdlane_f(xi, k);
+    xi -= (lane < k && k < n ? c[k] : 0.f) * xk;
+  }
+  if (lane < n) x[lane] = xi;
+  wsync();
+}
+
+// y = A x for a symmetric matrix stored in full (16-byte aligned rows).
 template <int NT>
 __device__ void symv(const float* A, int n, int ld, const float* x, float* y) {
-  for (int i = threadIdx.x; i < n; i += NT) {
-    float s = 0.f;
-    for (int j = 0; j < n; j++) s += (j <= i ? A[i * ld + j] : A[j * ld + i]) * x[j];
-    y[i] = s;
+  for (int i = (threadIdx.x & 63); i < n; i += NT) {
+    const float* r = A + i * ld;
+    float s0 = 0.f, s1 = 0.f;
+    int j = 0;
+    for (; j + 4 <= n; j += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(r + j);
+      const float4 b = *reinterpret_cast<const float4*>(x + j);
+      s0 += a.x * b.x + a.y * b.y;
+      s1 += a.z * b.z + a.w * b.w;
+    }
+    for (; j < n; j++) s0 += r[j] * x[j];
+    y[i] = s0 + s1;
   }
 }
 
@@ -377,14 +641,39 @@ __device__ __forceinline__ float row_state(int type, float D, float R, float fl,
 }
 
 // ---- the step kernel --------------------------------------------------------
-template <int NT, bool STEP>
-__global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo) {
+template <int WPB, bool STEP, int NVP>
+__global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo,
+                                                         const ImgOff Io) {
+  constexpr int NT = 64;  // one wave per world
   extern __shared__ float smem[];
-  const int w = blockIdx.x;
+  // shared model image -> LDS (whole workgroup, 16-byte coalesced)
+  {
+    const float4* src = reinterpret_cast<const float4*>(m.image);
+    float4* dst = reinterpret_cast<float4*>(smem);
+    for (int i = threadIdx.x; i < (Io.img_words >> 2); i += 64 * WPB) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  const int w = blockIdx.x * WPB + wave;
   if (w >= d.nworld) return;
-  const int tid = threadIdx.x;
-  float* S = smem;
-  int* SI = reinterpret_cast<int*>(smem);
+  const int tid = threadIdx.x & 63;
+  float* S = smem + Io.img_words + wave * Lo.total;
+  int* SI = reinterpret_cast<int*>(S);
+  {  // this world's copies of expanded model fields
+#define X_SZ(name) const int name = m.name;
+    MJH_MODEL_SIZES(X_SZ)
+#undef X_SZ
+#define X_WCOPY(type, name, count)                                              \
+    if (Io.w_##name >= 0) {                                                     \
+      const float* src = m.name + (long long)w * m.name##_wstride;              \
+      float* dst = S + Io.w_##name;                                             \
+      for (int i = tid; i < (count); i += 64) dst[i] = src[i];                  \
+    }
+    MJH_MODEL_WARRAYS(X_WCOPY)
+#undef X_WCOPY
+    (void)nchain; (void)ncolgeom; (void)npair; (void)nsensor; (void)nmocap; (void)nconmax; (void)njmax; (void)na; (void)nsensordata; (void)nq; (void)nv; (void)nu; (void)nbody; (void)njnt; (void)ngeom; (void)nsite;
+  }
+  wsync();
   const int nq = m.nq, nv = m.nv, nb = m.nbody, nu = m.nu, nj = m.njnt;
   const int ldm = Lo.ldm, ldj = Lo.ldj;
 
@@ -447,48 +736,57 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
   int* efc_type = SI + Lo.efc_type;
   int* efc_id = SI + Lo.efc_id;
   unsigned long long* efc_mask = reinterpret_cast<unsigned long long*>(S + Lo.efc_mask);
+  float* efc_h = S + Lo.efc_h;
+  int* arow = SI + Lo.arow;
+  int* arow_prev = SI + Lo.arow_prev;
+  float* ash = S + Lo.ash;
   float* red = S + Lo.red;
   int* redi = SI + Lo.red + 2 * (NT / 64) + 2;
   int* ints = SI + Lo.ints;
 
   // per-world model fields (stride 0 = shared)
-  const float* body_pos = wf(m.body_pos, m.body_pos_wstride, w);
-  const float* body_quat = wf(m.body_quat, m.body_quat_wstride, w);
-  const float* body_ipos = wf(m.body_ipos, m.body_ipos_wstride, w);
-  const float* body_iquat = wf(m.body_iquat, m.body_iquat_wstride, w);
-  const float* body_mass = wf(m.body_mass, m.body_mass_wstride, w);
-  const float* body_inertia = wf(m.body_inertia, m.body_inertia_wstride, w);
-  const float* jnt_range = wf(m.jnt_range, m.jnt_range_wstride, w);
-  const float* jnt_stiffness = wf(m.jnt_stiffness, m.jnt_stiffness_wstride, w);
-  const float* dof_armature = wf(m.dof_armature, m.dof_armature_wstride, w);
-  const float* dof_damping = wf(m.dof_damping, m.dof_damping_wstride, w);
-  const float* dof_frictionloss = wf(m.dof_frictionloss, m.dof_frictionloss_wstride, w);
-  const float* geom_pos = wf(m.geom_pos, m.geom_pos_wstride, w);
-  const float* geom_quat = wf(m.geom_quat, m.geom_quat_wstride, w);
-  const float* geom_friction = wf(m.geom_friction, m.geom_friction_wstride, w);
-  const float* site_pos = wf(m.site_pos, m.site_pos_wstride, w);
-  const float* site_quat = wf(m.site_quat, m.site_quat_wstride, w);
-  const float* qpos0 = wf(m.qpos0, m.qpos0_wstride, w);
+  const float* body_pos = WFIELD(body_pos);
+  const float* body_quat = WFIELD(body_quat);
+  const float* body_ipos = WFIELD(body_ipos);
+  const float* body_iquat = WFIELD(body_iquat);
+  const float* body_mass = WFIELD(body_mass);
+  const float* body_inertia = WFIELD(body_inertia);
+  const float* jnt_range = WFIELD(jnt_range);
+  const float* jnt_stiffness = WFIELD(jnt_stiffness);
+  const float* dof_armature = WFIELD(dof_armature);
+  const float* dof_damping = WFIELD(dof_damping);
+  const float* dof_frictionloss = WFIELD(dof_frictionloss);
+  const float* geom_pos = WFIELD(geom_pos);
+  const float* geom_quat = WFIELD(geom_quat);
+  const float* geom_friction = WFIELD(geom_friction);
+  const float* site_pos = WFIELD(site_pos);
+  const float* site_quat = WFIELD(site_quat);
+  const float* qpos0 = WFIELD(qpos0);
 
   const long long W = w;
+  (void)SI;
 
   // ---------------------------------------------------------------- load state
   for (int i = tid; i < nq; i += NT) qpos[i] = d.qpos[W * nq + i];
   for (int i = tid; i < nv; i += NT) qvel[i] = d.qvel[W * nv + i];
   if (tid < I_COUNT) ints[tid] = (tid == I_MISC) ? 0x7fffffff : 0;
-  __syncthreads();
+  wsync();
+  PROF(0);
+#ifdef MJH_PROFILE
+  if (tid == 0 && g_prof) for (int k = 12; k < 20; k++) g_prof[(long long)w * 32 + k] = 0;
+#endif
 
   // ---------------------------------------------------------------- kinematics
   // Each lane walks its body's chain root->body (no per-level barriers). The
   // per-body normalisation matches a level-by-level sweep exactly.
   for (int b = tid; b < nb; b += NT) {
     float p[3] = {0.f, 0.f, 0.f}, q[4] = {1.f, 0.f, 0.f, 0.f};
-    const int ca = m.body_chainadr[b], cn = (b == 0) ? 0 : m.body_chainnum[b];
+    const int ca = IMG_I(body_chainadr)[b], cn = (b == 0) ? 0 : IMG_I(body_chainnum)[b];
     for (int c = 0; c < cn; c++) {
-      const int k = m.body_chain[ca + c];
-      const int ja = m.body_jntadr[k], jn = m.body_jntnum[k];
-      if (jn == 1 && m.jnt_type[ja] == 0) {
-        const int qa = m.jnt_qposadr[ja];
+      const int k = IMG_I(body_chain)[ca + c];
+      const int ja = IMG_I(body_jntadr)[k], jn = IMG_I(body_jntnum)[k];
+      if (jn == 1 && IMG_I(jnt_type)[ja] == 0) {
+        const int qa = IMG_I(jnt_qposadr)[ja];
         p[0] = qpos[qa]; p[1] = qpos[qa + 1]; p[2] = qpos[qa + 2];
         q[0] = qpos[qa + 3]; q[1] = qpos[qa + 4]; q[2] = qpos[qa + 5]; q[3] = qpos[qa + 6];
         quat_normalize(q);
@@ -508,19 +806,19 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       for (int j = ja; j < ja + jn; j++) {
         float Rq[9], ax[3], anc[3];
         quat2mat(Rq, q);
-        mat_vec(ax, Rq, m.jnt_axis + 3 * j);
-        mat_vec(anc, Rq, m.jnt_pos + 3 * j);
+        mat_vec(ax, Rq, IMG_F(jnt_axis) + 3 * j);
+        mat_vec(anc, Rq, IMG_F(jnt_pos) + 3 * j);
         anc[0] += p[0]; anc[1] += p[1]; anc[2] += p[2];
-        const int qa = m.jnt_qposadr[j];
-        if (m.jnt_type[j] == 2) {
+        const int qa = IMG_I(jnt_qposadr)[j];
+        if (IMG_I(jnt_type)[j] == 2) {
           const float dd = qpos[qa] - qpos0[qa];
           p[0] += ax[0] * dd; p[1] += ax[1] * dd; p[2] += ax[2] * dd;
-        } else if (m.jnt_type[j] == 3) {
+        } else if (IMG_I(jnt_type)[j] == 3) {
           float ql[4], v[3];
-          axis_angle(ql, m.jnt_axis + 3 * j, qpos[qa] - qpos0[qa]);
+          axis_angle(ql, IMG_F(jnt_axis) + 3 * j, qpos[qa] - qpos0[qa]);
           quat_mul(q, q, ql);
           quat2mat(Rq, q);
-          mat_vec(v, Rq, m.jnt_pos + 3 * j);
+          mat_vec(v, Rq, IMG_F(jnt_pos) + 3 * j);
           p[0] = anc[0] - v[0]; p[1] = anc[1] - v[1]; p[2] = anc[2] - v[2];
         }
         if (k == b) {
@@ -544,11 +842,11 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
 #pragma unroll
     for (int k = 0; k < 9; k++) ximat[9 * b + k] = IM[k];
   }
-  __syncthreads();
+  wsync();
 
   // geoms (all written out; collision geoms kept in LDS) and sites
   for (int g = tid; g < m.ngeom; g += NT) {
-    const int b = m.geom_bodyid[g];
+    const int b = IMG_I(geom_bodyid)[g];
     float t[3], GR[9], GM[9];
     mat_vec(t, xmat + 9 * b, geom_pos + 3 * g);
     float gp[3] = {xpos[3 * b] + t[0], xpos[3 * b + 1] + t[1], xpos[3 * b + 2] + t[2]};
@@ -559,7 +857,7 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
     float* om = d.geom_xmat + W * m.ngeom * 9 + 9 * g;
 #pragma unroll
     for (int k = 0; k < 9; k++) om[k] = GM[k];
-    const int slot = m.geom_colslot[g];
+    const int slot = IMG_I(geom_colslot)[g];
     if (slot >= 0) {
       cgpos[3 * slot] = gp[0]; cgpos[3 * slot + 1] = gp[1]; cgpos[3 * slot + 2] = gp[2];
 #pragma unroll
@@ -567,7 +865,7 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
     }
   }
   for (int s = tid; s < m.nsite; s += NT) {
-    const int b = m.site_bodyid[s];
+    const int b = IMG_I(site_bodyid)[s];
     float t[3], SR[9], SM[9];
     mat_vec(t, xmat + 9 * b, site_pos + 3 * s);
     quat2mat(SR, site_quat + 4 * s);
@@ -578,11 +876,12 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
   }
 
   // ---------------------------------------------------------------- com_pos
+  PROF(1);
   // subtree com: lane b sums the bodies whose chain contains b
   for (int b = tid; b < nb; b += NT) {
     float ms = 0.f, mp[3] = {0.f, 0.f, 0.f};
     for (int k = 0; k < nb; k++) {
-      const bool in = (b == 0) || ((unsigned long long)m.body_treemask[k] >> b) & 1ull;
+      const bool in = (b == 0) || ((unsigned long long)IMG_L(body_treemask)[k] >> b) & 1ull;
       if (!in) continue;
       const float mk = body_mass[k];
       ms += mk;
@@ -595,11 +894,11 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       subtree_com[3 * b] = mp[0] * inv; subtree_com[3 * b + 1] = mp[1] * inv; subtree_com[3 * b + 2] = mp[2] * inv;
     }
   }
-  __syncthreads();
+  wsync();
   for (int b = tid; b < nb; b += NT) {
     float* ci = cinert + 10 * b;
     const float* R = ximat + 9 * b;
-    const float* c = subtree_com + 3 * m.body_rootid[b];
+    const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
     const float dd0 = xipos[3 * b] - c[0], dd1 = xipos[3 * b + 1] - c[1], dd2 = xipos[3 * b + 2] - c[2];
     const float* in = body_inertia + 3 * b;
     float I[6];  // xx yy zz xy xz yz of R diag(in) R^T
@@ -619,10 +918,10 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
     ci[6] = mm * dd0; ci[7] = mm * dd1; ci[8] = mm * dd2; ci[9] = mm;
   }
   for (int j = tid; j < nj; j += NT) {
-    const int b = m.jnt_bodyid[j], da = m.jnt_dofadr[j];
-    const float* c = subtree_com + 3 * m.body_rootid[b];
+    const int b = IMG_I(jnt_bodyid)[j], da = IMG_I(jnt_dofadr)[j];
+    const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
     float off[3] = {c[0] - xanchor[3 * j], c[1] - xanchor[3 * j + 1], c[2] - xanchor[3 * j + 2]};
-    const int t = m.jnt_type[j];
+    const int t = IMG_I(jnt_type)[j];
     if (t == 0) {
       for (int k = 0; k < 3; k++) {
         float* cd = cdof + 6 * (da + k);
@@ -643,14 +942,14 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       cross3(cd + 3, xaxis + 3 * j, off);
     }
   }
-  __syncthreads();
+  wsync();
 
   // ---------------------------------------------------------------- crb + M
   for (int b = tid; b < nb; b += NT) {
     float acc[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (b > 0)
       for (int k = b; k < nb; k++) {
-        if (!(((unsigned long long)m.body_treemask[k] >> b) & 1ull)) continue;
+        if (!(((unsigned long long)IMG_L(body_treemask)[k] >> b) & 1ull)) continue;
 #pragma unroll
         for (int c = 0; c < 10; c++) acc[c] += cinert[10 * k + c];
       }
@@ -658,11 +957,11 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
     for (int c = 0; c < 10; c++) crb[10 * b + c] = acc[c];
   }
   for (int i = tid; i < nv * ldm; i += NT) Mm[i] = 0.f;
-  __syncthreads();
+  wsync();
   for (int i = tid; i < nv; i += NT) {
     float buf[6];
-    inert_vec(buf, crb + 10 * m.dof_bodyid[i], cdof + 6 * i);
-    unsigned long long mask = (unsigned long long)m.body_dofmask[m.dof_bodyid[i]];
+    inert_vec(buf, crb + 10 * IMG_I(dof_bodyid)[i], cdof + 6 * i);
+    unsigned long long mask = (unsigned long long)IMG_L(body_dofmask)[IMG_I(dof_bodyid)[i]];
     mask &= (i == 63) ? ~0ull : ((2ull << i) - 1ull);
     while (mask) {
       const int j = __builtin_ctzll(mask);
@@ -671,16 +970,19 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       float s = cj[0] * buf[0] + cj[1] * buf[1] + cj[2] * buf[2] + cj[3] * buf[3] + cj[4] * buf[4] + cj[5] * buf[5];
       if (j == i) s += dof_armature[i];
       Mm[i * ldm + j] = s;
+      Mm[j * ldm + i] = s;  // full symmetric storage: contiguous row reads in M*v
     }
   }
-  __syncthreads();
+  wsync();
+  PROF(10);
   for (int i = tid; i < nv * ldm; i += NT) Lm[i] = Mm[i];
-  ldl_factor<NT>(Lm, nv, ldm);
+  ldl_factor_reg<NVP>(Lm, nv, ldm);
+  PROF(2);
 
   // ---------------------------------------------------------------- com_vel / rne (bias)
   for (int b = tid; b < nb; b += NT) {
     float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    unsigned long long mask = (unsigned long long)m.body_dofmask[b];
+    unsigned long long mask = (unsigned long long)IMG_L(body_dofmask)[b];
     while (mask) {
       const int j = __builtin_ctzll(mask);
       mask &= mask - 1;
@@ -691,33 +993,33 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
 #pragma unroll
     for (int c = 0; c < 6; c++) cvel[6 * b + c] = v[c];
   }
-  __syncthreads();
+  wsync();
   for (int i = tid; i < nv; i += NT) {
-    const int b = m.dof_bodyid[i], jnt = m.dof_jntid[i], da = m.jnt_dofadr[jnt];
-    const bool freej = m.jnt_type[jnt] == 0;
+    const int b = IMG_I(dof_bodyid)[i], jnt = IMG_I(dof_jntid)[i], da = IMG_I(jnt_dofadr)[jnt];
+    const bool freej = IMG_I(jnt_type)[jnt] == 0;
     if (freej && i - da < 3) {
       for (int c = 0; c < 6; c++) cdof_dot[6 * i + c] = 0.f;
       continue;
     }
     float v[6];
-    const int p = m.body_parentid[b];
+    const int p = IMG_I(body_parentid)[b];
 #pragma unroll
     for (int c = 0; c < 6; c++) v[c] = cvel[6 * p + c];
     // earlier dofs of this body: other joints fully, own free joint translations only
-    for (int k = m.body_dofadr[b]; k < i; k++) {
-      const int jk = m.dof_jntid[k];
+    for (int k = IMG_I(body_dofadr)[b]; k < i; k++) {
+      const int jk = IMG_I(dof_jntid)[k];
       if (jk == jnt && !(freej && k - da < 3)) continue;
 #pragma unroll
       for (int c = 0; c < 6; c++) v[c] += cdof[6 * k + c] * qvel[k];
     }
     cross_motion(cdof_dot + 6 * i, v, cdof + 6 * i);
   }
-  __syncthreads();
+  wsync();
   {
     const float g0 = -m.gravity_x, g1 = -m.gravity_y, g2 = -m.gravity_z;
     for (int b = tid; b < nb; b += NT) {
       float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
-      unsigned long long mask = (unsigned long long)m.body_dofmask[b];
+      unsigned long long mask = (unsigned long long)IMG_L(body_dofmask)[b];
       while (mask) {
         const int j = __builtin_ctzll(mask);
         mask &= mask - 1;
@@ -733,56 +1035,56 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       for (int c = 0; c < 6; c++) cfrc[6 * b + c] = (b == 0) ? 0.f : f1[c] + f3[c];
     }
   }
-  __syncthreads();
+  wsync();
   // subtree sums of cfrc into crb (crb no longer needed)
   for (int b = tid; b < nb; b += NT) {
     float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (b > 0)
       for (int k = b; k < nb; k++) {
-        if (!(((unsigned long long)m.body_treemask[k] >> b) & 1ull)) continue;
+        if (!(((unsigned long long)IMG_L(body_treemask)[k] >> b) & 1ull)) continue;
 #pragma unroll
         for (int c = 0; c < 6; c++) acc[c] += cfrc[6 * k + c];
       }
 #pragma unroll
     for (int c = 0; c < 6; c++) crb[6 * b + c] = acc[c];
   }
-  __syncthreads();
+  wsync();
 
   // ---------------------------------------------------------------- passive, actuation, smooth force
   for (int i = tid; i < nv; i += NT) {
     const float* cd = cdof + 6 * i;
-    const float* f = crb + 6 * m.dof_bodyid[i];
+    const float* f = crb + 6 * IMG_I(dof_bodyid)[i];
     qfrc_bias[i] = cd[0] * f[0] + cd[1] * f[1] + cd[2] * f[2] + cd[3] * f[3] + cd[4] * f[4] + cd[5] * f[5];
     float pas = -dof_damping[i] * qvel[i];
-    const int jnt = m.dof_jntid[i];
-    const int t = m.jnt_type[jnt];
+    const int jnt = IMG_I(dof_jntid)[i];
+    const int t = IMG_I(jnt_type)[jnt];
     if ((t == 2 || t == 3) && jnt_stiffness[jnt] != 0.f) {
-      const int qa = m.jnt_qposadr[jnt];
-      pas -= jnt_stiffness[jnt] * (qpos[qa] - m.qpos_spring[qa]);
+      const int qa = IMG_I(jnt_qposadr)[jnt];
+      pas -= jnt_stiffness[jnt] * (qpos[qa] - IMG_F(qpos_spring)[qa]);
     }
     qfrc_passive[i] = pas;
     qfrc_act[i] = 0.f;
   }
-  __syncthreads();
+  wsync();
   for (int i = tid; i < nu; i += NT) {
-    const int j = m.actuator_trnid[i];
-    const float gear = m.actuator_gear[i];
-    const float len = gear * qpos[m.jnt_qposadr[j]];
-    const float vel = gear * qvel[m.jnt_dofadr[j]];
+    const int j = IMG_I(actuator_trnid)[i];
+    const float gear = IMG_F(actuator_gear)[i];
+    const float len = gear * qpos[IMG_I(jnt_qposadr)[j]];
+    const float vel = gear * qvel[IMG_I(jnt_dofadr)[j]];
     float c = d.ctrl[W * nu + i];
-    if (m.actuator_ctrllimited[i]) c = clampf(c, m.actuator_ctrlrange[2 * i], m.actuator_ctrlrange[2 * i + 1]);
-    const float* gp = m.actuator_gainprm + 10 * i;
-    const float* bp = m.actuator_biasprm + 10 * i;
+    if (IMG_I(actuator_ctrllimited)[i]) c = clampf(c, IMG_F(actuator_ctrlrange)[2 * i], IMG_F(actuator_ctrlrange)[2 * i + 1]);
+    const float* gp = IMG_F(actuator_gainprm) + 10 * i;
+    const float* bp = IMG_F(actuator_biasprm) + 10 * i;
     float f = gp[0] * c + bp[0] + bp[1] * len + bp[2] * vel;
-    if (m.actuator_forcelimited[i]) f = clampf(f, m.actuator_forcerange[2 * i], m.actuator_forcerange[2 * i + 1]);
+    if (IMG_I(actuator_forcelimited)[i]) f = clampf(f, IMG_F(actuator_forcerange)[2 * i], IMG_F(actuator_forcerange)[2 * i + 1]);
     act_force[i] = f;
     d.actuator_force[W * nu + i] = f;
     d.actuator_length[W * nu + i] = len;
     d.actuator_velocity[W * nu + i] = vel;
     // one actuator per dof in mjlab models; atomic keeps it correct otherwise
-    atomicAdd(&qfrc_act[m.jnt_dofadr[j]], gear * f);
+    atomicAdd(&qfrc_act[IMG_I(jnt_dofadr)[j]], gear * f);
   }
-  __syncthreads();
+  wsync();
   {
     const float* xfrc = d.xfrc_applied + W * nb * 6;
     for (int i = tid; i < nv; i += NT) {
@@ -790,10 +1092,10 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       // J^T xfrc_applied at each body com
       const float* cd = cdof + 6 * i;
       for (int b = 1; b < nb; b++) {
-        if (!(((unsigned long long)m.body_dofmask[b] >> i) & 1ull)) continue;
+        if (!(((unsigned long long)IMG_L(body_dofmask)[b] >> i) & 1ull)) continue;
         const float* f = xfrc + 6 * b;
         if (f[0] == 0.f && f[1] == 0.f && f[2] == 0.f && f[3] == 0.f && f[4] == 0.f && f[5] == 0.f) continue;
-        const float* c = subtree_com + 3 * m.body_rootid[b];
+        const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
         float off[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
         cross3(t, cd, off);
         s += (cd[3] + t[0]) * f[0] + (cd[4] + t[1]) * f[1] + (cd[5] + t[2]) * f[2] + cd[0] * f[3] + cd[1] * f[4] + cd[2] * f[5];
@@ -802,7 +1104,8 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       qacc_smooth[i] = s;
     }
   }
-  ldl_solve<NT>(Lm, nv, ldm, qacc_smooth);
+  ldl_solve_reg<NVP>(Lm, nv, ldm, qacc_smooth);
+  PROF(3);
 
   // ---------------------------------------------------------------- collision
   {
@@ -812,24 +1115,24 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       Con cc[4];
       int n = 0, g1 = 0, g2 = 0;
       if (p < npair) {
-        g1 = m.pair_geom1[p];
-        g2 = m.pair_geom2[p];
-        const int s1 = m.geom_colslot[g1], s2 = m.geom_colslot[g2];
+        g1 = IMG_I(pair_geom1)[p];
+        g2 = IMG_I(pair_geom2)[p];
+        const int s1 = IMG_I(geom_colslot)[g1], s2 = IMG_I(geom_colslot)[g2];
         const float* p1 = cgpos + 3 * s1;
         const float* p2 = cgpos + 3 * s2;
         const float* m1 = cgmat + 9 * s1;
         const float* m2 = cgmat + 9 * s2;
-        const float margin = fmaxf(m.geom_margin[g1], m.geom_margin[g2]);
-        const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+        const float margin = fmaxf(IMG_F(geom_margin)[g1], IMG_F(geom_margin)[g2]);
+        const int t1 = IMG_I(geom_type)[g1], t2 = IMG_I(geom_type)[g2];
         float dif[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
         bool near;
         if (t1 == 0) {
           float nrm[3] = {m1[2], m1[5], m1[8]};
-          near = dot3(dif, nrm) <= margin + m.geom_rbound[g2];
+          near = dot3(dif, nrm) <= margin + IMG_F(geom_rbound)[g2];
         } else {
-          near = sqrtf(dot3(dif, dif)) <= margin + m.geom_rbound[g1] + m.geom_rbound[g2];
+          near = sqrtf(dot3(dif, dif)) <= margin + IMG_F(geom_rbound)[g1] + IMG_F(geom_rbound)[g2];
         }
-        if (near) n = narrowphase(t1, t2, p1, m1, m.geom_size + 3 * g1, p2, m2, m.geom_size + 3 * g2, margin, cc);
+        if (near) n = narrowphase(t1, t2, p1, m1, IMG_F(geom_size) + 3 * g1, p2, m2, IMG_F(geom_size) + 3 * g2, margin, cc);
       }
       int total;
       const int off = bscan<NT>(n, &total, redi);
@@ -838,30 +1141,30 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
         // contact parameters (mj_contactParam semantics)
         int condim;
         float fri[3], solref[2], solimp[5];
-        const int pr1 = m.geom_priority[g1], pr2 = m.geom_priority[g2];
+        const int pr1 = IMG_I(geom_priority)[g1], pr2 = IMG_I(geom_priority)[g2];
         if (pr1 != pr2) {
           const int g = pr1 > pr2 ? g1 : g2;
-          condim = m.geom_condim[g];
+          condim = IMG_I(geom_condim)[g];
           for (int k = 0; k < 3; k++) fri[k] = geom_friction[3 * g + k];
-          for (int k = 0; k < 2; k++) solref[k] = m.geom_solref[2 * g + k];
-          for (int k = 0; k < 5; k++) solimp[k] = m.geom_solimp[5 * g + k];
+          for (int k = 0; k < 2; k++) solref[k] = IMG_F(geom_solref)[2 * g + k];
+          for (int k = 0; k < 5; k++) solimp[k] = IMG_F(geom_solimp)[5 * g + k];
         } else {
-          condim = max(m.geom_condim[g1], m.geom_condim[g2]);
+          condim = max(IMG_I(geom_condim)[g1], IMG_I(geom_condim)[g2]);
           for (int k = 0; k < 3; k++) fri[k] = fmaxf(geom_friction[3 * g1 + k], geom_friction[3 * g2 + k]);
-          const float sm1 = m.geom_solmix[g1], sm2 = m.geom_solmix[g2];
+          const float sm1 = IMG_F(geom_solmix)[g1], sm2 = IMG_F(geom_solmix)[g2];
           float mix;
           if (sm1 >= MJH_MINVAL && sm2 >= MJH_MINVAL) mix = sm1 / (sm1 + sm2);
           else if (sm1 < MJH_MINVAL && sm2 < MJH_MINVAL) mix = 0.5f;
           else mix = sm1 < MJH_MINVAL ? 0.f : 1.f;
-          const float* r1 = m.geom_solref + 2 * g1;
-          const float* r2 = m.geom_solref + 2 * g2;
+          const float* r1 = IMG_F(geom_solref) + 2 * g1;
+          const float* r2 = IMG_F(geom_solref) + 2 * g2;
           if (r1[0] > 0.f && r2[0] > 0.f)
             for (int k = 0; k < 2; k++) solref[k] = mix * r1[k] + (1.f - mix) * r2[k];
           else
             for (int k = 0; k < 2; k++) solref[k] = fminf(r1[k], r2[k]);
-          for (int k = 0; k < 5; k++) solimp[k] = mix * m.geom_solimp[5 * g1 + k] + (1.f - mix) * m.geom_solimp[5 * g2 + k];
+          for (int k = 0; k < 5; k++) solimp[k] = mix * IMG_F(geom_solimp)[5 * g1 + k] + (1.f - mix) * IMG_F(geom_solimp)[5 * g2 + k];
         }
-        const float imargin = fmaxf(m.geom_margin[g1], m.geom_margin[g2]) - fmaxf(m.geom_gap[g1], m.geom_gap[g2]);
+        const float imargin = fmaxf(IMG_F(geom_margin)[g1], IMG_F(geom_margin)[g2]) - fmaxf(IMG_F(geom_gap)[g1], IMG_F(geom_gap)[g2]);
         for (int e = 0; e < n; e++) {
           const int ci = base_con + off + e;
           if (ci >= Lo.ncap) {
@@ -884,12 +1187,13 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
           con_efcadr[ci] = -1;
         }
       }
-      __syncthreads();
+      wsync();
       if (tid == 0) ints[I_NCON] = min(base_con + total, Lo.ncap);
-      __syncthreads();
+      wsync();
     }
   }
   const int ncon = ints[I_NCON];
+  PROF(4);
 
   // ---------------------------------------------------------------- make_constraint
   {
@@ -909,7 +1213,7 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
           efc_fl[r] = dof_frictionloss[i];
           efc_mask[r] = 1ull << i;
           efc_pos[r] = 0.f;
-          row_params(m.timestep, 0.f, 0.f, m.dof_invweight0[i], m.dof_solref + 2 * i, m.dof_solimp + 5 * i, qvel[i],
+          row_params(m.timestep, 0.f, 0.f, IMG_F(dof_invweight0)[i], IMG_F(dof_solref) + 2 * i, IMG_F(dof_solimp) + 5 * i, qvel[i],
                      efc_D + r, efc_R + r, efc_aref + r);
         }
       }
@@ -920,10 +1224,10 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       const int j = base + tid;
       int f = 0;
       float pos = 0.f, sgn = 0.f;
-      if (j < nj && m.jnt_limited[j] && (m.jnt_type[j] == 2 || m.jnt_type[j] == 3)) {
-        const float q = qpos[m.jnt_qposadr[j]];
+      if (j < nj && IMG_I(jnt_limited)[j] && (IMG_I(jnt_type)[j] == 2 || IMG_I(jnt_type)[j] == 3)) {
+        const float q = qpos[IMG_I(jnt_qposadr)[j]];
         const float dlo = q - jnt_range[2 * j], dhi = jnt_range[2 * j + 1] - q;
-        pos = fminf(dlo, dhi) - m.jnt_margin[j];
+        pos = fminf(dlo, dhi) - IMG_F(jnt_margin)[j];
         sgn = dlo < dhi ? 1.f : -1.f;
         f = pos < 0.f ? 1 : 0;
       }
@@ -932,14 +1236,14 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       if (f) {
         const int r = nefc + off;
         if (r < rcap) {
-          const int dof = m.jnt_dofadr[j];
+          const int dof = IMG_I(jnt_dofadr)[j];
           efc_type[r] = MJH_CNSTR_LIMIT_JOINT;
           efc_id[r] = j;
           efc_fl[r] = 0.f;
           efc_mask[r] = 1ull << dof;
-          efc_pos[r] = pos + m.jnt_margin[j];
+          efc_pos[r] = pos + IMG_F(jnt_margin)[j];
           jv[r] = sgn;  // temporarily hold the Jacobian sign
-          row_params(m.timestep, pos, pos, m.dof_invweight0[dof], m.jnt_solref + 2 * j, m.jnt_solimp + 5 * j,
+          row_params(m.timestep, pos, pos, IMG_F(dof_invweight0)[dof], IMG_F(jnt_solref) + 2 * j, IMG_F(jnt_solimp) + 5 * j,
                      sgn * qvel[dof], efc_D + r, efc_R + r, efc_aref + r);
         }
       }
@@ -964,28 +1268,28 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       }
       nefc += total;
     }
-    __syncthreads();
+    wsync();
     if (nefc > rcap) {
       if (tid == 0) ints[I_FLAGS] |= MJH_FLAG_EFC_OVERFLOW;
       nefc = max(nsimple, min(rcap, ints[I_MISC]));
     }
-    __syncthreads();
+    wsync();
     // zero J rows, write the single-dof rows
     for (int i = tid; i < nefc * ldj; i += NT) J[i] = 0.f;
-    __syncthreads();
+    wsync();
     for (int r = tid; r < nsimple; r += NT) {
       const int t = efc_type[r];
       if (t == MJH_CNSTR_FRICTION_DOF) J[r * ldj + efc_id[r]] = 1.f;
-      else J[r * ldj + m.jnt_dofadr[efc_id[r]]] = jv[r];
+      else J[r * ldj + IMG_I(jnt_dofadr)[efc_id[r]]] = jv[r];
     }
     // contact Jacobian rows: flat over (contact, dof)
     for (int item = tid; item < ncon * nv; item += NT) {
       const int ci = item / nv, dof = item - ci * nv;
       const int r0 = con_efcadr[ci];
       if (r0 < 0) continue;
-      const int b1 = m.geom_bodyid[con_geom[2 * ci]], b2 = m.geom_bodyid[con_geom[2 * ci + 1]];
-      const bool in1 = ((unsigned long long)m.body_dofmask[b1] >> dof) & 1ull;
-      const bool in2 = ((unsigned long long)m.body_dofmask[b2] >> dof) & 1ull;
+      const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
+      const bool in1 = ((unsigned long long)IMG_L(body_dofmask)[b1] >> dof) & 1ull;
+      const bool in2 = ((unsigned long long)IMG_L(body_dofmask)[b2] >> dof) & 1ull;
       const int dim = con_dim[ci];
       const int nr = dim == 1 ? 1 : 2 * (dim - 1);
       if (in1 == in2) {  // not in either chain, or in both (relative motion cancels)
@@ -994,7 +1298,7 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       const float sg = in2 ? 1.f : -1.f;
       const int bb = in2 ? b2 : b1;
       const float* cd = cdof + 6 * dof;
-      const float* c = subtree_com + 3 * m.body_rootid[bb];
+      const float* c = subtree_com + 3 * IMG_I(body_rootid)[bb];
       const float* cp = con_pos + 3 * ci;
       float off[3] = {cp[0] - c[0], cp[1] - c[1], cp[2] - c[2]}, t[3];
       cross3(t, cd, off);
@@ -1018,11 +1322,11 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
     for (int ci = tid; ci < ncon; ci += NT) {
       const int r0 = con_efcadr[ci];
       if (r0 < 0) continue;
-      const int b1 = m.geom_bodyid[con_geom[2 * ci]], b2 = m.geom_bodyid[con_geom[2 * ci + 1]];
+      const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
       const int dim = con_dim[ci];
       const int nr = dim == 1 ? 1 : 2 * (dim - 1);
       const unsigned long long msk =
-          (unsigned long long)m.body_dofmask[b1] ^ (unsigned long long)m.body_dofmask[b2];
+          (unsigned long long)IMG_L(body_dofmask)[b1] ^ (unsigned long long)IMG_L(body_dofmask)[b2];
       for (int e = 0; e < nr; e++) {
         const int r = r0 + e;
         efc_type[r] = dim == 1 ? MJH_CNSTR_CONTACT_FRICTIONLESS : MJH_CNSTR_CONTACT_PYRAMIDAL;
@@ -1032,27 +1336,28 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
         efc_pos[r] = con_dist[ci];
       }
     }
-    __syncthreads();
+    wsync();
     for (int r = tid; r < nefc; r += NT) {
       if (efc_type[r] != MJH_CNSTR_CONTACT_FRICTIONLESS && efc_type[r] != MJH_CNSTR_CONTACT_PYRAMIDAL) continue;
       const int ci = efc_id[r];
-      const int b1 = m.geom_bodyid[con_geom[2 * ci]], b2 = m.geom_bodyid[con_geom[2 * ci + 1]];
-      float invw = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+      const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
+      float invw = IMG_F(body_invweight0)[2 * b1] + IMG_F(body_invweight0)[2 * b2];
       if (con_dim[ci] > 1) {
         const float f0 = con_fric[5 * ci];
         invw = invw + f0 * f0 * invw;
         invw = invw * 2.f * f0 * f0 / m.impratio;
       }
       float jq = 0.f;
-      for (int k = 0; k < nv; k++) jq += J[r * ldj + k] * qvel[k];
+      jq = rowdot(J + r * ldj, qvel, nv);
       const float pos = con_dist[ci] - con_imargin[ci];
       row_params(m.timestep, pos, pos, invw, con_solref + 2 * ci, con_solimp + 5 * ci, jq, efc_D + r, efc_R + r,
                  efc_aref + r);
     }
     if (tid == 0) ints[I_NEFC] = nefc;
-    __syncthreads();
+    wsync();
   }
   const int nefc = ints[I_NEFC];
+  PROF(5);
 
   // ---------------------------------------------------------------- Newton solver
   const float scale = 1.f / (m.meaninertia * (float)(nv > 1 ? nv : 1));
@@ -1062,72 +1367,91 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       qacc[i] = qacc_smooth[i];
       qfrc_con[i] = 0.f;
     }
-    __syncthreads();
+    wsync();
   } else {
     // jaref = J x - aref ; Ma = M x ; forces, qfrc_constraint, cost
     auto eval_point = [&](const float* x) {
       symv<NT>(Mm, nv, ldm, x, Ma);
       for (int r = tid; r < nefc; r += NT) {
-        float s = 0.f;
-        for (int k = 0; k < nv; k++) s += J[r * ldj + k] * x[k];
-        jaref[r] = s - efc_aref[r];
+        jaref[r] = rowdot(J + r * ldj, x, nv) - efc_aref[r];
       }
-      __syncthreads();
+      wsync();
     };
     auto update_constraint = [&]() -> float {
       float c = 0.f;
       for (int r = tid; r < nefc; r += NT) {
         float f, cr;
-        row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], jaref[r], &f, &cr);
+        efc_h[r] = row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], jaref[r], &f, &cr);
         efc_force[r] = f;
         c += cr;
       }
       for (int i = tid; i < nv; i += NT) c += 0.5f * (Ma[i] - qfrc_smooth[i]) * (qacc[i] - qacc_smooth[i]);
-      __syncthreads();
+      wsync();
       for (int i = tid; i < nv; i += NT) {
-        float s = 0.f;
-        for (int r = 0; r < nefc; r++) {
-          const float f = efc_force[r];
-          if (f != 0.f && ((efc_mask[r] >> i) & 1ull)) s += J[r * ldj + i] * f;
+        // J^T f: entries outside a row's dof mask are exact zeros, so no test
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int r = 0;
+        for (; r + 4 <= nefc; r += 4) {
+          s0 += J[r * ldj + i] * efc_force[r];
+          s1 += J[(r + 1) * ldj + i] * efc_force[r + 1];
+          s2 += J[(r + 2) * ldj + i] * efc_force[r + 2];
+          s3 += J[(r + 3) * ldj + i] * efc_force[r + 3];
         }
-        qfrc_con[i] = s;
+        for (; r < nefc; r++) s0 += J[r * ldj + i] * efc_force[r];
+        qfrc_con[i] = (s0 + s1) + (s2 + s3);
       }
       return bsum<NT>(c, red);
     };
+    int nact_prev = -1, nfactor = 0;
     auto newton_direction = [&]() {
       for (int i = tid; i < nv; i += NT) grad[i] = Ma[i] - qfrc_smooth[i] - qfrc_con[i];
-      // H = M + J' diag(h) J  (lower triangle), stored in Lm
-      const int ntri = nv * (nv + 1) / 2;
-      for (int q = tid; q < ntri; q += NT) {
-        int i, j;
-        tri_rev(q, nv, i, j);
-        float s = Mm[i * ldm + j];
-        for (int r = 0; r < nefc; r++) {
-          const unsigned long long mk = efc_mask[r];
-          if (!((mk >> i) & 1ull) || !((mk >> j) & 1ull)) continue;
-          float f, cr;
-          const float h = row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], jaref[r], &f, &cr);
-          if (h == 0.f) continue;
-          s += h * J[r * ldj + i] * J[r * ldj + j];
+      // compact the rows in the quadratic zone: H = M + sum h_r J_r J_r^T
+      int nact = 0;
+      for (int base = 0; base < nefc; base += NT) {
+        const int r = base + tid;
+        const float h = r < nefc ? efc_h[r] : 0.f;
+        const int a = h > 0.f ? 1 : 0;
+        int total;
+        const int off = bscan<NT>(a, &total, redi);
+        if (a) {
+          arow[nact + off] = r;
+          ash[nact + off] = sqrtf(h);
         }
-        Lm[i * ldm + j] = s;
+        nact += total;
       }
-      ldl_factor<NT>(Lm, nv, ldm);
+      wsync();
+      // same active set as the factor in Lm -> H is identical, keep the factor
+      float diff = (nact != nact_prev) ? 1.f : 0.f;
+      if (diff == 0.f)
+        for (int k = tid; k < nact; k += NT) diff += arow[k] != arow_prev[k] ? 1.f : 0.f;
+      diff = bsum<NT>(diff, red);
+      if (diff != 0.f) {
+        unsigned long long th = PROF_NOW();
+        hessian_mfma<NT>(Mm, ldm, J, ldj, arow, ash, nact, nv, Lm);
+        PROF_ACC(15, th);
+        unsigned long long tf = PROF_NOW();
+        ldl_factor_reg<NVP>(Lm, nv, ldm);
+        PROF_ACC(16, tf);
+        for (int k = tid; k < nact; k += NT) arow_prev[k] = arow[k];
+        nact_prev = nact;
+        nfactor++;
+      }
       for (int i = tid; i < nv; i += NT) search[i] = grad[i];
-      ldl_solve<NT>(Lm, nv, ldm, search);
+      unsigned long long ts = PROF_NOW();
+      ldl_solve_reg<NVP>(Lm, nv, ldm, search);
+      PROF_ACC(17, ts);
       for (int i = tid; i < nv; i += NT) search[i] = -search[i];
-      __syncthreads();
+      wsync();
     };
 
     // warm start: the cheaper of qacc_warmstart and qacc_smooth
     for (int i = tid; i < nv; i += NT) qacc[i] = d.qacc_warmstart[W * nv + i];
-    __syncthreads();
+    wsync();
     eval_point(qacc);
     float cost = update_constraint();
     float cs = 0.f;
     for (int r = tid; r < nefc; r += NT) {
-      float s = 0.f;
-      for (int k = 0; k < nv; k++) s += J[r * ldj + k] * qacc_smooth[k];
+      const float s = rowdot(J + r * ldj, qacc_smooth, nv);
       float f, cr;
       row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], s - efc_aref[r], &f, &cr);
       cs += cr;
@@ -1135,22 +1459,21 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
     const float cost_smooth = bsum<NT>(cs, red);
     if (cost > cost_smooth) {
       for (int i = tid; i < nv; i += NT) qacc[i] = qacc_smooth[i];
-      __syncthreads();
+      wsync();
       eval_point(qacc);
       cost = update_constraint();
     }
-    __syncthreads();
+    wsync();
     newton_direction();
 
     for (int it = 0; it < m.iterations; it++) {
+      unsigned long long t_ls = PROF_NOW();
       // ---- exact line search along `search`
       symv<NT>(Mm, nv, ldm, search, Mv);
       for (int r = tid; r < nefc; r += NT) {
-        float s = 0.f;
-        for (int k = 0; k < nv; k++) s += J[r * ldj + k] * search[k];
-        jv[r] = s;
+        jv[r] = rowdot(J + r * ldj, search, nv);
       }
-      __syncthreads();
+      wsync();
       float g1 = 0.f, g2 = 0.f;
       for (int i = tid; i < nv; i += NT) {
         g1 += search[i] * (Ma[i] - qfrc_smooth[i]);
@@ -1186,17 +1509,22 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
           alpha = an;
         }
       }
+      PROF_ACC(12, t_ls);
       if (alpha == 0.f) break;
+      unsigned long long t_up = PROF_NOW();
       for (int i = tid; i < nv; i += NT) {
         qacc[i] += alpha * search[i];
         Ma[i] += alpha * Mv[i];
       }
       for (int r = tid; r < nefc; r += NT) jaref[r] += alpha * jv[r];
-      __syncthreads();
+      wsync();
       const float old = cost;
       cost = update_constraint();
-      __syncthreads();
+      wsync();
+      PROF_ACC(13, t_up);
+      unsigned long long t_nd = PROF_NOW();
       newton_direction();
+      PROF_ACC(14, t_nd);
       niter++;
       float gn = 0.f;
       for (int i = tid; i < nv; i += NT) gn += grad[i] * grad[i];
@@ -1205,14 +1533,15 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       if (improvement < m.tolerance || gradient < m.tolerance) break;
     }
   }
-  __syncthreads();
+  wsync();
 
   // ---------------------------------------------------------------- post-constraint acceleration (cacc)
+  PROF(6);
   {
     const float g0 = -m.gravity_x, g1 = -m.gravity_y, g2 = -m.gravity_z;
     for (int b = tid; b < nb; b += NT) {
       float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
-      unsigned long long mask = (unsigned long long)m.body_dofmask[b];
+      unsigned long long mask = (unsigned long long)IMG_L(body_dofmask)[b];
       while (mask) {
         const int j = __builtin_ctzll(mask);
         mask &= mask - 1;
@@ -1224,20 +1553,20 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
       for (int c = 0; c < 6; c++) cacc[6 * b + c] = a[c];
     }
   }
-  __syncthreads();
+  wsync();
 
   // ---------------------------------------------------------------- sensors
   {
     float* sd = d.sensordata + W * m.nsensordata;
     for (int s = 0; s < m.nsensor; s++) {
-      const int type = m.sensor_type[s], id = m.sensor_objid[s], adr = m.sensor_adr[s];
+      const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
       if (type == 40) {
         // contact sensor: lanes over contacts
-        const int bits = m.sensor_intprm[3 * s], reduce = m.sensor_intprm[3 * s + 1], nslot = m.sensor_intprm[3 * s + 2];
-        const int otype = m.sensor_objtype[s], rtype = m.sensor_reftype[s], rid = m.sensor_refid[s];
-        const int dim = m.sensor_dim[s];
+        const int bits = IMG_I(sensor_intprm)[3 * s], reduce = IMG_I(sensor_intprm)[3 * s + 1], nslot = IMG_I(sensor_intprm)[3 * s + 2];
+        const int otype = IMG_I(sensor_objtype)[s], rtype = IMG_I(sensor_reftype)[s], rid = IMG_I(sensor_refid)[s];
+        const int dim = IMG_I(sensor_dim)[s];
         for (int k = tid; k < dim; k += NT) sd[adr + k] = 0.f;
-        __syncthreads();
+        wsync();
         // match flags
         float cnt = 0.f, fx = 0.f, fy = 0.f, fz = 0.f;
         for (int base = 0; base < ncon; base += NT) {
@@ -1248,10 +1577,10 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
             const int g1 = con_geom[2 * ci], g2 = con_geom[2 * ci + 1];
             auto om = [&](int ty, int oid, int g) -> bool {
               if (oid < 0) return true;
-              const int gb = m.geom_bodyid[g];
+              const int gb = IMG_I(geom_bodyid)[g];
               if (ty == 5) return g == oid;
               if (ty == 1) return gb == oid;
-              if (ty == 2) return oid == 0 || (((unsigned long long)m.body_treemask[gb] >> oid) & 1ull);
+              if (ty == 2) return oid == 0 || (((unsigned long long)IMG_L(body_treemask)[gb] >> oid) & 1ull);
               return false;
             };
             int flip = 0;
@@ -1305,8 +1634,8 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
               if (bits & 16) { o[q++] = con_pos[3 * ci]; o[q++] = con_pos[3 * ci + 1]; o[q++] = con_pos[3 * ci + 2]; }
               const float* fr = con_frame + 9 * ci;
               const int g1 = con_geom[2 * ci];
-              const bool flipped = !(otype == 5 ? g1 == id : (otype == 1 ? m.geom_bodyid[g1] == id
-                                        : (id == 0 || (((unsigned long long)m.body_treemask[m.geom_bodyid[g1]] >> id) & 1ull))));
+              const bool flipped = !(otype == 5 ? g1 == id : (otype == 1 ? IMG_I(geom_bodyid)[g1] == id
+                                        : (id == 0 || (((unsigned long long)IMG_L(body_treemask)[IMG_I(geom_bodyid)[g1]] >> id) & 1ull))));
               const float sg = flipped ? -1.f : 1.f;
               if (bits & 32) { o[q++] = sg * fr[0]; o[q++] = sg * fr[1]; o[q++] = sg * fr[2]; }
               if (bits & 64) { o[q++] = sg * fr[3]; o[q++] = sg * fr[4]; o[q++] = sg * fr[5]; }
@@ -1314,7 +1643,7 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
           }
           cnt += (float)total;
           fx += Fw[0]; fy += Fw[1]; fz += Fw[2];
-          __syncthreads();
+          wsync();
         }
         float sx = fx, sy = fy;
         bsum2<NT>(sx, sy, red);
@@ -1331,14 +1660,14 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
             for (int sl = 0; sl < nslot && sl < (int)cnt; sl++) sd[adr + sl * width] = found;
           }
         }
-        __syncthreads();
+        wsync();
         continue;
       }
       if (tid != 0) continue;
       float* out = sd + adr;
       switch (type) {
         case 3: {  // gyro
-          const int b = m.site_bodyid[id];
+          const int b = IMG_I(site_bodyid)[id];
           float r[3];
           matT_vec(r, sxmat + 9 * id, cvel + 6 * b);
           out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
@@ -1346,8 +1675,8 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
         }
         case 2:
         case 1: {  // velocimeter / accelerometer
-          const int b = m.site_bodyid[id];
-          const float* c = subtree_com + 3 * m.body_rootid[b];
+          const int b = IMG_I(site_bodyid)[id];
+          const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
           const float* sp = sxpos + 3 * id;
           float dif[3] = {sp[0] - c[0], sp[1] - c[1], sp[2] - c[2]}, t[3], lin[3], r[3];
           const float* v = cvel + 6 * b;
@@ -1369,8 +1698,8 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
           break;
         }
         case 30: out[0] = sxpos[3 * id]; out[1] = sxpos[3 * id + 1]; out[2] = sxpos[3 * id + 2]; break;
-        case 9: out[0] = qpos[m.jnt_qposadr[id]]; break;
-        case 10: out[0] = qvel[m.jnt_dofadr[id]]; break;
+        case 9: out[0] = qpos[IMG_I(jnt_qposadr)[id]]; break;
+        case 10: out[0] = qvel[IMG_I(jnt_dofadr)[id]]; break;
         case 34: out[0] = subtree_com[3 * id]; out[1] = subtree_com[3 * id + 1]; out[2] = subtree_com[3 * id + 2]; break;
         case 31: {
           const float* R = sxmat + 9 * id;
@@ -1397,9 +1726,9 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
         case 36: {
           float msum = 0.f, lin[3] = {0.f, 0.f, 0.f};
           for (int b = 1; b < nb; b++) {
-            if (!(id == 0 || (((unsigned long long)m.body_treemask[b] >> id) & 1ull))) continue;
+            if (!(id == 0 || (((unsigned long long)IMG_L(body_treemask)[b] >> id) & 1ull))) continue;
             const float bm = cinert[10 * b + 9];
-            const float* c = subtree_com + 3 * m.body_rootid[b];
+            const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
             const float* v = cvel + 6 * b;
             float dif[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
             cross3(t, dif, v);
@@ -1412,9 +1741,9 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
           float L[3] = {0.f, 0.f, 0.f};
           const float* sc = subtree_com + 3 * id;
           for (int b = 1; b < nb; b++) {
-            if (!(id == 0 || (((unsigned long long)m.body_treemask[b] >> id) & 1ull))) continue;
+            if (!(id == 0 || (((unsigned long long)IMG_L(body_treemask)[b] >> id) & 1ull))) continue;
             const float bm = cinert[10 * b + 9];
-            const float* c = subtree_com + 3 * m.body_rootid[b];
+            const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
             const float* v = cvel + 6 * b;
             float dd[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
             cross3(t, dd, v);
@@ -1436,14 +1765,15 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
         default:
           break;
       }
-      const float cut = m.sensor_cutoff[s];
+      const float cut = IMG_F(sensor_cutoff)[s];
       if (cut > 0.f && type != 31)
-        for (int k = 0; k < m.sensor_dim[s]; k++) out[k] = clampf(out[k], -cut, cut);
+        for (int k = 0; k < IMG_I(sensor_dim)[s]; k++) out[k] = clampf(out[k], -cut, cut);
     }
   }
-  __syncthreads();
+  wsync();
 
   // ---------------------------------------------------------------- forward outputs
+  PROF(7);
   for (int i = tid; i < nb * 3; i += NT) {
     d.xpos[W * nb * 3 + i] = xpos[i];
     d.xipos[W * nb * 3 + i] = xipos[i];
@@ -1502,47 +1832,48 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
   }
 
   // ---------------------------------------------------------------- integration
+  PROF(8);
   if constexpr (STEP) {
     const float dt = m.timestep;
     float* qa_int = tmp;
     if (m.integrator == MJH_INT_IMPLICITFAST) {
       for (int i = tid; i < nv * ldm; i += NT) Lm[i] = Mm[i];
-      __syncthreads();
+      wsync();
       for (int i = tid; i < nv; i += NT) Lm[i * ldm + i] += dt * dof_damping[i];
-      __syncthreads();
+      wsync();
       for (int i = tid; i < nu; i += NT) {
-        if (m.actuator_forcelimited[i]) {
+        if (IMG_I(actuator_forcelimited)[i]) {
           const float f = act_force[i];
-          if (f <= m.actuator_forcerange[2 * i] || f >= m.actuator_forcerange[2 * i + 1]) continue;
+          if (f <= IMG_F(actuator_forcerange)[2 * i] || f >= IMG_F(actuator_forcerange)[2 * i + 1]) continue;
         }
-        const int dof = m.jnt_dofadr[m.actuator_trnid[i]];
-        const float g = m.actuator_gear[i];
-        atomicAdd(&Lm[dof * ldm + dof], -dt * g * g * m.actuator_biasprm[10 * i + 2]);
+        const int dof = IMG_I(jnt_dofadr)[IMG_I(actuator_trnid)[i]];
+        const float g = IMG_F(actuator_gear)[i];
+        atomicAdd(&Lm[dof * ldm + dof], -dt * g * g * IMG_F(actuator_biasprm)[10 * i + 2]);
       }
       for (int i = tid; i < nv; i += NT) qa_int[i] = qfrc_smooth[i] + qfrc_con[i];
-      ldl_factor<NT>(Lm, nv, ldm);
-      ldl_solve<NT>(Lm, nv, ldm, qa_int);
+      ldl_factor_reg<NVP>(Lm, nv, ldm);
+      ldl_solve_reg<NVP>(Lm, nv, ldm, qa_int);
     } else {
       float anyd = 0.f;
       for (int i = tid; i < nv; i += NT) anyd += dof_damping[i] > 0.f ? 1.f : 0.f;
       anyd = bsum<NT>(anyd, red);
       if (anyd > 0.f) {
         for (int i = tid; i < nv * ldm; i += NT) Lm[i] = Mm[i];
-        __syncthreads();
+        wsync();
         for (int i = tid; i < nv; i += NT) Lm[i * ldm + i] += dt * dof_damping[i];
         symv<NT>(Mm, nv, ldm, qacc, qa_int);
-        ldl_factor<NT>(Lm, nv, ldm);
-        ldl_solve<NT>(Lm, nv, ldm, qa_int);
+        ldl_factor_reg<NVP>(Lm, nv, ldm);
+        ldl_solve_reg<NVP>(Lm, nv, ldm, qa_int);
       } else {
         for (int i = tid; i < nv; i += NT) qa_int[i] = qacc[i];
-        __syncthreads();
+        wsync();
       }
     }
     for (int i = tid; i < nv; i += NT) qvel[i] += dt * qa_int[i];
-    __syncthreads();
+    wsync();
     for (int j = tid; j < nj; j += NT) {
-      const int q0 = m.jnt_qposadr[j], v0 = m.jnt_dofadr[j];
-      if (m.jnt_type[j] == 0) {
+      const int q0 = IMG_I(jnt_qposadr)[j], v0 = IMG_I(jnt_dofadr)[j];
+      if (IMG_I(jnt_type)[j] == 0) {
         qpos[q0] += dt * qvel[v0];
         qpos[q0 + 1] += dt * qvel[v0 + 1];
         qpos[q0 + 2] += dt * qvel[v0 + 2];
@@ -1559,13 +1890,14 @@ __global__ __launch_bounds__(NT) void step_kernel(const mjh_model m, const mjh_d
         qpos[q0] += dt * qvel[v0];
       }
     }
-    __syncthreads();
+    wsync();
     for (int i = tid; i < nq; i += NT) d.qpos[W * nq + i] = qpos[i];
     for (int i = tid; i < nv; i += NT) d.qvel[W * nv + i] = qvel[i];
     if (tid == 0) d.time[W] += dt;
   }
 
   // non-finite check on the new state
+  PROF(9);
   {
     float bad = 0.f;
     for (int i = tid; i < nq; i += NT) bad += isfinite(qpos[i]) ? 0.f : 1.f;
@@ -1580,19 +1912,74 @@ __global__ void repeat_kernel(float* dst, const float* src, long long nelem, lon
     dst[i] = src[i % nelem];
 }
 
+// ---- model image packing ------------------------------------------------------
+// One workgroup per model field copies it into the packed image (all fields in
+// parallel, ~µs); launched ahead of every step so in-place edits of shared
+// model fields take effect at the next step, as with MuJoCo Warp.
+__global__ void pack_kernel(const mjh_model m, const ImgOff io) {
+#define X_SZ(name) const int name = m.name;
+  MJH_MODEL_SIZES(X_SZ)
+#undef X_SZ
+  (void)nchain; (void)ncolgeom; (void)npair; (void)nsensor; (void)nmocap; (void)nconmax; (void)njmax; (void)na;
+  (void)nsensordata; (void)nq; (void)nv; (void)nu; (void)nbody; (void)njnt; (void)ngeom; (void)nsite;
+  unsigned int* img = reinterpret_cast<unsigned int*>(m.image);
+  int f = 0;
+#define X_PACK(type, name, count)                                                          \
+  if ((int)blockIdx.x == f) {                                                              \
+    const int words = (int)((count) * (int)(sizeof(type) / 4));                            \
+    const unsigned int* src = reinterpret_cast<const unsigned int*>(m.name);               \
+    for (int i = threadIdx.x; i < words; i += blockDim.x) img[io.name + i] = src[i];       \
+    return;                                                                                \
+  }                                                                                        \
+  f++;
+  MJH_MODEL_ARRAYS(X_PACK)
+  MJH_MODEL_WARRAYS(X_PACK)
+#undef X_PACK
+}
+
 // ---- host side ---------------------------------------------------------------
-Layout make_layout(const mjh_model* m, int nt) {
+inline int nvp_of(int nv) { return nv <= 20 ? 20 : (nv <= 36 ? 36 : 64); }
+ImgOff make_imgoff(const mjh_model* m) {
+  ImgOff io;
+  std::memset(&io, 0, sizeof(io));
+#define X_SZ(name) const int name = m->name;
+  MJH_MODEL_SIZES(X_SZ)
+#undef X_SZ
+  (void)nchain; (void)ncolgeom; (void)npair; (void)nsensor; (void)nmocap; (void)nconmax; (void)njmax; (void)na;
+  (void)nsensordata; (void)nq; (void)nv; (void)nu; (void)nbody; (void)njnt; (void)ngeom; (void)nsite;
+  int off = 0, nf = 0;
+#define X_OFF(type, name, count)                            \
+  io.name = off;                                            \
+  off += (((count) * (int)(sizeof(type) / 4)) + 1) & ~1;    \
+  nf++;
+  MJH_MODEL_ARRAYS(X_OFF)
+  MJH_MODEL_WARRAYS(X_OFF)
+#undef X_OFF
+  io.img_words = (off + 3) & ~3;
+  io.nfields = nf;
+#define X_W(type, name, count) io.w_##name = -1;
+  MJH_MODEL_WARRAYS(X_W)
+#undef X_W
+  return io;
+}
+
+// Per-world LDS layout. `budget` = LDS words available to one world.
+Layout make_layout(const mjh_model* m, ImgOff* io, int budget) {
   Layout L;
   std::memset(&L, 0, sizeof(L));
   int off = 0;
   auto take = [&](int n) {
     int o = off;
-    off += (n + 1) & ~1;  // keep 8-byte alignment for the int64 masks
+    off += (n + 3) & ~3;  // 16-byte alignment (float4 rows, int64 masks)
     return o;
   };
   const int nv = m->nv, nb = m->nbody, nj = m->njnt;
-  L.ldm = nv | 1;
-  L.ldj = nv | 1;
+  // rows 16-byte aligned with an odd float4 count: ds_read_b128 on a row per lane
+  // lands on distinct bank quads (conflict-free), and row reads vectorise
+  int ld = nvp_of(nv);  // == kernel's NVP (rows loaded whole into registers)
+  if (((ld >> 2) & 1) == 0) ld += 4;
+  L.ldm = ld;
+  L.ldj = ld;
   L.qpos = take(m->nq);
   L.qvel = take(nv); L.qacc = take(nv); L.qacc_smooth = take(nv); L.qfrc_smooth = take(nv);
   L.qfrc_bias = take(nv); L.qfrc_con = take(nv); L.qfrc_passive = take(nv); L.qfrc_act = take(nv);
@@ -1610,13 +1997,21 @@ Layout make_layout(const mjh_model* m, int nt) {
   L.con_pos = take(3 * C); L.con_frame = take(9 * C); L.con_dist = take(C); L.con_fric = take(5 * C);
   L.con_solref = take(2 * C); L.con_solimp = take(5 * C); L.con_imargin = take(C); L.con_dim = take(C);
   L.con_geom = take(2 * C); L.con_efcadr = take(C);
-  L.red = take(4 * (nt / 64) + 8);
+  L.red = take(16);
   L.ints = take(8);
-  // constraint rows: as many as fit in the LDS budget, up to njmax
+  {  // expanded (per-world) model fields
+    auto sz = [&](void) {};
+    (void)sz;
+    const int nq = m->nq, nbody = m->nbody, njnt = m->njnt, ngeom = m->ngeom, nsite = m->nsite;
+    (void)nq; (void)nbody; (void)njnt; (void)ngeom; (void)nsite;
+#define X_WL(type, name, count) io->w_##name = m->name##_wstride ? take((count)) : -1;
+    MJH_MODEL_WARRAYS(X_WL)
+#undef X_WL
+  }
+  // constraint rows: as many as fit in the remaining budget, up to njmax
   const int fixed = off;
-  const int per_row = L.ldj + 10 + 2;  // J row + 10 scalars + 64-bit mask
-  const int budget_words = (160 * 1024 / 4) / 2;  // two worlds per CU
-  int rcap = (budget_words - fixed - 8) / per_row;
+  const int per_row = L.ldj + 16 + 2;  // J row + per-row scalars/ints + 64-bit mask
+  int rcap = (budget - fixed - 16) / per_row;
   if (rcap > m->njmax) rcap = m->njmax;
   if (rcap < 1) rcap = 1;
   L.rcap = rcap;
@@ -1625,26 +2020,49 @@ Layout make_layout(const mjh_model* m, int nt) {
   L.efc_jv = take(rcap); L.efc_force = take(rcap); L.efc_fl = take(rcap); L.efc_pos = take(rcap);
   L.efc_type = take(rcap); L.efc_id = take(rcap);
   L.efc_mask = take(2 * rcap);
-  L.total = off;
+  L.efc_h = take(rcap); L.arow = take(rcap + 4); L.ash = take(rcap + 4); L.arow_prev = take(rcap + 4);
+  L.total = (off + 3) & ~3;
   return L;
 }
 
-constexpr int kThreads = 64;
+constexpr int kLdsBytes = 160 * 1024;
+constexpr int kWorldsPerBlock = 2;
+
+struct Plan {
+  ImgOff io;
+  Layout lo;
+  size_t shmem;
+};
+
+Plan make_plan(const mjh_model* m, int wpb) {
+  Plan p;
+  p.io = make_imgoff(m);
+  const int budget = (kLdsBytes / 4 - p.io.img_words) / wpb;
+  p.lo = make_layout(m, &p.io, budget);
+  p.shmem = (size_t)(p.io.img_words + wpb * p.lo.total) * 4;
+  return p;
+}
 
 template <bool STEP>
 int launch(const mjh_model* m, const mjh_data* d, void* stream) {
   if (mjh_model_check(m) != 0) return 1;
   if (d->nworld <= 0) return 0;
-  Layout L = make_layout(m, kThreads);
-  size_t shmem = (size_t)L.total * 4;
+  Plan p = make_plan(m, kWorldsPerBlock);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   static bool attr_set[2] = {false, false};
-  auto kern = step_kernel<kThreads, STEP>;
+  const int nvp = nvp_of(m->nv);
+  auto kern = nvp == 20 ? step_kernel<kWorldsPerBlock, STEP, 20>
+            : nvp == 36 ? step_kernel<kWorldsPerBlock, STEP, 36>
+                        : step_kernel<kWorldsPerBlock, STEP, 64>;
   if (!attr_set[STEP]) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (auto k : {step_kernel<kWorldsPerBlock, STEP, 20>, step_kernel<kWorldsPerBlock, STEP, 36>,
+                   step_kernel<kWorldsPerBlock, STEP, 64>})
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     attr_set[STEP] = true;
   }
-  hipLaunchKernelGGL(kern, dim3(d->nworld), dim3(kThreads), shmem, s, *m, *d, L);
+  hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields), dim3(256), 0, s, *m, p.io);
+  const int blocks = (d->nworld + kWorldsPerBlock - 1) / kWorldsPerBlock;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * kWorldsPerBlock), p.shmem, s, *m, *d, p.lo, p.io);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_err = std::string("step launch failed: ") + hipGetErrorString(e);
@@ -1664,23 +2082,33 @@ const char* mjh_last_error(void) { return g_err.c_str(); }
 size_t mjh_sizeof_model(void) { return sizeof(mjh_model); }
 size_t mjh_sizeof_data(void) { return sizeof(mjh_data); }
 
+int mjh_image_words(const mjh_model* m) { return make_imgoff(m).img_words; }
+
 int mjh_model_check(const mjh_model* m) {
   if (!m) { g_err = "null model"; return 1; }
   if (m->nv > 63 || m->nbody > 63) { g_err = "device path supports nv <= 63 and nbody <= 63"; return 1; }
   if (m->nconmax <= 0 || m->njmax <= 0) { g_err = "nconmax and njmax must be positive"; return 1; }
-  Layout L = make_layout(m, kThreads);
-  if ((size_t)L.total * 4 > 160 * 1024) { g_err = "per-world scratch exceeds LDS"; return 1; }
-  if (L.rcap < 8) { g_err = "too little LDS left for constraint rows"; return 1; }
-  for (int p = 0; p < m->npair; p++) {
-    (void)p;  // pair type support is validated by the compiler (host arrays)
-  }
+  Plan p = make_plan(m, kWorldsPerBlock);
+  if (!m->image || m->image_words < p.io.img_words) { g_err = "model image buffer missing or too small (mjh_image_words)"; return 1; }
+  if (p.shmem > (size_t)kLdsBytes) { g_err = "model image + per-world scratch exceed LDS"; return 1; }
+  if (p.lo.rcap < 8) { g_err = "too little LDS left for constraint rows"; return 1; }
   g_err.clear();
   return 0;
 }
 
-int mjh_scratch_bytes(const mjh_model* m) { return make_layout(m, kThreads).total * 4; }
+int mjh_scratch_bytes(const mjh_model* m) { return (int)make_plan(m, kWorldsPerBlock).shmem; }
 
-int mjh_efc_capacity(const mjh_model* m) { return make_layout(m, kThreads).rcap; }
+int mjh_efc_capacity(const mjh_model* m) { return make_plan(m, kWorldsPerBlock).lo.rcap; }
+
+int mjh_set_profile_buffer(void* ptr) {
+#ifdef MJH_PROFILE
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(ptr);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), &p, sizeof(p)) == hipSuccess ? 0 : 1;
+#else
+  (void)ptr;
+  return 1;
+#endif
+}
 
 int mjh_step(const mjh_model* m, const mjh_data* d, void* stream) { return launch<true>(m, d, stream); }
 

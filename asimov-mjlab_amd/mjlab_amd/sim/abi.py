@@ -74,6 +74,8 @@ def model_struct(real=ctypes.c_float):
       members.append((f.name, ctypes.c_void_p))
       members.append((f.name + "_wstride", ctypes.c_longlong))
   # MA and MW are interleaved in declaration order in C: MA list first, then MW list.
+  if real is ctypes.c_float:  # device descriptor: packed model-image scratch
+    members += [("image", ctypes.c_void_p), ("image_words", ctypes.c_int), ("_pad_image", ctypes.c_int)]
   return type("mjh_model" if real is ctypes.c_float else "or_model", (ctypes.Structure,), {"_fields_": members})
 
 

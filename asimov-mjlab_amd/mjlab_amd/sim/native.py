@@ -13,8 +13,12 @@ from pathlib import Path
 
 from mjlab_amd.sim import abi
 
+import os
+
 PKG = Path(__file__).resolve().parents[1]
-LIB_PATH = PKG / "libmjh.so"
+# MJH_LIB selects an alternative build of the same ABI (e.g. the phase-timing
+# build libmjh_prof.so used by tools/phase_profile.py).
+LIB_PATH = Path(os.environ.get("MJH_LIB", str(PKG / "libmjh.so")))
 ABI_VERSION = 1
 
 EXPORTS = (
@@ -24,6 +28,8 @@ EXPORTS = (
   "mjh_sizeof_data",
   "mjh_model_check",
   "mjh_scratch_bytes",
+  "mjh_image_words",
+  "mjh_set_profile_buffer",
   "mjh_efc_capacity",
   "mjh_step",
   "mjh_forward",
@@ -53,6 +59,8 @@ def lib() -> ctypes.CDLL:
   L.mjh_model_check.argtypes = [ctypes.c_void_p]
   L.mjh_scratch_bytes.argtypes = [ctypes.c_void_p]
   L.mjh_efc_capacity.argtypes = [ctypes.c_void_p]
+  L.mjh_image_words.argtypes = [ctypes.c_void_p]
+  L.mjh_set_profile_buffer.argtypes = [ctypes.c_void_p]
   for f in (L.mjh_step, L.mjh_forward):
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     f.restype = ctypes.c_int

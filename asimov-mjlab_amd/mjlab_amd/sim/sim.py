@@ -183,11 +183,26 @@ class Simulation:
       setattr(ms, name, t.data_ptr())
       if name in self._wstride:
         setattr(ms, name + "_wstride", self._wstride[name])
+    # packed model image scratch (staged into LDS by every launch)
+    if not hasattr(self, "_image"):
+      words = int(native.lib().mjh_image_words(ctypes.addressof(ms))) if self._native_ok() else 16
+      self._image = torch.zeros(words + 4, dtype=torch.float32, device=self.device)
+    ms.image = self._image.data_ptr()
+    ms.image_words = self._image.numel()
     ds = DS()
     ds.nworld = self.num_envs
     for name, t in self._data_flat.items():
       setattr(ds, name, t.data_ptr())
     self._mstruct, self._dstruct = ms, ds
+
+  def _native_ok(self) -> bool:
+    try:
+      native.lib()
+      return True
+    except native.NativeLibraryError:
+      if str(self.device).startswith("cuda"):
+        raise
+      return False
 
   def set_option(self, **kw) -> None:
     """Change solver/integrator options after construction (re-captures graphs)."""

@@ -63,6 +63,11 @@ typedef struct mjh_model {
 #define MJH_X_WARR(type, name, count) const type* name; long long name##_wstride;
   MJH_MODEL_WARRAYS(MJH_X_WARR)
 #undef MJH_X_WARR
+  /* caller-allocated device scratch for the packed model image
+     (mjh_image_words() 32-bit words, 16-byte aligned) */
+  float* image;
+  int image_words;
+  int _pad_image;
 } mjh_model;
 
 /* Data descriptor: one pointer per per-world array, (nworld, COUNT). */
@@ -89,8 +94,19 @@ size_t mjh_sizeof_data(void);
  * model can be stepped. Replaces put_model's checks (sim.py:116). */
 int mjh_model_check(const mjh_model* m);
 
-/* Bytes of per-world on-chip scratch the step kernel uses for this model. */
+/* Words of device scratch the caller must provide in m->image (the packed
+ * model image staged into LDS by every launch). */
+int mjh_image_words(const mjh_model* m);
+
+/* LDS bytes per workgroup the step kernel uses for this model. */
 int mjh_scratch_bytes(const mjh_model* m);
+
+/* Constraint rows per world that fit on chip (<= njmax); rows beyond it are
+ * dropped and reported through flags bit 1. */
+int mjh_efc_capacity(const mjh_model* m);
+
+/* Diagnostic builds only (-DMJH_PROFILE): per-world phase timestamps. */
+int mjh_set_profile_buffer(void* ptr);
 
 /* One physics step (mj_step: forward + implicitfast/Euler integration) for all
  * nworld worlds. Replaces mjwarp.step (sim.py:193-199). */

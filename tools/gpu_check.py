@@ -68,6 +68,12 @@ def main():
     err = np.abs(a - b)
     scale = np.abs(b).max() + 1e-9
     print(f"{k:16s} maxabs {err.max():.3e}  rel-to-max {err.max()/scale:.3e}  median {np.median(err):.2e}")
+  # per-world worst cases
+  e = np.abs(out["qvel"] - ref["qvel"]).max(axis=1)
+  worst = np.argsort(-e)[:6]
+  print("worst qvel worlds:", [(int(w), float(e[w]), int(out["solver_niter"][w, 0]), int(ref["solver_niter"][w, 0]), int(ref["nefc"][w, 0])) for w in worst])
+  conv = (ref["solver_niter"][:, 0] < 10) & (out["solver_niter"][:, 0] < 10)
+  print(f"converged worlds: {conv.sum()}/{N}; max qvel err on converged {e[conv].max():.3e}, unconverged {e[~conv].max() if (~conv).any() else 0:.3e}")
   # timing
   for n2 in (N,):
     torch.cuda.synchronize()

@@ -1,0 +1,54 @@
+"""Per-phase cycle breakdown of the step kernel (diagnostic build libmjh_prof.so).
+
+Run: MJH_LIB=asimov-mjlab_amd/mjlab_amd/libmjh_prof.so python tools/phase_profile.py [N]
+Stamps are s_memtime (shader clock) at phase boundaries, lane 0 of each world.
+"""
+
+import ctypes
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+os.environ.setdefault("MJH_LIB", str(ROOT / "asimov-mjlab_amd/mjlab_amd/libmjh_prof.so"))
+sys.path.insert(0, str(ROOT / "asimov-mjlab_amd"))
+sys.path.insert(0, str(ROOT / "tools"))
+
+import numpy as np
+import torch
+
+from gpu_check import g1_scene, random_states
+from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg, native
+
+NAMES = ["kinematics", "com/crb/M/factor", "rne/smooth/qacc_smooth", "collision", "constraints", "solver",
+         "cacc+sensors", "outputs", "integration"]
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+sc = g1_scene(N)
+m = sc.compile(50, 300)
+cfg = SimulationCfg(nconmax=50, njmax=300, mujoco=MujocoCfg(timestep=0.005, iterations=10, ls_iterations=20))
+buf = torch.zeros(N * 32, dtype=torch.int64, device="cuda:0")
+L = native.lib()
+L.mjh_set_profile_buffer.argtypes = [ctypes.c_void_p]
+assert L.mjh_set_profile_buffer(ctypes.c_void_p(buf.data_ptr())) == 0  # before any launch
+torch.cuda.synchronize()
+sim = Simulation(N, cfg, m, "cuda:0")
+rng = np.random.default_rng(0)
+st = random_states(m, N, rng)
+for k, v in st.items():
+  getattr(sim.data, k)[:] = torch.as_tensor(v, dtype=torch.float32, device="cuda:0").view_as(getattr(sim.data, k))
+for _ in range(3):
+  sim.step()
+torch.cuda.synchronize()
+p = buf.view(N, 32).cpu().numpy().astype(np.int64)
+d = np.diff(p[:, :10], axis=1)
+tot = p[:, 9] - p[:, 0]
+print(f"N={N} mean total cycles/world-step: {tot.mean():.0f} (max {tot.max()})")
+for i, n in enumerate(NAMES):
+  print(f"  {n:26s} {d[:, i].mean():10.0f}  ({100*d[:, i].mean()/tot.mean():5.1f}%)")
+print(f"  solver: linesearch {p[:,12].mean():.0f}  update {p[:,13].mean():.0f}  newton_dir {p[:,14].mean():.0f}")
+print(f"    newton_dir parts: hessian {p[:,15].mean():.0f}  factor {p[:,16].mean():.0f}  solve {p[:,17].mean():.0f}")
+print(f"  M factor alone: {(p[:,2]-p[:,10]).mean():.0f}  (com/crb/M before it: {(p[:,10]-p[:,1]).mean():.0f})")
+niter = sim.data.solver_niter.cpu().numpy()
+nefc = sim.data.nefc.cpu().numpy()
+print(f"  niter mean {niter.mean():.2f}  nefc mean {nefc.mean():.1f}  ncon mean {sim.data.ncon.float().mean().item():.1f}")
