@@ -1,0 +1,55 @@
+"""Generic reward terms (``src/mjlab/envs/mdp/rewards.py``)."""
+
+from __future__ import annotations
+
+import torch
+
+from mjlab_amd.managers.scene_entity_config import SceneEntityCfg
+from mjlab_amd.utils.string import resolve_matching_names_values
+
+_DEFAULT = SceneEntityCfg("robot")
+
+
+def is_alive(env) -> torch.Tensor:
+  return (~env.termination_manager.terminated).float()
+
+
+def is_terminated(env) -> torch.Tensor:
+  return env.termination_manager.terminated.float()
+
+
+def joint_torques_l2(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
+  return torch.sum(torch.square(env.scene[asset_cfg.name].data.actuator_force), dim=1)
+
+
+def joint_acc_l2(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
+  a = env.scene[asset_cfg.name]
+  return torch.sum(torch.square(a.data.joint_acc[:, asset_cfg.joint_ids]), dim=1)
+
+
+def action_rate_l2(env) -> torch.Tensor:
+  return torch.sum(torch.square(env.action_manager.action - env.action_manager.prev_action), dim=1)
+
+
+def joint_pos_limits(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
+  a = env.scene[asset_cfg.name]
+  lim = a.data.soft_joint_pos_limits
+  q = a.data.joint_pos[:, asset_cfg.joint_ids]
+  out = -(q - lim[:, asset_cfg.joint_ids, 0]).clip(max=0.0)
+  out += (q - lim[:, asset_cfg.joint_ids, 1]).clip(min=0.0)
+  return torch.sum(out, dim=1)
+
+
+class posture:
+  def __init__(self, cfg, env) -> None:
+    a = env.scene[cfg.params["asset_cfg"].name]
+    self.default_joint_pos = a.data.default_joint_pos
+    _, names = a.find_joints(cfg.params["asset_cfg"].joint_names)
+    _, _, std = resolve_matching_names_values(data=cfg.params["std"], list_of_strings=names)
+    self.std = torch.tensor(std, device=env.device, dtype=torch.float32)
+
+  def __call__(self, env, std, asset_cfg: SceneEntityCfg) -> torch.Tensor:
+    del std
+    a = env.scene[asset_cfg.name]
+    err = torch.square(a.data.joint_pos[:, asset_cfg.joint_ids] - self.default_joint_pos[:, asset_cfg.joint_ids])
+    return torch.exp(-torch.mean(err / (self.std**2), dim=1))

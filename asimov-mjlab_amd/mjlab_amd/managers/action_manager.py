@@ -1,0 +1,83 @@
+"""Action manager + terms (``src/mjlab/managers/action_manager.py:28-123``)."""
+
+from __future__ import annotations
+
+import torch
+
+from mjlab_amd.managers.manager_base import ManagerTermBase, as_mask
+
+
+class ActionTerm(ManagerTermBase):
+  def __init__(self, cfg, env) -> None:
+    super().__init__(env)
+    self.cfg = cfg
+    self._asset = env.scene[cfg.asset_name]
+
+  @property
+  def action_dim(self) -> int:
+    raise NotImplementedError
+
+  def process_actions(self, actions: torch.Tensor) -> None:
+    raise NotImplementedError
+
+  def apply_actions(self) -> None:
+    raise NotImplementedError
+
+
+class ActionManager:
+  def __init__(self, cfg: dict, env) -> None:
+    self._env = env
+    self.cfg = cfg
+    self._terms: dict[str, ActionTerm] = {}
+    for name, tcfg in cfg.items():
+      if tcfg is None:
+        continue
+      self._terms[name] = tcfg.class_type(tcfg, env)
+    n = env.num_envs
+    self._action = torch.zeros(n, self.total_action_dim, device=env.device)
+    self._prev_action = torch.zeros_like(self._action)
+
+  @property
+  def total_action_dim(self) -> int:
+    return sum(t.action_dim for t in self._terms.values())
+
+  @property
+  def action_term_dim(self) -> list[int]:
+    return [t.action_dim for t in self._terms.values()]
+
+  @property
+  def action(self) -> torch.Tensor:
+    return self._action
+
+  @property
+  def prev_action(self) -> torch.Tensor:
+    return self._prev_action
+
+  @property
+  def active_terms(self) -> list[str]:
+    return list(self._terms)
+
+  def get_term(self, name: str) -> ActionTerm:
+    return self._terms[name]
+
+  def reset(self, env_ids=None) -> dict:
+    m = as_mask(env_ids, self._env.num_envs, self._env.device)[:, None]
+    self._prev_action.masked_fill_(m, 0.0)
+    self._action.masked_fill_(m, 0.0)
+    for t in self._terms.values():
+      t.reset(env_ids)
+    return {}
+
+  def process_action(self, action: torch.Tensor) -> None:
+    if action.shape[1] != self.total_action_dim:
+      raise ValueError(f"Invalid action shape, expected: {self.total_action_dim}, received: {action.shape[1]}.")
+    self._prev_action.copy_(self._action)
+    self._action.copy_(action)
+    idx = 0
+    for t in self._terms.values():
+      t.process_actions(self._action[:, idx : idx + t.action_dim])
+      idx += t.action_dim
+
+  def apply_action(self) -> None:
+    for t in self._terms.values():
+      t.apply_actions()

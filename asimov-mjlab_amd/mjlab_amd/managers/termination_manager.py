@@ -1,0 +1,65 @@
+"""Termination manager (``src/mjlab/managers/termination_manager.py:25-100``)."""
+
+from __future__ import annotations
+
+import torch
+
+from mjlab_amd.managers.manager_base import as_mask
+
+
+class TerminationManager:
+  def __init__(self, cfg: dict, env) -> None:
+    self._env = env
+    self.cfg = cfg
+    self._term_names, self._term_cfgs, self._class_term_cfgs = [], [], []
+    for name, tcfg in cfg.items():
+      if tcfg is None:
+        continue
+      if isinstance(tcfg.func, type):
+        tcfg.func = tcfg.func(tcfg, env)
+        self._class_term_cfgs.append(tcfg)
+      self._term_names.append(name)
+      self._term_cfgs.append(tcfg)
+    n = env.num_envs
+    self._term_dones = {k: torch.zeros(n, dtype=torch.bool, device=env.device) for k in self._term_names}
+    self._truncated_buf = torch.zeros(n, dtype=torch.bool, device=env.device)
+    self._terminated_buf = torch.zeros_like(self._truncated_buf)
+
+  @property
+  def active_terms(self) -> list[str]:
+    return list(self._term_names)
+
+  @property
+  def dones(self) -> torch.Tensor:
+    return self._truncated_buf | self._terminated_buf
+
+  @property
+  def time_outs(self) -> torch.Tensor:
+    return self._truncated_buf
+
+  @property
+  def terminated(self) -> torch.Tensor:
+    return self._terminated_buf
+
+  def reset(self, env_ids=None) -> dict:
+    m = as_mask(env_ids, self._env.num_envs, self._env.device)
+    extras = {"Episode_Termination/" + k: (v & m).sum() for k, v in self._term_dones.items()}
+    for tcfg in self._class_term_cfgs:
+      if hasattr(tcfg.func, "reset"):
+        tcfg.func.reset(env_ids=env_ids)
+    return extras
+
+  def compute(self) -> torch.Tensor:
+    self._truncated_buf.zero_()
+    self._terminated_buf.zero_()
+    for name, tcfg in zip(self._term_names, self._term_cfgs):
+      value = tcfg.func(self._env, **tcfg.params)
+      if tcfg.time_out:
+        self._truncated_buf |= value
+      else:
+        self._terminated_buf |= value
+      self._term_dones[name].copy_(value)
+    return self._truncated_buf | self._terminated_buf
+
+  def get_term(self, name: str) -> torch.Tensor:
+    return self._term_dones[name]
