@@ -643,9 +643,10 @@ __device__ __forceinline__ float row_state(int type, float D, float R, float fl,
 // ---- the step kernel --------------------------------------------------------
 template <int WPB, bool STEP, int NVP>
 __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo,
-                                                         const ImgOff Io) {
+                                                         const ImgOff Io, const unsigned char* gate) {
   constexpr int NT = 64;  // one wave per world
   extern __shared__ float smem[];
+  if (gate != nullptr && *gate == 0) return;  // gated forward: nothing to recompute
   // shared model image -> LDS (whole workgroup, 16-byte coalesced)
   {
     const float4* src = reinterpret_cast<const float4*>(m.image);
@@ -2044,7 +2045,7 @@ Plan make_plan(const mjh_model* m, int wpb) {
 }
 
 template <bool STEP>
-int launch(const mjh_model* m, const mjh_data* d, void* stream) {
+int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream) {
   if (mjh_model_check(m) != 0) return 1;
   if (d->nworld <= 0) return 0;
   Plan p = make_plan(m, kWorldsPerBlock);
@@ -2062,7 +2063,7 @@ int launch(const mjh_model* m, const mjh_data* d, void* stream) {
   }
   hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields), dim3(256), 0, s, *m, p.io);
   const int blocks = (d->nworld + kWorldsPerBlock - 1) / kWorldsPerBlock;
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * kWorldsPerBlock), p.shmem, s, *m, *d, p.lo, p.io);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * kWorldsPerBlock), p.shmem, s, *m, *d, p.lo, p.io, gate);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_err = std::string("step launch failed: ") + hipGetErrorString(e);
@@ -2110,9 +2111,14 @@ int mjh_set_profile_buffer(void* ptr) {
 #endif
 }
 
-int mjh_step(const mjh_model* m, const mjh_data* d, void* stream) { return launch<true>(m, d, stream); }
+int mjh_step(const mjh_model* m, const mjh_data* d, void* stream) { return launch<true>(m, d, nullptr, stream); }
 
-int mjh_forward(const mjh_model* m, const mjh_data* d, void* stream) { return launch<false>(m, d, stream); }
+int mjh_forward(const mjh_model* m, const mjh_data* d, void* stream) { return launch<false>(m, d, nullptr, stream); }
+
+int mjh_forward_gated(const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream) {
+  if (!gate) { g_err = "null gate"; return 1; }
+  return launch<false>(m, d, gate, stream);
+}
 
 int mjh_repeat(float* dst, const float* src, long long nelem, int nworld, void* stream) {
   if (nelem <= 0 || nworld <= 0) return 0;

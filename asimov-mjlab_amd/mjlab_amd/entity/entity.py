@@ -249,8 +249,15 @@ class Entity:
     p = self.prefix
     bnames = [p + n for n in self.body_names]
     body_ids = [model.names["body"].index(n) for n in bnames]
-    geom_ids = [model.names["geom"].index(p + n) for n in self.geom_names]
-    site_ids = [model.names["site"].index(p + n) for n in self.site_names]
+    # geoms/sites may be unnamed: map them per body, in spec order (the
+    # compiler keeps each body's geoms/sites contiguous and in spec order)
+    gbody = np.asarray(model.geom_bodyid)
+    sbody = np.asarray(model.site_bodyid)
+    geom_ids, site_ids = [], []
+    for gb in body_ids:
+      geom_ids += [int(i) for i in np.nonzero(gbody == gb)[0]]
+      site_ids += [int(i) for i in np.nonzero(sbody == gb)[0]]
+    assert len(geom_ids) == len(self.geom_names) and len(site_ids) == len(self.site_names)
     joint_ids = [model.names["joint"].index(p + n) for n in self.joint_names]
     ctrl_ids = [model.names["actuator"].index(p + n) for n in self.actuator_names]
     jq, jv, fq, fv = [], [], [], []

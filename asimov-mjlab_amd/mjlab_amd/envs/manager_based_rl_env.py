@@ -1,0 +1,308 @@
+"""Manager-based environments (``src/mjlab/envs/manager_based_env.py`` and
+``src/mjlab/envs/manager_based_rl_env.py``).
+
+Same construction order, step order and reset semantics as the reference
+(``manager_based_rl_env.py:126-176``, ``_reset_idx`` ``:210-245``). What is
+different is *how* a step executes on the device:
+
+* resets are boolean masks, never ``nonzero()`` index lists, and the
+  "any env reset -> ``sim.forward()``" branch is decided on the device by
+  ``mjh_forward_gated`` — so the whole env step (action processing,
+  ``decimation`` physics steps, terminations, rewards, masked resets, the gated
+  forward, commands, interval events, observations) has no host sync and is
+  captured into ONE HIP graph, replayed each call to ``step``;
+* host-side schedules (curricula on ``common_step_counter``) run before the
+  replay; if they change a value baked into the graph (a reward weight), the
+  graph is re-captured. Command ranges live in device tensors and need no
+  re-capture.
+
+Returned tensors are the graph's persistent buffers: they are overwritten by
+the next ``step`` (clone to keep them), as with any CUDA/HIP graph output.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Any
+
+import numpy as np
+import torch
+
+from mjlab_amd.envs.mdp.events import reset_scene_to_default
+from mjlab_amd.managers.action_manager import ActionManager
+from mjlab_amd.managers.command_manager import CommandManager, NullCommandManager
+from mjlab_amd.managers.curriculum_manager import CurriculumManager, NullCurriculumManager
+from mjlab_amd.managers.event_manager import EventManager
+from mjlab_amd.managers.manager_base import as_mask
+from mjlab_amd.managers.manager_term_config import EventTermCfg
+from mjlab_amd.managers.observation_manager import ObservationManager
+from mjlab_amd.managers.reward_manager import RewardManager
+from mjlab_amd.managers.termination_manager import TerminationManager
+from mjlab_amd.scene import Scene, SceneCfg
+from mjlab_amd.sim.sim import Simulation, SimulationCfg
+
+
+@dataclass
+class Box:
+  """Shape-only stand-in for ``gym.spaces.Box`` (gymnasium is not a dependency)."""
+
+  shape: tuple[int, ...]
+  low: float = -math.inf
+  high: float = math.inf
+
+
+@dataclass(kw_only=True)
+class ManagerBasedEnvCfg:
+  decimation: int
+  scene: SceneCfg
+  observations: dict
+  actions: dict
+  events: dict = field(default_factory=lambda: {"reset_scene_to_default": EventTermCfg(func=reset_scene_to_default, mode="reset")})
+  seed: int | None = None
+  sim: SimulationCfg = field(default_factory=SimulationCfg)
+  viewer: Any = None
+
+
+@dataclass(kw_only=True)
+class ManagerBasedRlEnvCfg(ManagerBasedEnvCfg):
+  episode_length_s: float
+  rewards: dict
+  terminations: dict
+  commands: dict | None = None
+  curriculum: dict | None = None
+  is_finite_horizon: bool = False
+
+
+def seed_rng(seed: int) -> None:
+  """``src/mjlab/utils/random.py``: seed python/numpy/torch."""
+  import random
+
+  random.seed(seed)
+  np.random.seed(seed)
+  torch.manual_seed(seed)
+
+
+class ManagerBasedEnv:
+  def __init__(self, cfg: ManagerBasedEnvCfg, device: str) -> None:
+    self.cfg = cfg
+    if cfg.seed is not None:
+      cfg.seed = self.seed(cfg.seed)
+    self._sim_step_counter = 0
+    self.extras: dict = {"log": {}}
+    self.obs_buf: dict = {}
+    self.scene = Scene(cfg.scene, device=device)
+    self.sim = Simulation(num_envs=self.scene.num_envs, cfg=cfg.sim, model=self.scene.compile(), device=device)
+    if "cuda" in str(device) and torch.cuda.is_available():
+      torch.cuda.set_device(device)
+    self.scene.initialize(self.sim.mj_model, self.sim.model, self.sim.data)
+    self.load_managers()
+
+  num_envs = property(lambda self: self.scene.num_envs)
+  physics_dt = property(lambda self: self.cfg.sim.mujoco.timestep)
+  step_dt = property(lambda self: self.cfg.sim.mujoco.timestep * self.cfg.decimation)
+  device = property(lambda self: self.sim.device)
+
+  def load_managers(self) -> None:
+    self.event_manager = EventManager(self.cfg.events, self)
+    self.sim.expand_model_fields(self.event_manager.domain_randomization_fields)
+    self.action_manager = ActionManager(self.cfg.actions, self)
+    self.observation_manager = ObservationManager(self.cfg.observations, self)
+    if type(self) is ManagerBasedEnv and "startup" in self.event_manager.available_modes:
+      self.event_manager.apply(mode="startup")
+      self.sim.create_graph()
+
+  @staticmethod
+  def seed(seed: int = -1) -> int:
+    if seed == -1:
+      seed = int(np.random.randint(0, 10_000))
+    seed_rng(seed)
+    return seed
+
+  def reset(self, *, seed: int | None = None, env_ids=None, options=None):
+    del options
+    if seed is not None:
+      self.seed(seed)
+    self._reset_idx(as_mask(env_ids, self.num_envs, self.device))
+    self.scene.write_data_to_sim()
+    self.sim.forward()
+    self.obs_buf = self.observation_manager.compute(update_history=True)
+    return self.obs_buf, self.extras
+
+  def step(self, action: torch.Tensor):
+    self.action_manager.process_action(action.to(self.device))
+    for _ in range(self.cfg.decimation):
+      self._sim_step_counter += 1
+      self.action_manager.apply_action()
+      self.scene.write_data_to_sim()
+      self.sim.step()
+      self.scene.update(dt=self.physics_dt)
+    if "interval" in self.event_manager.available_modes:
+      self.event_manager.apply(mode="interval", dt=self.step_dt)
+    self.obs_buf = self.observation_manager.compute(update_history=True)
+    return self.obs_buf, self.extras
+
+  def close(self) -> None:
+    pass
+
+  def _reset_idx(self, mask: torch.Tensor) -> None:
+    self.scene.reset(mask)
+    if "reset" in self.event_manager.available_modes:
+      self.event_manager.apply(mode="reset", env_ids=mask, global_env_step_count=self._sim_step_counter // self.cfg.decimation)
+    log = self.extras.setdefault("log", {})
+    log.update(self.observation_manager.reset(mask))
+    log.update(self.action_manager.reset(mask))
+    log.update(self.event_manager.reset(mask))
+
+
+class ManagerBasedRlEnv(ManagerBasedEnv):
+  is_vector_env = True
+  metadata = {"render_modes": [None]}
+
+  def __init__(self, cfg: ManagerBasedRlEnvCfg, device: str, render_mode: str | None = None, use_graph: bool | None = None, **kwargs) -> None:
+    del kwargs
+    self.common_step_counter = 0
+    self.episode_length_buf = torch.zeros(cfg.scene.num_envs, device=device, dtype=torch.long)
+    self.render_mode = render_mode
+    super().__init__(cfg=cfg, device=device)
+    n = self.num_envs
+    self.reset_buf = torch.zeros(n, dtype=torch.bool, device=self.device)
+    self.reset_terminated = torch.zeros_like(self.reset_buf)
+    self.reset_time_outs = torch.zeros_like(self.reset_buf)
+    self.reward_buf = torch.zeros(n, device=self.device)
+    self._any_reset = torch.zeros(1, dtype=torch.bool, device=self.device)
+    self._env_step_t = torch.zeros((), dtype=torch.long, device=self.device)
+    self._action_in = torch.zeros(n, self.action_manager.total_action_dim, device=self.device)
+    self.use_graph = (str(self.device).startswith("cuda") and torch.cuda.is_available()) if use_graph is None else use_graph
+    self._graph: torch.cuda.CUDAGraph | None = None
+    self._graph_key = None
+    self._graph_out = None
+    self._eager_steps = 0
+    self.metadata = dict(self.metadata, render_fps=1.0 / self.step_dt)
+
+  @property
+  def max_episode_length_s(self) -> float:
+    return self.cfg.episode_length_s
+
+  @property
+  def max_episode_length(self) -> int:
+    return math.ceil(self.max_episode_length_s / self.step_dt)
+
+  def load_managers(self) -> None:
+    self.command_manager = CommandManager(self.cfg.commands, self) if self.cfg.commands is not None else NullCommandManager()
+    super().load_managers()
+    self.termination_manager = TerminationManager(self.cfg.terminations, self)
+    self.reward_manager = RewardManager(self.cfg.rewards, self)
+    self.curriculum_manager = (
+      CurriculumManager(self.cfg.curriculum, self) if self.cfg.curriculum is not None else NullCurriculumManager()
+    )
+    self._configure_spaces()
+    if "startup" in self.event_manager.available_modes:
+      self.event_manager.apply(mode="startup")
+      self.sim.create_graph()
+
+  def _configure_spaces(self) -> None:
+    self.single_observation_space = {}
+    for g, dim in self.observation_manager.group_obs_dim.items():
+      if self.observation_manager.group_obs_concatenate[g]:
+        self.single_observation_space[g] = Box(shape=tuple(dim))
+      else:
+        names = self.observation_manager.active_terms[g]
+        self.single_observation_space[g] = {t: Box(shape=tuple(d)) for t, d in zip(names, dim)}
+    self.single_action_space = Box(shape=(sum(self.action_manager.action_term_dim),))
+    self.action_space = Box(shape=(self.num_envs, *self.single_action_space.shape))
+
+  # ---- stepping ----
+  def step(self, action: torch.Tensor):
+    self._host_schedules()
+    self._action_in.copy_(action.to(self.device))
+    if self.use_graph and self._eager_steps >= 1:
+      key = self._capture_key()
+      if self._graph is None or key != self._graph_key:
+        self._capture(key)
+      self._graph.replay()
+      self.obs_buf = self._graph_out[0]
+      self.extras["log"] = dict(self._graph_out[1])
+    else:
+      self._step_body()
+      self._eager_steps += 1
+    self.extras["log"].update(self._curriculum_log)
+    self._sim_step_counter += self.cfg.decimation
+    self.common_step_counter += 1
+    return self.obs_buf, self.reward_buf, self.reset_terminated, self.reset_time_outs, self.extras
+
+  def _host_schedules(self) -> None:
+    """Host-side curriculum (``_reset_idx`` runs it first in the reference;
+    the velocity curricula depend only on ``common_step_counter``)."""
+    self._curriculum_log = {}
+    if not isinstance(self.curriculum_manager, NullCurriculumManager):
+      self.curriculum_manager.compute(env_ids=None)
+      self._curriculum_log = self.curriculum_manager.reset(None)
+    for name in self.command_manager.active_terms:
+      t = self.command_manager.get_term(name)
+      if hasattr(t, "sync_ranges"):
+        t.sync_ranges()
+
+  def _capture_key(self):
+    w = tuple(float(c.weight) for c in self.reward_manager._term_cfgs)
+    return (w, self.sim.struct_version)
+
+  def _capture(self, key) -> None:
+    self._graph = None
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+      self._step_body()
+      out = (self.obs_buf, dict(self.extras["log"]))
+    self._graph, self._graph_key, self._graph_out = g, key, out
+
+  def _step_body(self) -> None:
+    self.action_manager.process_action(self._action_in)
+    for _ in range(self.cfg.decimation):
+      self.action_manager.apply_action()
+      self.scene.write_data_to_sim()
+      self.sim.step()
+      self.scene.update(dt=self.physics_dt)
+    self.episode_length_buf += 1
+    self._env_step_t += 1
+    self.reset_buf.copy_(self.termination_manager.compute())
+    self.reset_terminated.copy_(self.termination_manager.terminated)
+    self.reset_time_outs.copy_(self.termination_manager.time_outs)
+    self.reward_buf.copy_(self.reward_manager.compute(dt=self.step_dt))
+    self._reset_idx(self.reset_buf)
+    self.scene.write_data_to_sim()
+    self._any_reset.copy_(self.reset_buf.any().view(1))
+    self.sim.forward_gated(self._any_reset)
+    self.command_manager.compute(dt=self.step_dt)
+    if "interval" in self.event_manager.available_modes:
+      self.event_manager.apply(mode="interval", dt=self.step_dt)
+    self.obs_buf = self.observation_manager.compute(update_history=True)
+
+  def reset(self, *, seed: int | None = None, env_ids=None, options=None):
+    del options
+    if seed is not None:
+      self.seed(seed)
+    mask = as_mask(env_ids, self.num_envs, self.device)
+    self._reset_idx(mask)
+    self.scene.write_data_to_sim()
+    self.sim.forward()
+    self.obs_buf = self.observation_manager.compute(update_history=True)
+    self._graph = None  # observation buffers were re-bound
+    self._eager_steps = 0
+    return self.obs_buf, self.extras
+
+  def _reset_idx(self, mask: torch.Tensor) -> None:
+    self.scene.reset(mask)
+    if "reset" in self.event_manager.available_modes:
+      self.event_manager.apply(mode="reset", env_ids=mask, global_env_step_count=self._env_step_t)
+    log = self.extras.setdefault("log", {})
+    log.update(self.observation_manager.reset(mask))
+    log.update(self.action_manager.reset(mask))
+    log.update(self.reward_manager.reset(mask))
+    log.update(self.command_manager.reset(mask))
+    log.update(self.event_manager.reset(mask))
+    log.update(self.termination_manager.reset(mask))
+    self.episode_length_buf.masked_fill_(mask, 0)
+
+  def render(self):
+    return None

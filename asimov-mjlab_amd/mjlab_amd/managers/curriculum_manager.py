@@ -8,6 +8,8 @@ from __future__ import annotations
 
 import torch
 
+from mjlab_amd.managers.manager_base import resolve_params
+
 
 class CurriculumManager:
   def __init__(self, cfg: dict, env) -> None:
@@ -17,6 +19,7 @@ class CurriculumManager:
     for name, tcfg in cfg.items():
       if tcfg is None:
         continue
+      resolve_params(env, tcfg)
       if isinstance(tcfg.func, type):
         tcfg.func = tcfg.func(tcfg, env)
       self._term_names.append(name)

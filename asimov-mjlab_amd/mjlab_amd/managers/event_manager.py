@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import torch
 
-from mjlab_amd.managers.manager_base import as_mask
+from mjlab_amd.managers.manager_base import as_mask, resolve_params
 
 
 class EventManager:
@@ -27,6 +27,7 @@ class EventManager:
     for name, tcfg in cfg.items():
       if tcfg is None:
         continue
+      resolve_params(env, tcfg)
       if isinstance(tcfg.func, type):
         tcfg.func = tcfg.func(tcfg, env)
       self._mode_term_names.setdefault(tcfg.mode, []).append(name)

@@ -26,6 +26,15 @@ def masked_mean(x: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
   return (x * w).sum() / w.sum().clamp(min=1.0)
 
 
+def resolve_params(env, term_cfg) -> None:
+  """Resolve SceneEntityCfg params against the scene (manager_base.py:86-93)."""
+  from mjlab_amd.managers.scene_entity_config import SceneEntityCfg
+
+  for value in getattr(term_cfg, "params", {}).values():
+    if isinstance(value, SceneEntityCfg):
+      value.resolve(env.scene)
+
+
 class ManagerTermBase:
   def __init__(self, env) -> None:
     self._env = env

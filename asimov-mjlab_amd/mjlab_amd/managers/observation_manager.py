@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import torch
 
-from mjlab_amd.managers.manager_base import as_mask
+from mjlab_amd.managers.manager_base import as_mask, resolve_params
 
 
 class ObservationManager:
@@ -32,6 +32,7 @@ class ObservationManager:
         if gcfg.history_length is not None:
           tcfg.history_length = gcfg.history_length
           tcfg.flatten_history_dim = gcfg.flatten_history_dim
+        resolve_params(env, tcfg)
         if isinstance(tcfg.func, type):
           tcfg.func = tcfg.func(tcfg, env)
           self._class_terms.append(tcfg.func)

@@ -4,7 +4,7 @@ from __future__ import annotations
 
 import torch
 
-from mjlab_amd.managers.manager_base import as_mask, masked_mean
+from mjlab_amd.managers.manager_base import as_mask, masked_mean, resolve_params
 
 
 class RewardManager:
@@ -17,6 +17,7 @@ class RewardManager:
     for name, tcfg in cfg.items():
       if tcfg is None:
         continue
+      resolve_params(env, tcfg)
       if isinstance(tcfg.func, type):
         tcfg.func = tcfg.func(tcfg, env)
         self._class_term_cfgs.append(tcfg)

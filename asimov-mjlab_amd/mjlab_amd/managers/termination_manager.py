@@ -4,7 +4,7 @@ from __future__ import annotations
 
 import torch
 
-from mjlab_amd.managers.manager_base import as_mask
+from mjlab_amd.managers.manager_base import as_mask, resolve_params
 
 
 class TerminationManager:
@@ -15,6 +15,7 @@ class TerminationManager:
     for name, tcfg in cfg.items():
       if tcfg is None:
         continue
+      resolve_params(env, tcfg)
       if isinstance(tcfg.func, type):
         tcfg.func = tcfg.func(tcfg, env)
         self._class_term_cfgs.append(tcfg)

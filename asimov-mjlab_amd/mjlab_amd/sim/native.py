@@ -33,6 +33,7 @@ EXPORTS = (
   "mjh_efc_capacity",
   "mjh_step",
   "mjh_forward",
+  "mjh_forward_gated",
   "mjh_repeat",
 )
 
@@ -64,6 +65,8 @@ def lib() -> ctypes.CDLL:
   for f in (L.mjh_step, L.mjh_forward):
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     f.restype = ctypes.c_int
+  L.mjh_forward_gated.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+  L.mjh_forward_gated.restype = ctypes.c_int
   L.mjh_repeat.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")

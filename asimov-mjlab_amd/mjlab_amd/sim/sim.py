@@ -194,6 +194,8 @@ class Simulation:
     for name, t in self._data_flat.items():
       setattr(ds, name, t.data_ptr())
     self._mstruct, self._dstruct = ms, ds
+    # bumped whenever the descriptors change: graphs that baked them are stale
+    self.struct_version = getattr(self, "struct_version", 0) + 1
 
   def _native_ok(self) -> bool:
     try:
@@ -307,13 +309,32 @@ class Simulation:
 
   def forward(self) -> None:
     self._require_gpu()
-    if self.forward_graph is not None:
+    if self.forward_graph is not None and not torch.cuda.is_current_stream_capturing():
       self.forward_graph.replay()
     else:
       self._launch_forward()
 
+  def forward_gated(self, gate: torch.Tensor) -> None:
+    """``forward()`` for all worlds iff the device scalar ``gate`` is non-zero.
+
+    The decision is taken on the device, so the env step can call this inside
+    a captured graph where the reference syncs on ``len(reset_env_ids) > 0``
+    (``manager_based_rl_env.py:155-160``)."""
+    self._require_gpu()
+    if gate.dtype not in (torch.bool, torch.uint8) or gate.numel() != 1 or not gate.is_cuda:
+      raise ValueError("gate must be a one-element bool/uint8 device tensor")
+    native.check(
+      native.lib().mjh_forward_gated(
+        ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), ctypes.c_void_p(gate.data_ptr()), self._stream()
+      ),
+      "mjh_forward_gated",
+    )
+
   def step(self) -> None:
     self._require_gpu()
+    if torch.cuda.is_current_stream_capturing():
+      self._launch_step()  # being captured into an enclosing (env-step) graph
+      return
     with self.nan_guard.watch(self.data):
       if self.step_graph is not None:
         self.step_graph.replay()

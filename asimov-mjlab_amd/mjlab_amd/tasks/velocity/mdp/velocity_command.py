@@ -1,0 +1,119 @@
+"""Uniform velocity command (``src/mjlab/tasks/velocity/mdp/velocity_command.py:22-123``).
+
+Mask-based and capturable: resampling draws for all envs and selects with the
+mask; ``ranges`` are mirrored into a device tensor (``sync_ranges``, called by
+the env on the host before each step) so curricula that edit
+``cfg.ranges`` take effect without re-capturing the step graph.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from mjlab_amd.managers.command_manager import CommandTerm
+from mjlab_amd.managers.manager_term_config import CommandTermCfg
+from mjlab_amd.utils.math import quat_apply, wrap_to_pi
+
+
+class UniformVelocityCommand(CommandTerm):
+  def __init__(self, cfg: "UniformVelocityCommandCfg", env) -> None:
+    super().__init__(cfg, env)
+    if cfg.heading_command and cfg.ranges.heading is None:
+      raise ValueError("heading_command=True but ranges.heading is set to None.")
+    if cfg.ranges.heading and not cfg.heading_command:
+      raise ValueError("ranges.heading is set but heading_command=False.")
+    self.robot = env.scene[cfg.asset_name]
+    n = self.num_envs
+    self.vel_command_b = torch.zeros(n, 3, device=self.device)
+    self.heading_target = torch.zeros(n, device=self.device)
+    self.heading_error = torch.zeros(n, device=self.device)
+    self.is_heading_env = torch.zeros(n, dtype=torch.bool, device=self.device)
+    self.is_standing_env = torch.zeros_like(self.is_heading_env)
+    self.metrics["error_vel_xy"] = torch.zeros(n, device=self.device)
+    self.metrics["error_vel_yaw"] = torch.zeros(n, device=self.device)
+    self._ranges_t = torch.zeros(4, 2, device=self.device)
+    self._ranges_host = None
+    self.sync_ranges()
+
+  @property
+  def command(self) -> torch.Tensor:
+    return self.vel_command_b
+
+  def sync_ranges(self) -> None:
+    r = self.cfg.ranges
+    host = (tuple(r.lin_vel_x), tuple(r.lin_vel_y), tuple(r.ang_vel_z), tuple(r.heading) if r.heading else (0.0, 0.0))
+    if host != self._ranges_host:
+      self._ranges_t.copy_(torch.tensor(host, dtype=torch.float32))
+      self._ranges_host = host
+
+  def _u(self, i: int) -> torch.Tensor:
+    lo, hi = self._ranges_t[i, 0], self._ranges_t[i, 1]
+    return torch.rand(self.num_envs, device=self.device) * (hi - lo) + lo
+
+  def _update_metrics(self) -> None:
+    max_command_step = self.cfg.resampling_time_range[1] / self._env.step_dt
+    d = self.robot.data
+    self.metrics["error_vel_xy"] += torch.norm(self.vel_command_b[:, :2] - d.root_link_lin_vel_b[:, :2], dim=-1) / max_command_step
+    self.metrics["error_vel_yaw"] += torch.abs(self.vel_command_b[:, 2] - d.root_link_ang_vel_b[:, 2]) / max_command_step
+
+  def _resample_command(self, mask: torch.Tensor) -> None:
+    new = torch.stack([self._u(0), self._u(1), self._u(2)], dim=-1)
+    self.vel_command_b.copy_(torch.where(mask[:, None], new, self.vel_command_b))
+    if self.cfg.heading_command:
+      self.heading_target.copy_(torch.where(mask, self._u(3), self.heading_target))
+      hv = torch.rand(self.num_envs, device=self.device) <= self.cfg.rel_heading_envs
+      self.is_heading_env.copy_(torch.where(mask, hv, self.is_heading_env))
+    sv = torch.rand(self.num_envs, device=self.device) <= self.cfg.rel_standing_envs
+    self.is_standing_env.copy_(torch.where(mask, sv, self.is_standing_env))
+    if self.cfg.init_velocity_prob > 0.0:
+      iv = mask & (torch.rand(self.num_envs, device=self.device) < self.cfg.init_velocity_prob)
+      d = self.robot.data
+      lin_b = d.root_link_lin_vel_b.clone()
+      lin_b[:, :2] = self.vel_command_b[:, :2]
+      ang_b = d.root_link_ang_vel_b.clone()
+      ang_b[:, 2] = self.vel_command_b[:, 2]
+      state = torch.cat([d.root_link_pos_w, d.root_link_quat_w, quat_apply(d.root_link_quat_w, lin_b), ang_b], dim=-1)
+      self.robot.write_root_state_to_sim(state, iv)
+
+  def _update_command(self) -> None:
+    if self.cfg.heading_command:
+      self.heading_error.copy_(wrap_to_pi(self.heading_target - self.robot.data.heading_w))
+      yaw = torch.clamp(self.cfg.heading_control_stiffness * self.heading_error, self._ranges_t[2, 0], self._ranges_t[2, 1])
+      self.vel_command_b[:, 2] = torch.where(self.is_heading_env, yaw, self.vel_command_b[:, 2])
+    self.vel_command_b.masked_fill_(self.is_standing_env[:, None], 0.0)
+
+
+@dataclass(kw_only=True)
+class UniformVelocityCommandCfg(CommandTermCfg):
+  asset_name: str
+  heading_command: bool = False
+  heading_control_stiffness: float = 1.0
+  rel_standing_envs: float = 0.0
+  rel_heading_envs: float = 1.0
+  init_velocity_prob: float = 0.0
+  class_type: type = UniformVelocityCommand
+
+  @dataclass
+  class Ranges:
+    lin_vel_x: tuple[float, float]
+    lin_vel_y: tuple[float, float]
+    ang_vel_z: tuple[float, float]
+    heading: tuple[float, float] | None = None
+
+  ranges: Ranges
+
+  @dataclass
+  class VizCfg:
+    z_offset: float = 0.2
+    scale: float = 0.5
+
+  viz: VizCfg = field(default_factory=VizCfg)
+
+  def __post_init__(self):
+    if self.heading_command and self.ranges.heading is None:
+      raise ValueError(
+        "The velocity command has heading commands active (heading_command=True) but "
+        "the `ranges.heading` parameter is set to None."
+      )

@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Benchmark: env steps/s on Mjlab-Velocity-Flat-Unitree-G1 @ 4096 envs/GPU.
+
+Contract ("Measurement"):
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--num-envs E]
+One process per GPU (torch.distributed.run for N > 1, RCCL backend). Each rank
+owns its own 4096-env environment (seed 42 + rank) — worlds are independent, so
+the work shards with weak scaling; after every env step the ranks all-gather
+the learner-facing outputs (policy obs, critic obs, reward, terminated,
+truncated) over RCCL, the one exchange the north star names.
+
+A "step" is one full env step of the manager-based RL env: action processing,
+4 physics sub-steps (the HIP step kernel), terminations, rewards, masked
+resets + gated forward, commands, push events and observations — captured in
+one HIP graph. Actions come from the random agent of the reference's
+`play --agent random` (2*U[0,1)-1, torch.Generator seeded 1234).
+
+Rank 0 prints ONE JSON line with, in addition to the contract fields:
+  roofline      — the dominant kernel (the fused physics step) measured live
+                  with HIP events on its stream: algorithmic bytes per launch
+                  (5,384 B per world per physics step) / average
+                  launch duration, against the 8 TB/s HBM peak. `traffic` is the
+                  PMC-measured HBM bytes per launch from profiles/ (or null).
+  cpu_baseline  — the CPU restatement (oracle/, float64, OpenMP over worlds) of
+                  the same physics step on this host's cores, bounded sample.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "asimov-mjlab_amd"))
+
+TASK = "Mjlab-Velocity-Flat-Unitree-G1"
+METRIC = "env steps/sec (whole node), Unitree G1 flat velocity task @ 4096 envs/GPU"
+B_PHYS_G1 = 5384  # algorithmic bytes per world per physics step
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse() -> argparse.Namespace:
+  p = argparse.ArgumentParser()
+  p.add_argument("--gpus", type=int, default=1)
+  p.add_argument("--steps", type=int, default=300)
+  p.add_argument("--warmup", type=int, default=30)
+  p.add_argument("--num-envs", type=int, default=4096)
+  p.add_argument("--task", default=TASK)
+  p.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL all-gather (N > 1)")
+  p.add_argument("--no-cpu-baseline", action="store_true")
+  p.add_argument("--cpu-sample-worlds", type=int, default=512)
+  p.add_argument("--kernel-launches", type=int, default=50)
+  return p.parse_args()
+
+
+def cpu_baseline(env, args) -> dict:
+  """Time the oracle (CPU restatement of the same physics step, float64,
+  OpenMP over worlds) on a bounded sample of this workload's worlds."""
+  sys.path.insert(0, str(REPO))
+  from oracle.oracle import Oracle
+
+  try:
+    cores = len(os.sched_getaffinity(0))
+  except AttributeError:
+    cores = os.cpu_count() or 1
+  cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
+  n = min(args.cpu_sample_worlds, env.num_envs)
+  d = env.sim.data
+  state = {k: getattr(d, k)[:n].detach().cpu().numpy() for k in ("qpos", "qvel", "act", "qacc_warmstart", "ctrl", "qfrc_applied", "xfrc_applied", "time")}
+  overrides = {}
+  m = env.sim.model
+  for name in env.event_manager.domain_randomization_fields:
+    overrides[name] = getattr(m, name)[:n].detach().cpu().numpy()
+  orc = Oracle(env.sim.mj_model, "f64", overrides=overrides)
+  orc.run(n, state, integrate=True, nthreads=cores)  # warm
+  reps, t0 = 0, time.perf_counter()
+  while True:
+    out = orc.run(n, state, integrate=True, nthreads=cores)
+    for k in ("qpos", "qvel", "qacc_warmstart", "time"):
+      state[k] = out[k]
+    reps += 1
+    el = time.perf_counter() - t0
+    if el > 10.0 or reps >= 400:
+      break
+  phys_per_s = n * reps / el
+  dec = env.cfg.decimation
+  return {
+    "value": phys_per_s / dec,
+    "unit": "env steps/sec (physics only: decimation x mj_step per env step)",
+    "cores": cores,
+    "kind": "port",
+    "sample": f"{n} G1 worlds x {reps} physics steps ({el:.1f} s) from the bench's live state, float64 oracle "
+    f"(oracle/oracle.c, OpenMP {cores} threads); env-layer cost excluded; MuJoCo C is not available",
+  }
+
+
+def main() -> None:
+  args = parse()
+  import torch
+  import torch.distributed as dist
+
+  world = int(os.environ.get("WORLD_SIZE", "1"))
+  rank = int(os.environ.get("RANK", "0"))
+  local = int(os.environ.get("LOCAL_RANK", "0"))
+  if world > 1:
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+  torch.cuda.set_device(local)
+  dev = f"cuda:{local}"
+
+  from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
+  from mjlab_amd.tasks import load_env_cfg
+
+  cfg = load_env_cfg(args.task)
+  cfg.scene.num_envs = args.num_envs
+  cfg.seed = 42 + rank
+  env = ManagerBasedRlEnv(cfg, device=dev)
+  env.reset()
+  gen = torch.Generator(device=dev)
+  gen.manual_seed(1234 + rank)
+  act = torch.empty(env.num_envs, env.action_manager.total_action_dim, device=dev)
+
+  def agent():
+    act.uniform_(0.0, 1.0, generator=gen)
+    return act.mul_(2.0).sub_(1.0)
+
+  gather_buf = None
+
+  def exchange(obs, rew, term, trunc):
+    nonlocal gather_buf
+    if world == 1 or args.no_gather:
+      return
+    packed = torch.cat([obs["policy"], obs["critic"], rew[:, None], term[:, None].float(), trunc[:, None].float()], dim=1)
+    if gather_buf is None:
+      gather_buf = torch.empty((world * packed.shape[0], packed.shape[1]), device=dev)
+    dist.all_gather_into_tensor(gather_buf, packed)
+
+  # graph capture happens on the 2nd step; these two setup steps are untimed
+  for _ in range(2 + args.warmup):
+    o, r, te, tr, _ = env.step(agent())
+    exchange(o, r, te, tr)
+  torch.cuda.synchronize()
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    o, r, te, tr, _ = env.step(agent())
+    exchange(o, r, te, tr)
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+  el = time.perf_counter() - t0
+  if world > 1:
+    t = torch.tensor([el], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+  n_total = args.num_envs * world
+  value = n_total * args.steps / el
+
+  # ---- dominant kernel: the fused physics step, HIP events on its stream ----
+  sim = env.sim
+  stream = torch.cuda.current_stream()
+  nefc = sim.data.nefc.float().mean().item()
+  niter = sim.data.solver_niter.float().mean().item()
+  e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+  L = args.kernel_launches
+  sim.step()
+  e0.record(stream)
+  for _ in range(L):
+    sim.step()
+  e1.record(stream)
+  torch.cuda.synchronize()
+  t_launch = e0.elapsed_time(e1) / 1e3 / L  # s per physics step (pack + step kernels)
+  bytes_per_launch = B_PHYS_G1 * args.num_envs
+  achieved = bytes_per_launch / t_launch / 1e9
+  traffic = None
+  tf = REPO / "profiles" / "step_kernel_traffic.json"
+  if tf.exists():
+    try:
+      tj = json.loads(tf.read_text())
+      if int(tj.get("num_envs", -1)) == args.num_envs:
+        traffic = tj.get("bytes_per_launch")
+    except (ValueError, OSError):
+      traffic = None
+  nv = sim.mj_model.nv
+  b_solve = niter * 4 * (nefc * nv + nv * nv + 6 * nefc + 4 * nv) + 4 * (nefc + 2 * nv)
+
+  cpu = None
+  if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    try:
+      cpu = cpu_baseline(env, args)
+    except Exception as e:  # noqa: BLE001 - a missing oracle build must not void the GPU line
+      cpu = {"value": None, "unit": "env steps/sec", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
+
+  if rank == 0:
+    line = {
+      "metric": METRIC,
+      "value": value,
+      "unit": "env steps/s",
+      "n_gpus": world,
+      "steps": args.steps,
+      "warmup": args.warmup,
+      "ms_per_step": el / args.steps * 1e3,
+      "higher_is_better": True,
+      "scaling": "weak",
+      "vs_baseline": None,
+      "dtype": "f32",
+      "data": "synthetic: random agent 2*U[0,1)-1 (seed 1234+rank), env seed 42+rank, DR/pushes/resets/commands on",
+      "config": {
+        "workload": f"{args.task}, num_envs={args.num_envs}/GPU, random agent",
+        "num_envs_per_gpu": args.num_envs,
+        "decimation": env.cfg.decimation,
+        "physics_steps_per_s": value * env.cfg.decimation,
+        "parallelism": f"env-sharded x{world}" + ("" if world == 1 or args.no_gather else " + RCCL all-gather of obs/reward/dones"),
+        "mean_nefc": nefc,
+        "mean_solver_iters": niter,
+      },
+      "roofline": {
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic,
+        "kernel": "step_kernel (+pack_kernel), one launch per physics step",
+        "launch_us": t_launch * 1e6,
+        "bytes_per_launch": bytes_per_launch,
+        "solver_streamed_model_gbs": b_solve * args.num_envs / t_launch / 1e9,
+      },
+      "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+  if world > 1:
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+  main()

@@ -1,0 +1,21 @@
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "asimov-mjlab_amd"))
+sys.path.insert(0, str(ROOT))
+
+
+def pytest_configure(config):
+  config.addinivalue_line("markers", "gpu: needs an MI355X (HIP step library on cuda:0)")
+
+
+@pytest.fixture(scope="session")
+def gpu():
+  import torch
+
+  if not torch.cuda.is_available():
+    pytest.skip("no GPU")
+  return "cuda:0"
