@@ -64,15 +64,14 @@ def reset_joints_by_offset(env, env_ids, position_range: tuple[float, float], ve
                            asset_cfg: SceneEntityCfg = _DEFAULT) -> None:
   m = as_mask(env_ids, env.num_envs, env.device)
   a = env.scene[asset_cfg.name]
-  j = asset_cfg.joint_ids
+  j = asset_cfg.joint_idx
   jp = a.data.default_joint_pos[:, j].clone()
   jp += torch.rand_like(jp) * (position_range[1] - position_range[0]) + position_range[0]
   lim = a.data.soft_joint_pos_limits[:, j]
   jp = jp.clamp_(lim[..., 0], lim[..., 1])
   jv = a.data.default_joint_vel[:, j].clone()
   jv += torch.rand_like(jv) * (velocity_range[1] - velocity_range[0]) + velocity_range[0]
-  jids = None if isinstance(j, slice) else torch.tensor(j, device=env.device)
-  a.write_joint_state_to_sim(jp, jv, env_ids=m, joint_ids=jids)
+  a.write_joint_state_to_sim(jp, jv, env_ids=m, joint_ids=None if isinstance(j, slice) else j)
 
 
 def push_by_setting_velocity(env, env_ids, velocity_range: dict, asset_cfg: SceneEntityCfg = _DEFAULT) -> None:
@@ -89,7 +88,7 @@ def apply_external_force_torque(env, env_ids, force_range, torque_range, asset_c
   nb = len(asset_cfg.body_ids) if isinstance(asset_cfg.body_ids, list) else a.num_bodies
   f = torch.rand(env.num_envs, nb, 3, device=env.device) * (force_range[1] - force_range[0]) + force_range[0]
   t = torch.rand(env.num_envs, nb, 3, device=env.device) * (torque_range[1] - torque_range[0]) + torque_range[0]
-  a.write_external_wrench_to_sim(f, t, env_ids=m, body_ids=asset_cfg.body_ids)
+  a.write_external_wrench_to_sim(f, t, env_ids=m, body_ids=asset_cfg.body_idx)
 
 
 @dataclass

@@ -23,13 +23,13 @@ def projected_gravity(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor
 
 def joint_pos_rel(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   a = env.scene[asset_cfg.name]
-  j = asset_cfg.joint_ids
+  j = asset_cfg.joint_idx
   return a.data.joint_pos[:, j] - a.data.default_joint_pos[:, j]
 
 
 def joint_vel_rel(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   a = env.scene[asset_cfg.name]
-  j = asset_cfg.joint_ids
+  j = asset_cfg.joint_idx
   return a.data.joint_vel[:, j] - a.data.default_joint_vel[:, j]
 
 

@@ -24,7 +24,7 @@ def joint_torques_l2(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
 
 def joint_acc_l2(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   a = env.scene[asset_cfg.name]
-  return torch.sum(torch.square(a.data.joint_acc[:, asset_cfg.joint_ids]), dim=1)
+  return torch.sum(torch.square(a.data.joint_acc[:, asset_cfg.joint_idx]), dim=1)
 
 
 def action_rate_l2(env) -> torch.Tensor:
@@ -34,9 +34,9 @@ def action_rate_l2(env) -> torch.Tensor:
 def joint_pos_limits(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   a = env.scene[asset_cfg.name]
   lim = a.data.soft_joint_pos_limits
-  q = a.data.joint_pos[:, asset_cfg.joint_ids]
-  out = -(q - lim[:, asset_cfg.joint_ids, 0]).clip(max=0.0)
-  out += (q - lim[:, asset_cfg.joint_ids, 1]).clip(min=0.0)
+  q = a.data.joint_pos[:, asset_cfg.joint_idx]
+  out = -(q - lim[:, asset_cfg.joint_idx, 0]).clip(max=0.0)
+  out += (q - lim[:, asset_cfg.joint_idx, 1]).clip(min=0.0)
   return torch.sum(out, dim=1)
 
 
@@ -51,5 +51,5 @@ class posture:
   def __call__(self, env, std, asset_cfg: SceneEntityCfg) -> torch.Tensor:
     del std
     a = env.scene[asset_cfg.name]
-    err = torch.square(a.data.joint_pos[:, asset_cfg.joint_ids] - self.default_joint_pos[:, asset_cfg.joint_ids])
+    err = torch.square(a.data.joint_pos[:, asset_cfg.joint_idx] - self.default_joint_pos[:, asset_cfg.joint_idx])
     return torch.exp(-torch.mean(err / (self.std**2), dim=1))

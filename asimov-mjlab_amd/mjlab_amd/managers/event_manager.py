@@ -93,7 +93,8 @@ class EventManager:
           last, once = self._reset_last_step[i], self._reset_once[i]
           valid = ((step - last) >= tcfg.min_step_count_between_reset) | ((last == 0) & ~once)
           m = m & valid
-        self._reset_last_step[i].masked_fill_(m, step)
+        last = self._reset_last_step[i]
+        last.copy_(torch.where(m, torch.as_tensor(step, device=last.device) if not isinstance(step, torch.Tensor) else step.to(last.dtype), last))
         self._reset_once[i] |= m
         tcfg.func(self._env, m, **tcfg.params)
       else:

@@ -27,6 +27,13 @@ class SceneEntityCfg:
   site_names: str | tuple[str, ...] | None = None
   site_ids: list[int] | slice = field(default_factory=lambda: slice(None))
   preserve_order: bool = False
+  # device-side copies of the resolved ids (slice(None) when all are selected):
+  # indexing a device tensor with a host list issues an H2D copy, which is
+  # illegal inside the captured env-step graph, so hot-path terms use these.
+  joint_idx: object = field(default_factory=lambda: slice(None), repr=False, compare=False)
+  body_idx: object = field(default_factory=lambda: slice(None), repr=False, compare=False)
+  geom_idx: object = field(default_factory=lambda: slice(None), repr=False, compare=False)
+  site_idx: object = field(default_factory=lambda: slice(None), repr=False, compare=False)
 
   def resolve(self, scene) -> None:
     ent = scene[self.name]
@@ -49,3 +56,9 @@ class SceneEntityCfg:
       elif isinstance(ids, list):
         all_names = getattr(ent, names_attr)
         setattr(self, names_attr, [all_names[i] for i in ids])
+    import torch
+
+    for _, ids_attr, _, _ in _FIELDS:
+      ids = getattr(self, ids_attr)
+      idx = slice(None) if isinstance(ids, slice) else torch.tensor(ids, dtype=torch.long, device=scene.device)
+      setattr(self, ids_attr.replace("_ids", "_idx"), idx)

@@ -10,7 +10,7 @@ _DEFAULT = SceneEntityCfg("robot")
 
 
 def foot_height(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
-  return env.scene[asset_cfg.name].data.site_pos_w[:, asset_cfg.site_ids, 2]
+  return env.scene[asset_cfg.name].data.site_pos_w[:, asset_cfg.site_idx, 2]
 
 
 def foot_air_time(env, sensor_name: str) -> torch.Tensor:

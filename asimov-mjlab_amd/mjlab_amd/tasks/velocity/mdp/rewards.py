@@ -42,7 +42,7 @@ def track_angular_velocity(env, std: float, command_name: str, asset_cfg: SceneE
 def flat_orientation(env, std: float, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   a = env.scene[asset_cfg.name]
   if asset_cfg.body_ids and not isinstance(asset_cfg.body_ids, slice):
-    q = a.data.body_link_quat_w[:, asset_cfg.body_ids, :].squeeze(1)
+    q = a.data.body_link_quat_w[:, asset_cfg.body_idx, :].squeeze(1)
     g = quat_apply_inverse(q, a.data.gravity_vec_w)
     xy = torch.sum(torch.square(g[:, :2]), dim=1)
   else:
@@ -55,7 +55,7 @@ def self_collision_cost(env, sensor_name: str) -> torch.Tensor:
 
 
 def body_angular_velocity_penalty(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
-  w = env.scene[asset_cfg.name].data.body_link_ang_vel_w[:, asset_cfg.body_ids, :].squeeze(1)
+  w = env.scene[asset_cfg.name].data.body_link_ang_vel_w[:, asset_cfg.body_idx, :].squeeze(1)
   return torch.sum(torch.square(w[:, :2]), dim=1)
 
 
@@ -79,8 +79,8 @@ def feet_air_time(env, sensor_name: str, threshold_min: float = 0.05, threshold_
 def feet_clearance(env, target_height: float, command_name: str | None = None, command_threshold: float = 0.01,
                    asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   a = env.scene[asset_cfg.name]
-  z = a.data.site_pos_w[:, asset_cfg.site_ids, 2]
-  v = torch.norm(a.data.site_lin_vel_w[:, asset_cfg.site_ids, :2], dim=-1)
+  z = a.data.site_pos_w[:, asset_cfg.site_idx, 2]
+  v = torch.norm(a.data.site_lin_vel_w[:, asset_cfg.site_idx, :2], dim=-1)
   cost = torch.sum(torch.abs(z - target_height) * v, dim=1)
   active = _command_active(env, command_name, command_threshold)
   return cost * active if active is not None else cost
@@ -97,7 +97,7 @@ class feet_swing_height:
                asset_cfg: SceneEntityCfg) -> torch.Tensor:
     a = env.scene[asset_cfg.name]
     cs = env.scene[sensor_name]
-    h = a.data.site_pos_w[:, asset_cfg.site_ids, 2]
+    h = a.data.site_pos_w[:, asset_cfg.site_idx, 2]
     in_air = cs.data.found == 0
     self.peak_heights.copy_(torch.where(in_air, torch.maximum(self.peak_heights, h), self.peak_heights))
     first = cs.compute_first_contact(dt=self.step_dt)
@@ -116,7 +116,7 @@ def feet_slip(env, sensor_name: str, command_name: str, command_threshold: float
   cs = env.scene[sensor_name]
   active = _command_active(env, command_name, command_threshold)
   in_contact = (cs.data.found > 0).float()
-  v = torch.norm(a.data.site_lin_vel_w[:, asset_cfg.site_ids, :2], dim=-1)
+  v = torch.norm(a.data.site_lin_vel_w[:, asset_cfg.site_idx, :2], dim=-1)
   cost = torch.sum(torch.square(v) * in_contact, dim=1) * active
   env.extras["log"]["Metrics/slip_velocity_mean"] = torch.sum(v * in_contact) / torch.clamp(torch.sum(in_contact), min=1)
   return cost
@@ -161,5 +161,5 @@ class variable_posture:
       + self.std_walking * walking.unsqueeze(1)
       + self.std_running * running.unsqueeze(1)
     )
-    err = torch.square(a.data.joint_pos[:, asset_cfg.joint_ids] - self.default_joint_pos[:, asset_cfg.joint_ids])
+    err = torch.square(a.data.joint_pos[:, asset_cfg.joint_idx] - self.default_joint_pos[:, asset_cfg.joint_idx])
     return torch.exp(-torch.mean(err / (std**2), dim=1))

@@ -92,11 +92,11 @@ def quat_from_matrix(matrix: torch.Tensor) -> torch.Tensor:
     ],
     dim=-2,
   )
-  flr = torch.tensor(0.1).to(dtype=q_abs.dtype, device=q_abs.device)
-  cand = quat_by / (2.0 * q_abs[..., None].max(flr))
+  # floor 0.1 as a scalar clamp (a host-made tensor here would be an H2D copy
+  # inside the captured env step); best-conditioned candidate, no sign fix-up
+  cand = quat_by / (2.0 * q_abs[..., None].clamp(min=0.1))
   idx = q_abs.argmax(dim=-1, keepdim=True)
-  out = torch.gather(cand, -2, idx[..., None].expand(*idx.shape, 4)).squeeze(-2)
-  return torch.where(out[..., 0:1] < 0, -out, out)
+  return torch.gather(cand, -2, idx[..., None].expand(*idx.shape, 4)).squeeze(-2)
 
 
 def yaw_quat(quat: torch.Tensor) -> torch.Tensor:

@@ -84,7 +84,7 @@ def cpu_baseline(env, args) -> dict:
       state[k] = out[k]
     reps += 1
     el = time.perf_counter() - t0
-    if el > 10.0 or reps >= 400:
+    if el > 10.0 or reps >= 20000:
       break
   phys_per_s = n * reps / el
   dec = env.cfg.decimation
