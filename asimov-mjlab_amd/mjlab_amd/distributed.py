@@ -1,0 +1,39 @@
+"""Multi-GPU env sharding: one process per GPU, each owning an
+independent shard of worlds; the only exchange is an all-gather of the
+learner-facing step outputs (RCCL over xGMI on the GPU box, gloo in tests)."""
+
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_seed(base_seed: int, rank: int) -> int:
+  """Per-rank env seed (rank r of a 42-seeded job uses 42 + r)."""
+  return base_seed + rank
+
+
+def pack_step_outputs(obs: dict, reward: torch.Tensor, terminated: torch.Tensor, truncated: torch.Tensor) -> torch.Tensor:
+  """(num_envs, D) float32: [obs groups in key order | reward | terminated | truncated]."""
+  parts = [obs[k].reshape(obs[k].shape[0], -1).float() for k in sorted(obs)]
+  parts += [reward[:, None].float(), terminated[:, None].float(), truncated[:, None].float()]
+  return torch.cat(parts, dim=1)
+
+
+class StepGather:
+  """All-gathers each rank's packed step outputs into one (world * num_envs, D)
+  buffer (rank-major) — one collective per env step, no other data-path traffic."""
+
+  def __init__(self, group=None) -> None:
+    self.group = group
+    self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+    self.buf: torch.Tensor | None = None
+
+  def __call__(self, obs, reward, terminated, truncated) -> torch.Tensor:
+    packed = pack_step_outputs(obs, reward, terminated, truncated)
+    if self.world == 1:
+      return packed
+    if self.buf is None or self.buf.shape != (self.world * packed.shape[0], packed.shape[1]):
+      self.buf = torch.empty((self.world * packed.shape[0], packed.shape[1]), dtype=packed.dtype, device=packed.device)
+    dist.all_gather_into_tensor(self.buf, packed.contiguous(), group=self.group)
+    return self.buf

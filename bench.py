@@ -117,7 +117,9 @@ def main() -> None:
 
   cfg = load_env_cfg(args.task)
   cfg.scene.num_envs = args.num_envs
-  cfg.seed = 42 + rank
+  from mjlab_amd.distributed import shard_seed
+
+  cfg.seed = shard_seed(42, rank)
   env = ManagerBasedRlEnv(cfg, device=dev)
   env.reset()
   gen = torch.Generator(device=dev)
@@ -128,16 +130,13 @@ def main() -> None:
     act.uniform_(0.0, 1.0, generator=gen)
     return act.mul_(2.0).sub_(1.0)
 
-  gather_buf = None
+  from mjlab_amd.distributed import StepGather
+
+  gather = StepGather()
 
   def exchange(obs, rew, term, trunc):
-    nonlocal gather_buf
-    if world == 1 or args.no_gather:
-      return
-    packed = torch.cat([obs["policy"], obs["critic"], rew[:, None], term[:, None].float(), trunc[:, None].float()], dim=1)
-    if gather_buf is None:
-      gather_buf = torch.empty((world * packed.shape[0], packed.shape[1]), device=dev)
-    dist.all_gather_into_tensor(gather_buf, packed)
+    if world > 1 and not args.no_gather:
+      gather(obs, rew, term, trunc)
 
   # graph capture happens on the 2nd step; these two setup steps are untimed
   for _ in range(2 + args.warmup):

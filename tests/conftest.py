@@ -19,3 +19,14 @@ def gpu():
   if not torch.cuda.is_available():
     pytest.skip("no GPU")
   return "cuda:0"
+
+
+def pytest_collection_modifyitems(config, items):
+  import torch
+
+  if torch.cuda.is_available():
+    return
+  skip = pytest.mark.skip(reason="needs a GPU (run with -m gpu on the MI355X box)")
+  for it in items:
+    if "gpu" in it.keywords:
+      it.add_marker(skip)

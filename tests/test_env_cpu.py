@@ -1,0 +1,118 @@
+"""Env layer on CPU with the oracle standing in for the physics
+(tests/oracle_sim.py): construction, dims, reset semantics, events, and that
+the env-step body is free of host syncs (so the GPU path can capture it)."""
+
+import math
+
+import pytest
+import torch
+
+from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
+from mjlab_amd.tasks import list_tasks, load_env_cfg
+from tests import oracle_sim
+from tests.capture_guard import CaptureGuard, CaptureHazard
+
+G1 = "Mjlab-Velocity-Flat-Unitree-G1"
+GO1 = "Mjlab-Velocity-Flat-Unitree-Go1"
+
+
+def make(task, n=6, seed=42):
+  cfg = load_env_cfg(task)
+  cfg.scene.num_envs = n
+  cfg.seed = seed
+  env = ManagerBasedRlEnv(cfg, device="cpu")
+  oracle_sim.attach(env.sim, env.event_manager.domain_randomization_fields)
+  return env
+
+
+def test_registry():
+  assert {G1, GO1} <= set(list_tasks())
+
+
+@pytest.mark.parametrize("task,dims,adim", [(G1, (99, 111), 29), (GO1, (48, 72), 12)])
+def test_dims_and_steps(task, dims, adim):
+  env = make(task)
+  assert env.observation_manager.group_obs_dim == {"policy": (dims[0],), "critic": (dims[1],)}
+  assert env.action_manager.total_action_dim == adim
+  obs, _ = env.reset()
+  for _ in range(3):
+    obs, rew, term, trunc, extras = env.step(2 * torch.rand(env.num_envs, adim) - 1)
+  assert obs["policy"].shape == (env.num_envs, dims[0]) and torch.isfinite(obs["critic"]).all()
+  assert rew.shape == (env.num_envs,) and torch.isfinite(rew).all()
+  assert (env.episode_length_buf == 3).all()
+  assert env.max_episode_length == math.ceil(20.0 / 0.02)
+
+
+def test_g1_reward_terms_and_weights():
+  env = make(G1, n=2)
+  w = {n: env.reward_manager.get_term_cfg(n).weight for n in env.reward_manager.active_terms}
+  assert w["track_linear_velocity"] == 2.0 and w["pose"] == 1.0 and w["self_collisions"] == -1.0
+  assert w["angular_momentum"] == -0.02 and w["body_ang_vel"] == -0.05 and w["soft_landing"] == -1e-5
+  assert len(w) == 14
+
+
+def test_foot_friction_randomized_at_startup():
+  env = make(G1, n=16)
+  fr = env.sim.model.geom_friction  # (N, ngeom, 3) after expansion
+  assert fr.shape[0] == 16
+  robot = env.scene["robot"]
+  ids, names = robot.find_geoms(r".*_foot\d_collision")
+  gids = robot.indexing.geom_ids[ids].long()
+  mu = fr[:, gids, 0]
+  assert (mu >= 0.3).all() and (mu <= 1.2).all() and mu.std() > 0.05
+  others = torch.ones(fr.shape[1], dtype=torch.bool)
+  others[gids] = False
+  assert torch.equal(fr[:, others], fr[:1, others].expand(16, -1, -1))
+
+
+def test_time_out_resets_masked_envs():
+  env = make(G1, n=4)
+  env.reset()
+  env.step(torch.zeros(4, 29))
+  env.episode_length_buf[1] = env.max_episode_length - 1
+  _, _, term, trunc, _ = env.step(torch.zeros(4, 29))
+  assert bool(trunc[1]) and not bool(trunc[0])
+  assert int(env.episode_length_buf[1]) == 0 and int(env.episode_length_buf[0]) == 2
+
+
+def test_reset_event_places_robot_near_origin():
+  env = make(G1, n=8)
+  env.reset()
+  root = env.scene["robot"].data.root_link_pos_w
+  d = root[:, :2] - env.scene.env_origins[:, :2]
+  assert (d.abs() <= 0.5 + 1e-5).all()
+
+
+def test_curriculum_updates_command_ranges():
+  env = make(G1, n=2)
+  env.reset()
+  env.common_step_counter = 5000 * 24 + 1
+  env.step(torch.zeros(2, 29))
+  term = env.command_manager.get_term("twist")
+  assert term.cfg.ranges.lin_vel_x == (-1.5, 2.0)
+  assert torch.allclose(term._ranges_t[0], torch.tensor([-1.5, 2.0]))
+
+
+@pytest.mark.parametrize("task", [G1, GO1])
+def test_step_body_is_capture_safe(task):
+  env = make(task, n=6)
+  env.sim.step = lambda: None
+  env.sim.forward_gated = lambda g: None
+  env.reset()
+  env.step(torch.zeros(6, env.action_manager.total_action_dim))
+  env.episode_length_buf[:3] = 10_000  # force resets inside the guarded body
+  with CaptureGuard():
+    env._step_body()
+
+
+def test_capture_guard_catches_hazards():
+  x = torch.zeros(4)
+  with CaptureGuard():
+    with pytest.raises(CaptureHazard):
+      x[[0, 1]]
+    with pytest.raises(CaptureHazard):
+      x.sum().item()
+    with pytest.raises(CaptureHazard):
+      x[x > 0]
+    with pytest.raises(CaptureHazard):
+      torch.tensor(0.1)

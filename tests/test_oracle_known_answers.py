@@ -1,0 +1,171 @@
+"""The oracle (CPU restatement of mj_step) against analytic known answers.
+
+Physics numerics are not pinned by the reference's own tests (MuJoCo / MuJoCo
+Warp are absent here: SURVEY.md §8c), so the oracle is pinned by closed-form
+results instead: free fall, torque-free momentum conservation, pendulum energy,
+a static stance carrying the robot's weight, and PD equilibrium."""
+
+import numpy as np
+import pytest
+
+from mjlab_amd.spec.compiler import compile_spec
+from mjlab_amd.spec.mjcf import read_mjcf_string
+from oracle.oracle import Oracle
+from tests.scenes import g1_scene_model
+
+FREE_BALL = """
+<mujoco>
+  <option timestep="0.005"/>
+  <worldbody>
+    <geom name="floor" type="plane" size="5 5 0.1"/>
+    <body name="ball" pos="0 0 1">
+      <freejoint/>
+      <geom type="sphere" size="0.1" mass="2"/>
+    </body>
+  </worldbody>
+</mujoco>
+"""
+
+PENDULUM = """
+<mujoco>
+  <option timestep="0.001"/>
+  <worldbody>
+    <body name="link1" pos="0 0 2">
+      <joint name="j1" type="hinge" axis="0 1 0"/>
+      <geom type="capsule" fromto="0 0 0 0.5 0 0" size="0.03" mass="1" contype="0" conaffinity="0"/>
+      <body name="link2" pos="0.5 0 0">
+        <joint name="j2" type="hinge" axis="0 1 0"/>
+        <geom type="capsule" fromto="0 0 0 0.5 0 0" size="0.03" mass="1" contype="0" conaffinity="0"/>
+      </body>
+    </body>
+  </worldbody>
+</mujoco>
+"""
+
+
+def _model(xml, **opt):
+  m = compile_spec(read_mjcf_string(xml), 16, 64)
+  for k, v in opt.items():
+    setattr(m, k, v)
+  return m
+
+
+def test_free_fall_first_step():
+  m = _model(FREE_BALL)
+  out = Oracle(m).run(1, {"qpos": m.qpos0[None]}, integrate=True)
+  g, dt = 9.81, m.timestep
+  assert out["ncon"][0, 0] == 0
+  np.testing.assert_allclose(out["qacc_smooth"][0], [0, 0, -g, 0, 0, 0], atol=1e-12)
+  np.testing.assert_allclose(out["qacc"][0], [0, 0, -g, 0, 0, 0], atol=1e-12)
+  assert out["qvel"][0, 2] == pytest.approx(-g * dt, abs=1e-12)
+  assert out["qpos"][0, 2] == pytest.approx(1.0 - g * dt * dt, abs=1e-12)  # semi-implicit Euler
+  assert out["time"][0, 0] == pytest.approx(dt)
+
+
+def test_ball_comes_to_rest_on_floor():
+  m = _model(FREE_BALL)
+  orc = Oracle(m)
+  st = {"qpos": m.qpos0[None].copy()}
+  st["qpos"][0, 2] = 0.12
+  for _ in range(400):
+    out = orc.run(1, st, integrate=True)
+    st = {k: out[k] for k in ("qpos", "qvel", "qacc_warmstart", "time")}
+  # resting: height ~ radius (soft contact penetration is small), normal force = m g
+  assert 0.095 < st["qpos"][0, 2] < 0.1005
+  assert abs(st["qvel"][0]).max() < 1e-3
+  fz = out["qfrc_constraint"][0, 2]
+  assert fz == pytest.approx(2 * 9.81, rel=1e-3)
+
+
+def test_momentum_conserved_without_gravity_or_contacts():
+  """Free-floating G1, no gravity, contacts off: internal PD torques cannot move
+  the centre of mass — subtree_com of the root moves with constant velocity."""
+  m = g1_scene_model(1)
+  m.gravity = np.zeros(3)
+  orc = Oracle(m)
+  st = {"qpos": m.key_qpos[None].copy(), "ctrl": m.key_ctrl[None] + 0.3}
+  st["qpos"][0, 2] += 5.0  # far above the floor
+  coms = []
+  for _ in range(40):
+    out = orc.run(1, st, integrate=True)
+    st = {k: out[k] for k in ("qpos", "qvel", "qacc_warmstart", "time")}
+    st["ctrl"] = m.key_ctrl[None] + 0.3
+    coms.append(out["subtree_com"][0, 6:9].copy())  # body 2 = robot root (0 world, 1 terrain)
+  # self-contacts may occur: internal forces, momentum still conserved
+  world_com = np.array(coms)
+  # zero initial momentum: the COM stays put (to the O(dt^2) error of
+  # integrating in generalized coordinates) while the limbs swing
+  assert np.abs(world_com - world_com[0]).max() < 1e-4
+  assert np.abs(st["qpos"][0, 7:] - m.key_qpos[7:]).max() > 0.05
+
+
+def test_pendulum_energy_bounded():
+  m = _model(PENDULUM)
+  orc = Oracle(m)
+  st = {"qpos": np.array([[0.3, 0.2]])}
+  mass = m.body_mass
+  g = 9.81
+
+  def energy(o):
+    # potential from body COM heights; kinetic from cvel (spatial velocity at com frame)
+    pe = sum(mass[b] * g * o["xipos"][0, 3 * b + 2] for b in range(1, m.nbody))
+    ke = 0.0
+    for b in range(1, m.nbody):
+      cv = o["cvel"][0, 6 * b : 6 * b + 6]
+      w, v0 = cv[:3], cv[3:]
+      r = o["xipos"][0, 3 * b : 3 * b + 3] - o["subtree_com"][0, 0:3]
+      v = v0 + np.cross(w, r)
+      R = o["ximat"][0, 9 * b : 9 * b + 9].reshape(3, 3)
+      I = R @ np.diag(m.body_inertia[b]) @ R.T
+      ke += 0.5 * mass[b] * v @ v + 0.5 * w @ I @ w
+    return pe, ke
+
+  es, kes = [], []
+  for _ in range(500):
+    out = orc.run(1, st, integrate=False)
+    pe_ke = energy(out)
+    es.append(pe_ke[0] + pe_ke[1])
+    kes.append(pe_ke[1])
+    out = orc.run(1, st, integrate=True)
+    st = {k: out[k] for k in ("qpos", "qvel", "qacc_warmstart", "time")}
+  es = np.array(es)
+  # semi-implicit Euler at dt=1ms: total energy drifts < 1% of the swing's kinetic energy
+  assert max(kes) > 1.0
+  assert np.ptp(es) / max(kes) < 1e-2
+
+
+def test_g1_static_stance_carries_weight():
+  """G1 dropped at its keyframe under PD hold: once the landing transient has
+  died out (1 s), the vertical constraint force on the free joint carries the
+  robot's weight m_total * g and the base has barely moved."""
+  m = g1_scene_model(1)
+  orc = Oracle(m)
+  st = {"qpos": m.key_qpos[None].copy(), "ctrl": m.key_ctrl[None].copy()}
+  fz = []
+  for _ in range(200):
+    out = orc.run(1, st, integrate=True)
+    st = {k: out[k] for k in ("qpos", "qvel", "qacc_warmstart", "time")}
+    st["ctrl"] = m.key_ctrl[None].copy()
+    fz.append(out["qfrc_constraint"][0, 2])
+  mtot = m.body_mass.sum()
+  assert np.mean(fz[150:]) == pytest.approx(mtot * 9.81, rel=0.02)
+  assert out["ncon"][0, 0] >= 4
+  assert abs(st["qpos"][0, 0]) < 0.1 and abs(st["qpos"][0, 2] - m.key_qpos[2]) < 0.05
+
+
+def test_pd_actuator_force_law():
+  """force = kp*(clamp(ctrl, range) - q) - kd*qdot, clamped to forcerange."""
+  m = g1_scene_model(1)
+  rng = np.random.default_rng(1)
+  st = {"qpos": m.key_qpos[None].copy(), "qvel": rng.normal(0, 1, (1, m.nv)), "ctrl": m.key_ctrl[None] + rng.uniform(-3, 3, (1, m.nu))}
+  st["qpos"][0, 2] += 2.0
+  out = Oracle(m).run(1, st, integrate=False)
+  for i in range(m.nu):
+    j = int(m.actuator_trnid[i, 0]) if m.actuator_trnid.ndim == 2 else int(m.actuator_trnid[i])
+    qa, va = int(m.jnt_qposadr[j]), int(m.jnt_dofadr[j])
+    kp, kd = m.actuator_gainprm[i, 0], -m.actuator_biasprm[i, 2]
+    lo, hi = m.actuator_ctrlrange[i]
+    c = np.clip(st["ctrl"][0, i], lo, hi)
+    f = kp * c - kp * st["qpos"][0, qa] - kd * st["qvel"][0, va]
+    flo, fhi = m.actuator_forcerange[i]
+    assert out["actuator_force"][0, i] == pytest.approx(np.clip(f, flo, fhi), rel=1e-9, abs=1e-9)
