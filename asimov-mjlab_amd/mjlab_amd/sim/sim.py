@@ -149,7 +149,7 @@ class Simulation:
     self.nan_guard = NanGuard(cfg.nan_guard, num_envs, model)
     if self.use_cuda_graph:
       native.check(native.lib().mjh_model_check(ctypes.addressof(self._mstruct)), "mjh_model_check")
-      self.forward()
+      self._launch_forward()
       self.create_graph()
 
   # ---- descriptors ----
@@ -195,7 +195,10 @@ class Simulation:
       setattr(ds, name, t.data_ptr())
     self._mstruct, self._dstruct = ms, ds
     # bumped whenever the descriptors change: graphs that baked them are stale
+    # and are re-captured lazily by the next step()/forward()
     self.struct_version = getattr(self, "struct_version", 0) + 1
+    self.step_graph = None
+    self.forward_graph = None
 
   def _native_ok(self) -> bool:
     try:
@@ -272,12 +275,9 @@ class Simulation:
     self.forward_graph = None
     if not self.use_cuda_graph:
       return
-    # warm-up launches outside capture (attribute setup), then capture
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-      self._launch_forward()
-    torch.cuda.current_stream().wait_stream(s)
+    # no warm-up launch here: it would run a real forward (and overwrite
+    # qacc_warmstart); the constructor's first forward() already set the
+    # kernels' LDS attributes outside any capture
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
       self._launch_step()
@@ -309,10 +309,12 @@ class Simulation:
 
   def forward(self) -> None:
     self._require_gpu()
-    if self.forward_graph is not None and not torch.cuda.is_current_stream_capturing():
-      self.forward_graph.replay()
-    else:
+    if torch.cuda.is_current_stream_capturing():
       self._launch_forward()
+      return
+    if self.forward_graph is None:
+      self.create_graph()
+    self.forward_graph.replay()
 
   def forward_gated(self, gate: torch.Tensor) -> None:
     """``forward()`` for all worlds iff the device scalar ``gate`` is non-zero.
@@ -335,11 +337,10 @@ class Simulation:
     if torch.cuda.is_current_stream_capturing():
       self._launch_step()  # being captured into an enclosing (env-step) graph
       return
+    if self.step_graph is None:
+      self.create_graph()
     with self.nan_guard.watch(self.data):
-      if self.step_graph is not None:
-        self.step_graph.replay()
-      else:
-        self._launch_step()
+      self.step_graph.replay()
 
   # ---- utilities ----
   def efc_capacity(self) -> int:

@@ -12,7 +12,8 @@ here once and cited by the tests:
 * constraint solve (qacc, qfrc_constraint): |d| <= 2e-2 * (1 + max|ref|) — the
   Newton solver stops on a tolerance test, and a float32 run can take one
   more/fewer iteration than the float64 one (MuJoCo Warp has the same property);
-* integrated state: qvel |d| <= 1e-2 * (1 + max|ref qvel|) (= dt * the qacc bound), qpos |d| <= 1e-4;
+* integrated state: qvel |d| <= 1e-2 * (1 + max|ref qvel|), qpos |d| <= 1e-4 + dt * (qvel bound)
+  (qpos integrates the new qvel);
 * sensordata: |d| <= 2e-2 * (1 + max|ref|) (contact forces come out of the solve).
 """
 
@@ -103,7 +104,7 @@ def _bound(ref: np.ndarray, rel: float) -> float:
   return rel * (1.0 + float(np.abs(ref).max(initial=0.0)))
 
 
-def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None) -> dict:
+def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: float = 0.005) -> dict:
   """Compare one step's outputs (arrays shaped (nworld, -1)). Returns
   {"maxerr": {field: max|d|}, "failures": [...], "int_mismatch_worlds": [...]}."""
   n = got["qpos"].shape[0]
@@ -136,7 +137,8 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None) -> dict
     check(k, _bound(ref[k][good], 1e-4))
   for k in SOLVE:
     check(k, _bound(ref[k][good], 2e-2))
-  check("qvel", _bound(ref["qvel"][good], 1e-2))
-  check("qpos", 1e-4)
+  qv_tol = _bound(ref["qvel"][good], 1e-2)
+  check("qvel", qv_tol)
+  check("qpos", 1e-4 + dt * qv_tol)
   check("sensordata", _bound(ref["sensordata"][good], 2e-2))
   return {"maxerr": maxerr, "failures": failures, "int_mismatch_worlds": bad_int}

@@ -107,8 +107,12 @@ def test_gated_forward():
   b = get(sim, n)
   for k in ("xpos", "qacc", "sensordata", "efc_force"):
     assert np.array_equal(a[k], b[k]), k  # gate 0: nothing recomputed
+  # forward saves qacc into qacc_warmstart (as MuJoCo's solver does), so
+  # restore the warm start before each call being compared
+  ws = sim.data.qacc_warmstart.clone()
   sim.forward_gated(torch.ones(1, dtype=torch.bool, device=DEV))
   c = get(sim, n)
+  sim.data.qacc_warmstart.copy_(ws)
   sim.forward()
   d = get(sim, n)
   for k in ("xpos", "qacc", "sensordata"):
