@@ -44,11 +44,54 @@ struct Layout {
   int J, ldj, efc_D, efc_R, efc_aref, efc_jaref, efc_jv, efc_force, efc_fl, efc_pos, efc_type, efc_id, efc_mask;
   int efc_h, arow, ash, arow_prev;
   int red, ints;
-  int total;
+  int total, gtotal;  // per-world words: LDS, global scratch
   int ncap, rcap;
 };
 
 enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
+
+// Where each per-world array lives: LDS (fast, but it bounds how many worlds
+// share a CU) or the per-world global scratch (L1/L2-resident; coalesced since
+// a world's scratch is one contiguous span). The solver's hot set — J, the row
+// state and the nv-vectors — stays in LDS; poses, inertias, contacts and the
+// mass matrix go to global scratch so more worlds (waves) fit per CU.
+// Inlining the solver helpers trades call overhead (callee-saved VGPR spills,
+// flat addressing of LDS through generic pointers) for register pressure.
+#ifndef MJH_SOLVER_INLINE
+#define MJH_SOLVER_INLINE
+#endif
+#ifndef MJH_COLL_INLINE
+#define MJH_COLL_INLINE
+#endif
+#ifndef MJH_PRESET
+#define MJH_PRESET 3
+#endif
+#define MJH_REGIONS(X)                                                                              \
+  X(qpos, 1) X(qvel, 0) X(qacc, 0) X(qacc_smooth, 0) X(qfrc_smooth, 0) X(qfrc_bias, 1) X(qfrc_con, 0)  \
+  X(qfrc_passive, 1) X(qfrc_act, 1) X(grad, 0) X(search, 0) X(Ma, 0) X(Mv, 0) X(tmp, 0) X(tmp2, 0)    \
+  X(xpos, 1) X(xquat, 1) X(xmat, 1) X(xipos, 1) X(ximat, 1) X(subtree_com, 1) X(cinert, 1) X(crb, 1)  \
+  X(cvel, 1) X(cacc, 1) X(cfrc, 1) X(xanchor, 1) X(xaxis, 1) X(cdof, 1) X(cdof_dot, 1)               \
+  X(cgpos, 1) X(cgmat, 1) X(sxpos, 1) X(sxmat, 1) X(M, 1) X(L, 1) X(act_force, 1)                    \
+  X(con_pos, 1) X(con_frame, 1) X(con_dist, 1) X(con_fric, 1) X(con_solref, 1) X(con_solimp, 1)       \
+  X(con_imargin, 1) X(con_dim, 1) X(con_geom, 1) X(con_efcadr, 1)                                     \
+  X(J, 0) X(efc_D, 0) X(efc_R, 0) X(efc_aref, 0) X(efc_jaref, 0) X(efc_jv, 0) X(efc_force, 0)        \
+  X(efc_fl, 0) X(efc_pos, 0) X(efc_type, 0) X(efc_id, 0) X(efc_mask, 0) X(efc_h, 0) X(arow, 0)       \
+  X(ash, 0) X(arow_prev, 0)
+struct Rg {
+#if MJH_PRESET == 0
+#define X_RG(name, r) static constexpr bool name = false;
+#elif MJH_PRESET == 2
+#define X_RG(name, r) static constexpr bool name = true;
+#elif MJH_PRESET == 3
+#define X_RG(name, r) static constexpr bool name = (r) != 0 || (#name[0] == 'J' && #name[1] == 0);
+#else
+#define X_RG(name, r) static constexpr bool name = (r) != 0;
+#endif
+  MJH_REGIONS(X_RG)
+#undef X_RG
+};
+#define SP(name) ((Rg::name ? G : S) + Lo.name)
+#define SPI(name) reinterpret_cast<int*>((Rg::name ? G : S) + Lo.name)
 
 thread_local std::string g_err;
 
@@ -76,7 +119,10 @@ __device__ unsigned long long* g_prof;
 // compiler not to move LDS accesses across this point (memory clobber) and the
 // outstanding LDS ops drained; no s_barrier, so waves of a workgroup that run
 // different worlds never wait for each other.
-__device__ __forceinline__ void wsync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Per-world arrays in global scratch are exchanged the same way: all waves of
+// a workgroup share the CU's L1, so draining vmcnt makes a lane's stores
+// visible to the wave's other lanes (workgroup scope, non-tgsplit).
+__device__ __forceinline__ void wsync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
 
 // Word offsets of every model array inside the LDS model image, and of the
 // per-world copies of expanded (domain-randomised) fields (-1: shared).
@@ -95,7 +141,7 @@ struct ImgOff {
 #define IMG_I(name) (reinterpret_cast<const int*>(smem + Io.name))
 #define IMG_F(name) (reinterpret_cast<const float*>(smem + Io.name))
 #define IMG_L(name) (reinterpret_cast<const long long*>(smem + Io.name))
-#define WFIELD(name) (Io.w_##name >= 0 ? (const float*)(S + Io.w_##name) : (const float*)(smem + Io.name))
+#define WFIELD(name) (m.name##_wstride ? (const float*)(m.name + W * m.name##_wstride) : (const float*)(smem + Io.name))
 
 // ---- block-level primitives -------------------------------------------------
 template <int NT>
@@ -306,7 +352,7 @@ __device__ void ldl_solve_fast(const float* A, int n, int ld, float* x) {
 // nact compacted active rows, on the f32 matrix cores (v_mfma_f32_16x16x4_f32:
 // exact fp32 FMA chains). Tiles of 16x16 on the lower block triangle.
 template <int NT>
-__device__ void hessian_mfma(const float* M, int ldm, const float* J, int ldj, const int* arow, const float* ash,
+__device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const float* J, int ldj, const int* arow, const float* ash,
                              int nact, int n, float* Hout) {
   typedef float v4f __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
@@ -385,7 +431,7 @@ __device__ __forceinline__ void load_row_lower(const float* A, int n, int ld, fl
 }
 
 template <int NVP>
-__device__ void ldl_factor_reg(float* A, int n, int ld) {
+__device__ MJH_SOLVER_INLINE void ldl_factor_reg(float* A, int n, int ld) {
   // Branch-free: lane i updates its whole row each step; entries right of the
   // diagonal are scratch never read back (only rdlane(a[k], j) with k < j, i.e.
   // lower-triangle values, crosses lanes), and rows >= n are identity rows, so
@@ -413,7 +459,7 @@ __device__ void ldl_factor_reg(float* A, int n, int ld) {
 
 // (L D L^T) x = b with the factor from ldl_factor_reg; x in LDS (in place).
 template <int NVP>
-__device__ void ldl_solve_reg(const float* A, int n, int ld, float* x) {
+__device__ MJH_SOLVER_INLINE void ldl_solve_reg(const float* A, int n, int ld, float* x) {
   const int lane = threadIdx.x & 63;
   float a[NVP], c[NVP];
   wsync();
@@ -441,7 +487,7 @@ __device__ void ldl_solve_reg(const float* A, int n, int ld, float* x) {
 
 // y = A x for a symmetric matrix stored in full (16-byte aligned rows).
 template <int NT>
-__device__ void symv(const float* A, int n, int ld, const float* x, float* y) {
+__device__ MJH_SOLVER_INLINE void symv(const float* A, int n, int ld, const float* x, float* y) {
   for (int i = (threadIdx.x & 63); i < n; i += NT) {
     const float* r = A + i * ld;
     float s0 = 0.f, s1 = 0.f;
@@ -501,7 +547,7 @@ __device__ __forceinline__ int plane_sphere(Con* c, float margin, const float* p
 }
 
 // Narrowphase for one pair (types ascending). Up to 4 contacts.
-__device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, const float* s1, const float* p2,
+__device__ MJH_COLL_INLINE int narrowphase(int t1, int t2, const float* p1, const float* m1, const float* s1, const float* p2,
                            const float* m2, const float* s2, float margin, Con* out) {
   if (t1 == 0 && t2 == 2) return plane_sphere(out, margin, p1, m1, p2, s2[0]);
   if (t1 == 0 && t2 == 3) {
@@ -660,87 +706,74 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
   const int tid = threadIdx.x & 63;
   float* S = smem + Io.img_words + wave * Lo.total;
   int* SI = reinterpret_cast<int*>(S);
-  {  // this world's copies of expanded model fields
-#define X_SZ(name) const int name = m.name;
-    MJH_MODEL_SIZES(X_SZ)
-#undef X_SZ
-#define X_WCOPY(type, name, count)                                              \
-    if (Io.w_##name >= 0) {                                                     \
-      const float* src = m.name + (long long)w * m.name##_wstride;              \
-      float* dst = S + Io.w_##name;                                             \
-      for (int i = tid; i < (count); i += 64) dst[i] = src[i];                  \
-    }
-    MJH_MODEL_WARRAYS(X_WCOPY)
-#undef X_WCOPY
-    (void)nchain; (void)ncolgeom; (void)npair; (void)nsensor; (void)nmocap; (void)nconmax; (void)njmax; (void)na; (void)nsensordata; (void)nq; (void)nv; (void)nu; (void)nbody; (void)njnt; (void)ngeom; (void)nsite;
-  }
-  wsync();
+  float* G = d.scratch + (long long)w * d.scratch_words;  // this world's global scratch
+  const long long W = w;
   const int nq = m.nq, nv = m.nv, nb = m.nbody, nu = m.nu, nj = m.njnt;
   const int ldm = Lo.ldm, ldj = Lo.ldj;
 
-  float* qpos = S + Lo.qpos;
-  float* qvel = S + Lo.qvel;
-  float* qacc = S + Lo.qacc;
-  float* qacc_smooth = S + Lo.qacc_smooth;
-  float* qfrc_smooth = S + Lo.qfrc_smooth;
-  float* qfrc_bias = S + Lo.qfrc_bias;
-  float* qfrc_con = S + Lo.qfrc_con;
-  float* qfrc_passive = S + Lo.qfrc_passive;
-  float* qfrc_act = S + Lo.qfrc_act;
-  float* grad = S + Lo.grad;
-  float* search = S + Lo.search;
-  float* Ma = S + Lo.Ma;
-  float* Mv = S + Lo.Mv;
-  float* tmp = S + Lo.tmp;
-  float* tmp2 = S + Lo.tmp2;
-  float* xpos = S + Lo.xpos;
-  float* xquat = S + Lo.xquat;
-  float* xmat = S + Lo.xmat;
-  float* xipos = S + Lo.xipos;
-  float* ximat = S + Lo.ximat;
-  float* subtree_com = S + Lo.subtree_com;
-  float* cinert = S + Lo.cinert;
-  float* crb = S + Lo.crb;
-  float* cvel = S + Lo.cvel;
-  float* cacc = S + Lo.cacc;
-  float* cfrc = S + Lo.cfrc;
-  float* xanchor = S + Lo.xanchor;
-  float* xaxis = S + Lo.xaxis;
-  float* cdof = S + Lo.cdof;
-  float* cdof_dot = S + Lo.cdof_dot;
-  float* cgpos = S + Lo.cgpos;
-  float* cgmat = S + Lo.cgmat;
-  float* sxpos = S + Lo.sxpos;
-  float* sxmat = S + Lo.sxmat;
-  float* Mm = S + Lo.M;
-  float* Lm = S + Lo.L;
-  float* act_force = S + Lo.act_force;
-  float* con_pos = S + Lo.con_pos;
-  float* con_frame = S + Lo.con_frame;
-  float* con_dist = S + Lo.con_dist;
-  float* con_fric = S + Lo.con_fric;
-  float* con_solref = S + Lo.con_solref;
-  float* con_solimp = S + Lo.con_solimp;
-  float* con_imargin = S + Lo.con_imargin;
-  int* con_dim = SI + Lo.con_dim;
-  int* con_geom = SI + Lo.con_geom;
-  int* con_efcadr = SI + Lo.con_efcadr;
-  float* J = S + Lo.J;
-  float* efc_D = S + Lo.efc_D;
-  float* efc_R = S + Lo.efc_R;
-  float* efc_aref = S + Lo.efc_aref;
-  float* jaref = S + Lo.efc_jaref;
-  float* jv = S + Lo.efc_jv;
-  float* efc_force = S + Lo.efc_force;
-  float* efc_fl = S + Lo.efc_fl;
-  float* efc_pos = S + Lo.efc_pos;
-  int* efc_type = SI + Lo.efc_type;
-  int* efc_id = SI + Lo.efc_id;
-  unsigned long long* efc_mask = reinterpret_cast<unsigned long long*>(S + Lo.efc_mask);
-  float* efc_h = S + Lo.efc_h;
-  int* arow = SI + Lo.arow;
-  int* arow_prev = SI + Lo.arow_prev;
-  float* ash = S + Lo.ash;
+  float* qpos = SP(qpos);
+  float* qvel = SP(qvel);
+  float* qacc = SP(qacc);
+  float* qacc_smooth = SP(qacc_smooth);
+  float* qfrc_smooth = SP(qfrc_smooth);
+  float* qfrc_bias = SP(qfrc_bias);
+  float* qfrc_con = SP(qfrc_con);
+  float* qfrc_passive = SP(qfrc_passive);
+  float* qfrc_act = SP(qfrc_act);
+  float* grad = SP(grad);
+  float* search = SP(search);
+  float* Ma = SP(Ma);
+  float* Mv = SP(Mv);
+  float* tmp = SP(tmp);
+  float* tmp2 = SP(tmp2);
+  float* xpos = SP(xpos);
+  float* xquat = SP(xquat);
+  float* xmat = SP(xmat);
+  float* xipos = SP(xipos);
+  float* ximat = SP(ximat);
+  float* subtree_com = SP(subtree_com);
+  float* cinert = SP(cinert);
+  float* crb = SP(crb);
+  float* cvel = SP(cvel);
+  float* cacc = SP(cacc);
+  float* cfrc = SP(cfrc);
+  float* xanchor = SP(xanchor);
+  float* xaxis = SP(xaxis);
+  float* cdof = SP(cdof);
+  float* cdof_dot = SP(cdof_dot);
+  float* cgpos = SP(cgpos);
+  float* cgmat = SP(cgmat);
+  float* sxpos = SP(sxpos);
+  float* sxmat = SP(sxmat);
+  float* Mm = SP(M);
+  float* Lm = SP(L);
+  float* act_force = SP(act_force);
+  float* con_pos = SP(con_pos);
+  float* con_frame = SP(con_frame);
+  float* con_dist = SP(con_dist);
+  float* con_fric = SP(con_fric);
+  float* con_solref = SP(con_solref);
+  float* con_solimp = SP(con_solimp);
+  float* con_imargin = SP(con_imargin);
+  int* con_dim = SPI(con_dim);
+  int* con_geom = SPI(con_geom);
+  int* con_efcadr = SPI(con_efcadr);
+  float* J = SP(J);
+  float* efc_D = SP(efc_D);
+  float* efc_R = SP(efc_R);
+  float* efc_aref = SP(efc_aref);
+  float* jaref = SP(efc_jaref);
+  float* jv = SP(efc_jv);
+  float* efc_force = SP(efc_force);
+  float* efc_fl = SP(efc_fl);
+  float* efc_pos = SP(efc_pos);
+  int* efc_type = SPI(efc_type);
+  int* efc_id = SPI(efc_id);
+  unsigned long long* efc_mask = reinterpret_cast<unsigned long long*>(SP(efc_mask));
+  float* efc_h = SP(efc_h);
+  int* arow = SPI(arow);
+  int* arow_prev = SPI(arow_prev);
+  float* ash = SP(ash);
   float* red = S + Lo.red;
   int* redi = SI + Lo.red + 2 * (NT / 64) + 2;
   int* ints = SI + Lo.ints;
@@ -764,7 +797,6 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
   const float* site_quat = WFIELD(site_quat);
   const float* qpos0 = WFIELD(qpos0);
 
-  const long long W = w;
   (void)SI;
 
   // ---------------------------------------------------------------- load state
@@ -1964,16 +1996,22 @@ ImgOff make_imgoff(const mjh_model* m) {
   return io;
 }
 
-// Per-world LDS layout. `budget` = LDS words available to one world.
-Layout make_layout(const mjh_model* m, ImgOff* io, int budget) {
+// Per-world layout: arrays go to LDS (`off`) or to the global scratch
+// (`goff`) according to the region table Rg. `budget` = LDS words available to
+// one world; the constraint-row capacity is what fits (LDS rows) or njmax.
+Layout make_layout(const mjh_model* m, int budget) {
   Layout L;
   std::memset(&L, 0, sizeof(L));
-  int off = 0;
-  auto take = [&](int n) {
-    int o = off;
-    off += (n + 3) & ~3;  // 16-byte alignment (float4 rows, int64 masks)
-    return o;
-  };
+  int off = 0, goff = 0;
+  auto al = [](int n) { return (n + 3) & ~3; };  // 16-byte alignment (float4 rows, int64 masks)
+#define TAKE(name, n)                 \
+  do {                                \
+    if (Rg::name) {                   \
+      L.name = goff; goff += al(n);   \
+    } else {                          \
+      L.name = off; off += al(n);     \
+    }                                 \
+  } while (0)
   const int nv = m->nv, nb = m->nbody, nj = m->njnt;
   // rows 16-byte aligned with an odd float4 count: ds_read_b128 on a row per lane
   // lands on distinct bank quads (conflict-free), and row reads vectorise
@@ -1981,53 +2019,52 @@ Layout make_layout(const mjh_model* m, ImgOff* io, int budget) {
   if (((ld >> 2) & 1) == 0) ld += 4;
   L.ldm = ld;
   L.ldj = ld;
-  L.qpos = take(m->nq);
-  L.qvel = take(nv); L.qacc = take(nv); L.qacc_smooth = take(nv); L.qfrc_smooth = take(nv);
-  L.qfrc_bias = take(nv); L.qfrc_con = take(nv); L.qfrc_passive = take(nv); L.qfrc_act = take(nv);
-  L.grad = take(nv); L.search = take(nv); L.Ma = take(nv); L.Mv = take(nv); L.tmp = take(nv); L.tmp2 = take(nv);
-  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
-  L.ximat = take(9 * nb); L.subtree_com = take(3 * nb); L.cinert = take(10 * nb); L.crb = take(10 * nb);
-  L.cvel = take(6 * nb); L.cacc = take(6 * nb); L.cfrc = take(6 * nb);
-  L.xanchor = take(3 * nj); L.xaxis = take(3 * nj); L.cdof = take(6 * nv); L.cdof_dot = take(6 * nv);
-  L.cgpos = take(3 * m->ncolgeom); L.cgmat = take(9 * m->ncolgeom);
-  L.sxpos = take(3 * m->nsite); L.sxmat = take(9 * m->nsite);
-  L.M = take(nv * L.ldm); L.L = take(nv * L.ldm);
-  L.act_force = take(m->nu);
+  TAKE(qpos, m->nq);
+  TAKE(qvel, nv); TAKE(qacc, nv); TAKE(qacc_smooth, nv); TAKE(qfrc_smooth, nv);
+  TAKE(qfrc_bias, nv); TAKE(qfrc_con, nv); TAKE(qfrc_passive, nv); TAKE(qfrc_act, nv);
+  TAKE(grad, nv); TAKE(search, nv); TAKE(Ma, nv); TAKE(Mv, nv); TAKE(tmp, nv); TAKE(tmp2, nv);
+  TAKE(xpos, 3 * nb); TAKE(xquat, 4 * nb); TAKE(xmat, 9 * nb); TAKE(xipos, 3 * nb);
+  TAKE(ximat, 9 * nb); TAKE(subtree_com, 3 * nb); TAKE(cinert, 10 * nb); TAKE(crb, 10 * nb);
+  TAKE(cvel, 6 * nb); TAKE(cacc, 6 * nb); TAKE(cfrc, 6 * nb);
+  TAKE(xanchor, 3 * nj); TAKE(xaxis, 3 * nj); TAKE(cdof, 6 * nv); TAKE(cdof_dot, 6 * nv);
+  TAKE(cgpos, 3 * m->ncolgeom); TAKE(cgmat, 9 * m->ncolgeom);
+  TAKE(sxpos, 3 * m->nsite); TAKE(sxmat, 9 * m->nsite);
+  TAKE(M, nv * L.ldm); TAKE(L, nv * L.ldm);
+  TAKE(act_force, m->nu);
   const int C = m->nconmax;
   L.ncap = C;
-  L.con_pos = take(3 * C); L.con_frame = take(9 * C); L.con_dist = take(C); L.con_fric = take(5 * C);
-  L.con_solref = take(2 * C); L.con_solimp = take(5 * C); L.con_imargin = take(C); L.con_dim = take(C);
-  L.con_geom = take(2 * C); L.con_efcadr = take(C);
-  L.red = take(16);
-  L.ints = take(8);
-  {  // expanded (per-world) model fields
-    auto sz = [&](void) {};
-    (void)sz;
-    const int nq = m->nq, nbody = m->nbody, njnt = m->njnt, ngeom = m->ngeom, nsite = m->nsite;
-    (void)nq; (void)nbody; (void)njnt; (void)ngeom; (void)nsite;
-#define X_WL(type, name, count) io->w_##name = m->name##_wstride ? take((count)) : -1;
-    MJH_MODEL_WARRAYS(X_WL)
-#undef X_WL
+  TAKE(con_pos, 3 * C); TAKE(con_frame, 9 * C); TAKE(con_dist, C); TAKE(con_fric, 5 * C);
+  TAKE(con_solref, 2 * C); TAKE(con_solimp, 5 * C); TAKE(con_imargin, C); TAKE(con_dim, C);
+  TAKE(con_geom, 2 * C); TAKE(con_efcadr, C);
+  L.red = off; off += al(16);
+  L.ints = off; off += al(8);
+  // constraint rows: as many as fit in the remaining LDS budget (rows in LDS)
+  // or njmax (rows in global scratch)
+  const int per_row_lds = (Rg::J ? 0 : L.ldj) + (Rg::efc_D ? 0 : 16 + 2);
+  int rcap = m->njmax;
+  if (per_row_lds > 0) {
+    const int r = (budget - off - 32) / per_row_lds;
+    if (r < rcap) rcap = r;
   }
-  // constraint rows: as many as fit in the remaining budget, up to njmax
-  const int fixed = off;
-  const int per_row = L.ldj + 16 + 2;  // J row + per-row scalars/ints + 64-bit mask
-  int rcap = (budget - fixed - 16) / per_row;
-  if (rcap > m->njmax) rcap = m->njmax;
   if (rcap < 1) rcap = 1;
   L.rcap = rcap;
-  L.J = take(rcap * L.ldj);
-  L.efc_D = take(rcap); L.efc_R = take(rcap); L.efc_aref = take(rcap); L.efc_jaref = take(rcap);
-  L.efc_jv = take(rcap); L.efc_force = take(rcap); L.efc_fl = take(rcap); L.efc_pos = take(rcap);
-  L.efc_type = take(rcap); L.efc_id = take(rcap);
-  L.efc_mask = take(2 * rcap);
-  L.efc_h = take(rcap); L.arow = take(rcap + 4); L.ash = take(rcap + 4); L.arow_prev = take(rcap + 4);
-  L.total = (off + 3) & ~3;
+  TAKE(J, rcap * L.ldj);
+  TAKE(efc_D, rcap); TAKE(efc_R, rcap); TAKE(efc_aref, rcap); TAKE(efc_jaref, rcap);
+  TAKE(efc_jv, rcap); TAKE(efc_force, rcap); TAKE(efc_fl, rcap); TAKE(efc_pos, rcap);
+  TAKE(efc_type, rcap); TAKE(efc_id, rcap);
+  TAKE(efc_mask, 2 * rcap);
+  TAKE(efc_h, rcap); TAKE(arow, rcap + 4); TAKE(ash, rcap + 4); TAKE(arow_prev, rcap + 4);
+#undef TAKE
+  L.total = al(off);
+  L.gtotal = al(goff) + 64;  // +256 B keeps worlds' spans on separate cache lines
   return L;
 }
 
+#ifndef MJH_WPB
+#define MJH_WPB 8
+#endif
 constexpr int kLdsBytes = 160 * 1024;
-constexpr int kWorldsPerBlock = 2;
+constexpr int kWorldsPerBlock = MJH_WPB;
 
 struct Plan {
   ImgOff io;
@@ -2039,7 +2076,7 @@ Plan make_plan(const mjh_model* m, int wpb) {
   Plan p;
   p.io = make_imgoff(m);
   const int budget = (kLdsBytes / 4 - p.io.img_words) / wpb;
-  p.lo = make_layout(m, &p.io, budget);
+  p.lo = make_layout(m, budget);
   p.shmem = (size_t)(p.io.img_words + wpb * p.lo.total) * 4;
   return p;
 }
@@ -2049,6 +2086,10 @@ int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, voi
   if (mjh_model_check(m) != 0) return 1;
   if (d->nworld <= 0) return 0;
   Plan p = make_plan(m, kWorldsPerBlock);
+  if (!d->scratch || d->scratch_words < p.lo.gtotal) {
+    g_err = "data scratch buffer missing or too small (mjh_scratch_words)";
+    return 1;
+  }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   static bool attr_set[2] = {false, false};
   const int nvp = nvp_of(m->nv);
@@ -2100,6 +2141,8 @@ int mjh_model_check(const mjh_model* m) {
 int mjh_scratch_bytes(const mjh_model* m) { return (int)make_plan(m, kWorldsPerBlock).shmem; }
 
 int mjh_efc_capacity(const mjh_model* m) { return make_plan(m, kWorldsPerBlock).lo.rcap; }
+
+long long mjh_scratch_words(const mjh_model* m) { return make_plan(m, kWorldsPerBlock).lo.gtotal; }
 
 int mjh_set_profile_buffer(void* ptr) {
 #ifdef MJH_PROFILE

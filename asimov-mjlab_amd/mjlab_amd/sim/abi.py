@@ -85,6 +85,8 @@ def data_struct(real=ctypes.c_float):
   for f in fields():
     if f.kind == "DA":
       members.append((f.name, ctypes.c_void_p))
+  if real is ctypes.c_float:  # device descriptor: per-world global scratch
+    members += [("scratch", ctypes.c_void_p), ("scratch_words", ctypes.c_longlong)]
   return type("mjh_data" if real is ctypes.c_float else "or_data", (ctypes.Structure,), {"_fields_": members})
 
 

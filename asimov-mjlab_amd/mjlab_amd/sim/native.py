@@ -19,7 +19,7 @@ PKG = Path(__file__).resolve().parents[1]
 # MJH_LIB selects an alternative build of the same ABI (e.g. the phase-timing
 # build libmjh_prof.so used by tools/phase_profile.py).
 LIB_PATH = Path(os.environ.get("MJH_LIB", str(PKG / "libmjh.so")))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 EXPORTS = (
   "mjh_abi_version",
@@ -31,6 +31,7 @@ EXPORTS = (
   "mjh_image_words",
   "mjh_set_profile_buffer",
   "mjh_efc_capacity",
+  "mjh_scratch_words",
   "mjh_step",
   "mjh_forward",
   "mjh_forward_gated",
@@ -61,6 +62,8 @@ def lib() -> ctypes.CDLL:
   L.mjh_scratch_bytes.argtypes = [ctypes.c_void_p]
   L.mjh_efc_capacity.argtypes = [ctypes.c_void_p]
   L.mjh_image_words.argtypes = [ctypes.c_void_p]
+  L.mjh_scratch_words.argtypes = [ctypes.c_void_p]
+  L.mjh_scratch_words.restype = ctypes.c_longlong
   L.mjh_set_profile_buffer.argtypes = [ctypes.c_void_p]
   for f in (L.mjh_step, L.mjh_forward):
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]

@@ -191,6 +191,12 @@ class Simulation:
     ms.image_words = self._image.numel()
     ds = DS()
     ds.nworld = self.num_envs
+    if not hasattr(self, "_scratch"):
+      words = int(native.lib().mjh_scratch_words(ctypes.addressof(ms))) if self._native_ok() else 16
+      self._scratch = torch.empty(self.num_envs * words, dtype=torch.float32, device=self.device)
+      self._scratch_words = words
+    ds.scratch = self._scratch.data_ptr()
+    ds.scratch_words = self._scratch_words
     for name, t in self._data_flat.items():
       setattr(ds, name, t.data_ptr())
     self._mstruct, self._dstruct = ms, ds

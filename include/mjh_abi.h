@@ -32,7 +32,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 1
+#define MJH_ABI_VERSION 2
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -77,6 +77,11 @@ typedef struct mjh_data {
 #define MJH_X_DATA(type, name, count) type* name;
   MJH_DATA_ARRAYS(MJH_X_DATA)
 #undef MJH_X_DATA
+  /* caller-allocated device scratch: nworld x scratch_words floats
+     (scratch_words >= mjh_scratch_words(m)); the step's per-world
+     intermediates that do not live in LDS */
+  float* scratch;
+  long long scratch_words;
 } mjh_data;
 
 /* Version of this ABI (MJH_ABI_VERSION). */
@@ -100,6 +105,9 @@ int mjh_image_words(const mjh_model* m);
 
 /* LDS bytes per workgroup the step kernel uses for this model. */
 int mjh_scratch_bytes(const mjh_model* m);
+
+/* Words of per-world global scratch the caller must provide in d->scratch. */
+long long mjh_scratch_words(const mjh_model* m);
 
 /* Constraint rows per world that fit on chip (<= njmax); rows beyond it are
  * dropped and reported through flags bit 1. */

@@ -16,7 +16,7 @@ ROOT = Path(__file__).resolve().parents[1]
 
 def declared_functions() -> list[str]:
   txt = (ROOT / "include" / "mjh_abi.h").read_text()
-  return re.findall(r"^\s*(?:int|size_t|const char\*)\s+(mjh_\w+)\s*\(", txt, flags=re.M)
+  return re.findall(r"^\s*(?:int|size_t|long long|const char\*)\s+(mjh_\w+)\s*\(", txt, flags=re.M)
 
 
 def test_header_declarations_match_exports():

@@ -1,0 +1,40 @@
+"""Time the physics step kernel alone at the bench size (diagnostic tool).
+
+usage: MJH_LIB=<lib.so> python tools/kernel_bench.py [N] [launches]
+Settles random G1 states for 20 steps, then times `launches` step launches
+with HIP events and reports ms/launch, world-steps/s, mean nefc and iterations.
+"""
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "asimov-mjlab_amd"))
+sys.path.insert(0, str(ROOT))
+import numpy as np
+import torch
+
+from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg
+from tests.scenes import g1_scene_model, random_states
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+launches = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+m = g1_scene_model(n)
+sim = Simulation(n, SimulationCfg(nconmax=50, njmax=300, mujoco=MujocoCfg(timestep=0.005, iterations=10, ls_iterations=20)), m, "cuda:0")
+st = random_states(m, n, np.random.default_rng(0), drop=0.03)
+for k, v in st.items():
+  t = getattr(sim.data, k)
+  t.copy_(torch.as_tensor(v, dtype=t.dtype, device="cuda:0").view_as(t))
+for _ in range(20):
+  sim.step()
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(launches):
+  sim.step()
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / launches
+print(f"{os.environ.get('MJH_LIB', 'libmjh.so')}: N={n} {ms:.3f} ms/launch  {n / ms * 1e3:,.0f} world-steps/s  "
+      f"nefc {sim.data.nefc.float().mean().item():.1f}  niter {sim.data.solver_niter.float().mean().item():.2f}  "
+      f"lds {sim.scratch_bytes()} rcap {sim.efc_capacity()} flags {int((sim.data.flags != 0).sum())}")
