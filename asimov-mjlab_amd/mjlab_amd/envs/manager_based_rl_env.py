@@ -238,14 +238,14 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     if not isinstance(self.curriculum_manager, NullCurriculumManager):
       self.curriculum_manager.compute(env_ids=None)
       self._curriculum_log = self.curriculum_manager.reset(None)
+    self.reward_manager.sync_weights()
     for name in self.command_manager.active_terms:
       t = self.command_manager.get_term(name)
       if hasattr(t, "sync_ranges"):
         t.sync_ranges()
 
   def _capture_key(self):
-    w = tuple(float(c.weight) for c in self.reward_manager._term_cfgs)
-    return (w, self.sim.struct_version)
+    return (self.reward_manager.active_pattern, self.sim.struct_version)
 
   def _capture(self, key) -> None:
     self._graph = None

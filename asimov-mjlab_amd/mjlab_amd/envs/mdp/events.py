@@ -15,7 +15,8 @@ import torch
 
 from mjlab_amd.managers.manager_base import as_mask
 from mjlab_amd.managers.scene_entity_config import SceneEntityCfg
-from mjlab_amd.utils.math import quat_from_euler_xyz, quat_mul
+from mjlab_amd.envops import quat_mul
+from mjlab_amd.utils.math import quat_from_euler_xyz
 
 _DEFAULT = SceneEntityCfg("robot")
 _AXES6 = ["x", "y", "z", "roll", "pitch", "yaw"]

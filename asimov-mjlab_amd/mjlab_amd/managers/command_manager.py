@@ -22,9 +22,13 @@ class CommandTerm(ManagerTermBase):
   def reset(self, env_ids=None) -> dict:
     m = as_mask(env_ids, self.num_envs, self.device)
     extras = {}
-    for k, v in self.metrics.items():
-      extras[k] = masked_mean(v, m)
-      v.masked_fill_(m, 0.0)
+    if self.metrics:
+      w = m.float()
+      vals = torch.stack(list(self.metrics.values()), dim=1)
+      means = (vals * w[:, None]).sum(0) / w.sum().clamp(min=1.0)
+      for i, (k, v) in enumerate(self.metrics.items()):
+        extras[k] = means[i]
+        v.masked_fill_(m, 0.0)
     self.command_counter.masked_fill_(m, 0)
     self._resample(m)
     return extras

@@ -4,7 +4,7 @@ from __future__ import annotations
 
 import torch
 
-from mjlab_amd.managers.manager_base import as_mask, masked_mean, resolve_params
+from mjlab_amd.managers.manager_base import as_mask, resolve_params
 
 
 class RewardManager:
@@ -23,10 +23,27 @@ class RewardManager:
         self._class_term_cfgs.append(tcfg)
       self._term_names.append(name)
       self._term_cfgs.append(tcfg)
-    n = env.num_envs
-    self._episode_sums = {k: torch.zeros(n, device=env.device) for k in self._term_names}
+    n, t = env.num_envs, len(self._term_names)
+    # one (N, T) accumulator; the per-term dict holds column views (API parity)
+    self._sums = torch.zeros(n, t, device=env.device)
+    self._episode_sums = {k: self._sums[:, i] for i, k in enumerate(self._term_names)}
     self._reward_buf = torch.zeros(n, device=env.device)
-    self._step_reward = torch.zeros(n, len(self._term_names), device=env.device)
+    self._step_reward = torch.zeros(n, t, device=env.device)
+    # weights live on the device, refreshed on the host before each (graph) step
+    self._w = torch.zeros(t, device=env.device)
+    self._w_host: tuple | None = None
+    self.sync_weights()
+
+  def sync_weights(self) -> None:
+    w = tuple(float(c.weight) for c in self._term_cfgs)
+    if w != self._w_host:
+      self._w.copy_(torch.tensor(w, dtype=torch.float32))
+      self._w_host = w
+
+  @property
+  def active_pattern(self) -> tuple[bool, ...]:
+    """Which terms are evaluated (weight != 0); changing it changes the op sequence."""
+    return tuple(float(c.weight) != 0.0 for c in self._term_cfgs)
 
   @property
   def active_terms(self) -> list[str]:
@@ -34,25 +51,32 @@ class RewardManager:
 
   def reset(self, env_ids=None) -> dict:
     m = as_mask(env_ids, self._env.num_envs, self._env.device)
-    extras = {}
-    for k, s in self._episode_sums.items():
-      extras["Episode_Reward/" + k] = masked_mean(s, m) / self._env.max_episode_length_s
-      s.masked_fill_(m, 0.0)
+    w = m.float()
+    means = (self._sums * w[:, None]).sum(0) / (w.sum().clamp(min=1.0) * self._env.max_episode_length_s)
+    extras = {"Episode_Reward/" + k: means[i] for i, k in enumerate(self._term_names)}
+    self._sums.masked_fill_(m[:, None], 0.0)
     for tcfg in self._class_term_cfgs:
       if hasattr(tcfg.func, "reset"):
         tcfg.func.reset(env_ids=env_ids)
     return extras
 
   def compute(self, dt: float) -> torch.Tensor:
-    self._reward_buf.zero_()
-    for i, (name, tcfg) in enumerate(zip(self._term_names, self._term_cfgs)):
-      if tcfg.weight == 0.0:
-        self._step_reward[:, i] = 0.0
-        continue
-      value = tcfg.func(self._env, **tcfg.params) * tcfg.weight * dt
-      self._reward_buf += value
-      self._episode_sums[name] += value
-      self._step_reward[:, i] = value / dt
+    """sum_i term_i * weight_i * dt (reward_manager.py:76-88); zero-weight terms
+    are skipped and report 0, as in the reference."""
+    vals = [
+      tcfg.func(self._env, **tcfg.params).float() if tcfg.weight != 0.0 else None
+      for tcfg in self._term_cfgs
+    ]
+    zero = None
+    for i, v in enumerate(vals):
+      if v is None:
+        zero = zero if zero is not None else torch.zeros_like(self._reward_buf)
+        vals[i] = zero
+    raw = torch.stack(vals, dim=1)  # (N, T) unweighted term values
+    weighted = raw * (self._w * dt)
+    self._step_reward.copy_(raw * self._w)  # value / dt = term * weight
+    self._sums += weighted
+    torch.sum(weighted, dim=1, out=self._reward_buf)
     return self._reward_buf
 
   def get_term_cfg(self, name: str):

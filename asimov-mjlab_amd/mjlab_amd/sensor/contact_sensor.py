@@ -16,6 +16,8 @@ from typing import Literal
 
 import torch
 
+from mjlab_amd import envops
+
 from mjlab_amd.spec.spec import SensorSpec, Spec
 
 _CONTACT_DATA_MAP = {"found": 0, "force": 1, "torque": 2, "dist": 3, "pos": 4, "normal": 5, "tangent": 6}
@@ -176,6 +178,9 @@ class ContactSensor:
       a, d = int(s.adr[0]), int(s.dim[0])
       slot.data_view = data.sensordata[:, a : a + d]
     self._data = data
+    # sensordata columns of the `found` slots, for the fused timer kernel
+    fcols = [int(model.sensor(sl.sensor_name).adr[0]) for sl in self._slots if sl.field_name == "found"]
+    self._found_cols = torch.tensor(fcols, dtype=torch.int32, device=device)
     if self.cfg.track_air_time:
       n = data.time.shape[0]
       k = len({s.primary_name for s in self._slots})
@@ -252,6 +257,11 @@ class ContactSensor:
 
   def _update_air_time_tracking(self) -> None:
     st = self._air_time_state
+    if self._found_cols.numel() == st.current_air_time.shape[1] and envops.air_time_update(
+      self._data.sensordata, self._found_cols, self._data.time, st.last_time, st.current_air_time, st.last_air_time,
+      st.current_contact_time, st.last_contact_time,
+    ):
+      return
     cd = self._extract_sensor_data()
     if cd.found is None:
       return

@@ -36,6 +36,10 @@ EXPORTS = (
   "mjh_forward",
   "mjh_forward_gated",
   "mjh_repeat",
+  "mjh_quat_rotate",
+  "mjh_quat_mul",
+  "mjh_velocity_from_cvel",
+  "mjh_air_time_update",
 )
 
 
@@ -71,6 +75,11 @@ def lib() -> ctypes.CDLL:
   L.mjh_forward_gated.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
   L.mjh_forward_gated.restype = ctypes.c_int
   L.mjh_repeat.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p]
+  ll, vp, ci = ctypes.c_longlong, ctypes.c_void_p, ctypes.c_int
+  L.mjh_quat_rotate.argtypes = [vp, ll, vp, ll, vp, ll, ci, vp]
+  L.mjh_quat_mul.argtypes = [vp, ll, vp, ll, vp, ll, vp]
+  L.mjh_velocity_from_cvel.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp]
+  L.mjh_air_time_update.argtypes = [vp, ll, vp, ci, vp, vp, vp, vp, vp, vp, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

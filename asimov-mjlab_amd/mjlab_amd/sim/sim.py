@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from mjlab_amd.sim import abi, native
-from mjlab_amd.sim.sim_data import BATCHED_STATIC, DATA_SHAPES, MODEL_SHAPES, Bridge, make_opt, shape_of
+from mjlab_amd.sim.sim_data import Epoch, BATCHED_STATIC, DATA_SHAPES, MODEL_SHAPES, Bridge, make_opt, shape_of
 from mjlab_amd.spec.compiler import Model
 
 _INTEGRATORS = {"euler": 0, "implicitfast": 3}
@@ -140,7 +140,8 @@ class Simulation:
       self._data_flat[f.name] = torch.zeros((num_envs, n), dtype=_TORCH_DT[f.ctype], device=device)
     self._data_flat["qpos"][:] = torch.as_tensor(model.qpos0, dtype=torch.float32, device=device)
     data_views = {n: self._data_view(n) for n in self._data_flat}
-    self._data_bridge = Bridge(data_views, nworld=num_envs)
+    self.epoch = Epoch()
+    self._data_bridge = Bridge(data_views, extra={"epoch": self.epoch}, nworld=num_envs)
 
     self._build_structs()
     self.use_cuda_graph = str(device).startswith("cuda") and torch.cuda.is_available()
@@ -315,6 +316,7 @@ class Simulation:
 
   def forward(self) -> None:
     self._require_gpu()
+    self.epoch.bump()
     if torch.cuda.is_current_stream_capturing():
       self._launch_forward()
       return
@@ -329,6 +331,7 @@ class Simulation:
     a captured graph where the reference syncs on ``len(reset_env_ids) > 0``
     (``manager_based_rl_env.py:155-160``)."""
     self._require_gpu()
+    self.epoch.bump()
     if gate.dtype not in (torch.bool, torch.uint8) or gate.numel() != 1 or not gate.is_cuda:
       raise ValueError("gate must be a one-element bool/uint8 device tensor")
     native.check(
@@ -340,6 +343,7 @@ class Simulation:
 
   def step(self) -> None:
     self._require_gpu()
+    self.epoch.bump()
     if torch.cuda.is_current_stream_capturing():
       self._launch_step()  # being captured into an enclosing (env-step) graph
       return
@@ -362,6 +366,7 @@ class Simulation:
   def load_state_dict(self, state: dict[str, torch.Tensor]) -> None:
     for k, v in state.items():
       self._data_flat[k].copy_(v)
+    self.epoch.bump()
 
 
 def detect_nans(data) -> torch.Tensor:

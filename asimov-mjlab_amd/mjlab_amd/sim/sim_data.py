@@ -113,6 +113,20 @@ def shape_of(spec: tuple, sizes: dict[str, int]) -> tuple[int, ...]:
   return tuple(sizes[s] if isinstance(s, str) else s for s in spec)
 
 
+class Epoch:
+  """Monotonic counter bumped whenever the sim data changes (step, forward,
+  state writes). Derived-quantity caches (EntityData, ContactSensor) key on
+  it; it is host state, so a captured graph replays the same cache hits."""
+
+  __slots__ = ("v",)
+
+  def __init__(self) -> None:
+    self.v = 0
+
+  def bump(self) -> None:
+    self.v += 1
+
+
 class Bridge:
   """Read-only attribute namespace over torch tensors (pointer-stable)."""
 

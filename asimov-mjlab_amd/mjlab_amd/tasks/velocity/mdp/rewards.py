@@ -9,7 +9,7 @@ from __future__ import annotations
 import torch
 
 from mjlab_amd.managers.scene_entity_config import SceneEntityCfg
-from mjlab_amd.utils.math import quat_apply_inverse
+from mjlab_amd.envops import quat_apply_inverse
 from mjlab_amd.utils.string import resolve_matching_names_values
 
 _DEFAULT = SceneEntityCfg("robot")

@@ -14,7 +14,8 @@ import torch
 
 from mjlab_amd.managers.command_manager import CommandTerm
 from mjlab_amd.managers.manager_term_config import CommandTermCfg
-from mjlab_amd.utils.math import quat_apply, wrap_to_pi
+from mjlab_amd.envops import quat_apply
+from mjlab_amd.utils.math import wrap_to_pi
 
 
 class UniformVelocityCommand(CommandTerm):
@@ -48,9 +49,10 @@ class UniformVelocityCommand(CommandTerm):
       self._ranges_t.copy_(torch.tensor(host, dtype=torch.float32))
       self._ranges_host = host
 
-  def _u(self, i: int) -> torch.Tensor:
-    lo, hi = self._ranges_t[i, 0], self._ranges_t[i, 1]
-    return torch.rand(self.num_envs, device=self.device) * (hi - lo) + lo
+  def _draw(self) -> torch.Tensor:
+    """(N, 4) uniform draws over [lin_vel_x, lin_vel_y, ang_vel_z, heading] ranges."""
+    lo, hi = self._ranges_t[:, 0], self._ranges_t[:, 1]
+    return torch.rand(self.num_envs, 4, device=self.device) * (hi - lo) + lo
 
   def _update_metrics(self) -> None:
     max_command_step = self.cfg.resampling_time_range[1] / self._env.step_dt
@@ -59,14 +61,13 @@ class UniformVelocityCommand(CommandTerm):
     self.metrics["error_vel_yaw"] += torch.abs(self.vel_command_b[:, 2] - d.root_link_ang_vel_b[:, 2]) / max_command_step
 
   def _resample_command(self, mask: torch.Tensor) -> None:
-    new = torch.stack([self._u(0), self._u(1), self._u(2)], dim=-1)
-    self.vel_command_b.copy_(torch.where(mask[:, None], new, self.vel_command_b))
+    new = self._draw()
+    self.vel_command_b.copy_(torch.where(mask[:, None], new[:, :3], self.vel_command_b))
+    u = torch.rand(self.num_envs, 2, device=self.device)
     if self.cfg.heading_command:
-      self.heading_target.copy_(torch.where(mask, self._u(3), self.heading_target))
-      hv = torch.rand(self.num_envs, device=self.device) <= self.cfg.rel_heading_envs
-      self.is_heading_env.copy_(torch.where(mask, hv, self.is_heading_env))
-    sv = torch.rand(self.num_envs, device=self.device) <= self.cfg.rel_standing_envs
-    self.is_standing_env.copy_(torch.where(mask, sv, self.is_standing_env))
+      self.heading_target.copy_(torch.where(mask, new[:, 3], self.heading_target))
+      self.is_heading_env.copy_(torch.where(mask, u[:, 0] <= self.cfg.rel_heading_envs, self.is_heading_env))
+    self.is_standing_env.copy_(torch.where(mask, u[:, 1] <= self.cfg.rel_standing_envs, self.is_standing_env))
     if self.cfg.init_velocity_prob > 0.0:
       iv = mask & (torch.rand(self.num_envs, device=self.device) < self.cfg.init_velocity_prob)
       d = self.robot.data

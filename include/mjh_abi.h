@@ -134,6 +134,29 @@ int mjh_forward_gated(const mjh_model* m, const mjh_data* d, const unsigned char
  * Replaces repeat_array_kernel (randomization.py:9-17). */
 int mjh_repeat(float* dst, const float* src, long long nelem, int nworld, void* stream);
 
+/* ---- fused env-layer kernels (mjh_envops.hip) ----
+ * Rows are addressed by a row stride in floats (last-dim stride 1); outputs are
+ * contiguous. They replace chains of torch ops in mjlab's entity/sensor reads,
+ * with the same formulas (isaaclab/utils/math.py, contact_sensor.py:327-367). */
+
+/* out[i] = q[i] (x) v[i] (x) q[i]^-1, or with q^-1 when inverse != 0
+ * (quat_apply / quat_apply_inverse). */
+int mjh_quat_rotate(const float* q, long long qs, const float* v, long long vs, float* out, long long n, int inverse,
+                    void* stream);
+
+/* out[i] = p[i] * q[i] (quat_mul). */
+int mjh_quat_mul(const float* p, long long ps, const float* q, long long qs, float* out, long long n, void* stream);
+
+/* out[i] = [cvel_lin - cvel_ang x (com - pos), cvel_ang] (entity/data.py:20-31). */
+int mjh_velocity_from_cvel(const float* pos, long long ps, const float* com, long long cs, const float* cvel, long long vs,
+                           float* out, long long n, void* stream);
+
+/* Contact-sensor air/contact timers for k tracked slots whose `found` values
+ * sit at sensordata[:, cols[j]] (contact_sensor.py:327-367). */
+int mjh_air_time_update(const float* sensordata, long long sds, const int* cols, int k, const float* time,
+                        float* last_time, float* cur_air, float* last_air, float* cur_con, float* last_con, long long n,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif

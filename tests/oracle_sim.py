@@ -18,6 +18,7 @@ def attach(sim, overrides_fields=()) -> None:
   state_fields = [f for f in INPUTS]
 
   def run(integrate: bool) -> None:
+    sim.epoch.bump()
     ov = {f: getattr(sim.model, f).detach().cpu().numpy() for f in overrides_fields}
     orc = Oracle(sim.mj_model, "f64", overrides=ov)
     st = {}

@@ -96,8 +96,8 @@ def test_curriculum_updates_command_ranges():
 @pytest.mark.parametrize("task", [G1, GO1])
 def test_step_body_is_capture_safe(task):
   env = make(task, n=6)
-  env.sim.step = lambda: None
-  env.sim.forward_gated = lambda g: None
+  env.sim.step = env.sim.epoch.bump
+  env.sim.forward_gated = lambda g: env.sim.epoch.bump()
   env.reset()
   env.step(torch.zeros(6, env.action_manager.total_action_dim))
   env.episode_length_buf[:3] = 10_000  # force resets inside the guarded body

@@ -1,0 +1,68 @@
+"""Fused env-layer kernels (csrc/mjh_envops.hip) vs their torch formulas."""
+
+import pytest
+import torch
+
+from mjlab_amd import envops
+from mjlab_amd.entity.data import compute_velocity_from_cvel
+from mjlab_amd.utils import math as M
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _q(n, g):
+  q = torch.randn(n, 4, generator=g, device=DEV)
+  return q / q.norm(dim=-1, keepdim=True)
+
+
+def test_quat_kernels_match_torch():
+  g = torch.Generator(device=DEV).manual_seed(0)
+  n = 5000
+  pose = torch.cat([torch.randn(n, 3, device=DEV, generator=g), _q(n, g)], dim=1)  # strided quaternion view
+  q = pose[:, 3:7]
+  vel = torch.randn(n, 6, device=DEV, generator=g)
+  v = vel[:, 0:3]
+  torch.testing.assert_close(envops.quat_apply_inverse(q, v), M.quat_apply_inverse(q, v), rtol=1e-5, atol=1e-5)
+  torch.testing.assert_close(envops.quat_apply(q, v), M.quat_apply(q, v), rtol=1e-5, atol=1e-5)
+  q2 = _q(n, g)
+  torch.testing.assert_close(envops.quat_mul(q, q2), M.quat_mul(q.contiguous(), q2), rtol=1e-5, atol=1e-5)
+  qb = q2[:1].expand(n, -1)  # row stride 0 broadcast
+  torch.testing.assert_close(envops.quat_mul(q, qb), M.quat_mul(q.contiguous(), qb.contiguous()), rtol=1e-5, atol=1e-5)
+
+
+def test_velocity_from_cvel_matches_torch():
+  g = torch.Generator(device=DEV).manual_seed(1)
+  n = 3000
+  xpos, com, cvel = (torch.randn(n, k, device=DEV, generator=g) for k in (3, 3, 6))
+  torch.testing.assert_close(
+    envops.velocity_from_cvel(xpos, com, cvel, compute_velocity_from_cvel), compute_velocity_from_cvel(xpos, com, cvel),
+    rtol=1e-5, atol=1e-5,
+  )
+
+
+def test_air_time_kernel_matches_torch_rule():
+  g = torch.Generator(device=DEV).manual_seed(2)
+  n, k = 1000, 2
+  sd = torch.zeros(n, 7, device=DEV)
+  cols = torch.tensor([1, 5], dtype=torch.int32, device=DEV)
+  st = [torch.rand(n, k, device=DEV, generator=g) * (torch.rand(n, k, device=DEV, generator=g) > 0.5) for _ in range(4)]
+  last_time = torch.rand(n, device=DEV, generator=g)
+  time = last_time + 0.005
+  sd[:, 1] = (torch.rand(n, device=DEV, generator=g) > 0.5).float() * 2
+  sd[:, 5] = (torch.rand(n, device=DEV, generator=g) > 0.5).float()
+  ca, la, cc, lc = (t.clone() for t in st)
+  # torch rule (contact_sensor.py air-time tracking)
+  el = (time - last_time)[:, None]
+  is_c = sd[:, [1, 5]] > 0
+  first_c = (ca > 0) & is_c
+  first_d = (cc > 0) & ~is_c
+  la_ref = torch.where(first_c, ca + el, la)
+  ca_ref = torch.where(~is_c, ca + el, torch.zeros_like(ca))
+  lc_ref = torch.where(first_d, cc + el, lc)
+  cc_ref = torch.where(is_c, cc + el, torch.zeros_like(cc))
+  lt = last_time.clone()
+  assert envops.air_time_update(sd, cols, time, lt, ca, la, cc, lc)
+  torch.cuda.synchronize()
+  for a, b in ((ca, ca_ref), (la, la_ref), (cc, cc_ref), (lc, lc_ref), (lt, time)):
+    torch.testing.assert_close(a, b)
