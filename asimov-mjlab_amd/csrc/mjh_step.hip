@@ -69,14 +69,14 @@ enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
 #define MJH_REGIONS(X)                                                                              \
   X(qpos, 1) X(qvel, 0) X(qacc, 0) X(qacc_smooth, 0) X(qfrc_smooth, 0) X(qfrc_bias, 1) X(qfrc_con, 0)  \
   X(qfrc_passive, 1) X(qfrc_act, 1) X(grad, 0) X(search, 0) X(Ma, 0) X(Mv, 0) X(tmp, 0) X(tmp2, 0)    \
-  X(xpos, 1) X(xquat, 1) X(xmat, 1) X(xipos, 1) X(ximat, 1) X(subtree_com, 1) X(cinert, 1) X(crb, 1)  \
-  X(cvel, 1) X(cacc, 1) X(cfrc, 1) X(xanchor, 1) X(xaxis, 1) X(cdof, 1) X(cdof_dot, 1)               \
+  X(xpos, 1) X(xquat, 1) X(xmat, 1) X(xipos, 1) X(ximat, 1) X(subtree_com, 1) X(cinert, 0) X(crb, 0)  \
+  X(cvel, 0) X(cacc, 1) X(cfrc, 0) X(xanchor, 1) X(xaxis, 1) X(cdof, 0) X(cdof_dot, 0)               \
   X(cgpos, 1) X(cgmat, 1) X(sxpos, 1) X(sxmat, 1) X(M, 1) X(L, 1) X(act_force, 1)                    \
   X(con_pos, 1) X(con_frame, 1) X(con_dist, 1) X(con_fric, 1) X(con_solref, 1) X(con_solimp, 1)       \
   X(con_imargin, 1) X(con_dim, 1) X(con_geom, 1) X(con_efcadr, 1)                                     \
   X(J, 0) X(efc_D, 0) X(efc_R, 0) X(efc_aref, 0) X(efc_jaref, 0) X(efc_jv, 0) X(efc_force, 0)        \
-  X(efc_fl, 0) X(efc_pos, 0) X(efc_type, 0) X(efc_id, 0) X(efc_mask, 0) X(efc_h, 0) X(arow, 0)       \
-  X(ash, 0) X(arow_prev, 0)
+  X(efc_fl, 0) X(efc_pos, 1) X(efc_type, 0) X(efc_id, 1) X(efc_mask, 1) X(efc_h, 0) X(arow, 0)       \
+  X(ash, 0) X(arow_prev, 1)
 struct Rg {
 #if MJH_PRESET == 0
 #define X_RG(name, r) static constexpr bool name = false;
@@ -143,14 +143,47 @@ struct ImgOff {
 #define IMG_L(name) (reinterpret_cast<const long long*>(smem + Io.name))
 #define WFIELD(name) (m.name##_wstride ? (const float*)(m.name + W * m.name##_wstride) : (const float*)(smem + Io.name))
 
+// ---- wave primitives on DPP (no LDS round trips) -----------------------------
+// dpp_ctrl: quad_perm 0x00-0xff, row_shr:n 0x110+n, row_mirror 0x140,
+// row_half_mirror 0x141, row_bcast:15 0x142, row_bcast:31 0x143 (GFX9 DPP).
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf, bool BOUND_ZERO = true>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, BANK_MASK, BOUND_ZERO));
+}
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf, bool BOUND_ZERO = true>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, BANK_MASK, BOUND_ZERO);
+}
+
+// sum over the 64 lanes, returned uniformly (lane 63 holds the total)
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dppf<0xB1>(v);          // quad_perm [1,0,3,2]
+  v += dppf<0x4E>(v);          // quad_perm [2,3,0,1]
+  v += dppf<0x141>(v);         // row_half_mirror: 8-lane sums
+  v += dppf<0x140>(v);         // row_mirror: 16-lane (row) sums
+  v += dppf<0x142, 0xa>(v);    // row_bcast:15 into rows 1, 3
+  v += dppf<0x143, 0xc>(v);    // row_bcast:31 into rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ int wave_incl_scan(int a) {
+  int x = a + dppi<0x111>(a) + dppi<0x112>(a) + dppi<0x113>(a);  // a[i-3..i] within the row
+  x += dppi<0x114, 0xf, 0xe>(x);  // row_shr:4 into banks 1-3
+  x += dppi<0x118, 0xf, 0xc>(x);  // row_shr:8 into banks 2-3
+  x += dppi<0x142, 0xa, 0xf, false>(x);  // row_bcast:15 into rows 1, 3
+  x += dppi<0x143, 0xc, 0xf, false>(x);  // row_bcast:31 into rows 2, 3
+  return x;
+}
+
 // ---- block-level primitives -------------------------------------------------
 template <int NT>
 __device__ __forceinline__ float bsum(float v, float* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if constexpr (NT == 64) {
-    return v;
+    return wave_sum(v);
   } else {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     wsync();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     wsync();
@@ -163,12 +196,15 @@ __device__ __forceinline__ float bsum(float v, float* red) {
 
 template <int NT>
 __device__ __forceinline__ void bsum2(float& a, float& b, float* red) {
+  if constexpr (NT == 64) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+  } else {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    a += __shfl_xor(a, o, 64);
-    b += __shfl_xor(b, o, 64);
-  }
-  if constexpr (NT != 64) {
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_xor(a, o, 64);
+      b += __shfl_xor(b, o, 64);
+    }
     wsync();
     if ((threadIdx.x & 63) == 0) {
       red[2 * (threadIdx.x >> 6)] = a;
@@ -188,14 +224,9 @@ __device__ __forceinline__ void bsum2(float& a, float& b, float* red) {
 template <int NT>
 __device__ __forceinline__ int bscan(int v, int* total, int* redi) {
   const int lane = threadIdx.x & 63;
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
+  const int x = wave_incl_scan(v);
   if constexpr (NT == 64) {
-    *total = __shfl(x, 63, 64);
+    *total = __builtin_amdgcn_readlane(x, 63);
     return x - v;
   } else {
     const int wv = threadIdx.x >> 6;
@@ -361,27 +392,30 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
   v4f acc[10];
 #pragma unroll
   for (int t = 0; t < 10; t++) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
-  int kk = kq;
-  int r = kk < nact ? arow[kk] : 0;
-  float sc = kk < nact ? ash[kk] : 0.f;
-  for (int k0 = 0; k0 < nact; k0 += 4) {
-    // this k-step's 4 rows (one per lane quarter), all column blocks at once
-    float v[4];
+  // software pipeline: the next k-step's J values are loaded (J may live in
+  // L2) while this step's MFMAs run
+  auto load = [&](int k, float (&v)[4]) {
+    const int r = k < nact ? arow[k] : 0;
+    const float sc = k < nact ? ash[k] : 0.f;
 #pragma unroll
     for (int b = 0; b < 4; b++) {
       const int c = b * 16 + ci;
       v[b] = (b < nb && c < n) ? J[r * ldj + c] * sc : 0.f;
     }
-    // prefetch the next k-step's row id / scale
-    const int kn = k0 + 4 + kq;
-    r = kn < nact ? arow[kn] : 0;
-    sc = kn < nact ? ash[kn] : 0.f;
+  };
+  float v[4];
+  load(kq, v);
+  for (int k0 = 0; k0 < nact; k0 += 4) {
+    float vn[4];
+    load(k0 + 4 + kq, vn);
     int t = 0;
 #pragma unroll
     for (int I = 0; I < 4; I++)
 #pragma unroll
       for (int Jb = 0; Jb <= I; Jb++, t++)
         if (I < nb) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[I], v[Jb], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int b = 0; b < 4; b++) v[b] = vn[b];
   }
   int t = 0;
 #pragma unroll
@@ -1120,14 +1154,22 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
   wsync();
   {
     const float* xfrc = d.xfrc_applied + W * nb * 6;
+    // bodies with a nonzero applied wrench, found with one load round (lane =
+    // body) instead of a dependent global-load chain per dof
+    bool nzf = false;
+    if (tid > 0 && tid < nb) {
+      const float* f = xfrc + 6 * tid;
+      nzf = f[0] != 0.f || f[1] != 0.f || f[2] != 0.f || f[3] != 0.f || f[4] != 0.f || f[5] != 0.f;
+    }
+    const unsigned long long nzb = __ballot(nzf);
     for (int i = tid; i < nv; i += NT) {
       float s = qfrc_passive[i] - qfrc_bias[i] + d.qfrc_applied[W * nv + i] + qfrc_act[i];
       // J^T xfrc_applied at each body com
       const float* cd = cdof + 6 * i;
-      for (int b = 1; b < nb; b++) {
+      for (unsigned long long bm = nzb; bm; bm &= bm - 1) {
+        const int b = __builtin_ctzll(bm);
         if (!(((unsigned long long)IMG_L(body_dofmask)[b] >> i) & 1ull)) continue;
         const float* f = xfrc + 6 * b;
-        if (f[0] == 0.f && f[1] == 0.f && f[2] == 0.f && f[3] == 0.f && f[4] == 0.f && f[5] == 0.f) continue;
         const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
         float off[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
         cross3(t, cd, off);
@@ -2040,10 +2082,14 @@ Layout make_layout(const mjh_model* m, int budget) {
   L.ints = off; off += al(8);
   // constraint rows: as many as fit in the remaining LDS budget (rows in LDS)
   // or njmax (rows in global scratch)
-  const int per_row_lds = (Rg::J ? 0 : L.ldj) + (Rg::efc_D ? 0 : 16 + 2);
+  // LDS words per constraint row (16-byte alignment padding is absorbed by
+  // the 32-word slack below)
+  const int per_row_lds = (Rg::J ? 0 : L.ldj) + !Rg::efc_D + !Rg::efc_R + !Rg::efc_aref + !Rg::efc_jaref +
+                          !Rg::efc_jv + !Rg::efc_force + !Rg::efc_fl + !Rg::efc_pos + !Rg::efc_type + !Rg::efc_id +
+                          2 * !Rg::efc_mask + !Rg::efc_h + !Rg::arow + !Rg::ash + !Rg::arow_prev;
   int rcap = m->njmax;
   if (per_row_lds > 0) {
-    const int r = (budget - off - 32) / per_row_lds;
+    const int r = (budget - off - 64) / per_row_lds;
     if (r < rcap) rcap = r;
   }
   if (rcap < 1) rcap = 1;

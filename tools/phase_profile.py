@@ -17,7 +17,8 @@ sys.path.insert(0, str(ROOT / "tools"))
 import numpy as np
 import torch
 
-from gpu_check import g1_scene, random_states
+sys.path.insert(0, str(ROOT))
+from tests.scenes import g1_scene, random_states
 from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg, native
 
 NAMES = ["kinematics", "com/crb/M/factor", "rne/smooth/qacc_smooth", "collision", "constraints", "solver",
@@ -34,10 +35,10 @@ assert L.mjh_set_profile_buffer(ctypes.c_void_p(buf.data_ptr())) == 0  # before 
 torch.cuda.synchronize()
 sim = Simulation(N, cfg, m, "cuda:0")
 rng = np.random.default_rng(0)
-st = random_states(m, N, rng)
+st = random_states(m, N, rng, drop=0.03)
 for k, v in st.items():
   getattr(sim.data, k)[:] = torch.as_tensor(v, dtype=torch.float32, device="cuda:0").view_as(getattr(sim.data, k))
-for _ in range(3):
+for _ in range(int(os.environ.get("SETTLE", "20"))):
   sim.step()
 torch.cuda.synchronize()
 p = buf.view(N, 32).cpu().numpy().astype(np.int64)
