@@ -134,3 +134,30 @@ int mjh_air_time_update(const float* sensordata, long long sds, const int* cols,
 }
 
 }  // extern "C"
+
+// ---- observation term post-processing, written into its slice of the group
+// buffer: out = clip(x + (u * (hi - lo) + lo), cmin, cmax) * scale
+// (observation_manager.py:163-176: noise -> clip -> scale; u = U[0,1) draws,
+// null when the term has no noise; clip skipped when cmin > cmax)
+namespace {
+__global__ void obs_term_kernel(const float* __restrict__ x, long long xs, const float* __restrict__ u, long long us,
+                                float lo, float hi, float cmin, float cmax, float scale, float* __restrict__ out,
+                                long long os, int w, long long n) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * w) return;
+  const long long e = t / w;
+  const int j = (int)(t - e * w);
+  float v = x[e * xs + j];
+  if (u) v = v + (u[e * us + j] * (hi - lo) + lo);
+  if (cmin <= cmax) v = fminf(fmaxf(v, cmin), cmax);
+  out[e * os + j] = v * scale;
+}
+}  // namespace
+
+extern "C" int mjh_obs_term(const float* x, long long xs, const float* u, long long us, float lo, float hi, float cmin,
+                            float cmax, float scale, float* out, long long os, int w, long long n, void* stream) {
+  if (n <= 0 || w <= 0) return 0;
+  hipLaunchKernelGGL(obs_term_kernel, dim3((int)((n * w + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, xs, u, us,
+                     lo, hi, cmin, cmax, scale, out, os, w, n);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -65,14 +65,30 @@ def _masked_write(dst: torch.Tensor, cols: torch.Tensor | slice, value: torch.Te
       dst[rows, cols.long()] = value
     return
   if env_ids.dtype == torch.bool:
-    cols_l = torch.arange(dst.shape[1], device=dst.device)[cols] if isinstance(cols, slice) else cols.long()
+    m = env_ids.view(-1, *([1] * (dst.dim() - 1)))
+    if isinstance(cols, slice):  # in place on the strided view: where + copy, no gather/scatter
+      cur = dst[:, cols]
+      cur.copy_(torch.where(m, value, cur))
+      return
+    cols_l = cols.long()
     cur = dst[:, cols_l]
     value = value.expand_as(cur) if value.dim() <= cur.dim() else value
-    dst[:, cols_l] = torch.where(env_ids.view(-1, *([1] * (cur.dim() - 1))), value, cur)
+    dst[:, cols_l] = torch.where(m, value, cur)
     return
   idx = env_ids.long()[:, None]
   cols_l = torch.arange(dst.shape[1], device=dst.device)[cols] if isinstance(cols, slice) else cols.long()
   dst[idx, cols_l] = value
+
+
+def _as_slice(idx: torch.Tensor):
+  """slice(a, b) if idx == arange(a, b) (checked once, at init), else idx."""
+  if idx.numel() == 0:
+    return idx
+  h = idx.detach().cpu()
+  a = int(h[0])
+  if torch.equal(h, torch.arange(a, a + h.numel(), dtype=h.dtype)):
+    return slice(a, a + h.numel())
+  return idx
 
 
 @dataclass
@@ -95,6 +111,27 @@ class EntityData:
   is_articulated: bool
   is_actuated: bool
 
+  def __post_init__(self) -> None:
+    # int64 copies of the index tensors, made once: `.long()` on the int32
+    # originals would launch a conversion kernel on every access
+    ix = self.indexing
+    self._ix = {
+      k: getattr(ix, k).long()
+      for k in ("body_ids", "geom_ids", "site_ids", "ctrl_ids", "joint_ids", "joint_q_adr", "joint_v_adr",
+                "free_joint_q_adr", "free_joint_v_adr")
+    }
+    self._ix["geom_bodyid"] = self.model.geom_bodyid[self._ix["geom_ids"]].long()
+    self._ix["site_bodyid"] = self.model.site_bodyid[self._ix["site_ids"]].long()
+    self._ix["root_quat_adr"] = self._ix["free_joint_q_adr"][3:7]
+    # column sets that are contiguous ranges (the usual case: one entity's
+    # joints/dofs/actuators/bodies are consecutive) are written through slices
+    self._cols = {k: _as_slice(v) for k, v in self._ix.items()}
+    gb = self._ix["body_ids"]
+    wcols = (gb[:, None] * 6 + torch.arange(6, device=gb.device)).reshape(-1)
+    self._cols["xfrc_all"] = _as_slice(wcols)
+    self._cols["xfrc_force"] = _as_slice((gb[:, None] * 6 + torch.arange(3, device=gb.device)).reshape(-1))
+    self._cols["xfrc_torque"] = _as_slice((gb[:, None] * 6 + 3 + torch.arange(3, device=gb.device)).reshape(-1))
+
   ROOT_POSE_DIM = 7
   ROOT_VEL_DIM = 6
   ROOT_STATE_DIM = 13
@@ -111,13 +148,13 @@ class EntityData:
     if self.is_fixed_base:
       raise ValueError("Cannot write root pose for fixed-base entity.")
     assert pose.shape[-1] == self.ROOT_POSE_DIM
-    _masked_write(self.data.qpos, self.indexing.free_joint_q_adr, pose, env_ids)
+    _masked_write(self.data.qpos, self._cols["free_joint_q_adr"], pose, env_ids)
 
   def write_root_velocity(self, velocity: torch.Tensor, env_ids=None) -> None:
     if self.is_fixed_base:
       raise ValueError("Cannot write root velocity for fixed-base entity.")
     assert velocity.shape[-1] == self.ROOT_VEL_DIM
-    qadr = self.indexing.free_joint_q_adr[3:7].long()
+    qadr = self._ix["root_quat_adr"]
     if env_ids is None or isinstance(env_ids, slice) or env_ids.dtype == torch.bool:
       quat_w = self.data.qpos[:, qadr] if not isinstance(env_ids, slice) else self.data.qpos[env_ids][:, qadr]
     else:
@@ -126,7 +163,7 @@ class EntityData:
       velocity = velocity.expand(quat_w.shape[0], -1)
     ang_b = quat_apply_inverse(quat_w, velocity[:, 3:])
     qv = torch.cat([velocity[:, :3], ang_b], dim=-1)
-    _masked_write(self.data.qvel, self.indexing.free_joint_v_adr, qv, env_ids)
+    _masked_write(self.data.qvel, self._cols["free_joint_v_adr"], qv, env_ids)
 
   def write_joint_state(self, position, velocity, joint_ids=None, env_ids=None) -> None:
     if not self.is_articulated:
@@ -137,43 +174,60 @@ class EntityData:
   def write_joint_position(self, position, joint_ids=None, env_ids=None) -> None:
     if not self.is_articulated:
       raise ValueError("Cannot write joint position for non-articulated entity.")
-    cols = self.indexing.joint_q_adr[joint_ids if joint_ids is not None else slice(None)]
+    cols = self._cols["joint_q_adr"] if joint_ids is None else self._ix["joint_q_adr"][joint_ids]
     _masked_write(self.data.qpos, cols, position, env_ids)
 
   def write_joint_velocity(self, velocity, joint_ids=None, env_ids=None) -> None:
     if not self.is_articulated:
       raise ValueError("Cannot write joint velocity for non-articulated entity.")
-    cols = self.indexing.joint_v_adr[joint_ids if joint_ids is not None else slice(None)]
+    cols = self._cols["joint_v_adr"] if joint_ids is None else self._ix["joint_v_adr"][joint_ids]
     _masked_write(self.data.qvel, cols, velocity, env_ids)
 
   def write_external_wrench(self, force, torque, body_ids=None, env_ids=None) -> None:
-    gb = self.indexing.body_ids[body_ids if body_ids is not None else slice(None)].long()
     xf = self.data.xfrc_applied
+    flat = xf.view(xf.shape[0], -1)
+    if body_ids is None:
+      fcols, tcols = self._cols["xfrc_force"], self._cols["xfrc_torque"]
+    else:
+      gb = self._ix["body_ids"][body_ids]
+      fcols = (gb[:, None] * 6 + torch.arange(3, device=gb.device)).reshape(-1)
+      tcols = fcols + 3
     if force is not None:
-      cols = (gb[:, None] * 6 + torch.arange(3, device=gb.device)).reshape(-1)
-      _masked_write(xf.view(xf.shape[0], -1), cols, force.reshape(force.shape[0], -1), env_ids)
+      _masked_write(flat, fcols, force.reshape(force.shape[0], -1), env_ids)
     if torque is not None:
-      cols = (gb[:, None] * 6 + 3 + torch.arange(3, device=gb.device)).reshape(-1)
-      _masked_write(xf.view(xf.shape[0], -1), cols, torque.reshape(torque.shape[0], -1), env_ids)
+      _masked_write(flat, tcols, torque.reshape(torque.shape[0], -1), env_ids)
 
   def write_ctrl(self, ctrl: torch.Tensor, ctrl_ids=None, env_ids=None) -> None:
     if not self.is_actuated:
       raise ValueError("Cannot write control for non-actuated entity.")
-    cols = self.indexing.ctrl_ids[ctrl_ids if ctrl_ids is not None else slice(None)]
+    cols = self._cols["ctrl_ids"] if ctrl_ids is None else self._ix["ctrl_ids"][ctrl_ids]
     _masked_write(self.data.ctrl, cols, ctrl, env_ids)
 
   def clear_state(self, env_ids=None) -> None:
+    """Zero applied generalized forces on the free joint, applied body wrenches
+    and controls of this entity (data.py:186-198)."""
     n = self.data.qpos.shape[0]
-    v = self.indexing.free_joint_v_adr
+    if env_ids is not None and not isinstance(env_ids, slice) and env_ids.dtype == torch.bool:
+      m = env_ids[:, None]
+      xf = self.data.xfrc_applied.view(n, -1)
+      for dst, key in ((self.data.qfrc_applied, "free_joint_v_adr"), (xf, "xfrc_all"), (self.data.ctrl, "ctrl_ids")):
+        cols = self._cols[key]
+        if key == "ctrl_ids" and not self.is_actuated:
+          continue
+        if isinstance(cols, slice):
+          dst[:, cols].masked_fill_(m, 0.0)
+        elif cols.numel():
+          dst[:, cols] = torch.where(m, 0.0, dst[:, cols])
+      return
+    rows = n if env_ids is None or isinstance(env_ids, slice) else env_ids.numel()
+    v = self._ix["free_joint_v_adr"]
     if v.numel():
-      _masked_write(self.data.qfrc_applied, v, torch.zeros(n if env_ids is None or isinstance(env_ids, slice) or env_ids.dtype == torch.bool else env_ids.numel(), v.numel(), device=self.data.qpos.device), env_ids)
-    gb = self.indexing.body_ids.long()
+      _masked_write(self.data.qfrc_applied, v, torch.zeros(rows, v.numel(), device=self.data.qpos.device), env_ids)
     xf = self.data.xfrc_applied.view(n, -1)
-    cols = (gb[:, None] * 6 + torch.arange(6, device=gb.device)).reshape(-1)
-    rows = n if env_ids is None or isinstance(env_ids, slice) or env_ids.dtype == torch.bool else env_ids.numel()
-    _masked_write(xf, cols, torch.zeros(rows, cols.numel(), device=xf.device), env_ids)
+    cols = self._ix["body_ids"][:, None] * 6 + torch.arange(6, device=xf.device)
+    _masked_write(xf, cols.reshape(-1), torch.zeros(rows, cols.numel(), device=xf.device), env_ids)
     if self.is_actuated:
-      c = self.indexing.ctrl_ids
+      c = self._ix["ctrl_ids"]
       _masked_write(self.data.ctrl, c, torch.zeros(rows, c.numel(), device=xf.device), env_ids)
 
   # ---- reads ----
@@ -203,74 +257,74 @@ class EntityData:
 
   @_cached
   def body_link_pose_w(self) -> torch.Tensor:
-    ids = self.indexing.body_ids.long()
+    ids = self._ix["body_ids"]
     return torch.cat([self.data.xpos[:, ids], self.data.xquat[:, ids]], dim=-1)
 
   @_cached
   def body_link_vel_w(self) -> torch.Tensor:
-    ids = self.indexing.body_ids.long()
+    ids = self._ix["body_ids"]
     com = self.data.subtree_com[:, self._root].unsqueeze(1)
     return compute_velocity_from_cvel(self.data.xpos[:, ids], com, self.data.cvel[:, ids])
 
   @_cached
   def body_com_pose_w(self) -> torch.Tensor:
-    ids = self.indexing.body_ids.long()
+    ids = self._ix["body_ids"]
     iq = self.model.body_iquat[:, ids].expand(self.data.xquat.shape[0], -1, -1)
     return torch.cat([self.data.xipos[:, ids], quat_mul(self.data.xquat[:, ids], iq)], dim=-1)
 
   @_cached
   def body_com_vel_w(self) -> torch.Tensor:
-    ids = self.indexing.body_ids.long()
+    ids = self._ix["body_ids"]
     com = self.data.subtree_com[:, self._root].unsqueeze(1)
     return compute_velocity_from_cvel(self.data.xipos[:, ids], com, self.data.cvel[:, ids])
 
   @property
   def body_external_wrench(self) -> torch.Tensor:
-    return self.data.xfrc_applied[:, self.indexing.body_ids.long()]
+    return self.data.xfrc_applied[:, self._ix["body_ids"]]
 
   @_cached
   def geom_pose_w(self) -> torch.Tensor:
-    ids = self.indexing.geom_ids.long()
+    ids = self._ix["geom_ids"]
     return torch.cat([self.data.geom_xpos[:, ids], quat_from_matrix(self.data.geom_xmat[:, ids])], dim=-1)
 
   @_cached
   def geom_vel_w(self) -> torch.Tensor:
-    ids = self.indexing.geom_ids.long()
-    bids = self.model.geom_bodyid[ids].long()
+    ids = self._ix["geom_ids"]
+    bids = self._ix["geom_bodyid"]
     com = self.data.subtree_com[:, self._root].unsqueeze(1)
     return compute_velocity_from_cvel(self.data.geom_xpos[:, ids], com, self.data.cvel[:, bids])
 
   @_cached
   def site_pose_w(self) -> torch.Tensor:
-    ids = self.indexing.site_ids.long()
+    ids = self._ix["site_ids"]
     return torch.cat([self.data.site_xpos[:, ids], quat_from_matrix(self.data.site_xmat[:, ids])], dim=-1)
 
   @_cached
   def site_vel_w(self) -> torch.Tensor:
-    ids = self.indexing.site_ids.long()
-    bids = self.model.site_bodyid[ids].long()
+    ids = self._ix["site_ids"]
+    bids = self._ix["site_bodyid"]
     com = self.data.subtree_com[:, self._root].unsqueeze(1)
     return compute_velocity_from_cvel(self.data.site_xpos[:, ids], com, self.data.cvel[:, bids])
 
   @property
   def joint_pos(self) -> torch.Tensor:
-    return self.data.qpos[:, self.indexing.joint_q_adr.long()]
+    return self.data.qpos[:, self._ix["joint_q_adr"]]
 
   @property
   def joint_vel(self) -> torch.Tensor:
-    return self.data.qvel[:, self.indexing.joint_v_adr.long()]
+    return self.data.qvel[:, self._ix["joint_v_adr"]]
 
   @property
   def joint_acc(self) -> torch.Tensor:
-    return self.data.qacc[:, self.indexing.joint_v_adr.long()]
+    return self.data.qacc[:, self._ix["joint_v_adr"]]
 
   @property
   def actuator_force(self) -> torch.Tensor:
-    return self.data.actuator_force[:, self.indexing.ctrl_ids.long()]
+    return self.data.actuator_force[:, self._ix["ctrl_ids"]]
 
   @property
   def generalized_force(self) -> torch.Tensor:
-    return self.data.qfrc_applied[:, self.indexing.free_joint_v_adr.long()]
+    return self.data.qfrc_applied[:, self._ix["free_joint_v_adr"]]
 
   root_link_pos_w = property(lambda s: s.root_link_pose_w[:, 0:3])
   root_link_quat_w = property(lambda s: s.root_link_pose_w[:, 3:7])
@@ -302,12 +356,12 @@ class EntityData:
   @_cached
   def _geom_pos_w(self) -> torch.Tensor:
     """== geom_pose_w[..., 0:3], without converting the frames to quaternions."""
-    return self.data.geom_xpos[:, self.indexing.geom_ids.long()]
+    return self.data.geom_xpos[:, self._ix["geom_ids"]]
 
   @_cached
   def _site_pos_w(self) -> torch.Tensor:
     """== site_pose_w[..., 0:3], without converting the frames to quaternions."""
-    return self.data.site_xpos[:, self.indexing.site_ids.long()]
+    return self.data.site_xpos[:, self._ix["site_ids"]]
 
   @_cached
   def projected_gravity_b(self) -> torch.Tensor:

@@ -88,3 +88,27 @@ def air_time_update(sensordata, cols, time, last_time, cur_air, last_air, cur_co
     "mjh_air_time_update",
   )
   return True
+
+
+def obs_term(x: torch.Tensor, out: torch.Tensor, u: torch.Tensor | None, lo: float, hi: float, clip, scale: float) -> bool:
+  """out[:] = clip(x + U(lo, hi), clip) * scale in one launch; False if unsupported."""
+  if not (x.is_cuda and out.is_cuda and x.dtype == torch.float32):
+    return False
+  if x.dim() == 1:
+    x2 = x.view(-1, 1)
+  elif x.dim() == 2:
+    x2 = x
+  else:
+    return False
+  n, w = x2.shape
+  if out.shape != (n, w) or out.stride(1) != 1 or x2.stride(1) != 1 or (u is not None and u.stride(1) != 1):
+    return False
+  cmin, cmax = (float(clip[0]), float(clip[1])) if clip else (1.0, -1.0)
+  native.check(
+    native.lib().mjh_obs_term(
+      _ptr(x2), x2.stride(0), _ptr(u) if u is not None else None, u.stride(0) if u is not None else 0, float(lo), float(hi),
+      cmin, cmax, float(scale), _ptr(out), out.stride(0), w, n, _stream(),
+    ),
+    "mjh_obs_term",
+  )
+  return True

@@ -54,6 +54,37 @@ class ObservationManager:
         dims.append(tuple(out.shape[1:]))
       self.group_obs_term_dim[gname] = dims
     self._obs_buffer = None
+    self._fused = {g: self._fused_plan(g) for g in self._group_terms}
+
+  def _fused_plan(self, gname: str):
+    """Per-term (offset, width, noise lo/hi or None, clip, scale) for groups that
+    can be assembled by the fused kernel: concatenated on the last dim, no
+    history, additive uniform (or no) noise, scalar scale."""
+    from mjlab_amd.utils.noise import UniformNoiseCfg
+
+    if not self._group_concat[gname] or self._group_concat_dim[gname] not in (-1, 1):
+      return None
+    plan, off = [], 0
+    for (tname, tcfg), dims in zip(self._group_terms[gname], self.group_obs_term_dim[gname]):
+      if tcfg.history_length > 0 or len(dims) > 1:
+        return None
+      w = dims[0] if dims else 1
+      noise = None
+      if tcfg.noise is not None:
+        nz = tcfg.noise
+        if not (isinstance(nz, UniformNoiseCfg) and nz.operation == "add"):
+          return None
+        if isinstance(nz.n_min, torch.Tensor) or isinstance(nz.n_max, torch.Tensor):
+          return None
+        noise = (float(nz.n_min), float(nz.n_max))
+      scale = 1.0
+      if tcfg.scale is not None:
+        if tcfg.scale.numel() != 1:
+          return None
+        scale = float(tcfg.scale.reshape(-1)[0])
+      plan.append((tcfg, off, w, noise, tcfg.clip, scale))
+      off += w
+    return plan, off
 
   @property
   def active_terms(self) -> dict[str, list[str]]:
@@ -88,9 +119,14 @@ class ObservationManager:
     return out
 
   def compute_group(self, group_name: str, update_history: bool = False):
+    fp = self._fused.get(group_name)
+    if fp is not None and str(self._env.device).startswith("cuda"):
+      out = self._compute_fused(fp)
+      if out is not None:
+        return out
     obs_terms = {}
     for tname, tcfg in self._group_terms[group_name]:
-      obs = tcfg.func(self._env, **tcfg.params).clone()
+      obs = tcfg.func(self._env, **tcfg.params).clone()  # noise/clip/scale act in place below
       if tcfg.noise is not None:
         obs = tcfg.noise.apply(obs)
       if tcfg.clip:
@@ -106,3 +142,20 @@ class ObservationManager:
     if self._group_concat[group_name]:
       return torch.cat(list(obs_terms.values()), dim=self._group_concat_dim[group_name])
     return obs_terms
+
+  def _compute_fused(self, fp):
+    """One fused launch per term writing straight into the group buffer (no
+    per-term clone/noise/scale chain, no final cat); one U[0,1) draw per group."""
+    from mjlab_amd import envops
+
+    plan, width = fp
+    n = self._env.num_envs
+    out = torch.empty((n, width), device=self._env.device)
+    u = torch.rand((n, width), device=self._env.device) if any(p[3] is not None for p in plan) else None
+    for tcfg, off, w, noise, clip, scale in plan:
+      x = tcfg.func(self._env, **tcfg.params)
+      lo, hi = noise if noise is not None else (0.0, 0.0)
+      uu = u[:, off : off + w] if noise is not None else None
+      if not envops.obs_term(x.float(), out[:, off : off + w], uu, lo, hi, clip, scale):
+        return None
+    return out

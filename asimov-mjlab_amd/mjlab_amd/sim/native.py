@@ -40,6 +40,7 @@ EXPORTS = (
   "mjh_quat_mul",
   "mjh_velocity_from_cvel",
   "mjh_air_time_update",
+  "mjh_obs_term",
 )
 
 
@@ -80,6 +81,8 @@ def lib() -> ctypes.CDLL:
   L.mjh_quat_mul.argtypes = [vp, ll, vp, ll, vp, ll, vp]
   L.mjh_velocity_from_cvel.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp]
   L.mjh_air_time_update.argtypes = [vp, ll, vp, ci, vp, vp, vp, vp, vp, vp, ll, vp]
+  cf = ctypes.c_float
+  L.mjh_obs_term.argtypes = [vp, ll, vp, ll, cf, cf, cf, cf, cf, vp, ll, ci, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

@@ -157,6 +157,12 @@ int mjh_air_time_update(const float* sensordata, long long sds, const int* cols,
                         float* last_time, float* cur_air, float* last_air, float* cur_con, float* last_con, long long n,
                         void* stream);
 
+/* One observation term's noise -> clip -> scale, written into its column slice
+ * of the group buffer (observation_manager.py:163-176). u: U[0,1) draws (NULL:
+ * no noise); clipping is skipped when cmin > cmax. */
+int mjh_obs_term(const float* x, long long xs, const float* u, long long us, float lo, float hi, float cmin, float cmax,
+                 float scale, float* out, long long os, int w, long long n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,3 +66,36 @@ def test_air_time_kernel_matches_torch_rule():
   torch.cuda.synchronize()
   for a, b in ((ca, ca_ref), (la, la_ref), (cc, cc_ref), (lc, lc_ref), (lt, time)):
     torch.testing.assert_close(a, b)
+
+
+def test_obs_term_kernel_matches_torch():
+  g = torch.Generator(device=DEV).manual_seed(3)
+  n = 777
+  x = torch.randn(n, 10, device=DEV, generator=g)[:, 2:7]  # strided input
+  out = torch.full((n, 12), -7.0, device=DEV)
+  u = torch.rand(n, 12, device=DEV, generator=g)
+  assert envops.obs_term(x, out[:, 3:8], u[:, 3:8], -0.5, 0.25, (-1.0, 1.5), 0.25)
+  ref = torch.clamp(x + (u[:, 3:8] * 0.75 - 0.5), -1.0, 1.5) * 0.25
+  torch.testing.assert_close(out[:, 3:8], ref)
+  assert (out[:, :3] == -7.0).all() and (out[:, 8:] == -7.0).all()
+  v = torch.randn(n, device=DEV, generator=g)  # 1-D term
+  assert envops.obs_term(v, out[:, 0:1], None, 0.0, 0.0, None, 2.0)
+  torch.testing.assert_close(out[:, 0], v * 2.0)
+
+
+def test_fused_observation_group_matches_generic():
+  from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
+  from mjlab_amd.tasks import load_env_cfg
+
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = 64
+  env = ManagerBasedRlEnv(cfg, device=DEV)
+  env.reset()
+  env.step(torch.zeros(64, 29, device=DEV))
+  om = env.observation_manager
+  assert om._fused["critic"] is not None and om._fused["policy"] is not None
+  fused = om.compute_group("critic")
+  plan = om._fused.pop("critic")
+  generic = om.compute_group("critic")
+  om._fused["critic"] = plan
+  torch.testing.assert_close(fused, generic, rtol=1e-6, atol=1e-6)
