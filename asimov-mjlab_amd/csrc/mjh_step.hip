@@ -82,6 +82,9 @@ struct Rg {
 #define X_RG(name, r) static constexpr bool name = false;
 #elif MJH_PRESET == 2
 #define X_RG(name, r) static constexpr bool name = true;
+#elif MJH_PRESET == 4
+#define X_RG(name, r) static constexpr bool name = (r) != 0 || (#name[0] == 'J' && #name[1] == 0) || \
+    (#name[0] == 'c' && (#name[1] == 'i' || #name[1] == 'r' || #name[1] == 'v' || #name[1] == 'f' || #name[1] == 'd'));
 #elif MJH_PRESET == 3
 #define X_RG(name, r) static constexpr bool name = (r) != 0 || (#name[0] == 'J' && #name[1] == 0);
 #else
@@ -431,6 +434,34 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
     }
 }
 
+// dot of an aligned row with an aligned vector, fully unrolled to the padded
+// size NVP so all loads of a row are in flight at once (rows may live in L2);
+// vector entries >= n are masked (padding may hold garbage)
+template <int NVP>
+__device__ __forceinline__ float rowdot_u(const float* r, const float* x, int n) {
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < NVP; j += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(r + j);
+    float4 b = *reinterpret_cast<const float4*>(x + j);
+    if (j + 4 > n) {
+      b.x = j < n ? b.x : 0.f;
+      b.y = j + 1 < n ? b.y : 0.f;
+      b.z = j + 2 < n ? b.z : 0.f;
+      b.w = j + 3 < n ? b.w : 0.f;
+    }
+    s0 += a.x * b.x + a.y * b.y;
+    s1 += a.z * b.z + a.w * b.w;
+  }
+  return s0 + s1;
+}
+
+// y = A x for the full symmetric (zero-padded) A, one row per lane
+template <int NT, int NVP>
+__device__ __forceinline__ void symv_u(const float* A, int n, int ld, const float* x, float* y) {
+  for (int i = (threadIdx.x & 63); i < n; i += NT) y[i] = rowdot_u<NVP>(A + i * ld, x, n);
+}
+
 // dot of an aligned row with an aligned vector (float4 loads, 2 accumulators)
 __device__ __forceinline__ float rowdot(const float* r, const float* x, int n) {
   float s0 = 0.f, s1 = 0.f;
@@ -735,8 +766,11 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
   }
   __syncthreads();
   const int wave = threadIdx.x >> 6;
-  const int w = blockIdx.x * WPB + wave;
-  if (w >= d.nworld) return;
+  const int slot = blockIdx.x * WPB + wave;
+  if (slot >= d.nworld) return;
+  // optional cost-sorted world order: a workgroup's worlds then take similar
+  // time, so its LDS is not held hostage by one slow world
+  const int w = d.world_order ? (int)d.world_order[slot] : slot;
   const int tid = threadIdx.x & 63;
   float* S = smem + Io.img_words + wave * Lo.total;
   int* SI = reinterpret_cast<int*>(S);
@@ -1423,7 +1457,7 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
         invw = invw * 2.f * f0 * f0 / m.impratio;
       }
       float jq = 0.f;
-      jq = rowdot(J + r * ldj, qvel, nv);
+      jq = rowdot_u<NVP>(J + r * ldj, qvel, nv);
       const float pos = con_dist[ci] - con_imargin[ci];
       row_params(m.timestep, pos, pos, invw, con_solref + 2 * ci, con_solimp + 5 * ci, jq, efc_D + r, efc_R + r,
                  efc_aref + r);
@@ -1446,9 +1480,9 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
   } else {
     // jaref = J x - aref ; Ma = M x ; forces, qfrc_constraint, cost
     auto eval_point = [&](const float* x) {
-      symv<NT>(Mm, nv, ldm, x, Ma);
+      symv_u<NT, NVP>(Mm, nv, ldm, x, Ma);
       for (int r = tid; r < nefc; r += NT) {
-        jaref[r] = rowdot(J + r * ldj, x, nv) - efc_aref[r];
+        jaref[r] = rowdot_u<NVP>(J + r * ldj, x, nv) - efc_aref[r];
       }
       wsync();
     };
@@ -1526,7 +1560,7 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
     float cost = update_constraint();
     float cs = 0.f;
     for (int r = tid; r < nefc; r += NT) {
-      const float s = rowdot(J + r * ldj, qacc_smooth, nv);
+      const float s = rowdot_u<NVP>(J + r * ldj, qacc_smooth, nv);
       float f, cr;
       row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], s - efc_aref[r], &f, &cr);
       cs += cr;
@@ -1544,9 +1578,9 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
     for (int it = 0; it < m.iterations; it++) {
       unsigned long long t_ls = PROF_NOW();
       // ---- exact line search along `search`
-      symv<NT>(Mm, nv, ldm, search, Mv);
+      symv_u<NT, NVP>(Mm, nv, ldm, search, Mv);
       for (int r = tid; r < nefc; r += NT) {
-        jv[r] = rowdot(J + r * ldj, search, nv);
+        jv[r] = rowdot_u<NVP>(J + r * ldj, search, nv);
       }
       wsync();
       float g1 = 0.f, g2 = 0.f;
@@ -1936,7 +1970,7 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
         for (int i = tid; i < nv * ldm; i += NT) Lm[i] = Mm[i];
         wsync();
         for (int i = tid; i < nv; i += NT) Lm[i * ldm + i] += dt * dof_damping[i];
-        symv<NT>(Mm, nv, ldm, qacc, qa_int);
+        symv_u<NT, NVP>(Mm, nv, ldm, qacc, qa_int);
         ldl_factor_reg<NVP>(Lm, nv, ldm);
         ldl_solve_reg<NVP>(Lm, nv, ldm, qa_int);
       } else {
@@ -2062,9 +2096,11 @@ Layout make_layout(const mjh_model* m, int budget) {
   L.ldm = ld;
   L.ldj = ld;
   TAKE(qpos, m->nq);
-  TAKE(qvel, nv); TAKE(qacc, nv); TAKE(qacc_smooth, nv); TAKE(qfrc_smooth, nv);
-  TAKE(qfrc_bias, nv); TAKE(qfrc_con, nv); TAKE(qfrc_passive, nv); TAKE(qfrc_act, nv);
-  TAKE(grad, nv); TAKE(search, nv); TAKE(Ma, nv); TAKE(Mv, nv); TAKE(tmp, nv); TAKE(tmp2, nv);
+  // dof vectors padded to NVP: the unrolled row dots read them whole
+  const int nvv = nvp_of(nv);
+  TAKE(qvel, nvv); TAKE(qacc, nvv); TAKE(qacc_smooth, nvv); TAKE(qfrc_smooth, nvv);
+  TAKE(qfrc_bias, nvv); TAKE(qfrc_con, nvv); TAKE(qfrc_passive, nvv); TAKE(qfrc_act, nvv);
+  TAKE(grad, nvv); TAKE(search, nvv); TAKE(Ma, nvv); TAKE(Mv, nvv); TAKE(tmp, nvv); TAKE(tmp2, nvv);
   TAKE(xpos, 3 * nb); TAKE(xquat, 4 * nb); TAKE(xmat, 9 * nb); TAKE(xipos, 3 * nb);
   TAKE(ximat, 9 * nb); TAKE(subtree_com, 3 * nb); TAKE(cinert, 10 * nb); TAKE(crb, 10 * nb);
   TAKE(cvel, 6 * nb); TAKE(cacc, 6 * nb); TAKE(cfrc, 6 * nb);

@@ -86,7 +86,7 @@ def data_struct(real=ctypes.c_float):
     if f.kind == "DA":
       members.append((f.name, ctypes.c_void_p))
   if real is ctypes.c_float:  # device descriptor: per-world global scratch
-    members += [("scratch", ctypes.c_void_p), ("scratch_words", ctypes.c_longlong)]
+    members += [("scratch", ctypes.c_void_p), ("scratch_words", ctypes.c_longlong), ("world_order", ctypes.c_void_p)]
   return type("mjh_data" if real is ctypes.c_float else "or_data", (ctypes.Structure,), {"_fields_": members})
 
 

@@ -100,6 +100,7 @@ class SimulationCfg:
   njmax: int | None = None
   ls_parallel: bool = True
   contact_sensor_maxmatch: int = 64
+  balance_worlds: bool = False  # cost-sorted wave assignment (measured: no gain on G1)
   mujoco: MujocoCfg = field(default_factory=MujocoCfg)
   nan_guard: NanGuardCfg = field(default_factory=NanGuardCfg)
 
@@ -198,6 +199,12 @@ class Simulation:
       self._scratch_words = words
     ds.scratch = self._scratch.data_ptr()
     ds.scratch_words = self._scratch_words
+    # worlds are handed to waves in order of last step's constraint count
+    # (refreshed on the device before every launch; results are order-free)
+    if not hasattr(self, "_order"):
+      self._order = torch.arange(self.num_envs, dtype=torch.int64, device=self.device)
+      self._order_keys = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+    ds.world_order = self._order.data_ptr() if self.cfg.balance_worlds else None
     for name, t in self._data_flat.items():
       setattr(ds, name, t.data_ptr())
     self._mstruct, self._dstruct = ms, ds
@@ -297,12 +304,18 @@ class Simulation:
   def _stream(self) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
+  def _refresh_order(self) -> None:
+    if self.cfg.balance_worlds and self.num_envs > 1:
+      torch.sort(self.data.nefc, stable=False, out=(self._order_keys, self._order))
+
   def _launch_step(self) -> None:
+    self._refresh_order()
     native.check(
       native.lib().mjh_step(ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), self._stream()), "mjh_step"
     )
 
   def _launch_forward(self) -> None:
+    self._refresh_order()
     native.check(
       native.lib().mjh_forward(ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), self._stream()),
       "mjh_forward",
@@ -334,6 +347,7 @@ class Simulation:
     self.epoch.bump()
     if gate.dtype not in (torch.bool, torch.uint8) or gate.numel() != 1 or not gate.is_cuda:
       raise ValueError("gate must be a one-element bool/uint8 device tensor")
+    self._refresh_order()
     native.check(
       native.lib().mjh_forward_gated(
         ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), ctypes.c_void_p(gate.data_ptr()), self._stream()

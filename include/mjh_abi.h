@@ -32,7 +32,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 2
+#define MJH_ABI_VERSION 3
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -82,6 +82,10 @@ typedef struct mjh_data {
      intermediates that do not live in LDS */
   float* scratch;
   long long scratch_words;
+  /* optional permutation of [0, nworld) (NULL = identity): the order in which
+     worlds are assigned to waves. Results do not depend on it; sorting worlds
+     by expected cost balances the waves of a workgroup. */
+  const long long* world_order;
 } mjh_data;
 
 /* Version of this ABI (MJH_ABI_VERSION). */
