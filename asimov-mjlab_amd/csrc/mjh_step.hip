@@ -64,7 +64,7 @@ enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
 #define MJH_COLL_INLINE
 #endif
 #ifndef MJH_PRESET
-#define MJH_PRESET 3
+#define MJH_PRESET 5
 #endif
 #define MJH_REGIONS(X)                                                                              \
   X(qpos, 1) X(qvel, 0) X(qacc, 0) X(qacc_smooth, 0) X(qfrc_smooth, 0) X(qfrc_bias, 1) X(qfrc_con, 0)  \
@@ -85,6 +85,11 @@ struct Rg {
 #elif MJH_PRESET == 4
 #define X_RG(name, r) static constexpr bool name = (r) != 0 || (#name[0] == 'J' && #name[1] == 0) || \
     (#name[0] == 'c' && (#name[1] == 'i' || #name[1] == 'r' || #name[1] == 'v' || #name[1] == 'f' || #name[1] == 'd'));
+#elif MJH_PRESET == 5
+// like 4 (body arrays global) but the mass-matrix / Hessian factor L in LDS
+#define X_RG(name, r) static constexpr bool name = ((r) != 0 || (#name[0] == 'J' && #name[1] == 0) || \
+    (#name[0] == 'c' && (#name[1] == 'i' || #name[1] == 'r' || #name[1] == 'v' || #name[1] == 'f' || #name[1] == 'd'))) && \
+    !(#name[0] == 'L' && #name[1] == 0);
 #elif MJH_PRESET == 3
 #define X_RG(name, r) static constexpr bool name = (r) != 0 || (#name[0] == 'J' && #name[1] == 0);
 #else
