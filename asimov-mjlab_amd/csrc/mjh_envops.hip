@@ -53,11 +53,11 @@ __global__ void quat_mul_kernel(const float* __restrict__ p, long long ps, const
 
 __global__ void velocity_from_cvel_kernel(const float* __restrict__ pos, long long ps, const float* __restrict__ com,
                                           long long cs, const float* __restrict__ cvel, long long vs,
-                                          float* __restrict__ out, long long n) {
+                                          float* __restrict__ out, long long n, int k) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float* p = pos + i * ps;
-  const float* c = com + i * cs;
+  const float* c = com + (i / k) * cs;  // k rows (bodies/sites) share their env's com
   const float* v = cvel + i * vs;
   const float ox = c[0] - p[0], oy = c[1] - p[1], oz = c[2] - p[2];
   const float wx = v[0], wy = v[1], wz = v[2];
@@ -115,10 +115,10 @@ int mjh_quat_mul(const float* p, long long ps, const float* q, long long qs, flo
 }
 
 int mjh_velocity_from_cvel(const float* pos, long long ps, const float* com, long long cs, const float* cvel, long long vs,
-                           float* out, long long n, void* stream) {
-  if (n <= 0) return 0;
+                           float* out, long long n, int k, void* stream) {
+  if (n <= 0 || k <= 0) return 0;
   hipLaunchKernelGGL(velocity_from_cvel_kernel, dim3(grid(n)), dim3(256), 0, (hipStream_t)stream, pos, ps, com, cs, cvel,
-                     vs, out, n);
+                     vs, out, n, k);
   return finish();
 }
 

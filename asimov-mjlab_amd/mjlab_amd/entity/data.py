@@ -68,7 +68,7 @@ def _masked_write(dst: torch.Tensor, cols: torch.Tensor | slice, value: torch.Te
     m = env_ids.view(-1, *([1] * (dst.dim() - 1)))
     if isinstance(cols, slice):  # in place on the strided view: where + copy, no gather/scatter
       cur = dst[:, cols]
-      cur.copy_(torch.where(m, value, cur))
+      torch.where(m, value, cur, out=cur)
       return
     cols_l = cols.long()
     cur = dst[:, cols_l]

@@ -59,18 +59,28 @@ def quat_mul(p: torch.Tensor, q: torch.Tensor) -> torch.Tensor:
 
 
 def velocity_from_cvel(pos: torch.Tensor, com: torch.Tensor, cvel: torch.Tensor, reference) -> torch.Tensor:
-  """``reference`` is the torch implementation (entity/data.py) for other layouts."""
+  """``reference`` is the torch implementation (entity/data.py) for other layouts.
+  2-D: (N, 3) rows; 3-D: (N, k, 3) contiguous rows sharing a (N, 1, 3) com."""
   if _rows(pos, 3) and _rows(com, 3) and _rows(cvel, 6) and pos.shape[0] == com.shape[0] == cvel.shape[0]:
-    n = pos.shape[0]
-    out = torch.empty((n, 6), dtype=torch.float32, device=pos.device)
-    native.check(
-      native.lib().mjh_velocity_from_cvel(
-        _ptr(pos), pos.stride(0), _ptr(com), com.stride(0), _ptr(cvel), cvel.stride(0), _ptr(out), n, _stream()
-      ),
-      "mjh_velocity_from_cvel",
-    )
-    return out
-  return reference(pos, com, cvel)
+    n, k, rows = pos.shape[0], 1, (pos, com, cvel)
+  elif (
+    pos.is_cuda and pos.dim() == 3 and cvel.dim() == 3 and com.dim() == 3 and pos.is_contiguous() and cvel.is_contiguous()
+    and com.shape[1] == 1 and com.stride(2) == 1 and pos.shape[:2] == cvel.shape[:2] and pos.shape[0] == com.shape[0]
+    and pos.shape[2] == 3 and cvel.shape[2] == 6 and pos.dtype == cvel.dtype == com.dtype == torch.float32
+  ):
+    n, k = pos.shape[0] * pos.shape[1], pos.shape[1]
+    rows = (pos.view(-1, 3), com[:, 0, :], cvel.view(-1, 6))
+  else:
+    return reference(pos, com, cvel)
+  p2, c2, v2 = rows
+  out = torch.empty((n, 6), dtype=torch.float32, device=pos.device)
+  native.check(
+    native.lib().mjh_velocity_from_cvel(
+      _ptr(p2), p2.stride(0), _ptr(c2), c2.stride(0), _ptr(v2), v2.stride(0), _ptr(out), n, k, _stream()
+    ),
+    "mjh_velocity_from_cvel",
+  )
+  return out.view(*pos.shape[:-1], 6)
 
 
 def air_time_update(sensordata, cols, time, last_time, cur_air, last_air, cur_con, last_con) -> bool:
@@ -112,3 +122,92 @@ def obs_term(x: torch.Tensor, out: torch.Tensor, u: torch.Tensor | None, lo: flo
     "mjh_obs_term",
   )
   return True
+
+
+# ---- fused reward terms (csrc/mjh_mdp.hip) -------------------------------------
+def _vec_out(n: int, device) -> torch.Tensor:
+  return torch.empty(n, dtype=torch.float32, device=device)
+
+
+def rew_track(cmd: torch.Tensor, v: torch.Tensor, std: float, angular: bool):
+  if not (_rows(cmd, 3) and _rows(v, 3) and cmd.shape[0] == v.shape[0]):
+    return None
+  out = _vec_out(cmd.shape[0], cmd.device)
+  native.check(native.lib().mjh_rew_track(_ptr(cmd), cmd.stride(0), _ptr(v), v.stride(0), 1.0 / (std * std), int(angular),
+                                          _ptr(out), cmd.shape[0], _stream()), "mjh_rew_track")
+  return out
+
+
+def rew_flat_orientation(q: torch.Tensor, g: torch.Tensor, std: float):
+  if not (_rows(q, 4) and _rows(g, 3) and q.shape[0] == g.shape[0]):
+    return None
+  out = _vec_out(q.shape[0], q.device)
+  native.check(native.lib().mjh_rew_flat_orientation(_ptr(q), q.stride(0), _ptr(g), g.stride(0), 1.0 / (std * std), _ptr(out),
+                                                     q.shape[0], _stream()), "mjh_rew_flat_orientation")
+  return out
+
+
+def rew_sqsum(x: torch.Tensor, k: int):
+  if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1 and x.shape[1] >= k):
+    return None
+  out = _vec_out(x.shape[0], x.device)
+  native.check(native.lib().mjh_rew_sqsum(_ptr(x), x.stride(0), k, _ptr(out), x.shape[0], _stream()), "mjh_rew_sqsum")
+  return out
+
+
+def rew_diffsq(a: torch.Tensor, b: torch.Tensor):
+  ok = all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 for t in (a, b))
+  if not ok or a.shape != b.shape:
+    return None
+  out = _vec_out(a.shape[0], a.device)
+  native.check(native.lib().mjh_rew_diffsq(_ptr(a), a.stride(0), _ptr(b), b.stride(0), a.shape[1], _ptr(out), a.shape[0],
+                                           _stream()), "mjh_rew_diffsq")
+  return out
+
+
+def rew_pos_limits(q: torch.Tensor, lim: torch.Tensor):
+  if not (q.is_cuda and q.dim() == 2 and q.stride(1) == 1 and lim.dim() == 3 and lim.shape[:2] == q.shape
+          and lim.stride(2) == 1 and lim.stride(1) == 2 and q.dtype == lim.dtype == torch.float32):
+    return None
+  out = _vec_out(q.shape[0], q.device)
+  native.check(native.lib().mjh_rew_pos_limits(_ptr(q), q.stride(0), _ptr(lim), lim.stride(0), q.shape[1], _ptr(out),
+                                               q.shape[0], _stream()), "mjh_rew_pos_limits")
+  return out
+
+
+def rew_posture(q, q0, std_stand, std_walk, std_run, cmd, walk_thr, run_thr):
+  ok = all(t.is_cuda and t.dtype == torch.float32 and t.stride(-1) == 1 for t in (q, q0, std_stand, std_walk, std_run, cmd))
+  if not ok or q.dim() != 2 or q0.shape != q.shape or not _rows(cmd, 3):
+    return None
+  if not all(t.is_contiguous() and t.numel() == q.shape[1] for t in (std_stand, std_walk, std_run)):
+    return None
+  out = _vec_out(q.shape[0], q.device)
+  native.check(native.lib().mjh_rew_posture(
+    _ptr(q), q.stride(0), _ptr(q0), q0.stride(0), _ptr(std_stand), _ptr(std_walk), _ptr(std_run), _ptr(cmd), cmd.stride(0),
+    float(walk_thr), float(run_thr), q.shape[1], _ptr(out), q.shape[0], _stream()), "mjh_rew_posture")
+  return out
+
+
+def rew_feet(pos: torch.Tensor, vel: torch.Tensor, found, cmd: torch.Tensor, target: float, thr_clear: float,
+             thr_slip: float, want: str):
+  """want = "clearance" -> (N,) cost; "slip" -> (cost, sum |v_xy|*found, sum found)."""
+  if not (pos.is_cuda and pos.dim() == 3 and vel.dim() == 3 and pos.stride(2) == 1 and vel.stride(2) == 1
+          and pos.stride(1) == 3 and vel.stride(1) >= 3 and pos.shape[:2] == vel.shape[:2] and _rows(cmd, 3)):
+    return None
+  if vel.stride(1) != 3 and vel.stride(1) != 6:
+    return None
+  n, k = pos.shape[0], pos.shape[1]
+  if vel.stride(1) != 3:
+    vel = vel.contiguous()
+  if found is not None and not (found.dim() == 2 and found.stride(1) == 1 and found.shape == (n, k) and found.dtype == torch.float32):
+    return None
+  z = pos[:, :, 2]
+  cl = _vec_out(n, pos.device) if want == "clearance" else None
+  outs = [_vec_out(n, pos.device) for _ in range(3)] if want == "slip" else [None, None, None]
+  native.check(native.lib().mjh_rew_feet(
+    ctypes.c_void_p(pos.data_ptr() + 8), pos.stride(0), _ptr(vel), vel.stride(0),
+    _ptr(found) if want == "slip" else None, found.stride(0) if want == "slip" else 0, _ptr(cmd), cmd.stride(0),
+    float(target), float(thr_clear), float(thr_slip), k, _ptr(cl) if cl is not None else None,
+    *[_ptr(t) if t is not None else None for t in outs], n, _stream()), "mjh_rew_feet")
+  del z
+  return cl if want == "clearance" else tuple(outs)

@@ -166,10 +166,11 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     self.render_mode = render_mode
     super().__init__(cfg=cfg, device=device)
     n = self.num_envs
-    self.reset_buf = torch.zeros(n, dtype=torch.bool, device=self.device)
-    self.reset_terminated = torch.zeros_like(self.reset_buf)
-    self.reset_time_outs = torch.zeros_like(self.reset_buf)
-    self.reward_buf = torch.zeros(n, device=self.device)
+    # the managers' persistent output buffers, aliased (graph outputs, no copies)
+    self.reset_buf = self.termination_manager._dones_buf
+    self.reset_terminated = self.termination_manager._terminated_buf
+    self.reset_time_outs = self.termination_manager._truncated_buf
+    self.reward_buf = self.reward_manager._reward_buf
     self._any_reset = torch.zeros(1, dtype=torch.bool, device=self.device)
     self._env_step_t = torch.zeros((), dtype=torch.long, device=self.device)
     self._action_in = torch.zeros(n, self.action_manager.total_action_dim, device=self.device)
@@ -265,13 +266,11 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
       self.scene.update(dt=self.physics_dt)
     self.episode_length_buf += 1
     self._env_step_t += 1
-    self.reset_buf.copy_(self.termination_manager.compute())
-    self.reset_terminated.copy_(self.termination_manager.terminated)
-    self.reset_time_outs.copy_(self.termination_manager.time_outs)
-    self.reward_buf.copy_(self.reward_manager.compute(dt=self.step_dt))
+    self.termination_manager.compute()  # -> reset_buf / reset_terminated / reset_time_outs
+    self.reward_manager.compute(dt=self.step_dt)  # -> reward_buf
     self._reset_idx(self.reset_buf)
     self.scene.write_data_to_sim()
-    self._any_reset.copy_(self.reset_buf.any().view(1))
+    torch.any(self.reset_buf, dim=0, keepdim=True, out=self._any_reset)
     self.sim.forward_gated(self._any_reset)
     self.command_manager.compute(dt=self.step_dt)
     if "interval" in self.event_manager.available_modes:

@@ -53,7 +53,14 @@ class JointAction(ActionTerm):
 
   def process_actions(self, actions: torch.Tensor) -> None:
     self._raw_actions.copy_(actions)
-    self._processed_actions.copy_(self._raw_actions * self._scale + self._offset)
+    # processed = raw * scale + offset (joint_actions.py:62-64), one fused launch
+    if isinstance(self._scale, torch.Tensor):
+      off = self._offset if isinstance(self._offset, torch.Tensor) else torch.full_like(self._raw_actions, self._offset)
+      torch.addcmul(off, self._raw_actions, self._scale, out=self._processed_actions)
+    elif isinstance(self._offset, torch.Tensor):
+      torch.add(self._offset, self._raw_actions, alpha=self._scale, out=self._processed_actions)
+    else:
+      torch.mul(self._raw_actions, self._scale, out=self._processed_actions).add_(self._offset)
 
   def reset(self, env_ids=None) -> None:
     self._raw_actions.masked_fill_(as_mask(env_ids, self.num_envs, self.device)[:, None], 0.0)

@@ -41,7 +41,7 @@ class CommandTerm(ManagerTermBase):
 
   def _resample(self, mask: torch.Tensor) -> None:
     lo, hi = self.cfg.resampling_time_range
-    self.time_left.copy_(torch.where(mask, torch.rand_like(self.time_left) * (hi - lo) + lo, self.time_left))
+    torch.where(mask, torch.rand_like(self.time_left) * (hi - lo) + lo, self.time_left, out=self.time_left)
     self._resample_command(mask)
     self.command_counter += mask.long()
 

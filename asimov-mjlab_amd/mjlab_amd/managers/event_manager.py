@@ -68,7 +68,7 @@ class EventManager:
           continue
         lo, hi = tcfg.interval_range_s
         t = self._interval_time_left[i]
-        t.copy_(torch.where(m, torch.rand_like(t) * (hi - lo) + lo, t))
+        torch.where(m, torch.rand_like(t) * (hi - lo) + lo, t, out=t)
     return {}
 
   def apply(self, mode: str, env_ids=None, dt: float | None = None, global_env_step_count: int | None = None):
@@ -82,7 +82,7 @@ class EventManager:
         t -= dt
         lo, hi = tcfg.interval_range_s
         due = t < 1e-6
-        t.copy_(torch.where(due, torch.rand_like(t) * (hi - lo) + lo, t))
+        torch.where(due, torch.rand_like(t) * (hi - lo) + lo, t, out=t)
         if tcfg.is_global_time:
           due = due.expand(self._env.num_envs)
         tcfg.func(self._env, due, **tcfg.params)
@@ -94,7 +94,7 @@ class EventManager:
           valid = ((step - last) >= tcfg.min_step_count_between_reset) | ((last == 0) & ~once)
           m = m & valid
         last = self._reset_last_step[i]
-        last.copy_(torch.where(m, torch.as_tensor(step, device=last.device) if not isinstance(step, torch.Tensor) else step.to(last.dtype), last))
+        torch.where(m, torch.as_tensor(step, device=last.device) if not isinstance(step, torch.Tensor) else step.to(last.dtype), last, out=last)
         self._reset_once[i] |= m
         tcfg.func(self._env, m, **tcfg.params)
       else:

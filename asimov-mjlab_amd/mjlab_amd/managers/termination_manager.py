@@ -25,6 +25,7 @@ class TerminationManager:
     self._term_dones = {k: torch.zeros(n, dtype=torch.bool, device=env.device) for k in self._term_names}
     self._truncated_buf = torch.zeros(n, dtype=torch.bool, device=env.device)
     self._terminated_buf = torch.zeros_like(self._truncated_buf)
+    self._dones_buf = torch.zeros_like(self._truncated_buf)
 
   @property
   def active_terms(self) -> list[str]:
@@ -32,7 +33,7 @@ class TerminationManager:
 
   @property
   def dones(self) -> torch.Tensor:
-    return self._truncated_buf | self._terminated_buf
+    return self._dones_buf
 
   @property
   def time_outs(self) -> torch.Tensor:
@@ -60,7 +61,8 @@ class TerminationManager:
       else:
         self._terminated_buf |= value
       self._term_dones[name].copy_(value)
-    return self._truncated_buf | self._terminated_buf
+    torch.bitwise_or(self._truncated_buf, self._terminated_buf, out=self._dones_buf)
+    return self._dones_buf
 
   def get_term(self, name: str) -> torch.Tensor:
     return self._term_dones[name]

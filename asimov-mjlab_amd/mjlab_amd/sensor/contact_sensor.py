@@ -206,7 +206,7 @@ class ContactSensor:
       m = env_ids[:, None]
       for t in (st.current_air_time, st.last_air_time, st.current_contact_time, st.last_contact_time):
         t.masked_fill_(m, 0.0)
-      st.last_time.copy_(torch.where(env_ids, self._data.time, st.last_time))
+      torch.where(env_ids, self._data.time, st.last_time, out=st.last_time)
       return
     ids = slice(None) if env_ids is None else env_ids
     st.current_air_time[ids] = 0.0
@@ -270,8 +270,8 @@ class ContactSensor:
     is_c = cd.found > 0
     first_c = (st.current_air_time > 0) & is_c
     first_d = (st.current_contact_time > 0) & ~is_c
-    st.last_air_time.copy_(torch.where(first_c, st.current_air_time + el, st.last_air_time))
-    st.current_air_time.copy_(torch.where(~is_c, st.current_air_time + el, torch.zeros_like(st.current_air_time)))
-    st.last_contact_time.copy_(torch.where(first_d, st.current_contact_time + el, st.last_contact_time))
-    st.current_contact_time.copy_(torch.where(is_c, st.current_contact_time + el, torch.zeros_like(st.current_contact_time)))
+    torch.where(first_c, st.current_air_time + el, st.last_air_time, out=st.last_air_time)
+    torch.where(~is_c, st.current_air_time + el, torch.zeros_like(st.current_air_time), out=st.current_air_time)
+    torch.where(first_d, st.current_contact_time + el, st.last_contact_time, out=st.last_contact_time)
+    torch.where(is_c, st.current_contact_time + el, torch.zeros_like(st.current_contact_time), out=st.current_contact_time)
     st.last_time.copy_(now)

@@ -19,7 +19,7 @@ PKG = Path(__file__).resolve().parents[1]
 # MJH_LIB selects an alternative build of the same ABI (e.g. the phase-timing
 # build libmjh_prof.so used by tools/phase_profile.py).
 LIB_PATH = Path(os.environ.get("MJH_LIB", str(PKG / "libmjh.so")))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 EXPORTS = (
   "mjh_abi_version",
@@ -41,6 +41,13 @@ EXPORTS = (
   "mjh_velocity_from_cvel",
   "mjh_air_time_update",
   "mjh_obs_term",
+  "mjh_rew_track",
+  "mjh_rew_flat_orientation",
+  "mjh_rew_sqsum",
+  "mjh_rew_diffsq",
+  "mjh_rew_pos_limits",
+  "mjh_rew_posture",
+  "mjh_rew_feet",
 )
 
 
@@ -79,10 +86,17 @@ def lib() -> ctypes.CDLL:
   ll, vp, ci = ctypes.c_longlong, ctypes.c_void_p, ctypes.c_int
   L.mjh_quat_rotate.argtypes = [vp, ll, vp, ll, vp, ll, ci, vp]
   L.mjh_quat_mul.argtypes = [vp, ll, vp, ll, vp, ll, vp]
-  L.mjh_velocity_from_cvel.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp]
+  L.mjh_velocity_from_cvel.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, ci, vp]
   L.mjh_air_time_update.argtypes = [vp, ll, vp, ci, vp, vp, vp, vp, vp, vp, ll, vp]
   cf = ctypes.c_float
   L.mjh_obs_term.argtypes = [vp, ll, vp, ll, cf, cf, cf, cf, cf, vp, ll, ci, ll, vp]
+  L.mjh_rew_track.argtypes = [vp, ll, vp, ll, cf, ci, vp, ll, vp]
+  L.mjh_rew_flat_orientation.argtypes = [vp, ll, vp, ll, cf, vp, ll, vp]
+  L.mjh_rew_sqsum.argtypes = [vp, ll, ci, vp, ll, vp]
+  L.mjh_rew_diffsq.argtypes = [vp, ll, vp, ll, ci, vp, ll, vp]
+  L.mjh_rew_pos_limits.argtypes = [vp, ll, vp, ll, ci, vp, ll, vp]
+  L.mjh_rew_posture.argtypes = [vp, ll, vp, ll, vp, vp, vp, vp, ll, cf, cf, ci, vp, ll, vp]
+  L.mjh_rew_feet.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, cf, cf, cf, ci, vp, vp, vp, vp, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 
 from mjlab_amd.managers.scene_entity_config import SceneEntityCfg
+from mjlab_amd import envops
 from mjlab_amd.envops import quat_apply_inverse
 from mjlab_amd.utils.string import resolve_matching_names_values
 
@@ -28,6 +29,9 @@ def _command_active(env, command_name, threshold) -> torch.Tensor | None:
 def track_linear_velocity(env, std: float, command_name: str, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   command = env.command_manager.get_command(command_name)
   actual = env.scene[asset_cfg.name].data.root_link_lin_vel_b
+  fused = envops.rew_track(command, actual, std, angular=False)
+  if fused is not None:
+    return fused
   err = torch.sum(torch.square(command[:, :2] - actual[:, :2]), dim=1) + torch.square(actual[:, 2])
   return torch.exp(-err / std**2)
 
@@ -35,6 +39,9 @@ def track_linear_velocity(env, std: float, command_name: str, asset_cfg: SceneEn
 def track_angular_velocity(env, std: float, command_name: str, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   command = env.command_manager.get_command(command_name)
   actual = env.scene[asset_cfg.name].data.root_link_ang_vel_b
+  fused = envops.rew_track(command, actual, std, angular=True)
+  if fused is not None:
+    return fused
   err = torch.square(command[:, 2] - actual[:, 2]) + torch.sum(torch.square(actual[:, :2]), dim=1)
   return torch.exp(-err / std**2)
 
@@ -43,6 +50,9 @@ def flat_orientation(env, std: float, asset_cfg: SceneEntityCfg = _DEFAULT) -> t
   a = env.scene[asset_cfg.name]
   if asset_cfg.body_ids and not isinstance(asset_cfg.body_ids, slice):
     q = a.data.body_link_quat_w[:, asset_cfg.body_idx, :].squeeze(1)
+    fused = envops.rew_flat_orientation(q, a.data.gravity_vec_w, std)
+    if fused is not None:
+      return fused
     g = quat_apply_inverse(q, a.data.gravity_vec_w)
     xy = torch.sum(torch.square(g[:, :2]), dim=1)
   else:
@@ -56,12 +66,14 @@ def self_collision_cost(env, sensor_name: str) -> torch.Tensor:
 
 def body_angular_velocity_penalty(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   w = env.scene[asset_cfg.name].data.body_link_ang_vel_w[:, asset_cfg.body_idx, :].squeeze(1)
-  return torch.sum(torch.square(w[:, :2]), dim=1)
+  fused = envops.rew_sqsum(w, 2)
+  return fused if fused is not None else torch.sum(torch.square(w[:, :2]), dim=1)
 
 
 def angular_momentum_penalty(env, sensor_name: str) -> torch.Tensor:
   h = env.scene[sensor_name].data
-  sq = torch.sum(torch.square(h), dim=-1)
+  sq = envops.rew_sqsum(h, 3) if h.dim() == 2 and h.shape[1] == 3 else None
+  sq = sq if sq is not None else torch.sum(torch.square(h), dim=-1)
   env.extras["log"]["Metrics/angular_momentum_mean"] = torch.mean(torch.sqrt(sq))
   return sq
 
@@ -79,6 +91,11 @@ def feet_air_time(env, sensor_name: str, threshold_min: float = 0.05, threshold_
 def feet_clearance(env, target_height: float, command_name: str | None = None, command_threshold: float = 0.01,
                    asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   a = env.scene[asset_cfg.name]
+  if command_name is not None and env.command_manager.get_command(command_name) is not None:
+    fused = envops.rew_feet(a.data.site_pos_w[:, asset_cfg.site_idx], a.data.site_lin_vel_w[:, asset_cfg.site_idx], None,
+                            env.command_manager.get_command(command_name), target_height, command_threshold, 0.0, "clearance")
+    if fused is not None:
+      return fused
   z = a.data.site_pos_w[:, asset_cfg.site_idx, 2]
   v = torch.norm(a.data.site_lin_vel_w[:, asset_cfg.site_idx, :2], dim=-1)
   cost = torch.sum(torch.abs(z - target_height) * v, dim=1)
@@ -99,7 +116,7 @@ class feet_swing_height:
     cs = env.scene[sensor_name]
     h = a.data.site_pos_w[:, asset_cfg.site_idx, 2]
     in_air = cs.data.found == 0
-    self.peak_heights.copy_(torch.where(in_air, torch.maximum(self.peak_heights, h), self.peak_heights))
+    torch.where(in_air, torch.maximum(self.peak_heights, h), self.peak_heights, out=self.peak_heights)
     first = cs.compute_first_contact(dt=self.step_dt)
     active = _command_active(env, command_name, command_threshold)
     err = self.peak_heights / target_height - 1.0
@@ -114,8 +131,15 @@ def feet_slip(env, sensor_name: str, command_name: str, command_threshold: float
               asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   a = env.scene[asset_cfg.name]
   cs = env.scene[sensor_name]
+  found = cs.data.found
+  fused = envops.rew_feet(a.data.site_pos_w[:, asset_cfg.site_idx], a.data.site_lin_vel_w[:, asset_cfg.site_idx],
+                          found, env.command_manager.get_command(command_name), 0.0, 0.0, command_threshold, "slip")
+  if fused is not None:
+    cost, vsum, cnt = fused
+    env.extras["log"]["Metrics/slip_velocity_mean"] = torch.sum(vsum) / torch.clamp(torch.sum(cnt), min=1)
+    return cost
   active = _command_active(env, command_name, command_threshold)
-  in_contact = (cs.data.found > 0).float()
+  in_contact = (found > 0).float()
   v = torch.norm(a.data.site_lin_vel_w[:, asset_cfg.site_idx, :2], dim=-1)
   cost = torch.sum(torch.square(v) * in_contact, dim=1) * active
   env.extras["log"]["Metrics/slip_velocity_mean"] = torch.sum(v * in_contact) / torch.clamp(torch.sum(in_contact), min=1)
@@ -161,5 +185,10 @@ class variable_posture:
       + self.std_walking * walking.unsqueeze(1)
       + self.std_running * running.unsqueeze(1)
     )
+    if isinstance(asset_cfg.joint_idx, slice) and asset_cfg.joint_idx == slice(None):
+      fused = envops.rew_posture(a.data.joint_pos, self.default_joint_pos, self.std_standing, self.std_walking,
+                                 self.std_running, command, walking_threshold, running_threshold)
+      if fused is not None:
+        return fused
     err = torch.square(a.data.joint_pos[:, asset_cfg.joint_idx] - self.default_joint_pos[:, asset_cfg.joint_idx])
     return torch.exp(-torch.mean(err / (std**2), dim=1))

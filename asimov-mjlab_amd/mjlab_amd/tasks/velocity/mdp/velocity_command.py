@@ -62,12 +62,12 @@ class UniformVelocityCommand(CommandTerm):
 
   def _resample_command(self, mask: torch.Tensor) -> None:
     new = self._draw()
-    self.vel_command_b.copy_(torch.where(mask[:, None], new[:, :3], self.vel_command_b))
+    torch.where(mask[:, None], new[:, :3], self.vel_command_b, out=self.vel_command_b)
     u = torch.rand(self.num_envs, 2, device=self.device)
     if self.cfg.heading_command:
-      self.heading_target.copy_(torch.where(mask, new[:, 3], self.heading_target))
-      self.is_heading_env.copy_(torch.where(mask, u[:, 0] <= self.cfg.rel_heading_envs, self.is_heading_env))
-    self.is_standing_env.copy_(torch.where(mask, u[:, 1] <= self.cfg.rel_standing_envs, self.is_standing_env))
+      torch.where(mask, new[:, 3], self.heading_target, out=self.heading_target)
+      torch.where(mask, u[:, 0] <= self.cfg.rel_heading_envs, self.is_heading_env, out=self.is_heading_env)
+    torch.where(mask, u[:, 1] <= self.cfg.rel_standing_envs, self.is_standing_env, out=self.is_standing_env)
     if self.cfg.init_velocity_prob > 0.0:
       iv = mask & (torch.rand(self.num_envs, device=self.device) < self.cfg.init_velocity_prob)
       d = self.robot.data

@@ -32,7 +32,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 3
+#define MJH_ABI_VERSION 4
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -151,9 +151,10 @@ int mjh_quat_rotate(const float* q, long long qs, const float* v, long long vs, 
 /* out[i] = p[i] * q[i] (quat_mul). */
 int mjh_quat_mul(const float* p, long long ps, const float* q, long long qs, float* out, long long n, void* stream);
 
-/* out[i] = [cvel_lin - cvel_ang x (com - pos), cvel_ang] (entity/data.py:20-31). */
+/* out[i] = [cvel_lin - cvel_ang x (com - pos), cvel_ang] (entity/data.py:20-31) for
+ * n rows; rows i share com row i / k (k bodies/sites per env). */
 int mjh_velocity_from_cvel(const float* pos, long long ps, const float* com, long long cs, const float* cvel, long long vs,
-                           float* out, long long n, void* stream);
+                           float* out, long long n, int k, void* stream);
 
 /* Contact-sensor air/contact timers for k tracked slots whose `found` values
  * sit at sensordata[:, cols[j]] (contact_sensor.py:327-367). */
@@ -166,6 +167,23 @@ int mjh_air_time_update(const float* sensordata, long long sds, const int* cols,
  * no noise); clipping is skipped when cmin > cmax. */
 int mjh_obs_term(const float* x, long long xs, const float* u, long long us, float lo, float hi, float cmin, float cmax,
                  float scale, float* out, long long os, int w, long long n, void* stream);
+
+/* ---- fused MDP terms (mjh_mdp.hip): one launch per reward term ----
+ * Formulas of src/mjlab/tasks/velocity/mdp/rewards.py and envs/mdp/rewards.py. */
+int mjh_rew_track(const float* cmd, long long cs, const float* v, long long vs, float inv_std2, int angular, float* out,
+                  long long n, void* stream);
+int mjh_rew_flat_orientation(const float* q, long long qs, const float* g, long long gs, float inv_std2, float* out,
+                             long long n, void* stream);
+int mjh_rew_sqsum(const float* x, long long xs, int k, float* out, long long n, void* stream);
+int mjh_rew_diffsq(const float* a, long long as, const float* b, long long bs, int k, float* out, long long n, void* stream);
+int mjh_rew_pos_limits(const float* q, long long qs, const float* lim, long long ls, int k, float* out, long long n,
+                       void* stream);
+int mjh_rew_posture(const float* q, long long qs, const float* q0, long long q0s, const float* std_stand,
+                    const float* std_walk, const float* std_run, const float* cmd, long long cs, float walk_thr,
+                    float run_thr, int k, float* out, long long n, void* stream);
+int mjh_rew_feet(const float* z, long long zs, const float* vel, long long vs, const float* found, long long fs,
+                 const float* cmd, long long cs, float target, float thr_clear, float thr_slip, int k, float* clearance,
+                 float* slip, float* slip_vsum, float* slip_cnt, long long n, void* stream);
 
 #ifdef __cplusplus
 }
