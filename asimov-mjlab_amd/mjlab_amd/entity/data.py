@@ -326,16 +326,18 @@ class EntityData:
   def generalized_force(self) -> torch.Tensor:
     return self.data.qfrc_applied[:, self._ix["free_joint_v_adr"]]
 
-  root_link_pos_w = property(lambda s: s.root_link_pose_w[:, 0:3])
-  root_link_quat_w = property(lambda s: s.root_link_pose_w[:, 3:7])
+  # == root_link_pose_w[:, 0:3] / [:, 3:7], read straight from the kinematics
+  # outputs (views: no gather or concatenation launched)
+  root_link_pos_w = property(lambda s: s.data.xpos[:, s._root])
+  root_link_quat_w = property(lambda s: s.data.xquat[:, s._root])
   root_link_lin_vel_w = property(lambda s: s.root_link_vel_w[:, 0:3])
   root_link_ang_vel_w = property(lambda s: s.root_link_vel_w[:, 3:6])
   root_com_pos_w = property(lambda s: s.root_com_pose_w[:, 0:3])
   root_com_quat_w = property(lambda s: s.root_com_pose_w[:, 3:7])
   root_com_lin_vel_w = property(lambda s: s.root_com_vel_w[:, 0:3])
   root_com_ang_vel_w = property(lambda s: s.root_com_vel_w[:, 3:6])
-  body_link_pos_w = property(lambda s: s.body_link_pose_w[..., 0:3])
-  body_link_quat_w = property(lambda s: s.body_link_pose_w[..., 3:7])
+  body_link_pos_w = property(lambda s: s._body_link_pos_w)
+  body_link_quat_w = property(lambda s: s._body_link_quat_w)
   body_link_lin_vel_w = property(lambda s: s.body_link_vel_w[..., 0:3])
   body_link_ang_vel_w = property(lambda s: s.body_link_vel_w[..., 3:6])
   body_com_pos_w = property(lambda s: s.body_com_pose_w[..., 0:3])
@@ -352,6 +354,16 @@ class EntityData:
   site_quat_w = property(lambda s: s.site_pose_w[..., 3:7])
   site_lin_vel_w = property(lambda s: s.site_vel_w[..., 0:3])
   site_ang_vel_w = property(lambda s: s.site_vel_w[..., 3:6])
+
+  @_cached
+  def _body_link_pos_w(self) -> torch.Tensor:
+    """== body_link_pose_w[..., 0:3]"""
+    return self.data.xpos[:, self._ix["body_ids"]]
+
+  @_cached
+  def _body_link_quat_w(self) -> torch.Tensor:
+    """== body_link_pose_w[..., 3:7]"""
+    return self.data.xquat[:, self._ix["body_ids"]]
 
   @_cached
   def _geom_pos_w(self) -> torch.Tensor:

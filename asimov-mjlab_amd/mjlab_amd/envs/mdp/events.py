@@ -32,6 +32,14 @@ def _ranges6(env, r: dict | None) -> tuple[torch.Tensor, torch.Tensor]:
   return cache[key]
 
 
+def _uniform6(env, n, ranges, lo, hi):
+  """U(lo, hi) draws for the 6 pose/velocity axes, or None when every range is
+  (0, 0): the offsets are then exactly zero and no random kernel is launched."""
+  if not ranges or all(tuple(v) == (0.0, 0.0) for v in ranges.values()):
+    return None
+  return torch.rand(n, 6, device=env.device) * (hi - lo) + lo
+
+
 def reset_scene_to_default(env, env_ids) -> None:
   m = as_mask(env_ids, env.num_envs, env.device)
   for ent in env.scene.entities.values():
@@ -49,14 +57,17 @@ def reset_root_state_uniform(env, env_ids, pose_range: dict, velocity_range: dic
   a = env.scene[asset_cfg.name]
   n = env.num_envs
   lo, hi = _ranges6(env, pose_range)
-  pose = torch.rand(n, 6, device=env.device) * (hi - lo) + lo
+  pose = _uniform6(env, n, pose_range, lo, hi)
   rs = a.data.default_root_state
   if a.is_fixed_base:
     raise ValueError(f"Cannot reset root state for fixed-base entity '{asset_cfg.name}'.")
+  if pose is None:
+    pose = torch.zeros(n, 6, device=env.device)
   pos = rs[:, 0:3] + pose[:, 0:3] + env.scene.env_origins
   quat = quat_mul(rs[:, 3:7], quat_from_euler_xyz(pose[:, 3], pose[:, 4], pose[:, 5]))
   vlo, vhi = _ranges6(env, velocity_range)
-  vel = rs[:, 7:13] + torch.rand(n, 6, device=env.device) * (vhi - vlo) + vlo
+  dv = _uniform6(env, n, velocity_range, vlo, vhi)
+  vel = rs[:, 7:13] if dv is None else rs[:, 7:13] + dv
   a.write_root_link_pose_to_sim(torch.cat([pos, quat], dim=-1), env_ids=m)
   a.write_root_link_velocity_to_sim(vel, env_ids=m)
 
@@ -67,11 +78,13 @@ def reset_joints_by_offset(env, env_ids, position_range: tuple[float, float], ve
   a = env.scene[asset_cfg.name]
   j = asset_cfg.joint_idx
   jp = a.data.default_joint_pos[:, j].clone()
-  jp += torch.rand_like(jp) * (position_range[1] - position_range[0]) + position_range[0]
+  if tuple(position_range) != (0.0, 0.0):  # (0, 0): exact zero offset, no draw
+    jp += torch.rand_like(jp) * (position_range[1] - position_range[0]) + position_range[0]
   lim = a.data.soft_joint_pos_limits[:, j]
   jp = jp.clamp_(lim[..., 0], lim[..., 1])
   jv = a.data.default_joint_vel[:, j].clone()
-  jv += torch.rand_like(jv) * (velocity_range[1] - velocity_range[0]) + velocity_range[0]
+  if tuple(velocity_range) != (0.0, 0.0):
+    jv += torch.rand_like(jv) * (velocity_range[1] - velocity_range[0]) + velocity_range[0]
   a.write_joint_state_to_sim(jp, jv, env_ids=m, joint_ids=None if isinstance(j, slice) else j)
 
 

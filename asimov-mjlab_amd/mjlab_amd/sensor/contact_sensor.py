@@ -234,26 +234,39 @@ class ContactSensor:
     return self._air_time_state
 
   def _extract_sensor_data(self) -> ContactData:
-    chunks: dict[str, list[torch.Tensor]] = {f: [] for f in self.cfg.fields}
-    for slot in self._slots:
-      dim = _CONTACT_DATA_DIMS[slot.field_name]
-      raw = slot.data_view.view(slot.data_view.size(0), -1, dim)
-      chunks[slot.field_name].append(raw)
+    """Slots of each field gathered in one indexed read of sensordata (instead of
+    a concatenation of per-slot views), cached until the next step/forward."""
+    ep = self._data.epoch.v
+    if getattr(self, "_cache_ep", None) == ep:
+      return ContactData(**vars(self._cache))
+    if not hasattr(self, "_field_cols"):
+      self._field_cols = {}
+      for f in self.cfg.fields:
+        cols = []
+        for slot in self._slots:
+          if slot.field_name == f:
+            a = slot.data_view.storage_offset() - self._data.sensordata.storage_offset()
+            cols += list(range(a, a + slot.data_view.shape[1]))
+        self._field_cols[f] = torch.tensor(cols, dtype=torch.long, device=self._data.sensordata.device)
     out = ContactData()
-    for f, cs in chunks.items():
-      cat = torch.cat(cs, dim=1)
+    sd = self._data.sensordata
+    n = sd.shape[0]
+    for f in self.cfg.fields:
+      dim = _CONTACT_DATA_DIMS[f]
+      cat = sd[:, self._field_cols[f]].view(n, -1, dim)
       if cat.size(-1) == 1:
         cat = cat.squeeze(-1)
       setattr(out, f, cat)
     if self.cfg.global_frame and self.cfg.reduce != "netforce":
-      n, t = out.normal, out.tangent
-      R = torch.stack([t, torch.cross(n, t, dim=-1), n], dim=-1)
-      has = torch.norm(n, dim=-1, keepdim=True) > 1e-8
+      nrm, t = out.normal, out.tangent
+      R = torch.stack([t, torch.cross(nrm, t, dim=-1), nrm], dim=-1)
+      has = torch.norm(nrm, dim=-1, keepdim=True) > 1e-8
       if out.force is not None:
         out.force = torch.where(has, torch.einsum("...ij,...j->...i", R, out.force), out.force)
       if out.torque is not None:
         out.torque = torch.where(has, torch.einsum("...ij,...j->...i", R, out.torque), out.torque)
-    return out
+    self._cache, self._cache_ep = out, ep
+    return ContactData(**vars(out))
 
   def _update_air_time_tracking(self) -> None:
     st = self._air_time_state
