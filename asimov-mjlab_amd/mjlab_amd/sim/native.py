@@ -48,6 +48,7 @@ EXPORTS = (
   "mjh_rew_pos_limits",
   "mjh_rew_posture",
   "mjh_rew_feet",
+  "mjh_velocity_command",
 )
 
 
@@ -96,6 +97,8 @@ def lib() -> ctypes.CDLL:
   L.mjh_rew_diffsq.argtypes = [vp, ll, vp, ll, ci, vp, ll, vp]
   L.mjh_rew_pos_limits.argtypes = [vp, ll, vp, ll, ci, vp, ll, vp]
   L.mjh_rew_posture.argtypes = [vp, ll, vp, ll, vp, vp, vp, vp, ll, cf, cf, ci, vp, ll, vp]
+  L.mjh_velocity_command.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, cf, cf, cf, cf, cf, cf, cf, ci, vp, vp, vp, vp, vp,
+                                     vp, vp, vp, vp, ll, vp]
   L.mjh_rew_feet.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, cf, cf, cf, ci, vp, vp, vp, vp, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")

@@ -54,6 +54,57 @@ class UniformVelocityCommand(CommandTerm):
     lo, hi = self._ranges_t[:, 0], self._ranges_t[:, 1]
     return torch.rand(self.num_envs, 4, device=self.device) * (hi - lo) + lo
 
+  def compute(self, dt: float) -> None:
+    """CommandTerm.compute (command_manager.py:53-67) with one (N, 8) uniform
+    draw per step: [timer, lin_x, lin_y, ang_z, heading, heading-env,
+    standing-env, init-velocity]. On the GPU the whole update is one fused
+    kernel (csrc/mjh_mdp.hip); the torch path below is its reference."""
+    u = torch.rand(self.num_envs, 8, device=self.device)
+    if self.cfg.init_velocity_prob == 0.0 and self._compute_fused(dt, u):
+      return
+    self._compute_torch(dt, u)
+
+  def _compute_fused(self, dt: float, u: torch.Tensor) -> bool:
+    if not self.vel_command_b.is_cuda:
+      return False
+    import ctypes
+
+    from mjlab_amd.sim import native
+
+    d = self.robot.data
+    lin, ang, q = d.root_link_lin_vel_b, d.root_link_ang_vel_b, d.root_link_quat_w
+    if not all(t.dim() == 2 and t.stride(1) == 1 for t in (lin, ang, q)):
+      return False
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    lo, hi = self.cfg.resampling_time_range
+    max_step = self.cfg.resampling_time_range[1] / self._env.step_dt
+    native.check(native.lib().mjh_velocity_command(
+      P(lin), lin.stride(0), P(ang), ang.stride(0), P(q), q.stride(0), P(u), u.stride(0), P(self._ranges_t),
+      float(dt), 1.0 / max_step, float(lo), float(hi), float(self.cfg.rel_heading_envs), float(self.cfg.rel_standing_envs),
+      float(self.cfg.heading_control_stiffness), int(self.cfg.heading_command), P(self.vel_command_b),
+      P(self.heading_target), P(self.heading_error), P(self.is_heading_env), P(self.is_standing_env), P(self.time_left),
+      P(self.command_counter), P(self.metrics["error_vel_xy"]), P(self.metrics["error_vel_yaw"]), self.num_envs,
+      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "mjh_velocity_command")
+    return True
+
+  def _compute_torch(self, dt: float, u: torch.Tensor) -> None:
+    self._update_metrics()
+    self.time_left -= dt
+    mask = self.time_left <= 0.0
+    lo, hi = self.cfg.resampling_time_range
+    torch.where(mask, u[:, 0] * (hi - lo) + lo, self.time_left, out=self.time_left)
+    r = self._ranges_t
+    new = u[:, 1:5] * (r[:, 1] - r[:, 0]) + r[:, 0]
+    torch.where(mask[:, None], new[:, :3], self.vel_command_b, out=self.vel_command_b)
+    if self.cfg.heading_command:
+      torch.where(mask, new[:, 3], self.heading_target, out=self.heading_target)
+      torch.where(mask, u[:, 5] <= self.cfg.rel_heading_envs, self.is_heading_env, out=self.is_heading_env)
+    torch.where(mask, u[:, 6] <= self.cfg.rel_standing_envs, self.is_standing_env, out=self.is_standing_env)
+    if self.cfg.init_velocity_prob > 0.0:
+      self._init_velocity(mask & (u[:, 7] < self.cfg.init_velocity_prob))
+    self.command_counter += mask.long()
+    self._update_command()
+
   def _update_metrics(self) -> None:
     max_command_step = self.cfg.resampling_time_range[1] / self._env.step_dt
     d = self.robot.data
@@ -69,14 +120,17 @@ class UniformVelocityCommand(CommandTerm):
       torch.where(mask, u[:, 0] <= self.cfg.rel_heading_envs, self.is_heading_env, out=self.is_heading_env)
     torch.where(mask, u[:, 1] <= self.cfg.rel_standing_envs, self.is_standing_env, out=self.is_standing_env)
     if self.cfg.init_velocity_prob > 0.0:
-      iv = mask & (torch.rand(self.num_envs, device=self.device) < self.cfg.init_velocity_prob)
-      d = self.robot.data
-      lin_b = d.root_link_lin_vel_b.clone()
-      lin_b[:, :2] = self.vel_command_b[:, :2]
-      ang_b = d.root_link_ang_vel_b.clone()
-      ang_b[:, 2] = self.vel_command_b[:, 2]
-      state = torch.cat([d.root_link_pos_w, d.root_link_quat_w, quat_apply(d.root_link_quat_w, lin_b), ang_b], dim=-1)
-      self.robot.write_root_state_to_sim(state, iv)
+      self._init_velocity(mask & (torch.rand(self.num_envs, device=self.device) < self.cfg.init_velocity_prob))
+
+  def _init_velocity(self, iv: torch.Tensor) -> None:
+    """Start the selected envs moving at their command (velocity_command.py:80-89)."""
+    d = self.robot.data
+    lin_b = d.root_link_lin_vel_b.clone()
+    lin_b[:, :2] = self.vel_command_b[:, :2]
+    ang_b = d.root_link_ang_vel_b.clone()
+    ang_b[:, 2] = self.vel_command_b[:, 2]
+    state = torch.cat([d.root_link_pos_w, d.root_link_quat_w, quat_apply(d.root_link_quat_w, lin_b), ang_b], dim=-1)
+    self.robot.write_root_state_to_sim(state, iv)
 
   def _update_command(self) -> None:
     if self.cfg.heading_command:

@@ -185,6 +185,16 @@ int mjh_rew_feet(const float* z, long long zs, const float* vel, long long vs, c
                  const float* cmd, long long cs, float target, float thr_clear, float thr_slip, int k, float* clearance,
                  float* slip, float* slip_vsum, float* slip_cnt, long long n, void* stream);
 
+/* UniformVelocityCommand.compute for all envs (velocity_command.py:65-101):
+ * metrics, timers, masked resampling from u (N, 8) uniform draws, heading
+ * control, standing override. Boolean buffers are torch.bool (1 byte). */
+int mjh_velocity_command(const float* lin_b, long long ls, const float* ang_b, long long as, const float* root_q,
+                         long long qs, const float* u, long long us, const float* ranges, float dt, float inv_max_step,
+                         float t_lo, float t_hi, float rel_heading, float rel_standing, float stiffness,
+                         int heading_command, float* cmd, float* heading_target, float* heading_error,
+                         unsigned char* is_heading, unsigned char* is_standing, float* time_left, long long* counter,
+                         float* err_xy, float* err_yaw, long long n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

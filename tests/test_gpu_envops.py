@@ -129,3 +129,34 @@ def test_fused_reward_terms_match_torch(monkeypatch):
   ref = evaluate()
   for name in fused:
     torch.testing.assert_close(fused[name].float(), ref[name].float(), rtol=2e-5, atol=2e-5, msg=name)
+
+
+def test_fused_velocity_command_matches_torch():
+  from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
+  from mjlab_amd.tasks import load_env_cfg
+
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = 256
+  env = ManagerBasedRlEnv(cfg, device=DEV)
+  env.reset()
+  for _ in range(5):
+    env.step(torch.zeros(256, 29, device=DEV))
+  term = env.command_manager.get_term("twist")
+  term.time_left[::3] = 0.001  # force resampling in a third of the envs
+  fields = ("vel_command_b", "heading_target", "heading_error", "is_heading_env", "is_standing_env", "time_left",
+            "command_counter")
+  snap = {f: getattr(term, f).clone() for f in fields}
+  msnap = {k: v.clone() for k, v in term.metrics.items()}
+  u = torch.rand(256, 8, device=DEV, generator=torch.Generator(device=DEV).manual_seed(9))
+  assert term._compute_fused(env.step_dt, u)
+  fused = {f: getattr(term, f).clone() for f in fields}
+  fm = {k: v.clone() for k, v in term.metrics.items()}
+  for f in fields:
+    getattr(term, f).copy_(snap[f])
+  for k in term.metrics:
+    term.metrics[k].copy_(msnap[k])
+  term._compute_torch(env.step_dt, u)
+  for f in fields:
+    torch.testing.assert_close(fused[f], getattr(term, f), rtol=1e-5, atol=1e-5, msg=f)
+  for k in fm:
+    torch.testing.assert_close(fm[k], term.metrics[k], rtol=1e-5, atol=1e-5, msg=k)
