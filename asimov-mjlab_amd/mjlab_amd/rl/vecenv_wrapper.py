@@ -1,0 +1,104 @@
+"""RSL-RL VecEnv contract over ManagerBasedRlEnv (``src/mjlab/rl/vecenv_wrapper.py:11-127``).
+
+rsl_rl and tensordict are not dependencies here; observations come back as
+``ObsDict`` — a dict of the group tensors with the ``batch_size`` attribute and
+``.to()`` the learner uses — and the wrapper does not subclass rsl_rl's VecEnv.
+Semantics otherwise follow the reference: reset at construction (rsl_rl never
+calls reset), optional action clipping, ``dones`` as long, and
+``extras["time_outs"]`` for infinite-horizon tasks. With ``gather`` set, each
+step's outputs are also all-gathered across ranks (mjlab_amd.distributed).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from mjlab_amd.envs.manager_based_rl_env import Box, ManagerBasedRlEnv
+
+
+class ObsDict(dict):
+  def __init__(self, data: dict, batch_size) -> None:
+    super().__init__(data)
+    self.batch_size = list(batch_size)
+
+  def to(self, device) -> "ObsDict":
+    return ObsDict({k: v.to(device) for k, v in self.items()}, self.batch_size)
+
+
+class RslRlVecEnvWrapper:
+  def __init__(self, env: ManagerBasedRlEnv, clip_actions: float | None = None, gather: bool = False) -> None:
+    self.env = env
+    self.clip_actions = clip_actions
+    self.num_envs = env.num_envs
+    self.device = torch.device(env.device)
+    self.max_episode_length = env.max_episode_length
+    self.num_actions = env.action_manager.total_action_dim
+    self._gather = None
+    if gather:
+      from mjlab_amd.distributed import StepGather
+
+      self._gather = StepGather()
+    self._modify_action_space()
+    self.env.reset()
+
+  @property
+  def cfg(self):
+    return self.env.cfg
+
+  @property
+  def unwrapped(self) -> ManagerBasedRlEnv:
+    return self.env
+
+  @property
+  def render_mode(self):
+    return self.env.render_mode
+
+  @property
+  def observation_space(self):
+    return self.env.single_observation_space
+
+  @property
+  def action_space(self):
+    return self.env.action_space
+
+  @classmethod
+  def class_name(cls) -> str:
+    return cls.__name__
+
+  @property
+  def episode_length_buf(self) -> torch.Tensor:
+    return self.env.episode_length_buf
+
+  @episode_length_buf.setter
+  def episode_length_buf(self, value: torch.Tensor) -> None:
+    self.env.episode_length_buf.copy_(value)  # pointer-stable (captured graph)
+
+  def seed(self, seed: int = -1) -> int:
+    return self.env.seed(seed)
+
+  def get_observations(self) -> ObsDict:
+    return ObsDict(self.env.observation_manager.compute(), [self.num_envs])
+
+  def reset(self):
+    obs, extras = self.env.reset()
+    return ObsDict(obs, [self.num_envs]), extras
+
+  def step(self, actions: torch.Tensor):
+    if self.clip_actions is not None:
+      actions = torch.clamp(actions, -self.clip_actions, self.clip_actions)
+    obs, rew, terminated, truncated, extras = self.env.step(actions)
+    dones = (terminated | truncated).to(dtype=torch.long)
+    if not self.cfg.is_finite_horizon:
+      extras["time_outs"] = truncated
+    if self._gather is not None:
+      extras["gathered"] = self._gather(obs, rew, terminated, truncated)
+    return ObsDict(obs, [self.num_envs]), rew, dones, extras
+
+  def close(self) -> None:
+    return self.env.close()
+
+  def _modify_action_space(self) -> None:
+    if self.clip_actions is None:
+      return
+    self.env.single_action_space = Box(shape=(self.num_actions,), low=-self.clip_actions, high=self.clip_actions)
+    self.env.action_space = Box(shape=(self.num_envs, self.num_actions), low=-self.clip_actions, high=self.clip_actions)
