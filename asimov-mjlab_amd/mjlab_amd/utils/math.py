@@ -139,3 +139,33 @@ def matrix_from_quat(q: torch.Tensor) -> torch.Tensor:
     -1,
   )
   return o.reshape(q.shape[:-1] + (3, 3))
+
+
+def quat_inv(q: torch.Tensor, eps: float = 1e-9) -> torch.Tensor:
+  """conj(q) / |q|^2 (isaaclab math.py:261-271)."""
+  return quat_conjugate(q) / q.pow(2).sum(dim=-1, keepdim=True).clamp(min=eps)
+
+
+def axis_angle_from_quat(quat: torch.Tensor, eps: float = 1.0e-6) -> torch.Tensor:
+  """Rotation vector of a (w, x, y, z) quaternion (math.py:478-505)."""
+  quat = quat * (1.0 - 2.0 * (quat[..., 0:1] < 0.0))
+  mag = torch.linalg.norm(quat[..., 1:], dim=-1)
+  half_angle = torch.atan2(mag, quat[..., 0])
+  angle = 2.0 * half_angle
+  s = torch.where(angle.abs() > eps, torch.sin(half_angle) / angle, 0.5 - angle * angle / 48)
+  return quat[..., 1:4] / s.unsqueeze(-1)
+
+
+def quat_error_magnitude(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
+  """|log(q1 q2^*)| (quat_box_minus, math.py:596-604,688-699)."""
+  shape = q1.shape
+  d = quat_mul(q1.reshape(-1, 4), quat_conjugate(q2).reshape(-1, 4)).view(shape)
+  return torch.norm(axis_angle_from_quat(d), dim=-1)
+
+
+def subtract_frame_transforms(t01, q01, t02=None, q02=None):
+  """T12 = T01^-1 T02 (math.py:832-864)."""
+  q10 = quat_inv(q01)
+  q12 = quat_mul(q10, q02) if q02 is not None else q10
+  t12 = quat_apply(q10, t02 - t01) if t02 is not None else quat_apply(q10, -t01)
+  return t12, q12

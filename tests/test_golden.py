@@ -32,6 +32,11 @@ def test_math_matches_reference():
     "quat_from_matrix": M.quat_from_matrix(mat),
     "yaw_quat": M.yaw_quat(q1),
     "wrap_to_pi": M.wrap_to_pi(ang),
+    "quat_inv": M.quat_inv(q1 * 1.3),
+    "axis_angle_from_quat": M.axis_angle_from_quat(q1),
+    "quat_error_magnitude": M.quat_error_magnitude(q1, q2),
+    "sft_pos": M.subtract_frame_transforms(v, q1, e, q2)[0],
+    "sft_quat": M.subtract_frame_transforms(v, q1, e, q2)[1],
   }
   for k, got in checks.items():
     np.testing.assert_allclose(got.numpy(), z[k], rtol=1e-5, atol=1e-6, err_msg=k)

@@ -98,6 +98,9 @@ def main() -> None:
     "quat_mul": M.quat_mul(q1, q2), "quat_apply": M.quat_apply(q1, v), "quat_apply_inverse": M.quat_apply_inverse(q1, v),
     "quat_from_euler_xyz": M.quat_from_euler_xyz(e[:, 0], e[:, 1], e[:, 2]), "matrix_from_quat": mat,
     "quat_from_matrix": M.quat_from_matrix(mat), "yaw_quat": M.yaw_quat(q1), "wrap_to_pi": M.wrap_to_pi(ang),
+    "quat_inv": M.quat_inv(q1 * 1.3), "axis_angle_from_quat": M.axis_angle_from_quat(q1),
+    "quat_error_magnitude": M.quat_error_magnitude(q1, q2),
+    "sft_pos": M.subtract_frame_transforms(v, q1, e, q2)[0], "sft_quat": M.subtract_frame_transforms(v, q1, e, q2)[1],
   }
   np.savez(OUT / "math.npz", **{k: t.numpy() for k, t in math_out.items()})
   # ---- entity velocity conversion ----
