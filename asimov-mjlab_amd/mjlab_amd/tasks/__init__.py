@@ -27,3 +27,4 @@ def load_env_cfg(task_id: str):
 
 def _load_all() -> None:
   from mjlab_amd.tasks.velocity import config  # noqa: F401
+  from mjlab_amd.tasks.tracking import config as _tracking  # noqa: F401

@@ -29,3 +29,46 @@ def test_env_graph_rollout(task, adim):
   assert ((env.sim.data.flags & 4) == 0).all()
   assert (env.episode_length_buf <= 60).all()
   assert native.LIB_PATH.name.startswith("libmjh")
+
+
+def _gpu_motion(tmp_path, frames=120):
+  from mjlab_amd.motion import KEYS, save_motion, synthetic_motion
+
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = frames
+  env = ManagerBasedRlEnv(cfg, device="cuda:0")
+  mot = synthetic_motion(env.sim, env.scene["robot"], num_frames=frames, fps=50.0)
+  path = tmp_path / "clip.npz"
+  save_motion(path, 50.0, **{k: mot[k] for k in KEYS})
+  return str(path)
+
+
+def test_tracking_graph_rollout(tmp_path):
+  """Config 4 (G1 flat tracking) captured and replayed; the relative body
+  targets (fused quaternion kernels) match the reference's torch formulas."""
+  from mjlab_amd.utils import math as M
+
+  cfg = load_env_cfg("Mjlab-Tracking-Flat-Unitree-G1")
+  cfg.scene.num_envs = 256
+  cfg.seed = 0
+  cfg.commands["motion"].motion_file = _gpu_motion(tmp_path)
+  env = ManagerBasedRlEnv(cfg, device="cuda:0")
+  env.reset()
+  g = torch.Generator(device="cuda:0").manual_seed(1)
+  for _ in range(40):
+    obs, rew, term, trunc, extras = env.step(0.2 * (2 * torch.rand(256, 29, device="cuda:0", generator=g) - 1))
+  assert env._graph is not None
+  assert torch.isfinite(obs["policy"]).all() and torch.isfinite(obs["critic"]).all() and torch.isfinite(rew).all()
+  assert obs["policy"].shape == (256, 160) and obs["critic"].shape == (256, 286)
+  c = env.command_manager.get_term("motion")
+  ts = c.time_steps
+  assert ((ts >= 0) & (ts < c.motion.time_step_total)).all()
+  torch.testing.assert_close(c.joint_pos, c.motion.joint_pos[ts], rtol=0, atol=0)
+  nb = len(c.cfg.body_names)
+  a_pos = c.anchor_pos_w[:, None].repeat(1, nb, 1)
+  r_pos = c.robot_anchor_pos_w[:, None].repeat(1, nb, 1)
+  delta_pos = r_pos.clone()
+  delta_pos[..., 2] = a_pos[..., 2]
+  delta_ori = M.yaw_quat(M.quat_mul(c.robot_anchor_quat_w[:, None].repeat(1, nb, 1), M.quat_inv(c.anchor_quat_w[:, None].repeat(1, nb, 1))))
+  torch.testing.assert_close(c.body_pos_relative_w, delta_pos + M.quat_apply(delta_ori, c.body_pos_w - a_pos), rtol=1e-5, atol=1e-5)
+  torch.testing.assert_close(c.body_quat_relative_w, M.quat_mul(delta_ori, c.body_quat_w), rtol=1e-5, atol=1e-5)
