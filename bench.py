@@ -40,6 +40,7 @@ sys.path.insert(0, str(REPO / "asimov-mjlab_amd"))
 TASK = "Mjlab-Velocity-Flat-Unitree-G1"
 METRIC = "env steps/sec (whole node), Unitree G1 flat velocity task @ 4096 envs/GPU"
 B_PHYS_G1 = 5384  # algorithmic bytes per world per physics step
+B_PHYS = {"Unitree-Go1": 3040}  # other robots; default G1
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
@@ -54,7 +55,28 @@ def parse() -> argparse.Namespace:
   p.add_argument("--no-cpu-baseline", action="store_true")
   p.add_argument("--cpu-sample-worlds", type=int, default=512)
   p.add_argument("--kernel-launches", type=int, default=50)
+  p.add_argument("--motion-file", default="", help="tracking tasks: motion npz (default: synthetic 500-frame clip)")
   return p.parse_args()
+
+
+def synthetic_motion_file(dev: str, frames: int = 500) -> str:
+  """Config 4's input: a smooth sinusoidal G1 joint trajectory
+  around the default pose, evaluated by one batched forward pass on the GPU
+  (mjlab_amd.motion), written in the csv_to_npz format."""
+  import tempfile
+
+  from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
+  from mjlab_amd.motion import KEYS, save_motion, synthetic_motion
+  from mjlab_amd.tasks import load_env_cfg
+
+  cfg = load_env_cfg(TASK)
+  cfg.scene.num_envs = frames
+  env = ManagerBasedRlEnv(cfg, device=dev)
+  mot = synthetic_motion(env.sim, env.scene["robot"], num_frames=frames, fps=50.0)
+  path = Path(tempfile.mkdtemp()) / "g1_synthetic_motion.npz"
+  save_motion(path, 50.0, **{k: mot[k] for k in KEYS})
+  del env
+  return str(path)
 
 
 def cpu_baseline(env, args) -> dict:
@@ -93,7 +115,7 @@ def cpu_baseline(env, args) -> dict:
     "unit": "env steps/sec (physics only: decimation x mj_step per env step)",
     "cores": cores,
     "kind": "port",
-    "sample": f"{n} G1 worlds x {reps} physics steps ({el:.1f} s) from the bench's live state, float64 oracle "
+    "sample": f"{n} {env.sim.mj_model.nv}-dof worlds x {reps} physics steps ({el:.1f} s) from the bench's live state, float64 oracle "
     f"(oracle/oracle.c, OpenMP {cores} threads); env-layer cost excluded; MuJoCo C is not available",
   }
 
@@ -117,6 +139,9 @@ def main() -> None:
 
   cfg = load_env_cfg(args.task)
   cfg.scene.num_envs = args.num_envs
+  motion = getattr(cfg, "commands", {}).get("motion") if isinstance(getattr(cfg, "commands", None), dict) else None
+  if motion is not None and not motion.motion_file:
+    motion.motion_file = args.motion_file or synthetic_motion_file(dev)
   from mjlab_amd.distributed import shard_seed
 
   cfg.seed = shard_seed(42, rank)
@@ -175,7 +200,8 @@ def main() -> None:
   e1.record(stream)
   torch.cuda.synchronize()
   t_launch = e0.elapsed_time(e1) / 1e3 / L  # s per physics step (pack + step kernels)
-  bytes_per_launch = B_PHYS_G1 * args.num_envs
+  b_phys = next((v for k, v in B_PHYS.items() if k in args.task), B_PHYS_G1)
+  bytes_per_launch = b_phys * args.num_envs
   achieved = bytes_per_launch / t_launch / 1e9
   traffic = None
   tf = REPO / "profiles" / "step_kernel_traffic.json"
@@ -198,7 +224,7 @@ def main() -> None:
 
   if rank == 0:
     line = {
-      "metric": METRIC,
+      "metric": METRIC if args.task == TASK else f"env steps/sec (whole node), {args.task} @ {args.num_envs} envs/GPU",
       "value": value,
       "unit": "env steps/s",
       "n_gpus": world,
@@ -209,7 +235,8 @@ def main() -> None:
       "scaling": "weak",
       "vs_baseline": None,
       "dtype": "f32",
-      "data": "synthetic: random agent 2*U[0,1)-1 (seed 1234+rank), env seed 42+rank, DR/pushes/resets/commands on",
+      "data": "synthetic: random agent 2*U[0,1)-1 (seed 1234+rank), env seed 42+rank, DR/pushes/resets/commands on"
+      + ("; synthetic 500-frame motion clip (mjlab_amd.motion)" if motion is not None and not args.motion_file else ""),
       "config": {
         "workload": f"{args.task}, num_envs={args.num_envs}/GPU, random agent",
         "num_envs_per_gpu": args.num_envs,
