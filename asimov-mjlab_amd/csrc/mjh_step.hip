@@ -67,7 +67,7 @@ enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
 #define MJH_PRESET 5
 #endif
 #define MJH_REGIONS(X)                                                                              \
-  X(qpos, 1) X(qvel, 0) X(qacc, 0) X(qacc_smooth, 0) X(qfrc_smooth, 0) X(qfrc_bias, 1) X(qfrc_con, 0)  \
+  X(qpos, 0) X(qvel, 0) X(qacc, 0) X(qacc_smooth, 0) X(qfrc_smooth, 0) X(qfrc_bias, 1) X(qfrc_con, 0)  \
   X(qfrc_passive, 1) X(qfrc_act, 1) X(grad, 0) X(search, 0) X(Ma, 0) X(Mv, 0) X(tmp, 0) X(tmp2, 0)    \
   X(xpos, 1) X(xquat, 1) X(xmat, 1) X(xipos, 1) X(ximat, 1) X(subtree_com, 1) X(cinert, 0) X(crb, 0)  \
   X(cvel, 0) X(cacc, 1) X(cfrc, 0) X(xanchor, 1) X(xaxis, 1) X(cdof, 0) X(cdof_dot, 0)               \
@@ -150,6 +150,14 @@ struct ImgOff {
 #define IMG_F(name) (reinterpret_cast<const float*>(smem + Io.name))
 #define IMG_L(name) (reinterpret_cast<const long long*>(smem + Io.name))
 #define WFIELD(name) (m.name##_wstride ? (const float*)(m.name + W * m.name##_wstride) : (const float*)(smem + Io.name))
+
+// ---- cross-lane exchange ------------------------------------------------------
+// lane k's value to every lane (k wave-uniform): v_readlane_b32
+__device__ __forceinline__ float rl(float v, int k) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+// lane src's value (src per lane): ds_bpermute; call with every lane active
+__device__ __forceinline__ float shfl(float v, int src) { return __shfl(v, src, 64); }
 
 // ---- wave primitives on DPP (no LDS round trips) -----------------------------
 // dpp_ctrl: quad_perm 0x00-0xff, row_shr:n 0x110+n, row_mirror 0x140,
@@ -885,6 +893,12 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
   // ---------------------------------------------------------------- kinematics
   // Each lane walks its body's chain root->body (no per-level barriers). The
   // per-body normalisation matches a level-by-level sweep exactly.
+  // nbody, nv <= 64 (mjh_model_check): lane b owns body b and lane i dof i, so
+  // the tree phases below keep per-body / per-dof quantities in registers and
+  // exchange them with v_readlane (uniform k) or ds_bpermute, instead of
+  // serial chains of dependent global-scratch loads.
+  const bool bl = tid < nb;
+  float r_xipos[3] = {0.f, 0.f, 0.f}, r_ximat[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int b = tid; b < nb; b += NT) {
     float p[3] = {0.f, 0.f, 0.f}, q[4] = {1.f, 0.f, 0.f, 0.f};
     const int ca = IMG_I(body_chainadr)[b], cn = (b == 0) ? 0 : IMG_I(body_chainnum)[b];
@@ -942,14 +956,16 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
     for (int k = 0; k < 9; k++) xmat[9 * b + k] = R[k];
     float t[3], IR[9], IM[9];
     mat_vec(t, R, body_ipos + 3 * b);
-    xipos[3 * b] = p[0] + t[0]; xipos[3 * b + 1] = p[1] + t[1]; xipos[3 * b + 2] = p[2] + t[2];
+    r_xipos[0] = p[0] + t[0]; r_xipos[1] = p[1] + t[1]; r_xipos[2] = p[2] + t[2];
+    xipos[3 * b] = r_xipos[0]; xipos[3 * b + 1] = r_xipos[1]; xipos[3 * b + 2] = r_xipos[2];
     quat2mat(IR, body_iquat + 4 * b);
     mat_mul(IM, R, IR);
 #pragma unroll
-    for (int k = 0; k < 9; k++) ximat[9 * b + k] = IM[k];
+    for (int k = 0; k < 9; k++) ximat[9 * b + k] = r_ximat[k] = IM[k];
   }
   wsync();
 
+  PROF(27);
   // geoms (all written out; collision geoms kept in LDS) and sites
   for (int g = tid; g < m.ngeom; g += NT) {
     const int b = IMG_I(geom_bodyid)[g];
@@ -970,6 +986,7 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
       for (int k = 0; k < 9; k++) cgmat[9 * slot + k] = GM[k];
     }
   }
+  PROF(28);
   for (int s = tid; s < m.nsite; s += NT) {
     const int b = IMG_I(site_bodyid)[s];
     float t[3], SR[9], SM[9];
@@ -983,30 +1000,37 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
 
   // ---------------------------------------------------------------- com_pos
   PROF(1);
-  // subtree com: lane b sums the bodies whose chain contains b
-  for (int b = tid; b < nb; b += NT) {
-    float ms = 0.f, mp[3] = {0.f, 0.f, 0.f};
+  const unsigned long long* tmk = reinterpret_cast<const unsigned long long*>(IMG_L(body_treemask));
+  const unsigned long long* dmk = reinterpret_cast<const unsigned long long*>(IMG_L(body_dofmask));
+  // subtree com: lane b sums the bodies k whose chain contains b (ascending k)
+  float r_sc[3];
+  {
+    const float bm = bl ? body_mass[tid] : 0.f;
+    float ms = 0.f, mp0 = 0.f, mp1 = 0.f, mp2 = 0.f;
     for (int k = 0; k < nb; k++) {
-      const bool in = (b == 0) || ((unsigned long long)IMG_L(body_treemask)[k] >> b) & 1ull;
-      if (!in) continue;
-      const float mk = body_mass[k];
-      ms += mk;
-      mp[0] += mk * xipos[3 * k]; mp[1] += mk * xipos[3 * k + 1]; mp[2] += mk * xipos[3 * k + 2];
+      const float mk = rl(bm, k), x0 = rl(r_xipos[0], k), x1 = rl(r_xipos[1], k), x2 = rl(r_xipos[2], k);
+      if (tid == 0 || ((tmk[k] >> tid) & 1ull)) {
+        ms += mk;
+        mp0 += mk * x0; mp1 += mk * x1; mp2 += mk * x2;
+      }
     }
     if (ms < MJH_MINVAL) {
-      subtree_com[3 * b] = xipos[3 * b]; subtree_com[3 * b + 1] = xipos[3 * b + 1]; subtree_com[3 * b + 2] = xipos[3 * b + 2];
+      r_sc[0] = r_xipos[0]; r_sc[1] = r_xipos[1]; r_sc[2] = r_xipos[2];
     } else {
       const float inv = 1.f / ms;
-      subtree_com[3 * b] = mp[0] * inv; subtree_com[3 * b + 1] = mp[1] * inv; subtree_com[3 * b + 2] = mp[2] * inv;
+      r_sc[0] = mp0 * inv; r_sc[1] = mp1 * inv; r_sc[2] = mp2 * inv;
     }
+    if (bl) { subtree_com[3 * tid] = r_sc[0]; subtree_com[3 * tid + 1] = r_sc[1]; subtree_com[3 * tid + 2] = r_sc[2]; }
   }
-  wsync();
-  for (int b = tid; b < nb; b += NT) {
-    float* ci = cinert + 10 * b;
-    const float* R = ximat + 9 * b;
-    const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
-    const float dd0 = xipos[3 * b] - c[0], dd1 = xipos[3 * b + 1] - c[1], dd2 = xipos[3 * b + 2] - c[2];
-    const float* in = body_inertia + 3 * b;
+  // cinert (lane b), about the subtree com of b's root body
+  float r_cin[10];
+  {
+    const int rt = bl ? IMG_I(body_rootid)[tid] : 0;
+    const float c0 = shfl(r_sc[0], rt), c1 = shfl(r_sc[1], rt), c2 = shfl(r_sc[2], rt);
+    const float* R = r_ximat;
+    const float dd0 = r_xipos[0] - c0, dd1 = r_xipos[1] - c1, dd2 = r_xipos[2] - c2;
+    const int bb = bl ? tid : 0;
+    const float* in = body_inertia + 3 * bb;
     float I[6];  // xx yy zz xy xz yz of R diag(in) R^T
     I[0] = R[0] * in[0] * R[0] + R[1] * in[1] * R[1] + R[2] * in[2] * R[2];
     I[1] = R[3] * in[0] * R[3] + R[4] * in[1] * R[4] + R[5] * in[2] * R[5];
@@ -1014,15 +1038,21 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
     I[3] = R[0] * in[0] * R[3] + R[1] * in[1] * R[4] + R[2] * in[2] * R[5];
     I[4] = R[0] * in[0] * R[6] + R[1] * in[1] * R[7] + R[2] * in[2] * R[8];
     I[5] = R[3] * in[0] * R[6] + R[4] * in[1] * R[7] + R[5] * in[2] * R[8];
-    const float mm = body_mass[b], dsq = dd0 * dd0 + dd1 * dd1 + dd2 * dd2;
-    ci[0] = I[0] + mm * (dsq - dd0 * dd0);
-    ci[1] = I[1] + mm * (dsq - dd1 * dd1);
-    ci[2] = I[2] + mm * (dsq - dd2 * dd2);
-    ci[3] = I[3] - mm * dd0 * dd1;
-    ci[4] = I[4] - mm * dd0 * dd2;
-    ci[5] = I[5] - mm * dd1 * dd2;
-    ci[6] = mm * dd0; ci[7] = mm * dd1; ci[8] = mm * dd2; ci[9] = mm;
+    const float mm = bl ? body_mass[bb] : 0.f, dsq = dd0 * dd0 + dd1 * dd1 + dd2 * dd2;
+    r_cin[0] = I[0] + mm * (dsq - dd0 * dd0);
+    r_cin[1] = I[1] + mm * (dsq - dd1 * dd1);
+    r_cin[2] = I[2] + mm * (dsq - dd2 * dd2);
+    r_cin[3] = I[3] - mm * dd0 * dd1;
+    r_cin[4] = I[4] - mm * dd0 * dd2;
+    r_cin[5] = I[5] - mm * dd1 * dd2;
+    r_cin[6] = mm * dd0; r_cin[7] = mm * dd1; r_cin[8] = mm * dd2; r_cin[9] = mm;
+    if (bl) {
+#pragma unroll
+      for (int c = 0; c < 10; c++) cinert[10 * tid + c] = r_cin[c];
+    }
   }
+  PROF(18);
+  wsync();  // subtree_com visible to the per-joint lanes
   for (int j = tid; j < nj; j += NT) {
     const int b = IMG_I(jnt_bodyid)[j], da = IMG_I(jnt_dofadr)[j];
     const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
@@ -1050,117 +1080,152 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
   }
   wsync();
 
+  PROF(19);
   // ---------------------------------------------------------------- crb + M
-  for (int b = tid; b < nb; b += NT) {
-    float acc[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (b > 0)
-      for (int k = b; k < nb; k++) {
-        if (!(((unsigned long long)IMG_L(body_treemask)[k] >> b) & 1ull)) continue;
+  // lane i's cdof row in registers
+  float r_cdof[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (tid < nv) {
 #pragma unroll
-        for (int c = 0; c < 10; c++) acc[c] += cinert[10 * k + c];
-      }
-#pragma unroll
-    for (int c = 0; c < 10; c++) crb[10 * b + c] = acc[c];
+    for (int c = 0; c < 6; c++) r_cdof[c] = cdof[6 * tid + c];
   }
-  for (int i = tid; i < nv * ldm; i += NT) Mm[i] = 0.f;
+  // crb (lane b) = sum of cinert over b's subtree, ascending k
+  float r_crb[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = 1; k < nb; k++) {
+    const bool in = tid > 0 && ((tmk[k] >> tid) & 1ull);
+#pragma unroll
+    for (int c = 0; c < 10; c++) {
+      const float x = rl(r_cin[c], k);
+      if (in) r_crb[c] += x;
+    }
+  }
+  PROF(20);
+  for (int i = tid; i < nv * ldm; i += NT) { Mm[i] = 0.f; Lm[i] = 0.f; }
   wsync();
-  for (int i = tid; i < nv; i += NT) {
-    float buf[6];
-    inert_vec(buf, crb + 10 * IMG_I(dof_bodyid)[i], cdof + 6 * i);
-    unsigned long long mask = (unsigned long long)IMG_L(body_dofmask)[IMG_I(dof_bodyid)[i]];
-    mask &= (i == 63) ? ~0ull : ((2ull << i) - 1ull);
-    while (mask) {
-      const int j = __builtin_ctzll(mask);
-      mask &= mask - 1;
-      const float* cj = cdof + 6 * j;
-      float s = cj[0] * buf[0] + cj[1] * buf[1] + cj[2] * buf[2] + cj[3] * buf[3] + cj[4] * buf[4] + cj[5] * buf[5];
-      if (j == i) s += dof_armature[i];
-      Mm[i * ldm + j] = s;
-      Mm[j * ldm + i] = s;  // full symmetric storage: contiguous row reads in M*v
+  {
+    // lane i: row/column i of M over the dofs j <= i of i's ancestor chain
+    const int bi = tid < nv ? IMG_I(dof_bodyid)[tid] : 0;
+    float cb[10], buf[6];
+#pragma unroll
+    for (int c = 0; c < 10; c++) cb[c] = shfl(r_crb[c], bi);
+    inert_vec(buf, cb, r_cdof);
+    unsigned long long mask = tid < nv ? dmk[bi] : 0ull;
+    mask &= (tid == 63) ? ~0ull : ((2ull << tid) - 1ull);
+    for (int j = 0; j < nv; j++) {
+      float cj[6];
+#pragma unroll
+      for (int c = 0; c < 6; c++) cj[c] = rl(r_cdof[c], j);
+      if ((mask >> j) & 1ull) {
+        float v = cj[0] * buf[0] + cj[1] * buf[1] + cj[2] * buf[2] + cj[3] * buf[3] + cj[4] * buf[4] + cj[5] * buf[5];
+        if (j == tid) v += dof_armature[tid];
+        Mm[tid * ldm + j] = v;
+        Mm[j * ldm + tid] = v;  // full symmetric storage: contiguous row reads in M*v
+        Lm[tid * ldm + j] = v;
+        Lm[j * ldm + tid] = v;
+      }
     }
   }
   wsync();
   PROF(10);
-  for (int i = tid; i < nv * ldm; i += NT) Lm[i] = Mm[i];
   ldl_factor_reg<NVP>(Lm, nv, ldm);
   PROF(2);
 
   // ---------------------------------------------------------------- com_vel / rne (bias)
-  for (int b = tid; b < nb; b += NT) {
-    float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    unsigned long long mask = (unsigned long long)IMG_L(body_dofmask)[b];
-    while (mask) {
-      const int j = __builtin_ctzll(mask);
-      mask &= mask - 1;
-      const float qv = qvel[j];
+  const float r_qv = tid < nv ? qvel[tid] : 0.f;
+  const unsigned long long r_dm = bl ? dmk[tid] : 0ull;
+  float r_cvel[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < nv; j++) {
+    const float q = rl(r_qv, j);
+    const bool in = (r_dm >> j) & 1ull;
 #pragma unroll
-      for (int c = 0; c < 6; c++) v[c] += cdof[6 * j + c] * qv;
+    for (int c = 0; c < 6; c++) {
+      const float x = rl(r_cdof[c], j);
+      if (in) r_cvel[c] += x * q;
     }
-#pragma unroll
-    for (int c = 0; c < 6; c++) cvel[6 * b + c] = v[c];
   }
-  wsync();
-  for (int i = tid; i < nv; i += NT) {
+  if (bl) {
+#pragma unroll
+    for (int c = 0; c < 6; c++) cvel[6 * tid + c] = r_cvel[c];
+  }
+  PROF(21);
+  // cdof_dot (lane i)
+  float r_cdd[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  {
+    const int i = tid < nv ? tid : 0;
     const int b = IMG_I(dof_bodyid)[i], jnt = IMG_I(dof_jntid)[i], da = IMG_I(jnt_dofadr)[jnt];
     const bool freej = IMG_I(jnt_type)[jnt] == 0;
-    if (freej && i - da < 3) {
-      for (int c = 0; c < 6; c++) cdof_dot[6 * i + c] = 0.f;
-      continue;
-    }
+    const int p = IMG_I(body_parentid)[b], d0 = IMG_I(body_dofadr)[b];
     float v[6];
-    const int p = IMG_I(body_parentid)[b];
 #pragma unroll
-    for (int c = 0; c < 6; c++) v[c] = cvel[6 * p + c];
+    for (int c = 0; c < 6; c++) v[c] = shfl(r_cvel[c], p);
     // earlier dofs of this body: other joints fully, own free joint translations only
-    for (int k = IMG_I(body_dofadr)[b]; k < i; k++) {
+    for (int k = 0; k < nv; k++) {
+      const float q = rl(r_qv, k);
       const int jk = IMG_I(dof_jntid)[k];
-      if (jk == jnt && !(freej && k - da < 3)) continue;
+      const bool use = k >= d0 && k < i && !(jk == jnt && !(freej && k - da < 3));
 #pragma unroll
-      for (int c = 0; c < 6; c++) v[c] += cdof[6 * k + c] * qvel[k];
+      for (int c = 0; c < 6; c++) {
+        const float x = rl(r_cdof[c], k);
+        if (use) v[c] += x * q;
+      }
     }
-    cross_motion(cdof_dot + 6 * i, v, cdof + 6 * i);
+    if (tid < nv && !(freej && i - da < 3)) cross_motion(r_cdd, v, r_cdof);
+    if (tid < nv) {
+#pragma unroll
+      for (int c = 0; c < 6; c++) cdof_dot[6 * tid + c] = r_cdd[c];
+    }
   }
-  wsync();
+  PROF(22);
+  // rne forward pass (lane b): bias acceleration and body forces
+  float r_cfrc[6];
   {
     const float g0 = -m.gravity_x, g1 = -m.gravity_y, g2 = -m.gravity_z;
-    for (int b = tid; b < nb; b += NT) {
-      float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
-      unsigned long long mask = (unsigned long long)IMG_L(body_dofmask)[b];
-      while (mask) {
-        const int j = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const float qv = qvel[j];
+    float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
+    for (int j = 0; j < nv; j++) {
+      const float q = rl(r_qv, j);
+      const bool in = (r_dm >> j) & 1ull;
 #pragma unroll
-        for (int c = 0; c < 6; c++) a[c] += cdof_dot[6 * j + c] * qv;
+      for (int c = 0; c < 6; c++) {
+        const float x = rl(r_cdd[c], j);
+        if (in) a[c] += x * q;
       }
-      float f1[6], f2[6], f3[6];
-      inert_vec(f1, cinert + 10 * b, a);
-      inert_vec(f2, cinert + 10 * b, cvel + 6 * b);
-      cross_force(f3, cvel + 6 * b, f2);
+    }
+    float f1[6], f2[6], f3[6];
+    inert_vec(f1, r_cin, a);
+    inert_vec(f2, r_cin, r_cvel);
+    cross_force(f3, r_cvel, f2);
 #pragma unroll
-      for (int c = 0; c < 6; c++) cfrc[6 * b + c] = (b == 0) ? 0.f : f1[c] + f3[c];
+    for (int c = 0; c < 6; c++) r_cfrc[c] = (tid == 0) ? 0.f : f1[c] + f3[c];
+  }
+  PROF(23);
+  // subtree sums of cfrc (lane b), ascending k
+  float r_bf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = 1; k < nb; k++) {
+    const bool in = tid > 0 && ((tmk[k] >> tid) & 1ull);
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+      const float x = rl(r_cfrc[c], k);
+      if (in) r_bf[c] += x;
     }
   }
-  wsync();
-  // subtree sums of cfrc into crb (crb no longer needed)
-  for (int b = tid; b < nb; b += NT) {
-    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (b > 0)
-      for (int k = b; k < nb; k++) {
-        if (!(((unsigned long long)IMG_L(body_treemask)[k] >> b) & 1ull)) continue;
+  if (bl) {
 #pragma unroll
-        for (int c = 0; c < 6; c++) acc[c] += cfrc[6 * k + c];
-      }
+    for (int c = 0; c < 6; c++) cfrc[6 * tid + c] = r_cfrc[c];
+  }
+  {
+    const int bi = tid < nv ? IMG_I(dof_bodyid)[tid] : 0;
+    float f[6];
 #pragma unroll
-    for (int c = 0; c < 6; c++) crb[6 * b + c] = acc[c];
+    for (int c = 0; c < 6; c++) f[c] = shfl(r_bf[c], bi);
+    if (tid < nv) {
+      const float* cd = r_cdof;
+      qfrc_bias[tid] = cd[0] * f[0] + cd[1] * f[1] + cd[2] * f[2] + cd[3] * f[3] + cd[4] * f[4] + cd[5] * f[5];
+    }
   }
   wsync();
 
+  PROF(24);
   // ---------------------------------------------------------------- passive, actuation, smooth force
   for (int i = tid; i < nv; i += NT) {
-    const float* cd = cdof + 6 * i;
-    const float* f = crb + 6 * IMG_I(dof_bodyid)[i];
-    qfrc_bias[i] = cd[0] * f[0] + cd[1] * f[1] + cd[2] * f[2] + cd[3] * f[3] + cd[4] * f[4] + cd[5] * f[5];
     float pas = -dof_damping[i] * qvel[i];
     const int jnt = IMG_I(dof_jntid)[i];
     const int t = IMG_I(jnt_type)[jnt];
@@ -1218,6 +1283,7 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
       qacc_smooth[i] = s;
     }
   }
+  PROF(25);
   ldl_solve_reg<NVP>(Lm, nv, ldm, qacc_smooth);
   PROF(3);
 
@@ -1652,19 +1718,29 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
   // ---------------------------------------------------------------- post-constraint acceleration (cacc)
   PROF(6);
   {
+    // lane b: sum over the dofs j of b's chain (ascending), lane j's rows via readlane
     const float g0 = -m.gravity_x, g1 = -m.gravity_y, g2 = -m.gravity_z;
-    for (int b = tid; b < nb; b += NT) {
-      float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
-      unsigned long long mask = (unsigned long long)IMG_L(body_dofmask)[b];
-      while (mask) {
-        const int j = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const float qv = qvel[j], qa = qacc[j];
+    float cd[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, cdd[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float qv_l = 0.f, qa_l = 0.f;
+    if (tid < nv) {
 #pragma unroll
-        for (int c = 0; c < 6; c++) a[c] += cdof_dot[6 * j + c] * qv + cdof[6 * j + c] * qa;
+      for (int c = 0; c < 6; c++) { cd[c] = cdof[6 * tid + c]; cdd[c] = cdof_dot[6 * tid + c]; }
+      qv_l = qvel[tid]; qa_l = qacc[tid];
+    }
+    const unsigned long long dm = bl ? dmk[tid] : 0ull;
+    float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
+    for (int j = 0; j < nv; j++) {
+      const float qv = rl(qv_l, j), qa = rl(qa_l, j);
+      const bool in = (dm >> j) & 1ull;
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        const float x = rl(cdd[c], j), y = rl(cd[c], j);
+        if (in) a[c] += x * qv + y * qa;
       }
+    }
+    if (bl) {
 #pragma unroll
-      for (int c = 0; c < 6; c++) cacc[6 * b + c] = a[c];
+      for (int c = 0; c < 6; c++) cacc[6 * tid + c] = a[c];
     }
   }
   wsync();
@@ -1777,7 +1853,63 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
         wsync();
         continue;
       }
-      if (tid != 0) continue;
+      if (type != 35 && type != 36) continue;
+      // subtree linvel / angmom: lanes over bodies, wave reductions
+      const unsigned long long* tmask = (const unsigned long long*)IMG_L(body_treemask);
+      auto in_tree = [&](int b) { return id == 0 || ((tmask[b] >> id) & 1ull); };
+      float msum = 0.f, l0 = 0.f, l1 = 0.f, l2 = 0.f;
+      for (int b = 1 + tid; b < nb; b += NT) {
+        if (!in_tree(b)) continue;
+        const float bm = cinert[10 * b + 9];
+        const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
+        const float* v = cvel + 6 * b;
+        float dif[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
+        cross3(t, dif, v);
+        msum += bm;
+        l0 += bm * (v[3] - t[0]); l1 += bm * (v[4] - t[1]); l2 += bm * (v[5] - t[2]);
+      }
+      bsum2<NT>(msum, l0, red);
+      bsum2<NT>(l1, l2, red);
+      float vc[3] = {0.f, 0.f, 0.f};
+      if (msum > MJH_MINVAL) { vc[0] = l0 / msum; vc[1] = l1 / msum; vc[2] = l2 / msum; }
+      float* out = sd + adr;
+      float o3[3] = {vc[0], vc[1], vc[2]};
+      if (type == 36) {
+        float L0 = 0.f, L1 = 0.f, L2 = 0.f;
+        const float* sc = subtree_com + 3 * id;
+        for (int b = 1 + tid; b < nb; b += NT) {
+          if (!in_tree(b)) continue;
+          const float bm = cinert[10 * b + 9];
+          const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
+          const float* v = cvel + 6 * b;
+          float dd[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
+          cross3(t, dd, v);
+          float vb[3] = {v[3] - t[0], v[4] - t[1], v[5] - t[2]};
+          const float* ci = cinert + 10 * b;
+          const float dsq = dot3(dd, dd);
+          float I[9] = {ci[0] - bm * (dsq - dd[0] * dd[0]), ci[3] + bm * dd[0] * dd[1], ci[4] + bm * dd[0] * dd[2],
+                        ci[3] + bm * dd[0] * dd[1], ci[1] - bm * (dsq - dd[1] * dd[1]), ci[5] + bm * dd[1] * dd[2],
+                        ci[4] + bm * dd[0] * dd[2], ci[5] + bm * dd[1] * dd[2], ci[2] - bm * (dsq - dd[2] * dd[2])};
+          float Iw[3], dx[3], dv[3];
+          mat_vec(Iw, I, v);
+          for (int k = 0; k < 3; k++) { dx[k] = xipos[3 * b + k] - sc[k]; dv[k] = (vb[k] - vc[k]) * bm; }
+          cross3(t, dx, dv);
+          L0 += Iw[0] + t[0]; L1 += Iw[1] + t[1]; L2 += Iw[2] + t[2];
+        }
+        float z = 0.f;
+        bsum2<NT>(L0, L1, red);
+        bsum2<NT>(L2, z, red);
+        o3[0] = L0; o3[1] = L1; o3[2] = L2;
+      }
+      if (tid == 0) {
+        const float cut = IMG_F(sensor_cutoff)[s];
+        for (int k = 0; k < 3; k++) out[k] = cut > 0.f ? clampf(o3[k], -cut, cut) : o3[k];
+      }
+    }
+    // remaining sensors are independent and cheap: one lane each
+    for (int s = tid; s < m.nsensor; s += NT) {
+      const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
+      if (type == 40 || type == 35 || type == 36) continue;
       float* out = sd + adr;
       switch (type) {
         case 3: {  // gyro
@@ -1834,46 +1966,6 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
           if (q[0] < 0.f) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
           quat_normalize(q);
           out[0] = q[0]; out[1] = q[1]; out[2] = q[2]; out[3] = q[3];
-          break;
-        }
-        case 35:
-        case 36: {
-          float msum = 0.f, lin[3] = {0.f, 0.f, 0.f};
-          for (int b = 1; b < nb; b++) {
-            if (!(id == 0 || (((unsigned long long)IMG_L(body_treemask)[b] >> id) & 1ull))) continue;
-            const float bm = cinert[10 * b + 9];
-            const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
-            const float* v = cvel + 6 * b;
-            float dif[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
-            cross3(t, dif, v);
-            msum += bm;
-            lin[0] += bm * (v[3] - t[0]); lin[1] += bm * (v[4] - t[1]); lin[2] += bm * (v[5] - t[2]);
-          }
-          float vc[3] = {0.f, 0.f, 0.f};
-          if (msum > MJH_MINVAL) { vc[0] = lin[0] / msum; vc[1] = lin[1] / msum; vc[2] = lin[2] / msum; }
-          if (type == 35) { out[0] = vc[0]; out[1] = vc[1]; out[2] = vc[2]; break; }
-          float L[3] = {0.f, 0.f, 0.f};
-          const float* sc = subtree_com + 3 * id;
-          for (int b = 1; b < nb; b++) {
-            if (!(id == 0 || (((unsigned long long)IMG_L(body_treemask)[b] >> id) & 1ull))) continue;
-            const float bm = cinert[10 * b + 9];
-            const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
-            const float* v = cvel + 6 * b;
-            float dd[3] = {xipos[3 * b] - c[0], xipos[3 * b + 1] - c[1], xipos[3 * b + 2] - c[2]}, t[3];
-            cross3(t, dd, v);
-            float vb[3] = {v[3] - t[0], v[4] - t[1], v[5] - t[2]};
-            const float* ci = cinert + 10 * b;
-            const float dsq = dot3(dd, dd);
-            float I[9] = {ci[0] - bm * (dsq - dd[0] * dd[0]), ci[3] + bm * dd[0] * dd[1], ci[4] + bm * dd[0] * dd[2],
-                          ci[3] + bm * dd[0] * dd[1], ci[1] - bm * (dsq - dd[1] * dd[1]), ci[5] + bm * dd[1] * dd[2],
-                          ci[4] + bm * dd[0] * dd[2], ci[5] + bm * dd[1] * dd[2], ci[2] - bm * (dsq - dd[2] * dd[2])};
-            float Iw[3], dx[3], dv[3];
-            mat_vec(Iw, I, v);
-            for (int k = 0; k < 3; k++) { dx[k] = xipos[3 * b + k] - sc[k]; dv[k] = (vb[k] - vc[k]) * bm; }
-            cross3(t, dx, dv);
-            L[0] += Iw[0] + t[0]; L[1] += Iw[1] + t[1]; L[2] += Iw[2] + t[2];
-          }
-          out[0] = L[0]; out[1] = L[1]; out[2] = L[2];
           break;
         }
         default:

@@ -211,3 +211,98 @@ def rew_feet(pos: torch.Tensor, vel: torch.Tensor, found, cmd: torch.Tensor, tar
     *[_ptr(t) if t is not None else None for t in outs], n, _stream()), "mjh_rew_feet")
   del z
   return cl if want == "clearance" else tuple(outs)
+
+
+# ---- rotations for resets and motion tracking --------------------------------
+def _rowsN(t: torch.Tensor, width: int) -> bool:
+  """(n, width) float32 rows on the GPU with unit last-dim stride (any row stride)."""
+  return t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.shape[1] == width and t.stride(1) == 1
+
+
+def _flat_rows(t: torch.Tensor, width: int):
+  """(..., width) -> (n, width) rows without a copy when possible, else None."""
+  if not (t.is_cuda and t.dtype == torch.float32 and t.shape[-1] == width and t.stride(-1) == 1):
+    return None
+  if t.dim() == 2:
+    return t
+  try:
+    return t.view(-1, width)
+  except RuntimeError:
+    return None
+
+
+def quat_from_euler_xyz(rpy: torch.Tensor) -> torch.Tensor:
+  """quat_from_euler_xyz(rpy[:, 0], rpy[:, 1], rpy[:, 2]) for (n, 3) rows."""
+  if not _rowsN(rpy, 3):
+    return M.quat_from_euler_xyz(rpy[:, 0], rpy[:, 1], rpy[:, 2])
+  n = rpy.shape[0]
+  out = torch.empty((n, 4), dtype=torch.float32, device=rpy.device)
+  native.check(native.lib().mjh_quat_from_euler(_ptr(rpy), rpy.stride(0), _ptr(out), n, _stream()), "mjh_quat_from_euler")
+  return out
+
+
+def quat_error_magnitude(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
+  a, b = _flat_rows(q1, 4), _flat_rows(q2, 4)
+  if a is None or b is None or q1.shape != q2.shape:
+    return M.quat_error_magnitude(q1, q2)
+  out = torch.empty(q1.shape[:-1], dtype=torch.float32, device=q1.device)
+  native.check(native.lib().mjh_quat_error(_ptr(a), a.stride(0), _ptr(b), b.stride(0), _ptr(out), a.shape[0], _stream()),
+               "mjh_quat_error")
+  return out
+
+
+def _env_rows(t: torch.Tensor, width: int):
+  """(N, width) or (N, k, width) float32 GPU tensor with unit last stride ->
+  (k, env stride, row stride), else None."""
+  if not (t.is_cuda and t.dtype == torch.float32 and t.shape[-1] == width and t.stride(-1) == 1):
+    return None
+  if t.dim() == 2:
+    return 1, t.stride(0), 0
+  if t.dim() == 3:
+    return t.shape[1], t.stride(0), t.stride(1)
+  return None
+
+
+def frame_subtract(t01, q01, t02, q02, want_t: bool = True, want_q: bool = True, qcols: int = 0):
+  """subtract_frame_transforms with (N, 3)/(N, 4) frames and (N, k, 3)/(N, k, 4)
+  or (N, 3)/(N, 4) targets. Returns (t12, q12), q12 optionally as the first
+  `qcols` columns of its rotation matrix, flattened per target row."""
+  et, eq = _env_rows(t02, 3), _env_rows(q02, 4)
+  ok = _rowsN(t01, 3) and _rowsN(q01, 4) and et is not None and eq is not None and et[0] == eq[0]
+  if not ok or t02.shape[:-1] != q02.shape[:-1] or t01.shape[0] != t02.shape[0]:
+    k = t02.shape[1] if t02.dim() == 3 else 1
+    if t02.dim() == 3:
+      t01, q01 = t01[:, None, :].expand(-1, k, -1), q01[:, None, :].expand(-1, k, -1)
+    t12, q12 = M.subtract_frame_transforms(t01, q01, t02, q02)
+    if qcols:
+      q12 = M.matrix_from_quat(q12)[..., :qcols].reshape(*q12.shape[:-1], 3 * qcols)
+    return (t12 if want_t else None), (q12 if want_q else None)
+  k = et[0]
+  n = t02.shape[0] * k
+  t12 = torch.empty((*t02.shape[:-1], 3), dtype=torch.float32, device=t02.device) if want_t else None
+  qw = 3 * qcols if qcols else 4
+  q12 = torch.empty((*q02.shape[:-1], qw), dtype=torch.float32, device=q02.device) if want_q else None
+  native.check(native.lib().mjh_frame_subtract(
+    _ptr(t01), t01.stride(0), _ptr(q01), q01.stride(0), _ptr(t02), et[1], et[2], _ptr(q02), eq[1], eq[2], k,
+    _ptr(t12) if t12 is not None else None, _ptr(q12) if q12 is not None else None, qcols, n, _stream()),
+    "mjh_frame_subtract")
+  return t12, q12
+
+
+def motion_relative(anchor_pos, anchor_quat, robot_anchor_pos, robot_anchor_quat, body_pos, body_quat, out_pos, out_quat) -> bool:
+  """MotionCommand's anchor-relative targets into out_pos (N, k, 3) / out_quat (N, k, 4);
+  False when the layout is not supported (caller runs the torch formulas)."""
+  ep, eq = _env_rows(body_pos, 3), _env_rows(body_quat, 4)
+  if ep is None or eq is None or ep[0] != eq[0] or body_pos.dim() != 3:
+    return False
+  if not all(_rowsN(t, w) for t, w in ((anchor_pos, 3), (anchor_quat, 4), (robot_anchor_pos, 3), (robot_anchor_quat, 4))):
+    return False
+  if not (out_pos.is_contiguous() and out_quat.is_contiguous() and out_pos.shape == body_pos.shape):
+    return False
+  k = ep[0]
+  native.check(native.lib().mjh_motion_relative(
+    _ptr(anchor_pos), anchor_pos.stride(0), _ptr(anchor_quat), anchor_quat.stride(0), _ptr(robot_anchor_pos),
+    robot_anchor_pos.stride(0), _ptr(robot_anchor_quat), robot_anchor_quat.stride(0), _ptr(body_pos), ep[1], ep[2],
+    _ptr(body_quat), eq[1], eq[2], k, _ptr(out_pos), _ptr(out_quat), body_pos.shape[0] * k, _stream()),
+    "mjh_motion_relative")
+  return True

@@ -15,8 +15,8 @@ import torch
 
 from mjlab_amd.managers.manager_base import as_mask
 from mjlab_amd.managers.scene_entity_config import SceneEntityCfg
+from mjlab_amd import envops
 from mjlab_amd.envops import quat_mul
-from mjlab_amd.utils.math import quat_from_euler_xyz
 
 _DEFAULT = SceneEntityCfg("robot")
 _AXES6 = ["x", "y", "z", "roll", "pitch", "yaw"]
@@ -64,7 +64,7 @@ def reset_root_state_uniform(env, env_ids, pose_range: dict, velocity_range: dic
   if pose is None:
     pose = torch.zeros(n, 6, device=env.device)
   pos = rs[:, 0:3] + pose[:, 0:3] + env.scene.env_origins
-  quat = quat_mul(rs[:, 3:7], quat_from_euler_xyz(pose[:, 3], pose[:, 4], pose[:, 5]))
+  quat = quat_mul(rs[:, 3:7], envops.quat_from_euler_xyz(pose[:, 3:6]))
   vlo, vhi = _ranges6(env, velocity_range)
   dv = _uniform6(env, n, velocity_range, vlo, vhi)
   vel = rs[:, 7:13] if dv is None else rs[:, 7:13] + dv

@@ -63,10 +63,14 @@ class RewardManager:
   def compute(self, dt: float) -> torch.Tensor:
     """sum_i term_i * weight_i * dt (reward_manager.py:76-88); zero-weight terms
     are skipped and report 0, as in the reference."""
-    vals = [
-      tcfg.func(self._env, **tcfg.params).float() if tcfg.weight != 0.0 else None
-      for tcfg in self._term_cfgs
-    ]
+    self._env.__dict__["_command_active_cache"] = {}  # shared command-activity masks, this pass only
+    try:
+      vals = [
+        tcfg.func(self._env, **tcfg.params).float() if tcfg.weight != 0.0 else None
+        for tcfg in self._term_cfgs
+      ]
+    finally:
+      self._env.__dict__.pop("_command_active_cache", None)
     zero = None
     for i, v in enumerate(vals):
       if v is None:

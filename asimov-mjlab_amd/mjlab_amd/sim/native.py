@@ -49,6 +49,10 @@ EXPORTS = (
   "mjh_rew_posture",
   "mjh_rew_feet",
   "mjh_velocity_command",
+  "mjh_quat_from_euler",
+  "mjh_quat_error",
+  "mjh_frame_subtract",
+  "mjh_motion_relative",
 )
 
 
@@ -100,6 +104,10 @@ def lib() -> ctypes.CDLL:
   L.mjh_velocity_command.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, cf, cf, cf, cf, cf, cf, cf, ci, vp, vp, vp, vp, vp,
                                      vp, vp, vp, vp, ll, vp]
   L.mjh_rew_feet.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, cf, cf, cf, ci, vp, vp, vp, vp, ll, vp]
+  L.mjh_quat_from_euler.argtypes = [vp, ll, vp, ll, vp]
+  L.mjh_quat_error.argtypes = [vp, ll, vp, ll, vp, ll, vp]
+  L.mjh_frame_subtract.argtypes = [vp, ll, vp, ll, vp, ll, ll, vp, ll, ll, ci, vp, vp, ci, ll, vp]
+  L.mjh_motion_relative.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, ll, vp, ll, ll, ci, vp, vp, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

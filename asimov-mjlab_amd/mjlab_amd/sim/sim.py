@@ -204,6 +204,7 @@ class Simulation:
     if not hasattr(self, "_order"):
       self._order = torch.arange(self.num_envs, dtype=torch.int64, device=self.device)
       self._order_keys = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+      self._order_cost = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
     ds.world_order = self._order.data_ptr() if self.cfg.balance_worlds else None
     for name, t in self._data_flat.items():
       setattr(ds, name, t.data_ptr())
@@ -306,7 +307,11 @@ class Simulation:
 
   def _refresh_order(self) -> None:
     if self.cfg.balance_worlds and self.num_envs > 1:
-      torch.sort(self.data.nefc, stable=False, out=(self._order_keys, self._order))
+      # expected cost of a world ~ (solver iterations + 2) x constraint rows of
+      # its previous step; most expensive first (longest-processing-time order)
+      torch.add(self.data.solver_niter.view(-1), 2, out=self._order_cost)
+      self._order_cost.mul_(self.data.nefc.view(-1))
+      torch.sort(self._order_cost, descending=True, stable=False, out=(self._order_keys, self._order))
 
   def _launch_step(self) -> None:
     self._refresh_order()

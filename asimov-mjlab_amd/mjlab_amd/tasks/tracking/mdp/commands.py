@@ -34,7 +34,8 @@ from mjlab_amd import envops
 from mjlab_amd.managers.command_manager import CommandTerm
 from mjlab_amd.managers.manager_term_config import CommandTermCfg
 from mjlab_amd.motion import load_motion
-from mjlab_amd.utils.math import quat_error_magnitude, quat_from_euler_xyz, quat_inv, yaw_quat
+from mjlab_amd.envops import quat_error_magnitude
+from mjlab_amd.utils.math import quat_inv, yaw_quat
 
 _AXES6 = ("x", "y", "z", "roll", "pitch", "yaw")
 
@@ -278,7 +279,7 @@ class MotionCommand(CommandTerm):
     if self._pose_any:
       r = torch.rand(n, 6, device=self.device) * (self._pose_hi - self._pose_lo) + self._pose_lo
       root_pos = root_pos + r[:, 0:3]
-      root_ori = envops.quat_mul(quat_from_euler_xyz(r[:, 3], r[:, 4], r[:, 5]), root_ori)
+      root_ori = envops.quat_mul(envops.quat_from_euler_xyz(r[:, 3:6]), root_ori)
     if self._vel_any:
       r = torch.rand(n, 6, device=self.device) * (self._vel_hi - self._vel_lo) + self._vel_lo
       root_lin_vel = root_lin_vel + r[:, 0:3]
@@ -299,11 +300,18 @@ class MotionCommand(CommandTerm):
 
     anchor_pos = self.anchor_pos_w
     robot_anchor_pos = self.robot_anchor_pos_w
+    if envops.motion_relative(anchor_pos, self.anchor_quat_w, robot_anchor_pos, self.robot_anchor_quat_w, self.body_pos_w,
+                              self.body_quat_w, self.body_pos_relative_w, self.body_quat_relative_w):
+      self._adaptive_update()
+      return
     delta_pos = torch.cat([robot_anchor_pos[:, 0:2], anchor_pos[:, 2:3]], dim=-1)
     delta_ori = yaw_quat(envops.quat_mul(self.robot_anchor_quat_w, quat_inv(self.anchor_quat_w)))
     self.body_quat_relative_w.copy_(_qmul(delta_ori[:, None, :], self.body_quat_w))
     self.body_pos_relative_w.copy_(delta_pos[:, None, :] + _qapply(delta_ori[:, None, :], self.body_pos_w - anchor_pos[:, None, :]))
 
+    self._adaptive_update()
+
+  def _adaptive_update(self) -> None:
     if self.cfg.sampling_mode == "adaptive":
       a = self.cfg.adaptive_alpha
       self.bin_failed_count.mul_(1 - a).add_(a * self._current_bin_failed)

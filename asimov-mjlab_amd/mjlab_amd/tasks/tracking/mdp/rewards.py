@@ -5,7 +5,7 @@ from __future__ import annotations
 
 import torch
 
-from mjlab_amd.utils.math import quat_error_magnitude
+from mjlab_amd.envops import quat_error_magnitude
 
 
 def _get_body_indexes(command, body_names: tuple[str, ...] | None):

@@ -17,13 +17,23 @@ _DEFAULT = SceneEntityCfg("robot")
 
 
 def _command_active(env, command_name, threshold) -> torch.Tensor | None:
+  """(|cmd_xy| + |cmd_yaw| > threshold) as float. The command does not change
+  while rewards are computed, so terms sharing (command, threshold) share one
+  evaluation per reward pass (the reward manager clears the cache)."""
   if command_name is None:
     return None
   command = env.command_manager.get_command(command_name)
   if command is None:
     return None
-  total = torch.norm(command[:, :2], dim=1) + torch.abs(command[:, 2])
-  return (total > threshold).float()
+  cache = env.__dict__.get("_command_active_cache")  # present only during a reward pass
+  key = (command_name, float(threshold))
+  v = cache.get(key) if cache is not None else None
+  if v is None:
+    total = torch.norm(command[:, :2], dim=1) + torch.abs(command[:, 2])
+    v = (total > threshold).float()
+    if cache is not None:
+      cache[key] = v
+  return v
 
 
 def track_linear_velocity(env, std: float, command_name: str, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
@@ -176,6 +186,11 @@ class variable_posture:
     del std_standing, std_walking, std_running
     a = env.scene[asset_cfg.name]
     command = env.command_manager.get_command(command_name)
+    if isinstance(asset_cfg.joint_idx, slice) and asset_cfg.joint_idx == slice(None):
+      fused = envops.rew_posture(a.data.joint_pos, self.default_joint_pos, self.std_standing, self.std_walking,
+                                 self.std_running, command, walking_threshold, running_threshold)
+      if fused is not None:
+        return fused
     total = torch.norm(command[:, :2], dim=1) + torch.abs(command[:, 2])
     standing = (total < walking_threshold).float()
     walking = ((total >= walking_threshold) & (total < running_threshold)).float()
@@ -185,10 +200,5 @@ class variable_posture:
       + self.std_walking * walking.unsqueeze(1)
       + self.std_running * running.unsqueeze(1)
     )
-    if isinstance(asset_cfg.joint_idx, slice) and asset_cfg.joint_idx == slice(None):
-      fused = envops.rew_posture(a.data.joint_pos, self.default_joint_pos, self.std_standing, self.std_walking,
-                                 self.std_running, command, walking_threshold, running_threshold)
-      if fused is not None:
-        return fused
     err = torch.square(a.data.joint_pos[:, asset_cfg.joint_idx] - self.default_joint_pos[:, asset_cfg.joint_idx])
     return torch.exp(-torch.mean(err / (std**2), dim=1))

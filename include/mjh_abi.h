@@ -195,6 +195,32 @@ int mjh_velocity_command(const float* lin_b, long long ls, const float* ang_b, l
                          unsigned char* is_heading, unsigned char* is_standing, float* time_left, long long* counter,
                          float* err_xy, float* err_yaw, long long n, void* stream);
 
+/* ---- rotations for resets and motion tracking (mjh_envops.hip) ----
+ * Formulas of isaaclab/utils/math.py as restated in mjlab_amd/utils/math.py. */
+
+/* out[i] = quat_from_euler_xyz(rpy[i][0], rpy[i][1], rpy[i][2]) (math.py quat_from_euler_xyz;
+ * used by events.py:45-84 reset_root_state_uniform and tracking/mdp/commands.py:332). */
+int mjh_quat_from_euler(const float* rpy, long long rs, float* out, long long n, void* stream);
+
+/* out[i] = |axis_angle(q1[i] (x) conj(q2[i]))| (quat_error_magnitude, used by
+ * tracking/mdp/rewards.py:33-40 and commands.py:227-242). */
+int mjh_quat_error(const float* q1, long long s1, const float* q2, long long s2, float* out, long long n, void* stream);
+
+/* subtract_frame_transforms (math.py) for n = envs x k target rows: frame e = i / k
+ * (row stride s*), target j = i % k at e * s + j * r (env stride s, row stride r):
+ * t12[i] = quat_apply(q01^-1, t02 - t01), q12[i] = q01^-1 (x) q02; either output may
+ * be NULL; qcols > 0 writes the first qcols columns of matrix_from_quat(q12)
+ * row-major instead of q12 (tracking/mdp/observations.py:18-69). */
+int mjh_frame_subtract(const float* t01, long long st01, const float* q01, long long sq01, const float* t02,
+                       long long st02, long long rt02, const float* q02, long long sq02, long long rq02, int k,
+                       float* t12, float* q12, int qcols, long long n, void* stream);
+
+/* MotionCommand anchor-relative body targets (tracking/mdp/commands.py:383-405)
+ * for n = envs x k body rows (body arrays: env stride s*, row stride r*). */
+int mjh_motion_relative(const float* ap, long long sap, const float* aq, long long saq, const float* rp, long long srp,
+                        const float* rq, long long srq, const float* bp, long long sbp, long long rbp, const float* bq,
+                        long long sbq, long long rbq, int k, float* out_p, float* out_q, long long n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

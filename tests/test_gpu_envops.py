@@ -160,3 +160,39 @@ def test_fused_velocity_command_matches_torch():
     torch.testing.assert_close(fused[f], getattr(term, f), rtol=1e-5, atol=1e-5, msg=f)
   for k in fm:
     torch.testing.assert_close(fm[k], term.metrics[k], rtol=1e-5, atol=1e-5, msg=k)
+
+
+def test_rotation_kernels_match_torch():
+  """quat_from_euler_xyz, quat_error_magnitude, subtract_frame_transforms (+ matrix
+  columns) and the MotionCommand relative targets vs the torch formulas."""
+  g = torch.Generator(device=DEV).manual_seed(3)
+  n, k = 1024, 14
+  draws = torch.rand(n, 6, device=DEV, generator=g) * 2 - 1  # strided rpy view
+  rpy = draws[:, 3:6]
+  torch.testing.assert_close(envops.quat_from_euler_xyz(rpy), M.quat_from_euler_xyz(rpy[:, 0], rpy[:, 1], rpy[:, 2]),
+                             rtol=1e-6, atol=1e-6)
+  q1, q2 = _q(n * k, g).view(n, k, 4), _q(n * k, g).view(n, k, 4)
+  q2[:5] = q1[:5]  # zero error: the small-angle branch
+  torch.testing.assert_close(envops.quat_error_magnitude(q1, q2), M.quat_error_magnitude(q1, q2), rtol=1e-5, atol=1e-5)
+  frame = torch.randn(n, 32, 7, device=DEV, generator=g)  # strided (env, body) layout like body_link_pose
+  frame[..., 3:7] = _q(n * 32, g).view(n, 32, 4)
+  t01, q01 = frame[:, 5, 0:3], frame[:, 5, 3:7]
+  t02, q02 = frame[:, 8:8 + k, 0:3], frame[:, 8:8 + k, 3:7]
+  t_ref, q_ref = M.subtract_frame_transforms(t01[:, None].expand(-1, k, -1), q01[:, None].expand(-1, k, -1), t02, q02)
+  t12, q12 = envops.frame_subtract(t01, q01, t02, q02)
+  torch.testing.assert_close(t12, t_ref, rtol=1e-5, atol=1e-5)
+  torch.testing.assert_close(q12, q_ref, rtol=1e-5, atol=1e-5)
+  _, m12 = envops.frame_subtract(t01, q01, t02, q02, want_t=False, qcols=2)
+  torch.testing.assert_close(m12, M.matrix_from_quat(q_ref)[..., :2].reshape(n, k, 6), rtol=1e-5, atol=1e-5)
+  t1, _ = envops.frame_subtract(t01, q01, frame[:, 9, 0:3], frame[:, 9, 3:7], want_q=False)  # one target per env
+  torch.testing.assert_close(t1, t_ref[:, 1], rtol=1e-5, atol=1e-5)
+  # motion-relative targets (commands.py:383-405)
+  ap, aq, rp, rq = frame[:, 1, 0:3], frame[:, 1, 3:7], frame[:, 2, 0:3], frame[:, 2, 3:7]
+  bp, bq = frame[:, 10:10 + k, 0:3], frame[:, 10:10 + k, 3:7]
+  op, oq = torch.empty(n, k, 3, device=DEV), torch.empty(n, k, 4, device=DEV)
+  assert envops.motion_relative(ap, aq, rp, rq, bp, bq, op, oq)
+  dpos = rp[:, None].repeat(1, k, 1).clone()
+  dpos[..., 2] = ap[:, None, 2]
+  dori = M.yaw_quat(M.quat_mul(rq[:, None].repeat(1, k, 1), M.quat_inv(aq[:, None].repeat(1, k, 1))))
+  torch.testing.assert_close(oq, M.quat_mul(dori, bq.contiguous()), rtol=1e-5, atol=1e-5)
+  torch.testing.assert_close(op, dpos + M.quat_apply(dori, bp - ap[:, None]), rtol=1e-5, atol=1e-5)

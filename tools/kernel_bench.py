@@ -20,7 +20,8 @@ from tests.scenes import g1_scene_model, random_states
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 launches = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 m = g1_scene_model(n)
-sim = Simulation(n, SimulationCfg(nconmax=50, njmax=300, mujoco=MujocoCfg(timestep=0.005, iterations=10, ls_iterations=20)), m, "cuda:0")
+sim = Simulation(n, SimulationCfg(nconmax=50, njmax=300, balance_worlds=os.environ.get("BALANCE") == "1",
+                                 mujoco=MujocoCfg(timestep=0.005, iterations=10, ls_iterations=20)), m, "cuda:0")
 st = random_states(m, n, np.random.default_rng(0), drop=0.03)
 for k, v in st.items():
   t = getattr(sim.data, k)

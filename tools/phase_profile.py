@@ -50,6 +50,19 @@ for i, n in enumerate(NAMES):
 print(f"  solver: linesearch {p[:,12].mean():.0f}  update {p[:,13].mean():.0f}  newton_dir {p[:,14].mean():.0f}")
 print(f"    newton_dir parts: hessian {p[:,15].mean():.0f}  factor {p[:,16].mean():.0f}  solve {p[:,17].mean():.0f}")
 print(f"  M factor alone: {(p[:,2]-p[:,10]).mean():.0f}  (com/crb/M before it: {(p[:,10]-p[:,1]).mean():.0f})")
+def seg(a, b):
+  return (p[:, b] - p[:, a]).mean()
+print(f"  kinematics: bodies {seg(0,27):.0f} geoms {seg(27,28):.0f} sites {seg(28,1):.0f}")
+print(f"  com: subtree+cinert {seg(1,18):.0f} cdof {seg(18,19):.0f} crb {seg(19,20):.0f} M-fill {seg(20,10):.0f} factor {seg(10,2):.0f}")
+print(f"  rne: cvel {seg(2,21):.0f} cdof_dot {seg(21,22):.0f} rne {seg(22,23):.0f} cfrc-sum+bias {seg(23,24):.0f} "
+      f"passive/act/smooth {seg(24,25):.0f} qacc_smooth solve {seg(25,3):.0f}")
 niter = sim.data.solver_niter.cpu().numpy()
 nefc = sim.data.nefc.cpu().numpy()
+wg = tot[: (N // 8) * 8].reshape(-1, 8)
+print(f"  workgroup (8 worlds) max/mean: {wg.max(1).mean():.0f} / {tot.mean():.0f}; "
+      f"p50 {np.percentile(tot, 50):.0f} p90 {np.percentile(tot, 90):.0f} p99 {np.percentile(tot, 99):.0f}")
+for nm, x in (("nefc", nefc), ("niter", niter)):
+  print(f"  corr(total, {nm}) = {np.corrcoef(tot, x.reshape(-1).astype(np.float64))[0, 1]:.2f}")
+srt = np.sort(tot)[: (N // 8) * 8].reshape(-1, 8)
+print(f"  if sorted by true cost: workgroup max mean {srt.max(1).mean():.0f}")
 print(f"  niter mean {niter.mean():.2f}  nefc mean {nefc.mean():.1f}  ncon mean {sim.data.ncon.float().mean().item():.1f}")
