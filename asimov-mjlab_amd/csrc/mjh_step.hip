@@ -419,19 +419,25 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
       v[b] = (b < nb && c < n) ? J[r * ldj + c] * sc : 0.f;
     }
   };
-  float v[4];
-  load(kq, v);
-  for (int k0 = 0; k0 < nact; k0 += 4) {
-    float vn[4];
-    load(k0 + 4 + kq, vn);
-    int t = 0;
+  // PF k-steps of J loads in flight (a ring unrolled by PF so every register
+  // index is static); same k order as a plain loop, so the sums are unchanged
+  constexpr int PF = 4;
+  float v[PF][4];
 #pragma unroll
-    for (int I = 0; I < 4; I++)
+  for (int s = 0; s < PF; s++) load(4 * s + kq, v[s]);
+  for (int k0 = 0; k0 < nact; k0 += 4 * PF) {
 #pragma unroll
-      for (int Jb = 0; Jb <= I; Jb++, t++)
-        if (I < nb) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[I], v[Jb], acc[t], 0, 0, 0);
+    for (int s = 0; s < PF; s++) {
+      if (k0 + 4 * s < nact) {
+        int t = 0;
 #pragma unroll
-    for (int b = 0; b < 4; b++) v[b] = vn[b];
+        for (int I = 0; I < 4; I++)
+#pragma unroll
+          for (int Jb = 0; Jb <= I; Jb++, t++)
+            if (I < nb) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[s][I], v[s][Jb], acc[t], 0, 0, 0);
+      }
+      if (k0 + 4 * (s + PF) < nact) load(k0 + 4 * (s + PF) + kq, v[s]);
+    }
   }
   int t = 0;
 #pragma unroll
@@ -1541,7 +1547,7 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
 
   // ---------------------------------------------------------------- Newton solver
   const float scale = 1.f / (m.meaninertia * (float)(nv > 1 ? nv : 1));
-  int niter = 0;
+  int niter = 0, nfactor_total = 0;
   if (nefc == 0) {
     for (int i = tid; i < nv; i += NT) {
       qacc[i] = qacc_smooth[i];
@@ -1568,9 +1574,23 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
       for (int i = tid; i < nv; i += NT) c += 0.5f * (Ma[i] - qfrc_smooth[i]) * (qacc[i] - qacc_smooth[i]);
       wsync();
       for (int i = tid; i < nv; i += NT) {
-        // J^T f: entries outside a row's dof mask are exact zeros, so no test
+        // J^T f: entries outside a row's dof mask are exact zeros, so no test.
+        // 16 rows of J loads in flight per round; accumulator k takes rows r = k
+        // mod 4 in increasing order (as a plain 4-way unrolled loop)
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
         int r = 0;
+        for (; r + 16 <= nefc; r += 16) {
+          float jj[16];
+#pragma unroll
+          for (int q = 0; q < 16; q++) jj[q] = J[(r + q) * ldj + i];
+#pragma unroll
+          for (int q = 0; q < 16; q += 4) {
+            s0 += jj[q] * efc_force[r + q];
+            s1 += jj[q + 1] * efc_force[r + q + 1];
+            s2 += jj[q + 2] * efc_force[r + q + 2];
+            s3 += jj[q + 3] * efc_force[r + q + 3];
+          }
+        }
         for (; r + 4 <= nefc; r += 4) {
           s0 += J[r * ldj + i] * efc_force[r];
           s1 += J[(r + 1) * ldj + i] * efc_force[r + 1];
@@ -1615,6 +1635,7 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
         for (int k = tid; k < nact; k += NT) arow_prev[k] = arow[k];
         nact_prev = nact;
         nfactor++;
+        nfactor_total++;
       }
       for (int i = tid; i < nv; i += NT) search[i] = grad[i];
       unsigned long long ts = PROF_NOW();
@@ -1717,6 +1738,9 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
 
   // ---------------------------------------------------------------- post-constraint acceleration (cacc)
   PROF(6);
+#ifdef MJH_PROFILE
+  if (tid == 0 && g_prof) g_prof[(long long)w * 32 + 29] = (unsigned long long)nfactor_total;
+#endif
   {
     // lane b: sum over the dofs j of b's chain (ascending), lane j's rows via readlane
     const float g0 = -m.gravity_x, g1 = -m.gravity_y, g2 = -m.gravity_z;

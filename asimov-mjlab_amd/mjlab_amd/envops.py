@@ -105,7 +105,7 @@ def obs_term(x: torch.Tensor, out: torch.Tensor, u: torch.Tensor | None, lo: flo
   if not (x.is_cuda and out.is_cuda and x.dtype == torch.float32):
     return False
   if x.dim() == 1:
-    x2 = x.view(-1, 1)
+    x2 = x.unsqueeze(1)  # (n, 1) with strides (s, 1)
   elif x.dim() == 2:
     x2 = x
   else:
@@ -305,4 +305,69 @@ def motion_relative(anchor_pos, anchor_quat, robot_anchor_pos, robot_anchor_quat
     robot_anchor_pos.stride(0), _ptr(robot_anchor_quat), robot_anchor_quat.stride(0), _ptr(body_pos), ep[1], ep[2],
     _ptr(body_quat), eq[1], eq[2], k, _ptr(out_pos), _ptr(out_quat), body_pos.shape[0] * k, _stream()),
     "mjh_motion_relative")
+  return True
+
+
+# ---- manager-level fusion (csrc/mjh_mgr.hip) -------------------------------------
+MAX_TERMS = 32
+
+
+class ObsTermDesc(ctypes.Structure):
+  """mjh_obs_term_desc (include/mjh_abi.h)."""
+  _fields_ = [("x", ctypes.c_void_p), ("xs", ctypes.c_longlong), ("w", ctypes.c_int), ("off", ctypes.c_int),
+              ("lo", ctypes.c_float), ("hi", ctypes.c_float), ("cmin", ctypes.c_float), ("cmax", ctypes.c_float),
+              ("scale", ctypes.c_float), ("noise", ctypes.c_int)]
+
+
+def _term_rows(x: torch.Tensor):
+  """(n,) or (n, w) float32 GPU rows with unit column stride -> (tensor, w), else None."""
+  if not (x.is_cuda and x.dtype == torch.float32):
+    return None
+  if x.dim() == 1:
+    x = x.unsqueeze(1)  # (n, 1) with strides (s, 1)
+  if x.dim() != 2 or (x.shape[1] > 1 and x.stride(1) != 1):
+    return None
+  return x, x.shape[1]
+
+
+def obs_group(xs: list, plan: list, u: torch.Tensor | None, out: torch.Tensor) -> bool:
+  """All terms of a concatenated observation group in one launch.
+  plan[i] = (tcfg, off, w, noise (lo, hi) | None, clip | None, scale)."""
+  if len(xs) > MAX_TERMS or not out.is_cuda or out.stride(1) != 1 or (u is not None and u.stride(1) != 1):
+    return False
+  n = out.shape[0]
+  descs = (ObsTermDesc * len(xs))()
+  for i, (x, (_, off, w, noise, clip, scale)) in enumerate(zip(xs, plan)):
+    r = _term_rows(x)
+    if r is None or r[1] != w or r[0].shape[0] != n:
+      return False
+    x2 = r[0]
+    cmin, cmax = (float(clip[0]), float(clip[1])) if clip else (1.0, -1.0)
+    lo, hi = noise if noise is not None else (0.0, 0.0)
+    descs[i] = ObsTermDesc(x2.data_ptr(), x2.stride(0), w, off, float(lo), float(hi), cmin, cmax, float(scale),
+                           int(noise is not None))
+  native.check(native.lib().mjh_obs_group(descs, len(xs), _ptr(u) if u is not None else None,
+                                          u.stride(0) if u is not None else 0, _ptr(out), out.stride(0), n, _stream()),
+               "mjh_obs_group")
+  return True
+
+
+def reward_combine(vals: list, weights: torch.Tensor, dt: float, reward: torch.Tensor, step_reward: torch.Tensor,
+                   sums: torch.Tensor) -> bool:
+  """RewardManager's weight/accumulate/sum over term vectors (None = weight-0 term) in one launch."""
+  T = len(vals)
+  if T > MAX_TERMS or not (reward.is_cuda and reward.is_contiguous() and step_reward.is_contiguous() and sums.is_contiguous()):
+    return False
+  n = reward.shape[0]
+  ptrs = (ctypes.c_void_p * max(T, 1))()
+  strides = (ctypes.c_longlong * max(T, 1))()
+  for i, v in enumerate(vals):
+    if v is None:
+      continue
+    if not (v.is_cuda and v.dtype == torch.float32 and v.dim() == 1 and v.shape[0] == n):
+      return False
+    ptrs[i] = v.data_ptr()
+    strides[i] = v.stride(0)
+  native.check(native.lib().mjh_reward_combine(ptrs, strides, T, _ptr(weights), float(dt), _ptr(reward),
+                                               _ptr(step_reward), _ptr(sums), n, _stream()), "mjh_reward_combine")
   return True

@@ -152,10 +152,12 @@ class ObservationManager:
     n = self._env.num_envs
     out = torch.empty((n, width), device=self._env.device)
     u = torch.rand((n, width), device=self._env.device) if any(p[3] is not None for p in plan) else None
-    for tcfg, off, w, noise, clip, scale in plan:
-      x = tcfg.func(self._env, **tcfg.params)
+    xs = [tcfg.func(self._env, **tcfg.params).float() for tcfg, *_ in plan]
+    if envops.obs_group(xs, plan, u, out):  # the whole group in one launch
+      return out
+    for x, (tcfg, off, w, noise, clip, scale) in zip(xs, plan):
       lo, hi = noise if noise is not None else (0.0, 0.0)
       uu = u[:, off : off + w] if noise is not None else None
-      if not envops.obs_term(x.float(), out[:, off : off + w], uu, lo, hi, clip, scale):
+      if not envops.obs_term(x, out[:, off : off + w], uu, lo, hi, clip, scale):
         return None
     return out

@@ -53,6 +53,8 @@ EXPORTS = (
   "mjh_quat_error",
   "mjh_frame_subtract",
   "mjh_motion_relative",
+  "mjh_obs_group",
+  "mjh_reward_combine",
 )
 
 
@@ -108,6 +110,8 @@ def lib() -> ctypes.CDLL:
   L.mjh_quat_error.argtypes = [vp, ll, vp, ll, vp, ll, vp]
   L.mjh_frame_subtract.argtypes = [vp, ll, vp, ll, vp, ll, ll, vp, ll, ll, ci, vp, vp, ci, ll, vp]
   L.mjh_motion_relative.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, ll, vp, ll, ll, ci, vp, vp, ll, vp]
+  L.mjh_obs_group.argtypes = [vp, ci, vp, ll, vp, ll, ll, vp]
+  L.mjh_reward_combine.argtypes = [vp, vp, ci, vp, cf, vp, vp, vp, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

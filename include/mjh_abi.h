@@ -221,6 +221,33 @@ int mjh_motion_relative(const float* ap, long long sap, const float* aq, long lo
                         const float* rq, long long srq, const float* bp, long long sbp, long long rbp, const float* bq,
                         long long sbq, long long rbq, int k, float* out_p, float* out_q, long long n, void* stream);
 
+/* ---- manager-level fusion (mjh_mgr.hip) ---- */
+#define MJH_MAX_TERMS 32
+
+/* One observation term of a concatenated group: its (n, w) input rows (row
+ * stride xs floats) land in columns [off, off + w) of the group buffer after
+ * noise (U[0,1) draws u[:, off + j] mapped to [lo, hi), when noise != 0),
+ * clipping (skipped when cmin > cmax) and scaling. */
+typedef struct mjh_obs_term_desc {
+  const float* x;
+  long long xs;
+  int w;
+  int off;
+  float lo, hi, cmin, cmax, scale;
+  int noise;
+} mjh_obs_term_desc;
+
+/* ObservationManager.compute for one concatenated group in one launch
+ * (observation_manager.py:156-195); terms are read from host memory at call time. */
+int mjh_obs_group(const mjh_obs_term_desc* terms, int nterms, const float* u, long long us, float* out, long long os,
+                  long long n, void* stream);
+
+/* RewardManager.compute's combination step (reward_manager.py:76-88) for nterms
+ * term vectors values[t] (row stride strides[t]; NULL = weight-0 term, value 0):
+ * step_reward[e, t] = v * w[t]; sums[e, t] += v * (w[t] * dt); reward[e] = sum_t. */
+int mjh_reward_combine(const float* const* values, const long long* strides, int nterms, const float* weights, float dt,
+                       float* reward, float* step_reward, float* sums, long long n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

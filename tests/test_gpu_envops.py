@@ -196,3 +196,39 @@ def test_rotation_kernels_match_torch():
   dori = M.yaw_quat(M.quat_mul(rq[:, None].repeat(1, k, 1), M.quat_inv(aq[:, None].repeat(1, k, 1))))
   torch.testing.assert_close(oq, M.quat_mul(dori, bq.contiguous()), rtol=1e-5, atol=1e-5)
   torch.testing.assert_close(op, dpos + M.quat_apply(dori, bp - ap[:, None]), rtol=1e-5, atol=1e-5)
+
+
+def test_reward_combine_matches_torch():
+  g = torch.Generator(device=DEV).manual_seed(4)
+  n, T = 777, 9
+  base = torch.randn(n, 2 * T, device=DEV, generator=g)
+  vals = [base[:, 2 * i] for i in range(T)]  # strided term vectors
+  vals[3] = None  # weight-0 term
+  w = torch.randn(T, device=DEV, generator=g)
+  w[3] = 0.0
+  dt = 0.02
+  sums0 = torch.randn(n, T, device=DEV, generator=g)
+  rew, step, sums = torch.empty(n, device=DEV), torch.empty(n, T, device=DEV), sums0.clone()
+  assert envops.reward_combine(vals, w, dt, rew, step, sums)
+  raw = torch.stack([v if v is not None else torch.zeros(n, device=DEV) for v in vals], 1)
+  weighted = raw * (w * dt)
+  torch.testing.assert_close(step, raw * w, rtol=1e-6, atol=1e-6)
+  torch.testing.assert_close(sums, sums0 + weighted, rtol=1e-6, atol=1e-6)
+  torch.testing.assert_close(rew, weighted.sum(1), rtol=1e-5, atol=1e-6)
+
+
+def test_obs_group_kernel_matches_per_term():
+  g = torch.Generator(device=DEV).manual_seed(5)
+  n = 513
+  a = torch.randn(n, 10, device=DEV, generator=g)
+  xs = [a[:, 0:3], a[:, 5], torch.randn(n, 7, device=DEV, generator=g)]
+  plan = [(None, 0, 3, (-0.5, 0.5), None, 0.25), (None, 3, 1, None, (-0.1, 0.1), 1.0), (None, 4, 7, (-1.0, 2.0), (-1.0, 1.0), 2.0)]
+  u = torch.rand(n, 11, device=DEV, generator=g)
+  out = torch.full((n, 11), float("nan"), device=DEV)
+  assert envops.obs_group(xs, plan, u, out)
+  ref = torch.cat([
+    (xs[0] + (u[:, 0:3] * 1.0 - 0.5)) * 0.25,
+    xs[1].view(-1, 1).clip(-0.1, 0.1),
+    (xs[2] + (u[:, 4:11] * 3.0 - 1.0)).clip(-1.0, 1.0) * 2.0,
+  ], 1)
+  torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)

@@ -11,6 +11,6 @@ for spec in "$@"; do
   [[ "$f" == *i* ]] && extra="$extra -DMJH_SOLVER_INLINE=__forceinline__"
   [[ "$f" == *c* ]] && extra="$extra -DMJH_COLL_INLINE=__forceinline__"
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude -DMJH_PRESET=$p -DMJH_WPB=$w $extra \
-    -o $out/libmjh_$spec.so asimov-mjlab_amd/csrc/mjh_step.hip asimov-mjlab_amd/csrc/mjh_envops.hip &
+    -o $out/libmjh_$spec.so asimov-mjlab_amd/csrc/mjh_step.hip asimov-mjlab_amd/csrc/mjh_envops.hip asimov-mjlab_amd/csrc/mjh_mdp.hip asimov-mjlab_amd/csrc/mjh_mgr.hip &
 done
 wait
