@@ -10,7 +10,7 @@ O=gpurun_out/$TAG
 mkdir -p $O
 t() { echo "[$(date +%T)] $*"; }
 t tests
-timeout -k 10 420 python -m pytest tests -m gpu -x -q > $O/gputests.log 2>&1 || { tail -30 $O/gputests.log; exit 1; }
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gputests.log 2>&1 || { tail -30 $O/gputests.log; exit 1; }
 tail -2 $O/gputests.log
 t breakdown
 timeout -k 10 240 python tools/env_breakdown.py > $O/eb.log 2>&1 || { tail -20 $O/eb.log; exit 1; }
