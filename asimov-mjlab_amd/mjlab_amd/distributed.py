@@ -21,12 +21,18 @@ def pack_step_outputs(obs: dict, reward: torch.Tensor, terminated: torch.Tensor,
 
 
 class StepGather:
-  """All-gathers each rank's packed step outputs into one (world * num_envs, D)
-  buffer (rank-major) — one collective per env step, no other data-path traffic."""
+  """Collects each rank's packed step outputs into one (world * num_envs, D)
+  buffer (rank-major) — one collective per env step, no other data-path traffic.
 
-  def __init__(self, group=None) -> None:
+  ``dst=None``: all-gather (every rank holds the full batch, the north star's
+  RCCL all-gather). ``dst=r``: gather to the learner rank ``r`` only (RCCL
+  gather: each rank sends its shard once; other ranks get ``None``)."""
+
+  def __init__(self, group=None, dst: int | None = None) -> None:
     self.group = group
+    self.dst = dst
     self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+    self.rank = dist.get_rank(group) if dist.is_initialized() else 0
     self.buf: torch.Tensor | None = None
 
   def __call__(self, obs, reward, terminated, truncated) -> torch.Tensor:
@@ -35,5 +41,11 @@ class StepGather:
       return packed
     if self.buf is None or self.buf.shape != (self.world * packed.shape[0], packed.shape[1]):
       self.buf = torch.empty((self.world * packed.shape[0], packed.shape[1]), dtype=packed.dtype, device=packed.device)
-    dist.all_gather_into_tensor(self.buf, packed.contiguous(), group=self.group)
-    return self.buf
+    if self.dst is None:
+      dist.all_gather_into_tensor(self.buf, packed.contiguous(), group=self.group)
+      return self.buf
+    if self.rank == self.dst:
+      dist.gather(packed.contiguous(), list(self.buf.chunk(self.world, dim=0)), dst=self.dst, group=self.group)
+      return self.buf
+    dist.gather(packed.contiguous(), None, dst=self.dst, group=self.group)
+    return None

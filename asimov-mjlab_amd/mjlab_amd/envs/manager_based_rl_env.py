@@ -173,6 +173,9 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     self.reward_buf = self.reward_manager._reward_buf
     self._any_reset = torch.zeros(1, dtype=torch.bool, device=self.device)
     self._env_step_t = torch.zeros((), dtype=torch.long, device=self.device)
+    # device counters [envs reset, env steps that ran the gated forward], accumulated
+    # inside the graph (no host sync); read with step_stats()
+    self._stats = torch.zeros(2, dtype=torch.long, device=self.device)
     self._action_in = torch.zeros(n, self.action_manager.total_action_dim, device=self.device)
     self.use_graph = (str(self.device).startswith("cuda") and torch.cuda.is_available()) if use_graph is None else use_graph
     self._graph: torch.cuda.CUDAGraph | None = None
@@ -271,6 +274,8 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     self._reset_idx(self.reset_buf)
     self.scene.write_data_to_sim()
     torch.any(self.reset_buf, dim=0, keepdim=True, out=self._any_reset)
+    self._stats[0] += self.reset_buf.sum()
+    self._stats[1:] += self._any_reset
     self.sim.forward_gated(self._any_reset)
     self.command_manager.compute(dt=self.step_dt)
     if "interval" in self.event_manager.available_modes:
@@ -302,6 +307,10 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     log.update(self.event_manager.reset(mask))
     log.update(self.termination_manager.reset(mask))
     self.episode_length_buf.masked_fill_(mask, 0)
+
+  def step_stats(self) -> torch.Tensor:
+    """Cumulative ``[envs reset, env steps whose gated forward ran]`` (device, long)."""
+    return self._stats
 
   def render(self):
     return None

@@ -87,6 +87,12 @@ class RslRlVecEnvWrapper:
     if self.clip_actions is not None:
       actions = torch.clamp(actions, -self.clip_actions, self.clip_actions)
     obs, rew, terminated, truncated, extras = self.env.step(actions)
+    # On the graph path the env returns its persistent graph buffers, which the
+    # next replay overwrites; rsl_rl keeps `obs` across env.step (act() stores
+    # it, process_env_step() copies it after the next step), so hand out fresh
+    # tensors as the reference's torch.cat does.
+    obs = {k: v.clone() for k, v in obs.items()}
+    rew = rew.clone()
     dones = (terminated | truncated).to(dtype=torch.long)
     if not self.cfg.is_finite_horizon:
       extras["time_outs"] = truncated

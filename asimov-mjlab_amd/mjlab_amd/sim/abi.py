@@ -60,7 +60,9 @@ def _ct(t: str, real):
 
 
 @lru_cache(maxsize=None)
-def model_struct(real=ctypes.c_float):
+def model_struct(real=ctypes.c_float, device: bool = True):
+  """ctypes mirror of ``mjh_model`` (device=True, float reals) or of the
+  oracle's ``or_model`` (device=False; float64 or float32 reals)."""
   members = []
   for f in fields():
     if f.kind == "MS":
@@ -74,20 +76,20 @@ def model_struct(real=ctypes.c_float):
       members.append((f.name, ctypes.c_void_p))
       members.append((f.name + "_wstride", ctypes.c_longlong))
   # MA and MW are interleaved in declaration order in C: MA list first, then MW list.
-  if real is ctypes.c_float:  # device descriptor: packed model-image scratch
+  if device:  # device descriptor: packed model-image scratch
     members += [("image", ctypes.c_void_p), ("image_words", ctypes.c_int), ("_pad_image", ctypes.c_int)]
-  return type("mjh_model" if real is ctypes.c_float else "or_model", (ctypes.Structure,), {"_fields_": members})
+  return type("mjh_model" if device else "or_model", (ctypes.Structure,), {"_fields_": members})
 
 
 @lru_cache(maxsize=None)
-def data_struct(real=ctypes.c_float):
+def data_struct(real=ctypes.c_float, device: bool = True):
   members = [("nworld", ctypes.c_int), ("_pad", ctypes.c_int)]
   for f in fields():
     if f.kind == "DA":
       members.append((f.name, ctypes.c_void_p))
-  if real is ctypes.c_float:  # device descriptor: per-world global scratch
+  if device:  # device descriptor: per-world global scratch
     members += [("scratch", ctypes.c_void_p), ("scratch_words", ctypes.c_longlong), ("world_order", ctypes.c_void_p)]
-  return type("mjh_data" if real is ctypes.c_float else "or_data", (ctypes.Structure,), {"_fields_": members})
+  return type("mjh_data" if device else "or_data", (ctypes.Structure,), {"_fields_": members})
 
 
 def size_names() -> list[str]:

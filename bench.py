@@ -2,18 +2,29 @@
 """Benchmark: env steps/s on Mjlab-Velocity-Flat-Unitree-G1 @ 4096 envs/GPU.
 
 Contract ("Measurement"):
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--num-envs E]
-One process per GPU (torch.distributed.run for N > 1, RCCL backend). Each rank
-owns its own 4096-env environment (seed 42 + rank) — worlds are independent, so
-the work shards with weak scaling; after every env step the ranks all-gather
-the learner-facing outputs (policy obs, critic obs, reward, terminated,
-truncated) over RCCL, the one exchange the north star names.
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--task T] [--num-envs E]
+One process per GPU. When started as a plain `python bench.py --gpus N` (N > 1),
+the script re-launches itself under `torch.distributed.run` with N ranks before
+touching the GPU (a child process, not an exec); when the driver launches it
+under torchrun it reads RANK / LOCAL_RANK / WORLD_SIZE and asserts
+WORLD_SIZE == --gpus. Each rank owns its own env shard (seed 42 + rank) —
+worlds are independent, so the work shards with weak scaling; after every env
+step the ranks all-gather the learner-facing outputs (policy obs, critic obs,
+reward, terminated, truncated) over RCCL, the one exchange the north star names.
 
 A "step" is one full env step of the manager-based RL env: action processing,
 4 physics sub-steps (the HIP step kernel), terminations, rewards, masked
 resets + gated forward, commands, push events and observations — captured in
 one HIP graph. Actions come from the random agent of the reference's
-`play --agent random` (2*U[0,1)-1, torch.Generator seeded 1234).
+`play --agent random` (2*U[0,1)-1, torch.Generator seeded 1234 + rank).
+
+Steady state. Episode lengths start uniformly random (rsl_rl's
+`init_at_random_ep_len=True`, which the reference's train.py:121 passes), and
+`--settle` untimed env steps (default 150) run before the W warmup steps, so
+the timed window sees the steady reset rate (and with it the forward pass that
+the reference runs over all worlds whenever any env resets,
+manager_based_rl_env.py:133-137) whatever --warmup the caller picks. The line
+reports resets per step and the fraction of timed steps that ran that forward.
 
 Rank 0 prints ONE JSON line with, in addition to the contract fields:
   roofline      — the dominant kernel (the fused physics step) measured live
@@ -21,8 +32,9 @@ Rank 0 prints ONE JSON line with, in addition to the contract fields:
                   (5,384 B per world per physics step) / average
                   launch duration, against the 8 TB/s HBM peak. `traffic` is the
                   PMC-measured HBM bytes per launch from profiles/ (or null).
-  cpu_baseline  — the CPU restatement (oracle/, float64, OpenMP over worlds) of
-                  the same physics step on this host's cores, bounded sample.
+  cpu_baseline  — the CPU restatement (oracle/, float64 and float32, OpenMP
+                  over worlds) of the same physics step on this host's cores,
+                  bounded sample of the live state.
 """
 
 from __future__ import annotations
@@ -30,6 +42,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -39,8 +53,11 @@ sys.path.insert(0, str(REPO / "asimov-mjlab_amd"))
 
 TASK = "Mjlab-Velocity-Flat-Unitree-G1"
 METRIC = "env steps/sec (whole node), Unitree G1 flat velocity task @ 4096 envs/GPU"
-B_PHYS_G1 = 5384  # algorithmic bytes per world per physics step
-B_PHYS = {"Unitree-Go1": 3040}  # other robots; default G1
+# per-task envs per GPU (BASELINE.json configs 2-4)
+DEFAULT_ENVS = {TASK: 4096, "Mjlab-Velocity-Flat-Unitree-Go1": 8192, "Mjlab-Tracking-Flat-Unitree-G1": 4096}
+# algorithmic bytes per world per physics step: G1 5,384 B, Go1 3,040 B
+B_PHYS = {"Unitree-Go1": 3040}
+B_PHYS_G1 = 5384
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
@@ -49,14 +66,28 @@ def parse() -> argparse.Namespace:
   p.add_argument("--gpus", type=int, default=1)
   p.add_argument("--steps", type=int, default=300)
   p.add_argument("--warmup", type=int, default=30)
-  p.add_argument("--num-envs", type=int, default=4096)
+  p.add_argument("--settle", type=int, default=150, help="untimed env steps before warmup (steady reset rate)")
+  p.add_argument("--num-envs", type=int, default=0, help="envs per GPU (default: the task's BASELINE config)")
   p.add_argument("--task", default=TASK)
   p.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL all-gather (N > 1)")
   p.add_argument("--no-cpu-baseline", action="store_true")
   p.add_argument("--cpu-sample-worlds", type=int, default=512)
+  p.add_argument("--cpu-seconds", type=float, default=8.0, help="per precision")
   p.add_argument("--kernel-launches", type=int, default=50)
   p.add_argument("--motion-file", default="", help="tracking tasks: motion npz (default: synthetic 500-frame clip)")
   return p.parse_args()
+
+
+def spawn_ranks(args) -> None:
+  """`python bench.py --gpus N` with no torchrun around it: run N ranks as a
+  child `torch.distributed.run` (before any GPU call) and exit with its code."""
+  with socket.socket() as s:
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+  cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+         "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *sys.argv[1:]]
+  env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+  sys.exit(subprocess.call(cmd, env=env))
 
 
 def synthetic_motion_file(dev: str, frames: int = 500) -> str:
@@ -80,8 +111,8 @@ def synthetic_motion_file(dev: str, frames: int = 500) -> str:
 
 
 def cpu_baseline(env, args) -> dict:
-  """Time the oracle (CPU restatement of the same physics step, float64,
-  OpenMP over worlds) on a bounded sample of this workload's worlds."""
+  """Time the oracle (CPU restatement of the same physics step, OpenMP over
+  worlds) on a bounded sample of this workload's worlds, float64 then float32."""
   sys.path.insert(0, str(REPO))
   from oracle.oracle import Oracle
 
@@ -92,82 +123,98 @@ def cpu_baseline(env, args) -> dict:
   cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
   n = min(args.cpu_sample_worlds, env.num_envs)
   d = env.sim.data
-  state = {k: getattr(d, k)[:n].detach().cpu().numpy() for k in ("qpos", "qvel", "act", "qacc_warmstart", "ctrl", "qfrc_applied", "xfrc_applied", "time")}
+  state0 = {k: getattr(d, k)[:n].detach().cpu().numpy() for k in ("qpos", "qvel", "act", "qacc_warmstart", "ctrl", "qfrc_applied", "xfrc_applied", "time")}
   overrides = {}
   m = env.sim.model
   for name in env.event_manager.domain_randomization_fields:
     overrides[name] = getattr(m, name)[:n].detach().cpu().numpy()
-  orc = Oracle(env.sim.mj_model, "f64", overrides=overrides)
-  orc.run(n, state, integrate=True, nthreads=cores)  # warm
-  reps, t0 = 0, time.perf_counter()
-  while True:
-    out = orc.run(n, state, integrate=True, nthreads=cores)
-    for k in ("qpos", "qvel", "qacc_warmstart", "time"):
-      state[k] = out[k]
-    reps += 1
-    el = time.perf_counter() - t0
-    if el > 10.0 or reps >= 20000:
-      break
-  phys_per_s = n * reps / el
   dec = env.cfg.decimation
+  res = {}
+  for prec in ("f64", "f32"):
+    state = {k: v.copy() for k, v in state0.items()}
+    orc = Oracle(env.sim.mj_model, prec, overrides=overrides)
+    orc.run(n, state, integrate=True, nthreads=cores)  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+      out = orc.run(n, state, integrate=True, nthreads=cores)
+      for k in ("qpos", "qvel", "qacc_warmstart", "time"):
+        state[k] = out[k]
+      reps += 1
+      el = time.perf_counter() - t0
+      if el > args.cpu_seconds or reps >= 20000:
+        break
+    res[prec] = (n * reps / el / dec, reps, el)
+  v64, r64, e64 = res["f64"]
+  v32, r32, e32 = res["f32"]
   return {
-    "value": phys_per_s / dec,
+    "value": v64,
     "unit": "env steps/sec (physics only: decimation x mj_step per env step)",
     "cores": cores,
     "kind": "port",
-    "sample": f"{n} {env.sim.mj_model.nv}-dof worlds x {reps} physics steps ({el:.1f} s) from the bench's live state, float64 oracle "
-    f"(oracle/oracle.c, OpenMP {cores} threads); env-layer cost excluded; MuJoCo C is not available",
+    "value_f32": v32,
+    "sample": f"{n} {env.sim.mj_model.nv}-dof worlds from the bench's live state, oracle/oracle.c with OpenMP {cores} threads: "
+    f"float64 {r64} physics steps ({e64:.1f} s) -> value; float32 {r32} steps ({e32:.1f} s) -> value_f32; "
+    "env-layer cost excluded; MuJoCo C is not available",
   }
 
 
 def main() -> None:
   args = parse()
+  if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    spawn_ranks(args)
   import torch
   import torch.distributed as dist
 
   world = int(os.environ.get("WORLD_SIZE", "1"))
   rank = int(os.environ.get("RANK", "0"))
   local = int(os.environ.get("LOCAL_RANK", "0"))
+  if world != args.gpus:
+    raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
   if world > 1:
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
   torch.cuda.set_device(local)
   dev = f"cuda:{local}"
+  num_envs = args.num_envs or DEFAULT_ENVS.get(args.task, 4096)
 
   from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
   from mjlab_amd.tasks import load_env_cfg
 
   cfg = load_env_cfg(args.task)
-  cfg.scene.num_envs = args.num_envs
+  cfg.scene.num_envs = num_envs
   motion = getattr(cfg, "commands", {}).get("motion") if isinstance(getattr(cfg, "commands", None), dict) else None
   if motion is not None and not motion.motion_file:
     motion.motion_file = args.motion_file or synthetic_motion_file(dev)
-  from mjlab_amd.distributed import shard_seed
+  from mjlab_amd.distributed import StepGather, shard_seed
 
   cfg.seed = shard_seed(42, rank)
   env = ManagerBasedRlEnv(cfg, device=dev)
   env.reset()
+  # rsl_rl OnPolicyRunner.learn(init_at_random_ep_len=True) (reference train.py:121)
+  g_ep = torch.Generator(device=dev)
+  g_ep.manual_seed(4321 + rank)
+  env.episode_length_buf.copy_(torch.randint(0, int(env.max_episode_length), (num_envs,), device=dev, generator=g_ep))
   gen = torch.Generator(device=dev)
   gen.manual_seed(1234 + rank)
-  act = torch.empty(env.num_envs, env.action_manager.total_action_dim, device=dev)
+  act = torch.empty(num_envs, env.action_manager.total_action_dim, device=dev)
 
   def agent():
     act.uniform_(0.0, 1.0, generator=gen)
     return act.mul_(2.0).sub_(1.0)
 
-  from mjlab_amd.distributed import StepGather
-
   gather = StepGather()
+  use_gather = world > 1 and not args.no_gather
 
   def exchange(obs, rew, term, trunc):
-    if world > 1 and not args.no_gather:
+    if use_gather:
       gather(obs, rew, term, trunc)
 
-  # graph capture happens on the 2nd step; these two setup steps are untimed
-  for _ in range(2 + args.warmup):
+  # graph capture happens on the 2nd step; settle + warmup steps are untimed
+  for _ in range(2 + args.settle + args.warmup):
     o, r, te, tr, _ = env.step(agent())
     exchange(o, r, te, tr)
   torch.cuda.synchronize()
+  stats0 = env.step_stats().clone()
   if world > 1:
     dist.barrier()
   torch.cuda.synchronize()
@@ -183,8 +230,22 @@ def main() -> None:
     t = torch.tensor([el], device=dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
-  n_total = args.num_envs * world
+  stats = (env.step_stats() - stats0).double().cpu()
+  resets_per_step = float(stats[0]) / args.steps
+  gate_rate = float(stats[1]) / args.steps
+  n_total = num_envs * world
   value = n_total * args.steps / el
+
+  # the per-step RCCL all-gather alone (same buffers), timed separately
+  gather_ms = None
+  if use_gather:
+    torch.cuda.synchronize()
+    dist.barrier()
+    tg = time.perf_counter()
+    for _ in range(args.steps):
+      exchange(o, r, te, tr)
+    torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - tg) / args.steps * 1e3
 
   # ---- dominant kernel: the fused physics step, HIP events on its stream ----
   sim = env.sim
@@ -201,14 +262,14 @@ def main() -> None:
   torch.cuda.synchronize()
   t_launch = e0.elapsed_time(e1) / 1e3 / L  # s per physics step (pack + step kernels)
   b_phys = next((v for k, v in B_PHYS.items() if k in args.task), B_PHYS_G1)
-  bytes_per_launch = b_phys * args.num_envs
+  bytes_per_launch = b_phys * num_envs
   achieved = bytes_per_launch / t_launch / 1e9
   traffic = None
   tf = REPO / "profiles" / "step_kernel_traffic.json"
   if tf.exists():
     try:
       tj = json.loads(tf.read_text())
-      if int(tj.get("num_envs", -1)) == args.num_envs:
+      if int(tj.get("num_envs", -1)) == num_envs and tj.get("task", TASK) == args.task:
         traffic = tj.get("bytes_per_launch")
     except (ValueError, OSError):
       traffic = None
@@ -224,7 +285,7 @@ def main() -> None:
 
   if rank == 0:
     line = {
-      "metric": METRIC if args.task == TASK else f"env steps/sec (whole node), {args.task} @ {args.num_envs} envs/GPU",
+      "metric": METRIC if (args.task == TASK and num_envs == 4096) else f"env steps/sec (whole node), {args.task} @ {num_envs} envs/GPU",
       "value": value,
       "unit": "env steps/s",
       "n_gpus": world,
@@ -235,14 +296,20 @@ def main() -> None:
       "scaling": "weak",
       "vs_baseline": None,
       "dtype": "f32",
-      "data": "synthetic: random agent 2*U[0,1)-1 (seed 1234+rank), env seed 42+rank, DR/pushes/resets/commands on"
+      "data": "synthetic: random agent 2*U[0,1)-1 (seed 1234+rank), env seed 42+rank, episode lengths start uniform "
+      "(init_at_random_ep_len), DR/pushes/resets/commands on"
       + ("; synthetic 500-frame motion clip (mjlab_amd.motion)" if motion is not None and not args.motion_file else ""),
       "config": {
-        "workload": f"{args.task}, num_envs={args.num_envs}/GPU, random agent",
-        "num_envs_per_gpu": args.num_envs,
+        "workload": f"{args.task}, num_envs={num_envs}/GPU, random agent",
+        "num_envs_per_gpu": num_envs,
         "decimation": env.cfg.decimation,
         "physics_steps_per_s": value * env.cfg.decimation,
-        "parallelism": f"env-sharded x{world}" + ("" if world == 1 or args.no_gather else " + RCCL all-gather of obs/reward/dones"),
+        "parallelism": f"env-sharded x{world}" + ("" if not use_gather else " + RCCL all-gather of obs/reward/dones"),
+        "world_size": world,
+        "settle_steps": args.settle,
+        "resets_per_step": resets_per_step,
+        "forward_gate_rate": gate_rate,
+        "gather_ms_per_step": gather_ms,
         "mean_nefc": nefc,
         "mean_solver_iters": niter,
       },
@@ -256,7 +323,7 @@ def main() -> None:
         "kernel": "step_kernel (+pack_kernel), one launch per physics step",
         "launch_us": t_launch * 1e6,
         "bytes_per_launch": bytes_per_launch,
-        "solver_streamed_model_gbs": b_solve * args.num_envs / t_launch / 1e9,
+        "solver_streamed_model_gbs": b_solve * num_envs / t_launch / 1e9,
       },
       "cpu_baseline": cpu,
     }

@@ -40,8 +40,8 @@ class Oracle:
     self.lib.oracle_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     self.lib.oracle_sizeof_model.restype = ctypes.c_size_t
     self.lib.oracle_sizeof_data.restype = ctypes.c_size_t
-    MS = abi.model_struct(self.real)
-    DS = abi.data_struct(self.real)
+    MS = abi.model_struct(self.real, device=False)
+    DS = abi.data_struct(self.real, device=False)
     assert ctypes.sizeof(MS) == self.lib.oracle_sizeof_model(), "oracle model struct layout mismatch"
     assert ctypes.sizeof(DS) == self.lib.oracle_sizeof_data(), "oracle data struct layout mismatch"
     self.sizes = abi.model_sizes(model)
@@ -69,7 +69,7 @@ class Oracle:
     self.ms = ms
 
   def run(self, nworld: int, state: dict, integrate: bool = True, nthreads: int = 1) -> dict:
-    DS = abi.data_struct(self.real)
+    DS = abi.data_struct(self.real, device=False)
     ds = DS()
     ds.nworld = nworld
     out = {}

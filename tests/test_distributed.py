@@ -29,6 +29,10 @@ def _worker(rank, world, port, q):
   term = torch.rand(n, generator=g) > 0.5
   trunc = torch.zeros(n, dtype=torch.bool)
   out = StepGather()(obs, rew, term, trunc)
+  to0 = StepGather(dst=0)(obs, rew, term, trunc)
+  assert (to0 is None) == (rank != 0)
+  if rank == 0:
+    assert torch.equal(to0, out)  # gather to the learner rank == all-gather there
   q.put((rank, out.clone(), pack_step_outputs(obs, rew, term, trunc)))
   dist.destroy_process_group()
 
@@ -61,3 +65,62 @@ def test_pack_layout():
   p = pack_step_outputs(obs, torch.tensor([5.0, 6.0]), torch.tensor([True, False]), torch.tensor([False, True]))
   assert p.shape == (2, 7)
   assert p[0].tolist() == [0.0, 1.0, 1.0, 1.0, 5.0, 1.0, 0.0]
+
+
+def _env_worker(rank, world, port, q):
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  torch.set_num_threads(1)
+  outs = _run_shard(rank, gather=True)
+  q.put((rank, outs))
+  dist.destroy_process_group()
+
+
+def _run_shard(rank, gather, n=3, steps=3):
+  """One rank's env shard (G1 velocity, seed 42 + rank, CPU oracle physics)."""
+  import sys
+  from pathlib import Path
+
+  sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+  from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
+  from mjlab_amd.tasks import load_env_cfg
+  from tests import oracle_sim
+
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = n
+  cfg.seed = shard_seed(42, rank)
+  env = ManagerBasedRlEnv(cfg, device="cpu")
+  oracle_sim.attach(env.sim, env.event_manager.domain_randomization_fields)
+  env.reset()
+  g = torch.Generator().manual_seed(1234 + rank)
+  sg = StepGather() if gather else None
+  outs = []
+  for _ in range(steps):
+    a = 2 * torch.rand(n, env.action_manager.total_action_dim, generator=g) - 1
+    obs, rew, term, trunc, _ = env.step(a)
+    own = pack_step_outputs(obs, rew, term, trunc).clone()
+    outs.append((own, sg(obs, rew, term, trunc).clone() if sg else None))
+  return outs
+
+
+def test_env_shards_world2_match_single_process():
+  """each rank's shard is bit-identical to a single-process run
+  with seed 42 + rank, and the all-gather returns the shards rank-major."""
+  world = 2
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  port = _free_port()
+  ps = [ctx.Process(target=_env_worker, args=(r, world, port, q)) for r in range(world)]
+  for p in ps:
+    p.start()
+  res = dict(q.get(timeout=300) for _ in range(world))
+  for p in ps:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  for r in range(world):
+    single = _run_shard(r, gather=False)
+    for t, (own, gathered) in enumerate(res[r]):
+      assert torch.equal(own, single[t][0]), (r, t)
+      full = torch.cat([res[k][t][0] for k in range(world)], dim=0)
+      assert torch.equal(gathered, full)

@@ -169,3 +169,19 @@ def test_pd_actuator_force_law():
     f = kp * c - kp * st["qpos"][0, qa] - kd * st["qvel"][0, va]
     flo, fhi = m.actuator_forcerange[i]
     assert out["actuator_force"][0, i] == pytest.approx(np.clip(f, flo, fhi), rel=1e-9, abs=1e-9)
+
+
+def test_oracle_struct_layouts_both_precisions():
+  """The ctypes mirrors of or_model/or_data match the compiled oracle in both
+  precisions (bench.py's cpu_baseline times float64 and float32)."""
+  import ctypes
+
+  from oracle.oracle import ORACLE_DIR, abi, build
+
+  build()
+  for prec, real in (("f64", ctypes.c_double), ("f32", ctypes.c_float)):
+    lib = ctypes.CDLL(str(ORACLE_DIR / f"liboracle_{prec}.so"))
+    lib.oracle_sizeof_model.restype = ctypes.c_size_t
+    lib.oracle_sizeof_data.restype = ctypes.c_size_t
+    assert ctypes.sizeof(abi.model_struct(real, device=False)) == lib.oracle_sizeof_model(), prec
+    assert ctypes.sizeof(abi.data_struct(real, device=False)) == lib.oracle_sizeof_data(), prec
