@@ -43,6 +43,7 @@ struct Layout {
   int con_pos, con_frame, con_dist, con_fric, con_solref, con_solimp, con_imargin, con_dim, con_geom, con_efcadr;
   int J, ldj, efc_D, efc_R, efc_aref, efc_jaref, efc_jv, efc_force, efc_fl, efc_pos, efc_type, efc_id, efc_mask;
   int efc_h, arow, ash, arow_prev;
+  int sidx;  // contact sensor: kept matches (contact index, ~index if flipped)
   int red, ints;
   int total, gtotal;  // per-world words: LDS, global scratch
   int ncap, rcap;
@@ -76,7 +77,7 @@ enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
   X(con_imargin, 1) X(con_dim, 1) X(con_geom, 1) X(con_efcadr, 1)                                     \
   X(J, 0) X(efc_D, 0) X(efc_R, 0) X(efc_aref, 0) X(efc_jaref, 0) X(efc_jv, 0) X(efc_force, 0)        \
   X(efc_fl, 0) X(efc_pos, 1) X(efc_type, 0) X(efc_id, 1) X(efc_mask, 1) X(efc_h, 0) X(arow, 0)       \
-  X(ash, 0) X(arow_prev, 1)
+  X(ash, 0) X(arow_prev, 1) X(sidx, 1)
 struct Rg {
 #if MJH_PRESET == 0
 #define X_RG(name, r) static constexpr bool name = false;
@@ -861,6 +862,7 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
   int* arow = SPI(arow);
   int* arow_prev = SPI(arow_prev);
   float* ash = SP(ash);
+  int* sidx = SPI(sidx);
   float* red = S + Lo.red;
   int* redi = SI + Lo.red + 2 * (NT / 64) + 2;
   int* ints = SI + Lo.ints;
@@ -1625,9 +1627,22 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
       if (diff == 0.f)
         for (int k = tid; k < nact; k += NT) diff += arow[k] != arow_prev[k] ? 1.f : 0.f;
       diff = bsum<NT>(diff, red);
+#ifdef MJH_DEBUG_ALWAYS_REBUILD
+      diff = 1.f;
+#endif
       if (diff != 0.f) {
         unsigned long long th = PROF_NOW();
+#ifdef MJH_DEBUG_PLAIN_HESSIAN
+        wsync();
+        for (int i = tid; i < nv; i += NT)
+          for (int j = 0; j <= i; j++) {
+            float hs = Mm[i * ldm + j];
+            for (int k = 0; k < nact; k++) hs += ash[k] * ash[k] * J[arow[k] * ldj + i] * J[arow[k] * ldj + j];
+            Lm[i * ldm + j] = hs;
+          }
+#else
         hessian_mfma<NT>(Mm, ldm, J, ldj, arow, ash, nact, nv, Lm);
+#endif
         PROF_ACC(15, th);
         unsigned long long tf = PROF_NOW();
         ldl_factor_reg<NVP>(Lm, nv, ldm);
@@ -1775,104 +1790,122 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
     for (int s = 0; s < m.nsensor; s++) {
       const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
       if (type == 40) {
-        // contact sensor: lanes over contacts
+        // contact sensor (MuJoCo mjSENS_CONTACT with mjlab's intprm encoding,
+        // contact_sensor.py:472-496): matches in contact order, capped at
+        // min(maxmatch, 64); then one lane per kept match.
         const int bits = IMG_I(sensor_intprm)[3 * s], reduce = IMG_I(sensor_intprm)[3 * s + 1], nslot = IMG_I(sensor_intprm)[3 * s + 2];
         const int otype = IMG_I(sensor_objtype)[s], rtype = IMG_I(sensor_reftype)[s], rid = IMG_I(sensor_refid)[s];
         const int dim = IMG_I(sensor_dim)[s];
+        const int cap = min(m.contact_sensor_maxmatch, 64);
         for (int k = tid; k < dim; k += NT) sd[adr + k] = 0.f;
-        wsync();
-        // match flags
-        float cnt = 0.f, fx = 0.f, fy = 0.f, fz = 0.f;
+        auto om = [&](int ty, int oid, int g) -> bool {
+          if (oid < 0) return true;
+          const int gb = IMG_I(geom_bodyid)[g];
+          if (ty == 5) return g == oid;
+          if (ty == 1) return gb == oid;
+          if (ty == 2) return oid == 0 || (((unsigned long long)IMG_L(body_treemask)[gb] >> oid) & 1ull);
+          return false;
+        };
+        int cnt = 0;
         for (int base = 0; base < ncon; base += NT) {
           const int ci = base + tid;
-          int match = 0;
-          float Fw[3] = {0.f, 0.f, 0.f};
+          int match = 0, flip = 0;
           if (ci < ncon) {
             const int g1 = con_geom[2 * ci], g2 = con_geom[2 * ci + 1];
-            auto om = [&](int ty, int oid, int g) -> bool {
-              if (oid < 0) return true;
-              const int gb = IMG_I(geom_bodyid)[g];
-              if (ty == 5) return g == oid;
-              if (ty == 1) return gb == oid;
-              if (ty == 2) return oid == 0 || (((unsigned long long)IMG_L(body_treemask)[gb] >> oid) & 1ull);
-              return false;
-            };
-            int flip = 0;
             if (om(otype, id, g1) && om(rtype, rid, g2)) match = 1;
             else if (om(otype, id, g2) && om(rtype, rid, g1)) { match = 1; flip = 1; }
-            if (match) {
-              const int r0 = con_efcadr[ci];
-              float F[3] = {0.f, 0.f, 0.f};
-              if (r0 >= 0) {
-                const int cdm = con_dim[ci];
-                if (cdm == 1) {
-                  F[0] = efc_force[r0];
-                } else {
-                  for (int e = 0; e < 2 * (cdm - 1); e++) F[0] += efc_force[r0 + e];
-                  for (int k = 1; k < 3 && k < cdm; k++) F[k] = con_fric[5 * ci + k - 1] * (efc_force[r0 + 2 * k - 2] - efc_force[r0 + 2 * k - 1]);
-                }
-              }
-              const float* fr = con_frame + 9 * ci;
-              const float sgn = flip ? 1.f : -1.f;
-              for (int a = 0; a < 3; a++) Fw[a] = sgn * (F[0] * fr[a] + F[1] * fr[3 + a] + F[2] * fr[6 + a]);
-              // non-netforce, single slot, reduce none: first match in contact order
-              if (reduce != 3) {
-                // slot fill handled below by the first matching lane (serialised)
-              }
-            }
           }
           int total;
           const int off = bscan<NT>(match, &total, redi);
-          if (reduce != 3 && match && off < nslot) {
-            // "none"/"mindist"/"maxforce" with the first nslot matches in contact order
-            // (mindist/maxforce reordering applied below for nslot == 1)
-            const int slot = (int)cnt + off;
-            if (slot < nslot) {
-              const int width = dim / nslot;
-              float* o = sd + adr + slot * width;
-              const int r0 = con_efcadr[ci];
-              float F[3] = {0.f, 0.f, 0.f};
-              if (r0 >= 0) {
-                const int cdm = con_dim[ci];
-                if (cdm == 1) F[0] = efc_force[r0];
-                else {
-                  for (int e = 0; e < 2 * (cdm - 1); e++) F[0] += efc_force[r0 + e];
-                  for (int k = 1; k < 3 && k < cdm; k++) F[k] = con_fric[5 * ci + k - 1] * (efc_force[r0 + 2 * k - 2] - efc_force[r0 + 2 * k - 1]);
-                }
-              }
-              int q = 0;
-              if (bits & 1) o[q++] = -1.f;  // patched with the total below
-              if (bits & 2) { o[q++] = F[0]; o[q++] = F[1]; o[q++] = F[2]; }
-              if (bits & 4) { o[q++] = 0.f; o[q++] = 0.f; o[q++] = 0.f; }
-              if (bits & 8) o[q++] = con_dist[ci];
-              if (bits & 16) { o[q++] = con_pos[3 * ci]; o[q++] = con_pos[3 * ci + 1]; o[q++] = con_pos[3 * ci + 2]; }
-              const float* fr = con_frame + 9 * ci;
-              const int g1 = con_geom[2 * ci];
-              const bool flipped = !(otype == 5 ? g1 == id : (otype == 1 ? IMG_I(geom_bodyid)[g1] == id
-                                        : (id == 0 || (((unsigned long long)IMG_L(body_treemask)[IMG_I(geom_bodyid)[g1]] >> id) & 1ull))));
-              const float sg = flipped ? -1.f : 1.f;
-              if (bits & 32) { o[q++] = sg * fr[0]; o[q++] = sg * fr[1]; o[q++] = sg * fr[2]; }
-              if (bits & 64) { o[q++] = sg * fr[3]; o[q++] = sg * fr[4]; o[q++] = sg * fr[5]; }
+          if (match && cnt + off < cap) sidx[cnt + off] = flip ? ~ci : ci;
+          cnt += total;
+        }
+        wsync();
+        const int nm = min(cnt, cap);
+        if (nm == 0) continue;
+        // lane k < nm: match k. F = contact force/torque in the contact frame
+        // (mj_contactForce for pyramidal cones), Fw/Tw = on the primary, world frame
+        const bool own = tid < nm;
+        const int code = own ? sidx[tid] : 0;
+        const int ci = code < 0 ? ~code : code;
+        const float sgn = code < 0 ? 1.f : -1.f;
+        float F[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, Fw[3] = {0.f, 0.f, 0.f}, Tw[3] = {0.f, 0.f, 0.f};
+        float cpos[3] = {0.f, 0.f, 0.f}, cdist = 0.f;
+        const float* fr = con_frame + 9 * ci;
+        if (own) {
+          const int r0 = con_efcadr[ci];
+          if (r0 >= 0) {
+            const int cdm = con_dim[ci];
+            if (cdm == 1) {
+              F[0] = efc_force[r0];
+            } else {
+              for (int e = 0; e < 2 * (cdm - 1); e++) F[0] += efc_force[r0 + e];
+              for (int k = 1; k < cdm && k < 6; k++) F[k] = con_fric[5 * ci + k - 1] * (efc_force[r0 + 2 * k - 2] - efc_force[r0 + 2 * k - 1]);
             }
           }
-          cnt += (float)total;
-          fx += Fw[0]; fy += Fw[1]; fz += Fw[2];
-          wsync();
-        }
-        float sx = fx, sy = fy;
-        bsum2<NT>(sx, sy, red);
-        const float sz = bsum<NT>(fz, red);
-        const float found = fminf(cnt, (float)m.contact_sensor_maxmatch);
-        if (tid == 0 && cnt > 0.f) {
-          if (reduce == 3) {
-            int q = 0;
-            float* o = sd + adr;
-            if (bits & 1) o[q++] = found;
-            if (bits & 2) { o[q++] = sx; o[q++] = sy; o[q++] = sz; }
-          } else if (bits & 1) {
-            const int width = dim / nslot;
-            for (int sl = 0; sl < nslot && sl < (int)cnt; sl++) sd[adr + sl * width] = found;
+          for (int a = 0; a < 3; a++) {
+            Fw[a] = sgn * (F[0] * fr[a] + F[1] * fr[3 + a] + F[2] * fr[6 + a]);
+            Tw[a] = sgn * (F[3] * fr[a] + F[4] * fr[3 + a] + F[5] * fr[6 + a]);
+            cpos[a] = con_pos[3 * ci + a];
           }
+          cdist = con_dist[ci];
+        }
+        const float found = (float)nm;
+        if (reduce == 3) {
+          // netforce: net wrench at the force-weighted centroid (weights |Fw|)
+          const float fn = sqrtf(dot3(Fw, Fw));
+          float nx = Fw[0], ny = Fw[1], nz = Fw[2], cx = fn * cpos[0], cy = fn * cpos[1], cz = fn * cpos[2], ws = fn, z = 0.f;
+          bsum2<NT>(nx, ny, red);
+          bsum2<NT>(nz, ws, red);
+          bsum2<NT>(cx, cy, red);
+          bsum2<NT>(cz, z, red);
+          float dmin = own ? cdist : 3.0e38f;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) dmin = fminf(dmin, __shfl_xor(dmin, o, 64));
+          float cen[3];
+          if (ws > MJH_MINVAL) { cen[0] = cx / ws; cen[1] = cy / ws; cen[2] = cz / ws; }
+          else { cen[0] = rl(cpos[0], 0); cen[1] = rl(cpos[1], 0); cen[2] = rl(cpos[2], 0); }
+          float rr[3] = {cpos[0] - cen[0], cpos[1] - cen[1], cpos[2] - cen[2]}, t[3];
+          cross3(t, rr, Fw);
+          float tx = own ? t[0] + Tw[0] : 0.f, ty = own ? t[1] + Tw[1] : 0.f, tz = own ? t[2] + Tw[2] : 0.f, z2 = 0.f;
+          bsum2<NT>(tx, ty, red);
+          bsum2<NT>(tz, z2, red);
+          if (tid == 0) {
+            float* o = sd + adr;
+            int q = 0;
+            if (bits & 1) o[q++] = found;
+            if (bits & 2) { o[q++] = nx; o[q++] = ny; o[q++] = nz; }
+            if (bits & 4) { o[q++] = tx; o[q++] = ty; o[q++] = tz; }
+            if (bits & 8) o[q++] = dmin;
+            if (bits & 16) { o[q++] = cen[0]; o[q++] = cen[1]; o[q++] = cen[2]; }
+            if (bits & 32) { o[q++] = 0.f; o[q++] = 0.f; o[q++] = 0.f; }
+            if (bits & 64) { o[q++] = 0.f; o[q++] = 0.f; o[q++] = 0.f; }
+          }
+          wsync();
+          continue;
+        }
+        // none: contact order; mindist: dist ascending; maxforce: |F| descending
+        // (stable: ties keep contact order)
+        int rank = tid;
+        if (reduce == 1 || reduce == 2) {
+          const float key = reduce == 1 ? cdist : -sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]);
+          rank = 0;
+          for (int j = 0; j < nm; j++) {
+            const float kj = rl(key, j);
+            rank += (kj < key || (kj == key && j < tid)) ? 1 : 0;
+          }
+        }
+        if (own && rank < nslot) {
+          float* o = sd + adr + rank * (dim / nslot);
+          const float sg = code < 0 ? -1.f : 1.f;  // normal primary -> secondary
+          int q = 0;
+          if (bits & 1) o[q++] = found;
+          if (bits & 2) { o[q++] = F[0]; o[q++] = F[1]; o[q++] = F[2]; }
+          if (bits & 4) { o[q++] = F[3]; o[q++] = F[4]; o[q++] = F[5]; }
+          if (bits & 8) o[q++] = cdist;
+          if (bits & 16) { o[q++] = cpos[0]; o[q++] = cpos[1]; o[q++] = cpos[2]; }
+          if (bits & 32) { o[q++] = sg * fr[0]; o[q++] = sg * fr[1]; o[q++] = sg * fr[2]; }
+          if (bits & 64) { o[q++] = sg * fr[3]; o[q++] = sg * fr[4]; o[q++] = sg * fr[5]; }
         }
         wsync();
         continue;
@@ -2257,6 +2290,7 @@ Layout make_layout(const mjh_model* m, int budget) {
   TAKE(efc_type, rcap); TAKE(efc_id, rcap);
   TAKE(efc_mask, 2 * rcap);
   TAKE(efc_h, rcap); TAKE(arow, rcap + 4); TAKE(ash, rcap + 4); TAKE(arow_prev, rcap + 4);
+  TAKE(sidx, 64);
 #undef TAKE
   L.total = al(off);
   L.gtotal = al(goff) + 64;  // +256 B keeps worlds' spans on separate cache lines

@@ -1190,14 +1190,14 @@ static void sensors(const or_model* m, ws_t* w, real* sd) {
         }
         int order[64], nfill;
         for (int k = 0; k < nmatch; k++) order[k] = k;
-        if (reduce == 1 || reduce == 2) { /* selection sort by dist asc / force norm desc */
-          for (int a = 0; a < nmatch; a++)
-            for (int b2 = a + 1; b2 < nmatch; b2++) {
-              real ka, kb;
-              if (reduce == 1) { ka = w->con[match[order[a]]].dist; kb = w->con[match[order[b2]]].dist; }
-              else { ka = -norm3(F[order[a]]); kb = -norm3(F[order[b2]]); }
-              if (kb < ka) { int t = order[a]; order[a] = order[b2]; order[b2] = t; }
-            }
+        if (reduce == 1 || reduce == 2) { /* stable sort by dist asc / contact-frame force norm desc */
+          real key[64];
+          for (int k = 0; k < nmatch; k++) key[k] = reduce == 1 ? w->con[match[k]].dist : -norm3(F[k]);
+          for (int k = 0; k < nmatch; k++) {
+            int rank = 0;
+            for (int j = 0; j < nmatch; j++) rank += (key[j] < key[k] || (key[j] == key[k] && j < k)) ? 1 : 0;
+            order[rank] = k;
+          }
         }
         real* o = out;
         if (reduce == 3) {

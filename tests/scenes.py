@@ -53,6 +53,28 @@ def g1_scene(num_envs: int) -> Scene:
   return Scene(cfg, "cpu")
 
 
+def g1_sensor_scene(num_envs: int) -> Scene:
+  """G1 with contact sensors exercising every reduction and field
+  (contact_sensor.py:16-47): maxforce and mindist with several slots, netforce
+  with the full wrench, and the torque field."""
+  allf = ("found", "force", "torque", "dist", "pos", "normal", "tangent")
+  feet = r"^(left_ankle_roll_link|right_ankle_roll_link)$"
+  sensors = (
+    ContactSensorCfg(name="maxf", primary=ContactMatch(mode="subtree", pattern=feet, entity="robot"),
+                     secondary=ContactMatch(mode="body", pattern="terrain"), fields=allf, reduce="maxforce", num_slots=3),
+    ContactSensorCfg(name="mind", primary=ContactMatch(mode="geom", pattern=r".*_foot\d_collision$", entity="robot"),
+                     secondary=ContactMatch(mode="body", pattern="terrain"), fields=("found", "dist", "pos", "normal"),
+                     reduce="mindist", num_slots=2),
+    ContactSensorCfg(name="net", primary=ContactMatch(mode="subtree", pattern=feet, entity="robot"),
+                     secondary=ContactMatch(mode="body", pattern="terrain"), fields=("found", "force", "torque", "dist", "pos"),
+                     reduce="netforce"),
+    ContactSensorCfg(name="none", primary=ContactMatch(mode="body", pattern=feet, entity="robot"),
+                     fields=("found", "force", "torque"), reduce="none", num_slots=2),
+  )
+  cfg = SceneCfg(num_envs=num_envs, terrain=TerrainImporterCfg(), entities={"robot": get_g1_robot_cfg()}, sensors=sensors)
+  return Scene(cfg, "cpu")
+
+
 def go1_scene(num_envs: int) -> Scene:
   feet = ("FR", "FL", "RR", "RL")
   geoms = tuple(f"{n}_foot_collision" for n in feet)
@@ -104,41 +126,196 @@ def _bound(ref: np.ndarray, rel: float) -> float:
   return rel * (1.0 + float(np.abs(ref).max(initial=0.0)))
 
 
-def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: float = 0.005) -> dict:
-  """Compare one step's outputs (arrays shaped (nworld, -1)). Returns
-  {"maxerr": {field: max|d|}, "failures": [...], "int_mismatch_worlds": [...]}."""
+# A contact / constraint row whose activation test sits within this distance of
+# its threshold may legitimately flip between float32 and float64 (kinematics
+# agree to 5e-5); integer mismatches are accepted only when every differing
+# contact or row is such a borderline one.
+BORDERLINE = 2e-4
+# Solver outputs (per world, relative to 1 + max|ref| of that world). The
+# Newton solver stops on a tolerance test or at `iterations` (10), and its line
+# search stops at |d cost/d alpha| <= ls_tolerance * |initial|: float32 and
+# float64 iterates can differ by a few % after an iteration in ill-conditioned
+# worlds, yet converge to the same qacc (1e-6 relative with the cap lifted,
+# test_converged_solver_parity). Measured on MI355X, N=4096 (round 2): median
+# 1.8e-6, 99.9 % quantile 3.0e-4, max 6.2e-3. Bounds: SOLVE_REL for at least
+# SOLVE_FRAC of the worlds, SOLVE_MAX (5x the observed max) for every world.
+SOLVE_REL = 2e-3
+SOLVE_FRAC = 0.995
+SOLVE_MAX = 3e-2
+
+
+def _contacts(d: dict, w: int) -> list[tuple[int, int]]:
+  nc = int(d["ncon"][w, 0])
+  g = d["contact_geom"][w, : 2 * nc].reshape(nc, 2)
+  return [(int(a), int(b)) for a, b in g]
+
+
+def align_contacts(got: dict, ref: dict, w: int) -> tuple[list[tuple[int, int]], list[int], list[int]]:
+  """Pairs (i_gpu, j_ref) of the same contact: same geom pair, matched by
+  nearest contact position (a capsule end can be found on one side only).
+  Returns (pairs, unmatched gpu indices, unmatched ref indices)."""
+  cg, cr = _contacts(got, w), _contacts(ref, w)
+  pg = got["contact_pos"][w].reshape(-1, 3)
+  pr = ref["contact_pos"][w].reshape(-1, 3)
+  used, pairs = set(), []
+  for i, k in enumerate(cg):
+    best, bd = -1, 1e-2
+    for j, kk in enumerate(cr):
+      if kk != k or j in used:
+        continue
+      dd = float(np.abs(pg[i] - pr[j]).max())
+      if dd < bd:
+        best, bd = j, dd
+    if best >= 0:
+      used.add(best)
+      pairs.append((i, best))
+  mg = {i for i, _ in pairs}
+  return pairs, [i for i in range(len(cg)) if i not in mg], [j for j in range(len(cr)) if j not in used]
+
+
+def int_mismatch_reason(got: dict, ref: dict, w: int) -> tuple[str, bool] | None:
+  """None if the world's integer outputs are identical, else (reason,
+  borderline) where borderline says every differing item sits at its threshold."""
+  cg, cr = _contacts(got, w), _contacts(ref, w)
+  ne_g, ne_r = int(got["nefc"][w, 0]), int(ref["nefc"][w, 0])
+  same = cg == cr and ne_g == ne_r
+  same = same and np.array_equal(got["efc_type"][w, :ne_g], ref["efc_type"][w, :ne_r])
+  same = same and np.array_equal(got["efc_id"][w, :ne_g], ref["efc_id"][w, :ne_r])
+  if same:
+    return None
+  reasons, border = [], True
+  pairs, ug, ur = align_contacts(got, ref, w)
+  for side, d, idx in (("gpu", got, ug), ("oracle", ref, ur)):
+    for i in idx:
+      dist = float(d["contact_dist"][w, i])
+      imar = float(d["contact_includemargin"][w, i])
+      reasons.append(f"contact {(int(d['contact_geom'][w, 2 * i]), int(d['contact_geom'][w, 2 * i + 1]))} only on {side} (dist {dist:.2e})")
+      border &= abs(dist) <= BORDERLINE or abs(dist - imar) <= BORDERLINE
+  # contacts on both sides whose row inclusion differs
+  for i, j in pairs:
+    a_in = int(got["contact_efc_address"][w, i]) >= 0
+    b_in = int(ref["contact_efc_address"][w, j]) >= 0
+    if a_in != b_in:
+      pos = float(ref["contact_dist"][w, j] - ref["contact_includemargin"][w, j])
+      reasons.append(f"contact {cr[j]} rows on {'gpu' if a_in else 'oracle'} only (dist-margin {pos:.2e})")
+      border &= abs(pos) <= BORDERLINE
+
+  # limit / friction rows: compare the non-contact row sets
+  def simple_rows(d, ne):
+    t, i, pos = d["efc_type"][w, :ne], d["efc_id"][w, :ne], d["efc_pos"][w, :ne]
+    return {(int(a), int(b)): float(c) for a, b, c in zip(t, i, pos) if a < 2}
+
+  rg, rr = simple_rows(got, ne_g), simple_rows(ref, ne_r)
+  for k in set(rg) ^ set(rr):
+    pos = rg.get(k, rr.get(k))
+    reasons.append(f"row {k} on {'gpu' if k in rg else 'oracle'} only (pos {pos:.2e})")
+    border &= abs(pos) <= BORDERLINE
+  if not reasons:
+    reasons.append("contact or row order differs")
+    border = False
+  return "; ".join(reasons), border
+
+
+def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: float = 0.005, solve_rel: float = SOLVE_REL,
+                 solve_frac: float = SOLVE_FRAC, solve_max: float = SOLVE_MAX) -> dict:
+  """Compare one step's outputs (arrays shaped (nworld, -1)).
+
+  Integer outputs (contacts by geom pair, nefc, efc types/ids) are compared
+  per world; a mismatching world must be explained by borderline contacts or
+  rows (`int_mismatch_reason`). Kinematics and smooth dynamics are checked on
+  EVERY world (they do not depend on contacts); contact geometry (dist, pos,
+  frame) on every contact present on both sides (aligned by geom pair); the
+  constraint rows (efc_pos/D/aref/force) and the solver, integration and
+  sensor outputs on every world whose integer outputs agree.
+  Returns {"maxerr", "failures", "int_mismatch_worlds", "int_mismatch_reasons",
+  "int_match_rate"}."""
   n = got["qpos"].shape[0]
-  sel = np.arange(n) if worlds is None else worlds
+  sel = np.arange(n) if worlds is None else np.asarray(worlds)
   failures: list[str] = []
   maxerr: dict[str, float] = {}
-  bad_int = []
+  bad_int, reasons = [], {}
   for w in sel:
-    nc, ne = int(ref["ncon"][w, 0]), int(ref["nefc"][w, 0])
-    ok = int(got["ncon"][w, 0]) == nc and int(got["nefc"][w, 0]) == ne
-    ok = ok and np.array_equal(got["contact_geom"][w, : 2 * nc], ref["contact_geom"][w, : 2 * nc])
-    ok = ok and np.array_equal(got["efc_type"][w, :ne], ref["efc_type"][w, :ne])
-    ok = ok and np.array_equal(got["efc_id"][w, :ne], ref["efc_id"][w, :ne])
-    if not ok:
+    r = int_mismatch_reason(got, ref, int(w))
+    if r is not None:
       bad_int.append(int(w))
-  if bad_int:
-    failures.append(f"integer outputs differ in worlds {bad_int[:8]}")
-  good = np.array([w for w in sel if w not in set(bad_int)], dtype=int)
+      reasons[int(w)] = r[0]
+      if not r[1]:
+        failures.append(f"integer outputs differ in world {int(w)} (not borderline): {r[0]}")
+  good = np.array([w for w in sel if int(w) not in reasons], dtype=int)
 
-  def check(name: str, tol: float) -> None:
-    a, b = got[name][good], ref[name][good]
+  def check(name: str, tol: float, rows=None) -> None:
+    rows = good if rows is None else rows
+    a, b = got[name][rows], ref[name][rows]
     e = float(np.abs(a - b).max(initial=0.0))
     maxerr[name] = e
     if not np.isfinite(a).all() or e > tol:
       failures.append(f"{name}: max|d|={e:.3e} > {tol:.3e}")
 
+  def check_rel(name: str, rel: float, rows=None, scale_name: str | None = None, scale: float = 1.0, floor: float = 0.0,
+                frac: float = 1.0, rel_max: float | None = None) -> None:
+    """per world: max|d_w| <= scale * rel * (1 + max|ref_w[scale_name]|) + floor
+    for at least `frac` of the worlds, and with rel_max (if given) for all."""
+    rows = good if rows is None else rows
+    if len(rows) == 0:
+      return
+    a, b = got[name][rows], ref[name][rows]
+    s_ref = ref[scale_name or name][rows]
+    d = np.abs(a - b).max(axis=1)
+    unit = scale * (1.0 + np.abs(s_ref).max(axis=1))
+    ratio = d / (rel * unit + floor)
+    maxerr[name] = float(d.max(initial=0.0))
+    maxerr[name + "/bound"] = float(ratio.max(initial=0.0))
+    n_over = int((ratio > 1).sum())
+    if not np.isfinite(a).all():
+      failures.append(f"{name}: non-finite values")
+    if n_over > max(1 if frac < 1.0 else 0, int((1.0 - frac) * len(rows))):
+      w = int(np.argmax(ratio))
+      failures.append(f"{name}: {n_over}/{len(rows)} worlds over the bound; world {int(rows[w])} max|d|={d[w]:.3e}")
+    if rel_max is not None:
+      rmax = d / (rel_max * unit + floor)
+      if (rmax > 1).any():
+        w = int(np.argmax(rmax))
+        failures.append(f"{name}: world {int(rows[w])} max|d|={d[w]:.3e} > hard bound {rel_max * unit[w] + floor:.3e}")
+
   for k in KIN:
-    check(k, 5e-5)
+    check(k, 5e-5, sel)
   for k in SMOOTH:
-    check(k, _bound(ref[k][good], 1e-4))
+    check_rel(k, 1e-4, sel)
+  # contact geometry, aligned by geom pair, on every world
+  cd, cp, cf = [0.0], [0.0], [0.0]
+  for w in sel:
+    for i, j in align_contacts(got, ref, int(w))[0]:
+      cd.append(abs(float(got["contact_dist"][w, i] - ref["contact_dist"][w, j])))
+      cp.append(float(np.abs(got["contact_pos"][w, 3 * i : 3 * i + 3] - ref["contact_pos"][w, 3 * j : 3 * j + 3]).max()))
+      # the normal is determined; the tangent basis follows it (make_frame)
+      cf.append(float(np.abs(got["contact_frame"][w, 9 * i : 9 * i + 9] - ref["contact_frame"][w, 9 * j : 9 * j + 9]).max()))
+  for name, v, tol in (("contact_dist", cd, 5e-5), ("contact_pos", cp, 5e-5), ("contact_frame", cf, 1e-3)):
+    maxerr[name] = max(v)
+    if max(v) > tol:
+      failures.append(f"{name}: max|d|={max(v):.3e} > {tol:.3e}")
+  # constraint rows on integer-identical worlds (rows are in the same order)
+  if len(good):
+    ne = ref["nefc"][good, 0].astype(int)
+    mask = np.arange(ref["efc_pos"].shape[1])[None, :] < ne[:, None]
+    for k, rel in (("efc_pos", 5e-5), ("efc_D", 1e-3), ("efc_aref", 1e-3), ("efc_force", solve_rel)):
+      a, b = got[k][good][mask], ref[k][good][mask]
+      tol = 5e-5 if k == "efc_pos" else _bound(b, rel if k != "efc_force" else solve_max)
+      e = float(np.abs(a - b).max(initial=0.0))
+      maxerr[k] = e
+      if not np.isfinite(a).all() or e > tol:
+        failures.append(f"{k}: max|d|={e:.3e} > {tol:.3e}")
+  sv = dict(frac=solve_frac, rel_max=solve_max)
   for k in SOLVE:
-    check(k, _bound(ref[k][good], 2e-2))
-  qv_tol = _bound(ref["qvel"][good], 1e-2)
-  check("qvel", qv_tol)
-  check("qpos", 1e-4 + dt * qv_tol)
-  check("sensordata", _bound(ref["sensordata"][good], 2e-2))
-  return {"maxerr": maxerr, "failures": failures, "int_mismatch_worlds": bad_int}
+    check_rel(k, solve_rel, **sv)
+  # qvel' = qvel + dt * qacc_int, where implicitfast solves (M + dt*D) qacc_int
+  # = f (bounded here by 2x the qacc error), and qpos integrates qvel'
+  check_rel("qvel", solve_rel, scale_name="qacc", scale=2 * dt, floor=1e-5, **sv)
+  check_rel("qpos", solve_rel, scale_name="qacc", scale=2 * dt * dt, floor=1e-5, **sv)
+  check_rel("sensordata", solve_rel, **sv)
+  return {
+    "maxerr": maxerr,
+    "failures": failures,
+    "int_mismatch_worlds": bad_int,
+    "int_mismatch_reasons": reasons,
+    "int_match_rate": 1.0 - len(bad_int) / max(1, len(sel)),
+  }

@@ -7,7 +7,7 @@ import torch
 
 from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg
 from oracle.oracle import INPUTS, Oracle
-from tests.scenes import compare_step, g1_scene_model, go1_scene_model, random_states
+from tests.scenes import compare_step, g1_scene_model, g1_sensor_scene, go1_scene_model, random_states
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -33,13 +33,15 @@ def get(sim, n):
   return {k: getattr(sim.data, k).detach().cpu().numpy().reshape(n, -1) for k in sim.data.fields()}
 
 
-def assert_parity(got, ref, n, max_int_mismatch=None):
+def assert_parity(got, ref, n, min_int_rate=0.98, tag=""):
+  """compare_step must report no failure (every integer mismatch explained by
+  a borderline contact/row; floats within tests/scenes.py tolerances), and at
+  least `min_int_rate` of the worlds must have bit-identical integer outputs."""
   rep = compare_step(got, ref)
-  allowed = max(1, n // 100) if max_int_mismatch is None else max_int_mismatch
-  bad = rep["int_mismatch_worlds"]
-  assert len(bad) <= allowed, rep["failures"]
-  other = [f for f in rep["failures"] if not f.startswith("integer")]
-  assert not other, (other, rep["maxerr"])
+  print(f"[parity{tag}] int_match_rate={rep['int_match_rate']:.4f} mismatches={rep['int_mismatch_reasons']} "
+        f"maxerr={ {k: f'{v:.2e}' for k, v in rep['maxerr'].items()} }")
+  assert not rep["failures"], (rep["failures"], rep["maxerr"])
+  assert rep["int_match_rate"] >= min_int_rate, rep["int_mismatch_reasons"]
   return rep
 
 
@@ -54,7 +56,7 @@ def test_single_step_parity(name, integrate):
   sim.step() if integrate else sim.forward()
   got = get(sim, n)
   ref = Oracle(m).run(n, st, integrate=integrate)
-  assert_parity(got, ref, n)
+  assert_parity(got, ref, n, tag=f" {name} integrate={integrate}")
   assert (got["ncon"] > 0).mean() > 0.5  # the states exercise contacts
 
 
@@ -74,7 +76,7 @@ def test_trajectory_parity_along_gpu_rollout():
     sim.step()
     nxt = get(sim, n)
     ref = orc.run(n, state, integrate=True)
-    rep = assert_parity(nxt, ref, n, max_int_mismatch=2)
+    rep = assert_parity(nxt, ref, n, min_int_rate=0.95, tag=f" step {k}")
     worst = max(worst, rep["maxerr"]["qvel"])
   assert worst < 0.05
 
@@ -160,3 +162,58 @@ def test_full_size_determinism_and_world_independence():
   p = perm.numpy()
   for k in ("qpos", "qvel", "qacc", "sensordata", "ncon"):
     assert np.array_equal(c[k], a[k][p]), k
+
+
+def test_full_size_integer_parity_rate():
+  """N=4096 (the bench size), one step from random stance states against the
+  float64 oracle: >= 99.9 % of worlds have bit-identical integer outputs
+  (contacts, rows), every mismatch is borderline, and every float check holds."""
+  n = 4096
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(11))
+  sim = make_sim(m, n)
+  put(sim, st)
+  sim.step()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=True, nthreads=8)
+  assert_parity(got, ref, n, min_int_rate=0.999, tag=" N=4096")
+
+
+def test_contact_sensor_reductions_and_fields():
+  """maxforce / mindist (top-k, stable), netforce (net wrench at the
+  force-weighted centroid) and none, with found/force/torque/dist/pos/normal/
+  tangent, against the oracle (oracle/oracle.c sensors())."""
+  n = 256
+  m = g1_sensor_scene(n).compile(50, 300)
+  st = random_states(m, n, np.random.default_rng(12))
+  sim = make_sim(m, n)
+  put(sim, st)
+  sim.forward()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=False)
+  rep = assert_parity(got, ref, n, tag=" sensors")
+  good = np.array([w for w in range(n) if w not in rep["int_mismatch_reasons"]])
+  sd_g, sd_r = got["sensordata"][good], ref["sensordata"][good]
+  assert (np.abs(sd_r) > 0).sum(axis=0).min() >= 0  # shape sanity
+  assert np.abs(sd_g - sd_r).max() <= 2e-3 * (1 + np.abs(sd_r).max())
+  assert (sd_r != 0).any(axis=0).mean() > 0.5  # most sensor entries are exercised
+
+
+def test_converged_solver_parity():
+  """With the iteration cap lifted (iterations 100, tolerance 1e-10) the HIP
+  Newton solver and the float64 oracle converge to the same qacc in EVERY
+  world (the capped comparisons differ only in where each stops)."""
+  n = 512
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(11))
+  cfg = dict(CFG, mujoco=MujocoCfg(timestep=0.005, iterations=100, ls_iterations=50, tolerance=1e-10))
+  sim = Simulation(n, SimulationCfg(**cfg), m, DEV)
+  put(sim, st)
+  sim.forward()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=False)
+  # float32 round-off at convergence: measured max 1.4e-5 (qacc), 2.7e-5
+  # (qfrc_constraint), 2.2e-5 (sensordata) relative; bound 1e-4 for every world
+  rep = compare_step(got, ref, solve_rel=1e-4, solve_frac=1.0, solve_max=1e-4)
+  print("[converged]", rep["int_match_rate"], {k: f"{v:.2e}" for k, v in rep["maxerr"].items() if "/" in k})
+  assert not rep["failures"], rep["failures"]

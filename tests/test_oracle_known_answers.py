@@ -185,3 +185,20 @@ def test_oracle_struct_layouts_both_precisions():
     lib.oracle_sizeof_data.restype = ctypes.c_size_t
     assert ctypes.sizeof(abi.model_struct(real, device=False)) == lib.oracle_sizeof_model(), prec
     assert ctypes.sizeof(abi.data_struct(real, device=False)) == lib.oracle_sizeof_data(), prec
+
+
+def test_compare_step_oracle_f32_vs_f64():
+  """The parity checker itself (tests/scenes.py compare_step): the oracle's
+  float32 build passes against its float64 build with integer outputs
+  identical, so the tolerances are attainable by a correct float32 step."""
+  import numpy as np
+
+  from oracle.oracle import Oracle
+  from tests.scenes import compare_step, g1_sensor_scene, random_states
+
+  n = 64
+  m = g1_sensor_scene(n).compile(50, 300)
+  st = random_states(m, n, np.random.default_rng(12))
+  rep = compare_step(Oracle(m, "f32").run(n, st, integrate=True), Oracle(m).run(n, st, integrate=True))
+  assert not rep["failures"], rep["failures"]
+  assert rep["int_match_rate"] >= 0.98
