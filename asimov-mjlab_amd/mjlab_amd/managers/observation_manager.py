@@ -55,6 +55,9 @@ class ObservationManager:
       self.group_obs_term_dim[gname] = dims
     self._obs_buffer = None
     self._fused = {g: self._fused_plan(g) for g in self._group_terms}
+    # optional fixed noise draws per group, (N, group width) in U[0,1): replaces
+    # the group's uniform draw in the fused path (used to replay golden vectors)
+    self.noise_override: dict[str, torch.Tensor] = {}
 
   def _fused_plan(self, gname: str):
     """Per-term (offset, width, noise lo/hi or None, clip, scale) for groups that
@@ -121,7 +124,7 @@ class ObservationManager:
   def compute_group(self, group_name: str, update_history: bool = False):
     fp = self._fused.get(group_name)
     if fp is not None and str(self._env.device).startswith("cuda"):
-      out = self._compute_fused(fp)
+      out = self._compute_fused(fp, self.noise_override.get(group_name))
       if out is not None:
         return out
     obs_terms = {}
@@ -143,7 +146,7 @@ class ObservationManager:
       return torch.cat(list(obs_terms.values()), dim=self._group_concat_dim[group_name])
     return obs_terms
 
-  def _compute_fused(self, fp):
+  def _compute_fused(self, fp, u_fixed=None):
     """One fused launch per term writing straight into the group buffer (no
     per-term clone/noise/scale chain, no final cat); one U[0,1) draw per group."""
     from mjlab_amd import envops
@@ -151,7 +154,9 @@ class ObservationManager:
     plan, width = fp
     n = self._env.num_envs
     out = torch.empty((n, width), device=self._env.device)
-    u = torch.rand((n, width), device=self._env.device) if any(p[3] is not None for p in plan) else None
+    u = None
+    if any(p[3] is not None for p in plan):
+      u = u_fixed if u_fixed is not None else torch.rand((n, width), device=self._env.device)
     xs = [tcfg.func(self._env, **tcfg.params).float() for tcfg, *_ in plan]
     if envops.obs_group(xs, plan, u, out):  # the whole group in one launch
       return out

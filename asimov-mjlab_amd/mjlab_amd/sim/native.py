@@ -7,6 +7,7 @@ ABI version, every physics call raises. Build it with
 
 from __future__ import annotations
 
+import collections
 import ctypes
 from functools import lru_cache
 from pathlib import Path
@@ -121,7 +122,13 @@ def lib() -> ctypes.CDLL:
   return L
 
 
+# launches per C-ABI entry point (host-side tally; tests use it to prove which
+# HIP kernels a code path ran)
+CALLS: "collections.Counter[str]" = collections.Counter()
+
+
 def check(rc: int, what: str) -> None:
+  CALLS[what] += 1
   if rc != 0:
     msg = lib().mjh_last_error().decode()
     raise RuntimeError(f"{what} failed ({rc}): {msg}")

@@ -245,18 +245,22 @@ class MotionCommand(CommandTerm):
     new = ((bins + u[1]) / self.bin_count * (T - 1)).long()
     torch.where(mask, new, self.time_steps, out=self.time_steps)
 
+    # the reference updates the sampling metrics only when some env resampled
     H = -(p * (p + 1e-12).log()).sum()
     pmax, imax = p.max(dim=0)
-    self.metrics["sampling_entropy"].copy_((H / math.log(self.bin_count)).expand(self.num_envs))
-    self.metrics["sampling_top1_prob"].copy_(pmax.expand(self.num_envs))
-    self.metrics["sampling_top1_bin"].copy_((imax.float() / self.bin_count).expand(self.num_envs))
+    any_r = mask.any()
+    for key, val in (("sampling_entropy", H / math.log(self.bin_count)), ("sampling_top1_prob", pmax),
+                     ("sampling_top1_bin", imax.float() / self.bin_count)):
+      mt = self.metrics[key]
+      torch.where(any_r, val.expand(self.num_envs), mt, out=mt)
 
   def _uniform_sampling(self, mask: torch.Tensor) -> None:
     new = torch.randint(0, self.motion.time_step_total, (self.num_envs,), device=self.device)
     torch.where(mask, new, self.time_steps, out=self.time_steps)
-    self.metrics["sampling_entropy"].fill_(1.0)
-    self.metrics["sampling_top1_prob"].fill_(1.0 / self.bin_count)
-    self.metrics["sampling_top1_bin"].fill_(0.5)
+    any_r = mask.any()
+    for key, val in (("sampling_entropy", 1.0), ("sampling_top1_prob", 1.0 / self.bin_count), ("sampling_top1_bin", 0.5)):
+      mt = self.metrics[key]
+      torch.where(any_r, torch.full_like(mt, val), mt, out=mt)
 
   def _resample_command(self, mask: torch.Tensor) -> None:
     """commands.py:309-375 for the envs selected by ``mask``."""
