@@ -29,6 +29,29 @@ __global__ void obs_group_kernel(const ObsArgs a, const float* __restrict__ u, l
   out[e * os + d.off + j] = v * d.scale;
 }
 
+// one workgroup: count the worlds per flag bit, publish, accumulate, clear
+__global__ void flag_stats_kernel(int* __restrict__ flags, long long n, mjh_i64* __restrict__ stats) {
+  __shared__ int cnt[3];
+  if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  int c0 = 0, c1 = 0, c2 = 0;
+  for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+    const int f = flags[i];
+    c0 += f & MJH_FLAG_CONTACT_OVERFLOW ? 1 : 0;
+    c1 += f & MJH_FLAG_EFC_OVERFLOW ? 1 : 0;
+    c2 += f & MJH_FLAG_NONFINITE ? 1 : 0;
+    flags[i] = 0;
+  }
+  if (c0) atomicAdd(&cnt[0], c0);  // LDS atomics
+  if (c1) atomicAdd(&cnt[1], c1);
+  if (c2) atomicAdd(&cnt[2], c2);
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    stats[threadIdx.x] = cnt[threadIdx.x];
+    stats[3 + threadIdx.x] += cnt[threadIdx.x];
+  }
+}
+
 struct RewArgs {
   const float* v[MJH_MAX_TERMS];
   long long vs[MJH_MAX_TERMS];
@@ -89,6 +112,11 @@ int mjh_reward_combine(const float* const* values, const long long* strides, int
   a.nterms = nterms;
   hipLaunchKernelGGL(reward_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
                      weights, dt, reward, step_reward, sums, n);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int mjh_flag_stats(int* flags_acc, long long nworld, mjh_i64* stats, void* stream) {
+  hipLaunchKernelGGL(flag_stats_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, flags_acc, nworld, stats);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

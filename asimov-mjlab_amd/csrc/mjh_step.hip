@@ -91,6 +91,13 @@ struct Rg {
 #define X_RG(name, r) static constexpr bool name = ((r) != 0 || (#name[0] == 'J' && #name[1] == 0) || \
     (#name[0] == 'c' && (#name[1] == 'i' || #name[1] == 'r' || #name[1] == 'v' || #name[1] == 'f' || #name[1] == 'd'))) && \
     !(#name[0] == 'L' && #name[1] == 0);
+#elif MJH_PRESET == 6
+// like 5, and the constraint-row arrays in global scratch as well: ~7 KB of LDS
+// per world (nv-vectors + the factor), so 16 worlds share a CU and rcap = njmax
+#define X_RG(name, r) static constexpr bool name = ((r) != 0 || (#name[0] == 'J' && #name[1] == 0) || \
+    (#name[0] == 'c' && (#name[1] == 'i' || #name[1] == 'r' || #name[1] == 'v' || #name[1] == 'f' || #name[1] == 'd')) || \
+    (#name[0] == 'e' && #name[1] == 'f' && #name[2] == 'c') || (#name[0] == 'a' && (#name[1] == 'r' || #name[1] == 's'))) && \
+    !(#name[0] == 'L' && #name[1] == 0);
 #elif MJH_PRESET == 3
 #define X_RG(name, r) static constexpr bool name = (r) != 0 || (#name[0] == 'J' && #name[1] == 0);
 #else
@@ -772,8 +779,11 @@ __device__ __forceinline__ float row_state(int type, float D, float R, float fl,
 }
 
 // ---- the step kernel --------------------------------------------------------
+#ifndef MJH_MINWAVES
+#define MJH_MINWAVES 1
+#endif
 template <int WPB, bool STEP, int NVP>
-__global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo,
+__global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo,
                                                          const ImgOff Io, const unsigned char* gate) {
   constexpr int NT = 64;  // one wave per world
   extern __shared__ float smem[];
@@ -2166,7 +2176,11 @@ __global__ __launch_bounds__(64 * WPB) void step_kernel(const mjh_model m, const
     for (int i = tid; i < nq; i += NT) bad += isfinite(qpos[i]) ? 0.f : 1.f;
     for (int i = tid; i < nv; i += NT) bad += (isfinite(qvel[i]) && isfinite(qacc[i])) ? 0.f : 1.f;
     bad = bsum<NT>(bad, red);
-    if (tid == 0) d.flags[W] = ints[I_FLAGS] | (bad > 0.f ? MJH_FLAG_NONFINITE : 0);
+    if (tid == 0) {
+      const int f = ints[I_FLAGS] | (bad > 0.f ? MJH_FLAG_NONFINITE : 0);
+      d.flags[W] = f;
+      d.flags_acc[W] |= f;  // sticky until the caller clears it (overflow/NaN statistics)
+    }
   }
 }
 

@@ -177,7 +177,11 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     # inside the graph (no host sync); read with step_stats()
     self._stats = torch.zeros(2, dtype=torch.long, device=self.device)
     self._action_in = torch.zeros(n, self.action_manager.total_action_dim, device=self.device)
-    self.use_graph = (str(self.device).startswith("cuda") and torch.cuda.is_available()) if use_graph is None else use_graph
+    if use_graph is None:
+      # the NaN guard captures and checks the state around every physics step on
+      # the host (debug aid), so an enabled guard runs the env step eagerly
+      use_graph = str(self.device).startswith("cuda") and torch.cuda.is_available() and not cfg.sim.nan_guard.enabled
+    self.use_graph = use_graph
     self._graph: torch.cuda.CUDAGraph | None = None
     self._graph_key = None
     self._graph_out = None
@@ -277,6 +281,13 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     self._stats[0] += self.reset_buf.sum()
     self._stats[1:] += self._any_reset
     self.sim.forward_gated(self._any_reset)
+    # capacity / NaN statistics of this env step's physics passes (device
+    # counters, no sync): worlds that dropped contacts or constraint rows
+    fs = self.sim.flag_stats()
+    log = self.extras.setdefault("log", {})
+    log["Sim/contact_overflow_worlds"] = fs[0]
+    log["Sim/efc_overflow_worlds"] = fs[1]
+    log["Sim/nonfinite_worlds"] = fs[2]
     self.command_manager.compute(dt=self.step_dt)
     if "interval" in self.event_manager.available_modes:
       self.event_manager.apply(mode="interval", dt=self.step_dt)

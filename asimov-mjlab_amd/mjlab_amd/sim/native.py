@@ -20,7 +20,7 @@ PKG = Path(__file__).resolve().parents[1]
 # MJH_LIB selects an alternative build of the same ABI (e.g. the phase-timing
 # build libmjh_prof.so used by tools/phase_profile.py).
 LIB_PATH = Path(os.environ.get("MJH_LIB", str(PKG / "libmjh.so")))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 EXPORTS = (
   "mjh_abi_version",
@@ -56,6 +56,7 @@ EXPORTS = (
   "mjh_motion_relative",
   "mjh_obs_group",
   "mjh_reward_combine",
+  "mjh_flag_stats",
 )
 
 
@@ -113,6 +114,7 @@ def lib() -> ctypes.CDLL:
   L.mjh_motion_relative.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, ll, vp, ll, ll, ci, vp, vp, ll, vp]
   L.mjh_obs_group.argtypes = [vp, ci, vp, ll, vp, ll, ll, vp]
   L.mjh_reward_combine.argtypes = [vp, vp, ci, vp, cf, vp, vp, vp, ll, vp]
+  L.mjh_flag_stats.argtypes = [vp, ll, vp, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

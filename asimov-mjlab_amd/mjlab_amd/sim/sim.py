@@ -17,8 +17,12 @@ Differences by construction (MI355X-first):
 from __future__ import annotations
 
 import ctypes
+import json
+from collections import deque
 from contextlib import contextmanager
 from dataclasses import dataclass, field
+from datetime import datetime
+from pathlib import Path
 from typing import Literal
 
 import numpy as np
@@ -74,24 +78,93 @@ class NanGuardCfg:
 
 
 class NanGuard:
-  """Disabled-by-default NaN watcher (``src/mjlab/utils/nan_guard.py:16-104``).
+  """Rolling buffer of physics states, dumped to disk when NaN/Inf appears
+  (``src/mjlab/utils/nan_guard.py:26-171``).
 
-  Enabled, it reads the per-world ``flags`` word the kernel sets on
-  non-finite state after each step (one host sync per step, debug only).
+  Disabled (the default) every call is a no-op. Enabled, ``capture`` copies
+  the mjSTATE_PHYSICS state of every world to the host before each step (one
+  sync per step: a debugging aid, as in the reference) and ``check_and_dump``
+  writes the buffered states of the first ``max_envs_to_dump`` non-finite
+  worlds to ``nan_dump_<timestamp>.npz``. The state layout is MuJoCo's
+  mjSTATE_PHYSICS = [qpos (nq), qvel (nv), act (na)] in float64 (the models
+  here have no plugin or history state). Deviations, both because MuJoCo is
+  absent: metadata is stored as a JSON string (loadable without pickle) instead
+  of a pickled dict, and the model is saved as ``model_<timestamp>.npz`` (the
+  compiled model's arrays) instead of an MJB file.
   """
 
   def __init__(self, cfg: NanGuardCfg, num_envs: int, model) -> None:
     self.cfg = cfg
+    self.enabled = cfg.enabled
     self.num_envs = num_envs
     self.tripped: torch.Tensor | None = None
+    if not self.enabled:
+      return
+    self.buffer_size = cfg.buffer_size
+    self.output_dir = Path(cfg.output_dir)
+    self.max_envs_to_dump = cfg.max_envs_to_dump
+    self.buffer: deque = deque(maxlen=self.buffer_size)
+    self.step_counter = 0
+    self._dumped = False
+    self.model = model
+    self.state_size = int(model.nq + model.nv + model.na)
+
+  def capture(self, data) -> None:
+    if not self.enabled:
+      return
+    parts = [data.qpos, data.qvel] + ([data.act] if self.model.na > 0 else [])
+    states = torch.cat([p.reshape(p.shape[0], -1) for p in parts], dim=1).double().cpu().numpy()
+    self.buffer.append({"step": self.step_counter, "states": states})
+    self.step_counter += 1
 
   @contextmanager
   def watch(self, data):
+    self.capture(data)
     yield
-    if self.cfg.enabled:
-      bad = (data.flags & 4) != 0
-      if bool(bad.any()):
-        self.tripped = bad.nonzero().flatten()
+    self.check_and_dump(data)
+
+  @staticmethod
+  def detect_nans(data) -> torch.Tensor:
+    """Per-world bool: NaN/Inf in qpos, qvel, qacc or qacc_warmstart (nan_guard.py:86-104)."""
+    m = torch.zeros(data.qpos.shape[0], dtype=torch.bool, device=data.qpos.device)
+    for t in (data.qpos, data.qvel, data.qacc, data.qacc_warmstart):
+      m |= ~torch.isfinite(t).all(dim=-1)
+    return m
+
+  def check_and_dump(self, data) -> bool:
+    if not self.enabled or self._dumped:
+      return False
+    bad = self.detect_nans(data)
+    if not bool(bad.any()):
+      return False
+    ids = torch.where(bad)[0].cpu().numpy().tolist()
+    self.tripped = bad.nonzero().flatten()
+    self._dump_buffer(ids)
+    self._dumped = True
+    return True
+
+  def _dump_buffer(self, nan_env_ids: list[int]) -> Path:
+    self.output_dir.mkdir(parents=True, exist_ok=True)
+    stamp = datetime.now().strftime("%Y%m%d_%H%M%S")
+    fname = self.output_dir / f"nan_dump_{stamp}.npz"
+    mname = self.output_dir / f"model_{stamp}.npz"
+    envs = nan_env_ids[: self.max_envs_to_dump]
+    out = {f"states_step_{it['step']:06d}": it["states"][envs] for it in self.buffer}
+    meta = {
+      "num_envs_total": self.num_envs, "num_envs_dumped": len(envs), "nan_env_ids": nan_env_ids,
+      "dumped_env_ids": list(envs), "state_size": self.state_size, "buffer_size": len(self.buffer),
+      "detection_step": self.step_counter, "timestamp": stamp, "model_file": mname.name,
+      "note": "States in mjSTATE_PHYSICS layout [qpos, qvel, act] (float64).",
+    }
+    out["_metadata"] = np.array(json.dumps(meta))
+    np.savez_compressed(fname, **out)
+    np.savez_compressed(mname, **{k: np.asarray(v) for k, v in abi.model_host_arrays(self.model).items()})
+    for link, target in ((self.output_dir / "nan_dump_latest.npz", fname), (self.output_dir / "model_latest.npz", mname)):
+      link.unlink(missing_ok=True)
+      link.symlink_to(target.name)
+    print(f"[NanGuard] Detected NaN/Inf at step {self.step_counter}; envs {nan_env_ids[:10]}; "
+          f"dumped {len(envs)} envs x {len(self.buffer)} states to {fname}")
+    return fname
 
 
 @dataclass(kw_only=True)
@@ -160,6 +233,8 @@ class Simulation:
     if name in MODEL_SHAPES:
       shp = shape_of(MODEL_SHAPES[name], self.sizes)
       if name in self._wstride or name in BATCHED_STATIC:
+        if flat.numel() == 0:  # empty field (e.g. no actuators): dim0 cannot be inferred
+          return flat.view(self.num_envs if name in self._wstride else 1, *shp)
         return flat.view(-1, *shp)
       return flat.view(*shp)
     return flat
@@ -372,6 +447,25 @@ class Simulation:
       self.step_graph.replay()
 
   # ---- utilities ----
+  def flag_stats(self) -> torch.Tensor:
+    """(6,) int64 device tensor: worlds whose physics passes since the last call
+    dropped contacts (nconmax) / constraint rows (efc capacity) / went
+    non-finite, then the running totals of the same; clears data.flags_acc.
+    No host sync (one single-workgroup launch; capturable)."""
+    if not hasattr(self, "_flag_stats"):
+      self._flag_stats = torch.zeros(6, dtype=torch.int64, device=self.device)
+    fa = self.data.flags_acc.view(-1)
+    if self.use_cuda_graph:
+      native.check(native.lib().mjh_flag_stats(ctypes.c_void_p(fa.data_ptr()), fa.numel(),
+                                               ctypes.c_void_p(self._flag_stats.data_ptr()), self._stream()),
+                   "mjh_flag_stats")
+    else:
+      cur = torch.stack([((fa & b) != 0).sum() for b in (1, 2, 4)])
+      self._flag_stats[:3] = cur
+      self._flag_stats[3:] += cur
+      fa.zero_()
+    return self._flag_stats
+
   def efc_capacity(self) -> int:
     return int(native.lib().mjh_efc_capacity(ctypes.addressof(self._mstruct)))
 
@@ -389,9 +483,5 @@ class Simulation:
 
 
 def detect_nans(data) -> torch.Tensor:
-  """Per-world bool: non-finite qpos/qvel/qacc (``utils/nan_guard.py`` semantics)."""
-  return (
-    ~torch.isfinite(data.qpos).all(dim=-1)
-    | ~torch.isfinite(data.qvel).all(dim=-1)
-    | ~torch.isfinite(data.qacc).all(dim=-1)
-  )
+  """Per-world bool: non-finite qpos/qvel/qacc/qacc_warmstart (``utils/nan_guard.py:86-104``)."""
+  return NanGuard.detect_nans(data)

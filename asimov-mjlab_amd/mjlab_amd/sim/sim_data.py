@@ -69,6 +69,7 @@ DATA_SHAPES: dict[str, tuple] = {
   "efc_force": ("njmax",),
   "solver_niter": (),
   "flags": (),
+  "flags_acc": (),
 }
 
 MODEL_SHAPES: dict[str, tuple] = {

@@ -18,7 +18,9 @@
  *     mjh_last_error() returns a thread-local message. Runtime overflow of the
  *     per-world contact/constraint capacity (nconmax/njmax) is reported through
  *     the per-world `flags` array (bit 0: contacts dropped, bit 1: constraint
- *     rows dropped, bit 2: non-finite state), never by a host sync.
+ *     rows dropped, bit 2: non-finite state), never by a host sync; the
+ *     `flags_acc` array ORs them across launches until the caller clears it
+ *     (mjh_flag_stats counts and clears it on the device).
  */
 #ifndef MJH_ABI_H_
 #define MJH_ABI_H_
@@ -32,7 +34,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 4
+#define MJH_ABI_VERSION 5
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -247,6 +249,12 @@ int mjh_obs_group(const mjh_obs_term_desc* terms, int nterms, const float* u, lo
  * step_reward[e, t] = v * w[t]; sums[e, t] += v * (w[t] * dt); reward[e] = sum_t. */
 int mjh_reward_combine(const float* const* values, const long long* strides, int nterms, const float* weights, float dt,
                        float* reward, float* step_reward, float* sums, long long n, void* stream);
+
+/* Capacity/NaN statistics from the sticky per-world flags (data->flags_acc),
+ * one workgroup, no host sync: stats[0..2] = worlds with contacts dropped /
+ * constraint rows dropped / non-finite state since the last call, stats[3..5]
+ * += the same (running totals); flags_acc is cleared. */
+int mjh_flag_stats(int* flags_acc, long long nworld, mjh_i64* stats, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1386,6 +1386,7 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   for (int k = 0; k < nq; k++) if (!isfinite(d->qpos[(size_t)wi * nq + k])) w->flags |= 4;
   for (int k = 0; k < nv; k++) if (!isfinite(d->qvel[(size_t)wi * nv + k]) || !isfinite(w->qacc[k])) w->flags |= 4;
   d->flags[wi] = w->flags;
+  d->flags_acc[wi] |= w->flags;
 }
 
 int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int nthreads) {

@@ -27,6 +27,10 @@ def test_env_graph_rollout(task, adim):
   assert env._graph is not None
   assert torch.isfinite(obs["policy"]).all() and torch.isfinite(obs["critic"]).all() and torch.isfinite(rew).all()
   assert ((env.sim.data.flags & 4) == 0).all()
+  log = extras["log"]
+  for k in ("Sim/contact_overflow_worlds", "Sim/efc_overflow_worlds", "Sim/nonfinite_worlds"):
+    assert k in log and int(log[k]) >= 0
+  assert int(log["Sim/nonfinite_worlds"]) == 0
   assert (env.episode_length_buf <= 60).all()
   assert native.LIB_PATH.name.startswith("libmjh")
 

@@ -132,6 +132,19 @@ def test_overflow_is_flagged_not_fatal():
   assert (got["ncon"] <= 4).all()
   assert ((got["flags"] & 1) != 0).any()
   assert np.isfinite(got["qvel"]).all()
+  # surfaced without a sync: sticky flags (OR over launches) counted and
+  # cleared on the device by flag_stats
+  assert np.array_equal(got["flags_acc"] & got["flags"], got["flags"])
+  sim.step()
+  f2 = sim.data.flags.clone()
+  acc = sim.data.flags_acc.clone()
+  assert torch.equal(acc & f2, f2)
+  n_or = int(((acc & 1) != 0).sum())
+  st = sim.flag_stats().cpu().numpy()
+  assert st[0] == n_or and st[3] == n_or and n_or > 0
+  assert int(sim.data.flags_acc.abs().sum()) == 0
+  st = sim.flag_stats().cpu().numpy()
+  assert st[0] == 0 and st[3] == n_or  # running total kept
 
 
 def test_full_size_determinism_and_world_independence():
@@ -217,3 +230,53 @@ def test_converged_solver_parity():
   rep = compare_step(got, ref, solve_rel=1e-4, solve_frac=1.0, solve_max=1e-4)
   print("[converged]", rep["int_match_rate"], {k: f"{v:.2e}" for k, v in rep["maxerr"].items() if "/" in k})
   assert not rep["failures"], rep["failures"]
+
+
+def test_known_answers_on_gpu():
+  """The analytic known answers that pin the oracle (test_oracle_known_answers)
+  hold for the HIP step too: crossed capsules, box corners on a plane, and the
+  incline stick/slip threshold (float32 tolerances)."""
+  from tests import test_oracle_known_answers as KA
+
+  def sim_of(xml, n=1):
+    m = KA._model(xml)
+    # MujocoCfg.apply sets the model's options (sim.py:42-94), gravity included
+    opt = MujocoCfg(timestep=m.timestep, iterations=10, ls_iterations=20, gravity=tuple(float(x) for x in m.gravity))
+    sim = Simulation(n, SimulationCfg(nconmax=16, njmax=64, mujoco=opt), m, DEV)
+    put(sim, {"qpos": np.tile(m.qpos0[None], (n, 1))})
+    return m, sim
+
+  m, sim = sim_of(KA._free_body_xml("""
+    <body name="a" pos="0 0 0.5"><freejoint/><geom type="capsule" fromto="-0.3 0 0 0.3 0 0" size="0.05"/></body>
+    <body name="b" pos="0.1 0.05 0.58"><freejoint/><geom type="capsule" fromto="0 -0.3 0 0 0.3 0" size="0.05"/></body>
+  """, gravity="0 0 0"))
+  sim.forward()
+  o = get(sim, 1)
+  assert o["ncon"][0, 0] == 1
+  assert o["contact_dist"][0, 0] == pytest.approx(-0.02, abs=1e-6)
+  np.testing.assert_allclose(o["contact_pos"][0, 0:3], [0.1, 0.0, 0.54], atol=1e-6)
+
+  m, sim = sim_of(KA._free_body_xml("""<body name="box" pos="0 0 0.04"><freejoint/><geom type="box" size="0.2 0.1 0.05"/></body>""",
+                                    plane='<geom name="floor" type="plane" size="5 5 0.1"/>'))
+  sim.forward()
+  o = get(sim, 1)
+  assert o["ncon"][0, 0] == 4
+  np.testing.assert_allclose(o["contact_dist"][0, :4], -0.01, atol=1e-6)
+  np.testing.assert_allclose(np.abs(o["contact_pos"][0, :12].reshape(4, 3)[:, :2]), [[0.2, 0.1]] * 4, atol=1e-6)
+
+  mu, g = 0.65, 9.81
+  for tan_theta, slides in ((0.5, False), (0.8, True)):
+    th = np.arctan(tan_theta)
+    m, sim = sim_of(KA._free_body_xml(
+      f"""<body name="blk" pos="0 0 0.05"><freejoint/><geom type="box" size="0.1 0.1 0.05" mass="1" friction="{mu} 0.005 0.0001"/></body>""",
+      gravity=f"{g * np.sin(th)} 0 {-g * np.cos(th)}",
+      plane=f'<geom name="floor" type="plane" size="5 5 0.1" friction="{mu} 0.005 0.0001"/>'))
+    vx = []
+    for _ in range(500):
+      sim.step()
+      vx.append(sim.data.qvel[0, 0].item())
+    if slides:
+      a = (vx[-1] - vx[249]) / (250 * m.timestep)
+      assert a == pytest.approx(g * (np.sin(th) - mu * np.cos(th)), rel=0.05)
+    else:
+      assert abs(vx[-1]) < 5e-3 and abs(sim.data.qpos[0, 0].item()) < 5e-3

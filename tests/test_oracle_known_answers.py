@@ -202,3 +202,87 @@ def test_compare_step_oracle_f32_vs_f64():
   rep = compare_step(Oracle(m, "f32").run(n, st, integrate=True), Oracle(m).run(n, st, integrate=True))
   assert not rep["failures"], rep["failures"]
   assert rep["int_match_rate"] >= 0.98
+
+
+def _free_body_xml(bodies: str, gravity: str = "0 0 -9.81", plane: str = "") -> str:
+  return f"""
+<mujoco>
+  <option timestep="0.002" gravity="{gravity}"/>
+  <worldbody>
+    {plane}
+    {bodies}
+  </worldbody>
+</mujoco>
+"""
+
+
+def test_capsule_capsule_crossing_distance_and_frame():
+  """Two crossed capsules (x- and y-axis, radius 0.05, centres 0.08 apart in z):
+  one contact, dist = 0.08 - 0.1 = -0.02, normal along z, position midway
+  between the surfaces on the common normal (MuJoCo's segment-segment test)."""
+  xml = _free_body_xml("""
+    <body name="a" pos="0 0 0.5"><freejoint/><geom type="capsule" fromto="-0.3 0 0 0.3 0 0" size="0.05"/></body>
+    <body name="b" pos="0.1 0.05 0.58"><freejoint/><geom type="capsule" fromto="0 -0.3 0 0 0.3 0" size="0.05"/></body>
+  """, gravity="0 0 0")
+  m = _model(xml)
+  out = Oracle(m).run(1, {"qpos": m.qpos0[None]}, integrate=False)
+  assert out["ncon"][0, 0] == 1
+  assert out["contact_dist"][0, 0] == pytest.approx(-0.02, abs=1e-12)
+  n = out["contact_frame"][0, 0:3]
+  assert abs(abs(n[2]) - 1.0) < 1e-12 and abs(n[0]) < 1e-12 and abs(n[1]) < 1e-12
+  np.testing.assert_allclose(out["contact_pos"][0, 0:3], [0.1, 0.0, 0.54], atol=1e-12)
+
+
+def test_capsule_capsule_separated_no_contact():
+  xml = _free_body_xml("""
+    <body name="a" pos="0 0 0.5"><freejoint/><geom type="capsule" fromto="-0.3 0 0 0.3 0 0" size="0.05"/></body>
+    <body name="b" pos="0 0 0.62"><freejoint/><geom type="capsule" fromto="0 -0.3 0 0 0.3 0" size="0.05"/></body>
+  """, gravity="0 0 0")
+  m = _model(xml)
+  out = Oracle(m).run(1, {"qpos": m.qpos0[None]}, integrate=False)
+  assert out["ncon"][0, 0] == 0  # surfaces 0.02 apart, zero margin
+
+
+def test_box_plane_corner_contacts():
+  """Box (half sizes 0.2 x 0.1 x 0.05) sunk 0.01 into the floor, axis aligned:
+  four corner contacts with dist -0.01 and normal +z (the Go1 trunk's pair)."""
+  xml = _free_body_xml("""<body name="box" pos="0 0 0.04"><freejoint/><geom type="box" size="0.2 0.1 0.05"/></body>""",
+                       plane='<geom name="floor" type="plane" size="5 5 0.1"/>')
+  m = _model(xml)
+  out = Oracle(m).run(1, {"qpos": m.qpos0[None]}, integrate=False)
+  nc = int(out["ncon"][0, 0])
+  assert nc == 4
+  dist = out["contact_dist"][0, :nc]
+  np.testing.assert_allclose(dist, -0.01, atol=1e-12)
+  pos = out["contact_pos"][0, : 3 * nc].reshape(nc, 3)
+  corners = {(round(abs(x), 9), round(abs(y), 9)) for x, y in pos[:, :2]}
+  assert corners == {(0.2, 0.1)} and len({(np.sign(x), np.sign(y)) for x, y in pos[:, :2]}) == 4
+  for i in range(nc):
+    np.testing.assert_allclose(out["contact_frame"][0, 9 * i : 9 * i + 3], [0, 0, 1], atol=1e-12)
+
+
+@pytest.mark.parametrize("tan_theta,slides", [(0.5, False), (0.8, True)])
+def test_block_on_incline_stick_slip_threshold(tan_theta, slides):
+  """A block on a plane with friction mu = 0.65 under gravity tilted by theta
+  (equivalent to an incline): it sticks when tan(theta) < mu and slides with
+  a = g (sin(theta) - mu cos(theta)) when tan(theta) > mu (pyramidal cone,
+  condim 3)."""
+  mu, g = 0.65, 9.81
+  th = np.arctan(tan_theta)
+  grav = f"{g * np.sin(th)} 0 {-g * np.cos(th)}"
+  xml = _free_body_xml(
+    f"""<body name="blk" pos="0 0 0.05"><freejoint/><geom type="box" size="0.1 0.1 0.05" mass="1" friction="{mu} 0.005 0.0001"/></body>""",
+    gravity=grav, plane=f'<geom name="floor" type="plane" size="5 5 0.1" friction="{mu} 0.005 0.0001"/>')
+  m = _model(xml)
+  orc = Oracle(m)
+  st = {"qpos": m.qpos0[None].copy()}
+  vx = []
+  for _ in range(500):  # 1 s
+    out = orc.run(1, st, integrate=True)
+    st = {k: out[k] for k in ("qpos", "qvel", "qacc_warmstart", "time")}
+    vx.append(st["qvel"][0, 0])
+  if slides:
+    a = (vx[-1] - vx[249]) / (250 * m.timestep)
+    assert a == pytest.approx(g * (np.sin(th) - mu * np.cos(th)), rel=0.05)
+  else:
+    assert abs(vx[-1]) < 5e-3 and abs(st["qpos"][0, 0]) < 5e-3

@@ -1,6 +1,9 @@
 """Kernel census of one captured env step (run under rocprofv3 --kernel-trace --stats).
-Setup steps are eager; then exactly K graph replays, so per-step counts = calls / K
-for kernels that only run inside the graph."""
+
+Steady state: random actions, episode lengths start uniform (resets and the
+gated forward fire as in the bench). Setup steps are eager; then exactly K
+graph replays, so per-step counts = calls / K for kernels that only run inside
+the graph. usage: python tools/env_kernel_census.py [task] [N] [K]"""
 import sys
 from pathlib import Path
 
@@ -11,16 +14,21 @@ import torch
 from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
 from mjlab_amd.tasks import load_env_cfg
 
-K = 50
-cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
-cfg.scene.num_envs = 4096
+task = sys.argv[1] if len(sys.argv) > 1 else "Mjlab-Velocity-Flat-Unitree-G1"
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+K = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+cfg = load_env_cfg(task)
+cfg.scene.num_envs = N
 env = ManagerBasedRlEnv(cfg, device="cuda:0")
 env.reset()
-a = torch.zeros(4096, 29, device="cuda:0")
-for _ in range(3):
-  env.step(a)
+g = torch.Generator(device="cuda:0").manual_seed(0)
+env.episode_length_buf.random_(0, int(env.max_episode_length), generator=g)
+adim = env.action_manager.total_action_dim
+acts = [2 * torch.rand(N, adim, device="cuda:0", generator=g) - 1 for _ in range(4)]
+for i in range(3):
+  env.step(acts[i % 4])
 torch.cuda.synchronize()
-for _ in range(K):
-  env.step(a)
+for i in range(K):
+  env.step(acts[i % 4])
 torch.cuda.synchronize()
-print("done")
+print("done", K)
