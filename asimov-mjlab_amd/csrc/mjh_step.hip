@@ -110,6 +110,7 @@ struct Rg {
 #define SPI(name) reinterpret_cast<int*>((Rg::name ? G : S) + Lo.name)
 
 thread_local std::string g_err;
+bool g_disable_spec = false;  // mjh_set_specialization(0): always the generic instance
 
 #ifdef MJH_PROFILE
 __device__ unsigned long long* g_prof;
@@ -778,14 +779,73 @@ __device__ __forceinline__ float row_state(int type, float D, float R, float fl,
   *force = 0.f; *cost = 0.f; return 0.f;
 }
 
+// ---- model specialisation -----------------------------------------------------
+// A kernel instance with SPEC >= 0 takes the model sizes, the per-world layout
+// and the model-image offsets as compile-time constants (mjh_spec_table.h,
+// generated by tools/gen_spec.py from the benchmark models): every LDS/global
+// scratch address folds into an instruction offset instead of living in
+// (spilled) scalar registers. SPEC = -1 is the generic instance. The host picks
+// a specialisation only when the model's launch plan matches it exactly.
+struct Sizes {
+#define X_SZS(name) int name;
+  MJH_MODEL_SIZES(X_SZS)
+#undef X_SZS
+};
+constexpr int kSizeInts = sizeof(Sizes) / 4;
+constexpr int kLayoutInts = sizeof(Layout) / 4;
+constexpr int kImgInts = sizeof(ImgOff) / 4;
+constexpr int kPlanInts = 1 + kSizeInts + kLayoutInts + kImgInts;
+
+template <int K> __device__ __forceinline__ Sizes spec_sizes(const mjh_model& m) {
+  Sizes z;
+#define X_SZG(name) z.name = m.name;
+  MJH_MODEL_SIZES(X_SZG)
+#undef X_SZG
+  return z;
+}
+// Word offsets (per world) of every data array inside one contiguous slab laid
+// out in MJH_DATA_ARRAYS order, array f starting at nworld * offset(f): when the
+// caller allocated the data that way (the Simulation does; checked on the host
+// per launch), a specialised instance derives every data pointer from d.qpos
+// with compile-time offsets instead of holding ~50 pointers in registers.
+struct DataOff {
+#define X_DOF(type, name, count) long long name;
+  MJH_DATA_ARRAYS(X_DOF)
+#undef X_DOF
+};
+__host__ __device__ __forceinline__ DataOff data_offsets(const Sizes& Z) {
+#define X_DZ(name) const int name = Z.name;
+  MJH_MODEL_SIZES(X_DZ)
+#undef X_DZ
+  DataOff o{};
+  long long k = 0;
+#define X_DO(type, name, count) o.name = k; k += ((count) > 1 ? (count) : 1);
+  MJH_DATA_ARRAYS(X_DO)
+#undef X_DO
+  (void)nchain; (void)ncolgeom; (void)npair; (void)nsensor; (void)nmocap; (void)nconmax; (void)njmax; (void)na;
+  (void)nsensordata; (void)nq; (void)nv; (void)nu; (void)nbody; (void)njnt; (void)ngeom; (void)nsite;
+  return o;
+}
+template <int K> __device__ __forceinline__ Layout spec_layout(const Layout& a) { return a; }
+template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) { return a; }
+
+#include "mjh_spec_table.h"
+
 // ---- the step kernel --------------------------------------------------------
 #ifndef MJH_MINWAVES
 #define MJH_MINWAVES 1
 #endif
-template <int WPB, bool STEP, int NVP>
-__global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo,
-                                                         const ImgOff Io, const unsigned char* gate) {
+template <int WPB, bool STEP, int NVP, int SPEC = -1, bool SLAB = false>
+__global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo_,
+                                                         const ImgOff Io_, const unsigned char* gate) {
   constexpr int NT = 64;  // one wave per world
+  const Layout Lo = spec_layout<SPEC>(Lo_);
+  const ImgOff Io = spec_imgoff<SPEC>(Io_);
+  const Sizes Z = spec_sizes<SPEC>(m);
+  const DataOff DO = data_offsets(Z);
+  char* const slab = reinterpret_cast<char*>(d.qpos);
+  const long long nw4 = 4ll * d.nworld;
+#define DP(name) (SLAB ? reinterpret_cast<decltype(d.name)>(slab + DO.name * nw4) : d.name)
   extern __shared__ float smem[];
   if (gate != nullptr && *gate == 0) return;  // gated forward: nothing to recompute
   // shared model image -> LDS (whole workgroup, 16-byte coalesced)
@@ -806,7 +866,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   int* SI = reinterpret_cast<int*>(S);
   float* G = d.scratch + (long long)w * d.scratch_words;  // this world's global scratch
   const long long W = w;
-  const int nq = m.nq, nv = m.nv, nb = m.nbody, nu = m.nu, nj = m.njnt;
+  const int nq = Z.nq, nv = Z.nv, nb = Z.nbody, nu = Z.nu, nj = Z.njnt;
   const int ldm = Lo.ldm, ldj = Lo.ldj;
 
   float* qpos = SP(qpos);
@@ -899,8 +959,8 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   (void)SI;
 
   // ---------------------------------------------------------------- load state
-  for (int i = tid; i < nq; i += NT) qpos[i] = d.qpos[W * nq + i];
-  for (int i = tid; i < nv; i += NT) qvel[i] = d.qvel[W * nv + i];
+  for (int i = tid; i < nq; i += NT) qpos[i] = DP(qpos)[W * nq + i];
+  for (int i = tid; i < nv; i += NT) qvel[i] = DP(qvel)[W * nv + i];
   if (tid < I_COUNT) ints[tid] = (tid == I_MISC) ? 0x7fffffff : 0;
   wsync();
   PROF(0);
@@ -985,16 +1045,16 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
 
   PROF(27);
   // geoms (all written out; collision geoms kept in LDS) and sites
-  for (int g = tid; g < m.ngeom; g += NT) {
+  for (int g = tid; g < Z.ngeom; g += NT) {
     const int b = IMG_I(geom_bodyid)[g];
     float t[3], GR[9], GM[9];
     mat_vec(t, xmat + 9 * b, geom_pos + 3 * g);
     float gp[3] = {xpos[3 * b] + t[0], xpos[3 * b + 1] + t[1], xpos[3 * b + 2] + t[2]};
     quat2mat(GR, geom_quat + 4 * g);
     mat_mul(GM, xmat + 9 * b, GR);
-    float* og = d.geom_xpos + W * m.ngeom * 3 + 3 * g;
+    float* og = DP(geom_xpos) + W * Z.ngeom * 3 + 3 * g;
     og[0] = gp[0]; og[1] = gp[1]; og[2] = gp[2];
-    float* om = d.geom_xmat + W * m.ngeom * 9 + 9 * g;
+    float* om = DP(geom_xmat) + W * Z.ngeom * 9 + 9 * g;
 #pragma unroll
     for (int k = 0; k < 9; k++) om[k] = GM[k];
     const int slot = IMG_I(geom_colslot)[g];
@@ -1005,7 +1065,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     }
   }
   PROF(28);
-  for (int s = tid; s < m.nsite; s += NT) {
+  for (int s = tid; s < Z.nsite; s += NT) {
     const int b = IMG_I(site_bodyid)[s];
     float t[3], SR[9], SM[9];
     mat_vec(t, xmat + 9 * b, site_pos + 3 * s);
@@ -1260,22 +1320,22 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     const float gear = IMG_F(actuator_gear)[i];
     const float len = gear * qpos[IMG_I(jnt_qposadr)[j]];
     const float vel = gear * qvel[IMG_I(jnt_dofadr)[j]];
-    float c = d.ctrl[W * nu + i];
+    float c = DP(ctrl)[W * nu + i];
     if (IMG_I(actuator_ctrllimited)[i]) c = clampf(c, IMG_F(actuator_ctrlrange)[2 * i], IMG_F(actuator_ctrlrange)[2 * i + 1]);
     const float* gp = IMG_F(actuator_gainprm) + 10 * i;
     const float* bp = IMG_F(actuator_biasprm) + 10 * i;
     float f = gp[0] * c + bp[0] + bp[1] * len + bp[2] * vel;
     if (IMG_I(actuator_forcelimited)[i]) f = clampf(f, IMG_F(actuator_forcerange)[2 * i], IMG_F(actuator_forcerange)[2 * i + 1]);
     act_force[i] = f;
-    d.actuator_force[W * nu + i] = f;
-    d.actuator_length[W * nu + i] = len;
-    d.actuator_velocity[W * nu + i] = vel;
+    DP(actuator_force)[W * nu + i] = f;
+    DP(actuator_length)[W * nu + i] = len;
+    DP(actuator_velocity)[W * nu + i] = vel;
     // one actuator per dof in mjlab models; atomic keeps it correct otherwise
     atomicAdd(&qfrc_act[IMG_I(jnt_dofadr)[j]], gear * f);
   }
   wsync();
   {
-    const float* xfrc = d.xfrc_applied + W * nb * 6;
+    const float* xfrc = DP(xfrc_applied) + W * nb * 6;
     // bodies with a nonzero applied wrench, found with one load round (lane =
     // body) instead of a dependent global-load chain per dof
     bool nzf = false;
@@ -1285,7 +1345,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     }
     const unsigned long long nzb = __ballot(nzf);
     for (int i = tid; i < nv; i += NT) {
-      float s = qfrc_passive[i] - qfrc_bias[i] + d.qfrc_applied[W * nv + i] + qfrc_act[i];
+      float s = qfrc_passive[i] - qfrc_bias[i] + DP(qfrc_applied)[W * nv + i] + qfrc_act[i];
       // J^T xfrc_applied at each body com
       const float* cd = cdof + 6 * i;
       for (unsigned long long bm = nzb; bm; bm &= bm - 1) {
@@ -1307,7 +1367,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
 
   // ---------------------------------------------------------------- collision
   {
-    const int npair = m.npair;
+    const int npair = Z.npair;
     for (int base = 0; base < npair; base += NT) {
       const int p = base + tid;
       Con cc[4];
@@ -1671,7 +1731,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     };
 
     // warm start: the cheaper of qacc_warmstart and qacc_smooth
-    for (int i = tid; i < nv; i += NT) qacc[i] = d.qacc_warmstart[W * nv + i];
+    for (int i = tid; i < nv; i += NT) qacc[i] = DP(qacc_warmstart)[W * nv + i];
     wsync();
     eval_point(qacc);
     float cost = update_constraint();
@@ -1796,8 +1856,8 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
 
   // ---------------------------------------------------------------- sensors
   {
-    float* sd = d.sensordata + W * m.nsensordata;
-    for (int s = 0; s < m.nsensor; s++) {
+    float* sd = DP(sensordata) + W * Z.nsensordata;
+    for (int s = 0; s < Z.nsensor; s++) {
       const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
       if (type == 40) {
         // contact sensor (MuJoCo mjSENS_CONTACT with mjlab's intprm encoding,
@@ -1974,7 +2034,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
       }
     }
     // remaining sensors are independent and cheap: one lane each
-    for (int s = tid; s < m.nsensor; s += NT) {
+    for (int s = tid; s < Z.nsensor; s += NT) {
       const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
       if (type == 40 || type == 35 || type == 36) continue;
       float* out = sd + adr;
@@ -2048,60 +2108,60 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   // ---------------------------------------------------------------- forward outputs
   PROF(7);
   for (int i = tid; i < nb * 3; i += NT) {
-    d.xpos[W * nb * 3 + i] = xpos[i];
-    d.xipos[W * nb * 3 + i] = xipos[i];
-    d.subtree_com[W * nb * 3 + i] = subtree_com[i];
+    DP(xpos)[W * nb * 3 + i] = xpos[i];
+    DP(xipos)[W * nb * 3 + i] = xipos[i];
+    DP(subtree_com)[W * nb * 3 + i] = subtree_com[i];
   }
-  for (int i = tid; i < nb * 4; i += NT) d.xquat[W * nb * 4 + i] = xquat[i];
+  for (int i = tid; i < nb * 4; i += NT) DP(xquat)[W * nb * 4 + i] = xquat[i];
   for (int i = tid; i < nb * 9; i += NT) {
-    d.xmat[W * nb * 9 + i] = xmat[i];
-    d.ximat[W * nb * 9 + i] = ximat[i];
+    DP(xmat)[W * nb * 9 + i] = xmat[i];
+    DP(ximat)[W * nb * 9 + i] = ximat[i];
   }
   for (int i = tid; i < nb * 6; i += NT) {
-    d.cvel[W * nb * 6 + i] = cvel[i];
-    d.cacc[W * nb * 6 + i] = cacc[i];
+    DP(cvel)[W * nb * 6 + i] = cvel[i];
+    DP(cacc)[W * nb * 6 + i] = cacc[i];
   }
   for (int i = tid; i < nj * 3; i += NT) {
-    d.xanchor[W * nj * 3 + i] = xanchor[i];
-    d.xaxis[W * nj * 3 + i] = xaxis[i];
+    DP(xanchor)[W * nj * 3 + i] = xanchor[i];
+    DP(xaxis)[W * nj * 3 + i] = xaxis[i];
   }
-  for (int i = tid; i < m.nsite * 3; i += NT) d.site_xpos[W * m.nsite * 3 + i] = sxpos[i];
-  for (int i = tid; i < m.nsite * 9; i += NT) d.site_xmat[W * m.nsite * 9 + i] = sxmat[i];
+  for (int i = tid; i < Z.nsite * 3; i += NT) DP(site_xpos)[W * Z.nsite * 3 + i] = sxpos[i];
+  for (int i = tid; i < Z.nsite * 9; i += NT) DP(site_xmat)[W * Z.nsite * 9 + i] = sxmat[i];
   for (int i = tid; i < nv; i += NT) {
-    d.qfrc_bias[W * nv + i] = qfrc_bias[i];
-    d.qfrc_passive[W * nv + i] = qfrc_passive[i];
-    d.qfrc_actuator[W * nv + i] = qfrc_act[i];
-    d.qfrc_smooth[W * nv + i] = qfrc_smooth[i];
-    d.qfrc_constraint[W * nv + i] = qfrc_con[i];
-    d.qacc_smooth[W * nv + i] = qacc_smooth[i];
-    d.qacc[W * nv + i] = qacc[i];
-    d.qacc_warmstart[W * nv + i] = qacc[i];
+    DP(qfrc_bias)[W * nv + i] = qfrc_bias[i];
+    DP(qfrc_passive)[W * nv + i] = qfrc_passive[i];
+    DP(qfrc_actuator)[W * nv + i] = qfrc_act[i];
+    DP(qfrc_smooth)[W * nv + i] = qfrc_smooth[i];
+    DP(qfrc_constraint)[W * nv + i] = qfrc_con[i];
+    DP(qacc_smooth)[W * nv + i] = qacc_smooth[i];
+    DP(qacc)[W * nv + i] = qacc[i];
+    DP(qacc_warmstart)[W * nv + i] = qacc[i];
   }
   for (int ci = tid; ci < ncon; ci += NT) {
-    const long long o = W * m.nconmax + ci;
-    d.contact_dist[o] = con_dist[ci];
-    for (int k = 0; k < 3; k++) d.contact_pos[3 * o + k] = con_pos[3 * ci + k];
-    for (int k = 0; k < 9; k++) d.contact_frame[9 * o + k] = con_frame[9 * ci + k];
-    for (int k = 0; k < 5; k++) d.contact_friction[5 * o + k] = con_fric[5 * ci + k];
-    d.contact_includemargin[o] = con_imargin[ci];
-    d.contact_dim[o] = con_dim[ci];
-    d.contact_geom[2 * o] = con_geom[2 * ci];
-    d.contact_geom[2 * o + 1] = con_geom[2 * ci + 1];
-    d.contact_efc_address[o] = con_efcadr[ci];
+    const long long o = W * Z.nconmax + ci;
+    DP(contact_dist)[o] = con_dist[ci];
+    for (int k = 0; k < 3; k++) DP(contact_pos)[3 * o + k] = con_pos[3 * ci + k];
+    for (int k = 0; k < 9; k++) DP(contact_frame)[9 * o + k] = con_frame[9 * ci + k];
+    for (int k = 0; k < 5; k++) DP(contact_friction)[5 * o + k] = con_fric[5 * ci + k];
+    DP(contact_includemargin)[o] = con_imargin[ci];
+    DP(contact_dim)[o] = con_dim[ci];
+    DP(contact_geom)[2 * o] = con_geom[2 * ci];
+    DP(contact_geom)[2 * o + 1] = con_geom[2 * ci + 1];
+    DP(contact_efc_address)[o] = con_efcadr[ci];
   }
   for (int r = tid; r < nefc; r += NT) {
-    const long long o = W * m.njmax + r;
-    d.efc_type[o] = efc_type[r];
-    d.efc_id[o] = efc_id[r];
-    d.efc_pos[o] = efc_pos[r];
-    d.efc_D[o] = efc_D[r];
-    d.efc_aref[o] = efc_aref[r];
-    d.efc_force[o] = efc_force[r];
+    const long long o = W * Z.njmax + r;
+    DP(efc_type)[o] = efc_type[r];
+    DP(efc_id)[o] = efc_id[r];
+    DP(efc_pos)[o] = efc_pos[r];
+    DP(efc_D)[o] = efc_D[r];
+    DP(efc_aref)[o] = efc_aref[r];
+    DP(efc_force)[o] = efc_force[r];
   }
   if (tid == 0) {
-    d.ncon[W] = ncon;
-    d.nefc[W] = nefc;
-    d.solver_niter[W] = niter;
+    DP(ncon)[W] = ncon;
+    DP(nefc)[W] = nefc;
+    DP(solver_niter)[W] = niter;
   }
 
   // ---------------------------------------------------------------- integration
@@ -2164,9 +2224,9 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
       }
     }
     wsync();
-    for (int i = tid; i < nq; i += NT) d.qpos[W * nq + i] = qpos[i];
-    for (int i = tid; i < nv; i += NT) d.qvel[W * nv + i] = qvel[i];
-    if (tid == 0) d.time[W] += dt;
+    for (int i = tid; i < nq; i += NT) DP(qpos)[W * nq + i] = qpos[i];
+    for (int i = tid; i < nv; i += NT) DP(qvel)[W * nv + i] = qvel[i];
+    if (tid == 0) DP(time)[W] += dt;
   }
 
   // non-finite check on the new state
@@ -2178,12 +2238,13 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     bad = bsum<NT>(bad, red);
     if (tid == 0) {
       const int f = ints[I_FLAGS] | (bad > 0.f ? MJH_FLAG_NONFINITE : 0);
-      d.flags[W] = f;
-      d.flags_acc[W] |= f;  // sticky until the caller clears it (overflow/NaN statistics)
+      DP(flags)[W] = f;
+      DP(flags_acc)[W] |= f;  // sticky until the caller clears it (overflow/NaN statistics)
     }
   }
 }
 
+#undef DP
 __global__ void repeat_kernel(float* dst, const float* src, long long nelem, long long total) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
     dst[i] = src[i % nelem];
@@ -2332,6 +2393,57 @@ Plan make_plan(const mjh_model* m, int wpb) {
   return p;
 }
 
+void plan_to_ints(const Plan& p, const mjh_model* m, int* v) {
+  v[0] = nvp_of(m->nv);
+  int k = 1;
+#define X_SZP(name) v[k++] = m->name;
+  MJH_MODEL_SIZES(X_SZP)
+#undef X_SZP
+  std::memcpy(v + k, &p.lo, sizeof(Layout));
+  std::memcpy(v + k + kLayoutInts, &p.io, sizeof(ImgOff));
+}
+
+// whether every data array sits in one slab at nworld * data_offsets() (the
+// Simulation's allocation), so a specialised instance may derive the pointers
+bool data_is_slab(const mjh_model* m, const mjh_data* d) {
+  Sizes z;
+#define X_SZH(name) z.name = m->name;
+  MJH_MODEL_SIZES(X_SZH)
+#undef X_SZH
+  const DataOff o = data_offsets(z);
+  const char* base = reinterpret_cast<const char*>(d->qpos);
+  bool ok = true;
+#define X_SL(type, name, count) ok = ok && reinterpret_cast<const char*>(d->name) == base + 4ll * o.name * d->nworld;
+  MJH_DATA_ARRAYS(X_SL)
+#undef X_SL
+  return ok;
+}
+
+// the specialised instance whose plan equals this model's, or -1
+int find_spec(const Plan& p, const mjh_model* m) {
+  if (MJH_NSPEC == 0) return -1;
+  int v[kPlanInts];
+  plan_to_ints(p, m, v);
+  for (int k = 0; k < MJH_NSPEC; k++)
+    if (std::memcmp(v, kSpecPlan[k], sizeof(v)) == 0) return k;
+  return -1;
+}
+
+template <bool STEP, int K>
+void launch_spec(int k, const Plan& p, const mjh_model* m, const mjh_data* d, const unsigned char* gate, hipStream_t s,
+                 int blocks) {
+  if constexpr (K < MJH_NSPEC) {
+    if (k != K) return launch_spec<STEP, K + 1>(k, p, m, d, gate, s, blocks);
+    auto kern = step_kernel<kWorldsPerBlock, STEP, kSpecNvp[K], K, true>;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * kWorldsPerBlock), p.shmem, s, *m, *d, p.lo, p.io, gate);
+  }
+}
+
 template <bool STEP>
 int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream) {
   if (mjh_model_check(m) != 0) return 1;
@@ -2355,7 +2467,12 @@ int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, voi
   }
   hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields), dim3(256), 0, s, *m, p.io);
   const int blocks = (d->nworld + kWorldsPerBlock - 1) / kWorldsPerBlock;
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * kWorldsPerBlock), p.shmem, s, *m, *d, p.lo, p.io, gate);
+  // specialised instances assume the slab data layout (data_is_slab)
+  const int k = (g_disable_spec || !data_is_slab(m, d)) ? -1 : find_spec(p, m);
+  if (k >= 0)
+    launch_spec<STEP, 0>(k, p, m, d, gate, s, blocks);
+  else
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * kWorldsPerBlock), p.shmem, s, *m, *d, p.lo, p.io, gate);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_err = std::string("step launch failed: ") + hipGetErrorString(e);
@@ -2392,6 +2509,26 @@ int mjh_model_check(const mjh_model* m) {
 int mjh_scratch_bytes(const mjh_model* m) { return (int)make_plan(m, kWorldsPerBlock).shmem; }
 
 int mjh_efc_capacity(const mjh_model* m) { return make_plan(m, kWorldsPerBlock).lo.rcap; }
+
+extern const int mjh_layout_ints = kLayoutInts;  // for tools/gen_spec.py
+
+int mjh_set_specialization(int enable) {
+  g_disable_spec = enable == 0;
+  return 0;
+}
+
+int mjh_spec_index(const mjh_model* m) { return find_spec(make_plan(m, kWorldsPerBlock), m); }
+
+int mjh_data_is_slab(const mjh_model* m, const mjh_data* d) { return data_is_slab(m, d) ? 1 : 0; }
+
+int mjh_plan_ints(const mjh_model* m, int* out, int cap) {
+  const Plan p = make_plan(m, kWorldsPerBlock);
+  int v[kPlanInts];
+  plan_to_ints(p, m, v);
+  if (cap < kPlanInts) return -1;
+  for (int i = 0; i < kPlanInts; i++) out[i] = v[i];
+  return kPlanInts;
+}
 
 long long mjh_scratch_words(const mjh_model* m) { return make_plan(m, kWorldsPerBlock).lo.gtotal; }
 

@@ -32,6 +32,10 @@ EXPORTS = (
   "mjh_image_words",
   "mjh_set_profile_buffer",
   "mjh_efc_capacity",
+  "mjh_plan_ints",
+  "mjh_spec_index",
+  "mjh_data_is_slab",
+  "mjh_set_specialization",
   "mjh_scratch_words",
   "mjh_step",
   "mjh_forward",
@@ -82,6 +86,12 @@ def lib() -> ctypes.CDLL:
   L.mjh_model_check.argtypes = [ctypes.c_void_p]
   L.mjh_scratch_bytes.argtypes = [ctypes.c_void_p]
   L.mjh_efc_capacity.argtypes = [ctypes.c_void_p]
+  L.mjh_plan_ints.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+  L.mjh_spec_index.argtypes = [ctypes.c_void_p]
+  L.mjh_data_is_slab.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+  L.mjh_set_specialization.argtypes = [ctypes.c_int]
+  if os.environ.get("MJH_SPEC") == "0":  # A/B timing: generic kernel instance only
+    L.mjh_set_specialization(0)
   L.mjh_image_words.argtypes = [ctypes.c_void_p]
   L.mjh_scratch_words.argtypes = [ctypes.c_void_p]
   L.mjh_scratch_words.restype = ctypes.c_longlong

@@ -208,10 +208,17 @@ class Simulation:
     self._model_bridge = Bridge(model_views, extra={"opt": make_opt(model, cfg)}, nworld=num_envs)
 
     # ---- data buffers ----
+    # one slab, array f at num_envs * (words per world of the arrays before it),
+    # header order: specialised kernel instances derive every data pointer
+    # from qpos with compile-time offsets (mjh_data_is_slab)
     self._data_flat: dict[str, torch.Tensor] = {}
-    for f in abi.data_array_fields():
-      n = max(1, abi.count(f, self.sizes))
-      self._data_flat[f.name] = torch.zeros((num_envs, n), dtype=_TORCH_DT[f.ctype], device=device)
+    counts = [(f, max(1, abi.count(f, self.sizes))) for f in abi.data_array_fields()]
+    self._slab = torch.zeros(num_envs * sum(c for _, c in counts), dtype=torch.float32, device=device)
+    off = 0
+    for f, c in counts:
+      v = self._slab[off * num_envs : (off + c) * num_envs].view(num_envs, c)
+      self._data_flat[f.name] = v if _TORCH_DT[f.ctype] == torch.float32 else v.view(_TORCH_DT[f.ctype])
+      off += c
     self._data_flat["qpos"][:] = torch.as_tensor(model.qpos0, dtype=torch.float32, device=device)
     data_views = {n: self._data_view(n) for n in self._data_flat}
     self.epoch = Epoch()

@@ -119,6 +119,25 @@ long long mjh_scratch_words(const mjh_model* m);
  * dropped and reported through flags bit 1. */
 int mjh_efc_capacity(const mjh_model* m);
 
+/* Build-time introspection (tools/gen_spec.py): the launch plan of model m as
+ * ints — [nvp, model sizes (MJH_MODEL_SIZES order), per-world layout, model
+ * image offsets] — written to out (capacity cap). Returns the count, or -1 if
+ * cap is too small. Used to compile model-specialized kernel instances whose
+ * layout offsets and sizes are compile-time constants. */
+int mjh_plan_ints(const mjh_model* m, int* out, int cap);
+
+/* Index of the compiled model-specialised instance the step/forward launches
+ * of model m use (-1: the generic instance). */
+int mjh_spec_index(const mjh_model* m);
+
+/* 1 if every data array of d lies in one slab, array f at nworld * (words per
+ * world of the arrays before f, MJH_DATA_ARRAYS order) from d->qpos — the
+ * layout specialised instances require (otherwise the generic one runs). */
+int mjh_data_is_slab(const mjh_model* m, const mjh_data* d);
+
+/* 0: always launch the generic instance (A/B timing, tests); 1: default. */
+int mjh_set_specialization(int enable);
+
 /* Diagnostic builds only (-DMJH_PROFILE): per-world phase timestamps. */
 int mjh_set_profile_buffer(void* ptr);
 

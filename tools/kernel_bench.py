@@ -1,9 +1,12 @@
 """Time the physics step kernel alone at the bench size (diagnostic tool).
 
-usage: MJH_LIB=<lib.so> python tools/kernel_bench.py [N] [launches]
-Settles random G1 states for 20 steps, then times `launches` step launches
-with HIP events and reports ms/launch, world-steps/s, mean nefc and iterations.
+usage: [MJH_LIB=<lib.so>] [MJH_SPEC=0] python tools/kernel_bench.py [N] [launches] [task]
+Builds the task's model exactly as the env does (so the model-specialised
+instance is used unless MJH_SPEC=0), settles random states for 20 steps, then
+times `launches` step launches with HIP events and reports ms/launch,
+world-steps/s, mean nefc and iterations.
 """
+import ctypes
 import os
 import sys
 from pathlib import Path
@@ -14,14 +17,18 @@ sys.path.insert(0, str(ROOT))
 import numpy as np
 import torch
 
-from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg
-from tests.scenes import g1_scene_model, random_states
+from mjlab_amd.scene.scene import Scene
+from mjlab_amd.sim import Simulation, native
+from mjlab_amd.tasks import load_env_cfg
+from tests.scenes import random_states
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 launches = int(sys.argv[2]) if len(sys.argv) > 2 else 40
-m = g1_scene_model(n)
-sim = Simulation(n, SimulationCfg(nconmax=50, njmax=300, balance_worlds=os.environ.get("BALANCE") == "1",
-                                 mujoco=MujocoCfg(timestep=0.005, iterations=10, ls_iterations=20)), m, "cuda:0")
+task = sys.argv[3] if len(sys.argv) > 3 else "Mjlab-Velocity-Flat-Unitree-G1"
+cfg = load_env_cfg(task)
+cfg.scene.num_envs = n
+m = Scene(cfg.scene, device="cuda:0").compile()
+sim = Simulation(n, cfg.sim, m, "cuda:0")
 st = random_states(m, n, np.random.default_rng(0), drop=0.03)
 for k, v in st.items():
   t = getattr(sim.data, k)
@@ -36,6 +43,7 @@ for _ in range(launches):
 e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / launches
-print(f"{os.environ.get('MJH_LIB', 'libmjh.so')}: N={n} {ms:.3f} ms/launch  {n / ms * 1e3:,.0f} world-steps/s  "
+spec = native.lib().mjh_spec_index(ctypes.addressof(sim._mstruct)) if os.environ.get("MJH_SPEC") != "0" else -1
+print(f"{os.environ.get('MJH_LIB', 'libmjh.so')} spec={spec}: {task} N={n} {ms:.3f} ms/launch  {n / ms * 1e3:,.0f} world-steps/s  "
       f"nefc {sim.data.nefc.float().mean().item():.1f}  niter {sim.data.solver_niter.float().mean().item():.2f}  "
       f"lds {sim.scratch_bytes()} rcap {sim.efc_capacity()} flags {int((sim.data.flags != 0).sum())}")
