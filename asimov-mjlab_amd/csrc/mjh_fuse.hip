@@ -1,0 +1,414 @@
+// mjh_fuse.hip — fused reset-path / event / command kernels for the env layer
+// (gfx950).
+//
+// The masked reset of a manager-based env (manager_based_rl_env.py:210-245 of
+// the reference: events, then every manager's reset with its episode logs) is
+// ~80 small torch launches per env step at 4096 envs, each a few microseconds
+// of dispatch for microseconds of work. These kernels do each manager's (or
+// event term's) whole masked update in one launch:
+//   * masked column means (+ row clear) — RewardManager.reset episode sums,
+//     CommandTerm.reset metrics;
+//   * masked flag counts — TerminationManager.reset episode logs;
+//   * uniform draws selected by a mask — interval-event and command timers;
+//   * reset_root_state_uniform / reset_joints_by_offset /
+//     push_by_setting_velocity (envs/mdp/events.py) with their EntityData
+//     writes into qpos / qvel;
+//   * UniformVelocityCommand resampling (velocity_command.py:103-123).
+//
+// Random draws come from a counter-based generator (splitmix64 finalizer over
+// seed, call-site key, a device step counter and the element index): stateless,
+// so the draws of a captured graph change with the step counter at every
+// replay and no host RNG state is consumed inside the graph. Distributions are
+// the reference's (U[lo, hi) per element); the stream is not torch's (the
+// reference's stream is already not reproduced by mask-based resets).
+#include <hip/hip_runtime.h>
+
+#include "../../include/mjh_abi.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+inline int grid(long long n) { return (int)((n + kBlock - 1) / kBlock); }
+int finish() { return hipGetLastError() == hipSuccess ? 0 : 2; }
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// U[0, 1) with 24 random bits, element `idx` of the draw keyed (seed, key, step)
+struct Rng {
+  unsigned long long base;
+  __device__ Rng(unsigned long long seed, unsigned long long key, const mjh_i64* ctr) {
+    const unsigned long long step = ctr ? (unsigned long long)*ctr : 0ull;
+    base = mix64(seed ^ mix64(key ^ mix64(step + 0x9e3779b97f4a7c15ull)));
+  }
+  __device__ __forceinline__ float u01(unsigned long long idx) const {
+    return (float)(mix64(base + (idx + 1ull) * 0x9e3779b97f4a7c15ull) >> 40) * (1.f / 16777216.f);
+  }
+};
+
+__device__ __forceinline__ bool on(const unsigned char* mask, long long e) { return mask == nullptr || mask[e] != 0; }
+
+// ---- rotations (formulas of mjh_envops.hip / utils/math.py) ------------------
+__device__ __forceinline__ void qmul(float o[4], const float a[4], const float b[4]) {
+  const float ww = (a[3] + a[1]) * (b[1] + b[2]);
+  const float yy = (a[0] - a[2]) * (b[0] + b[3]);
+  const float zz = (a[0] + a[2]) * (b[0] - b[3]);
+  const float xx = ww + yy + zz;
+  const float qq = 0.5f * (xx + (a[3] - a[1]) * (b[1] - b[2]));
+  o[0] = qq - ww + (a[3] - a[2]) * (b[2] - b[3]);
+  o[1] = qq - xx + (a[1] + a[0]) * (b[1] + b[0]);
+  o[2] = qq - yy + (a[0] - a[1]) * (b[2] + b[3]);
+  o[3] = qq - zz + (a[3] + a[2]) * (b[0] - b[1]);
+}
+__device__ __forceinline__ void qeuler(float o[4], float roll, float pitch, float yaw) {
+  const float cy = cosf(yaw * 0.5f), sy = sinf(yaw * 0.5f);
+  const float cr = cosf(roll * 0.5f), sr = sinf(roll * 0.5f);
+  const float cp = cosf(pitch * 0.5f), sp = sinf(pitch * 0.5f);
+  o[0] = cy * cr * cp + sy * sr * sp;
+  o[1] = cy * sr * cp - sy * cr * sp;
+  o[2] = cy * cr * sp + sy * sr * cp;
+  o[3] = sy * cr * cp - cy * sr * sp;
+}
+// quat_apply_inverse(q, v)
+__device__ __forceinline__ void qrot_inv(float o[3], const float q[4], const float v[3]) {
+  const float w = q[0], x = q[1], y = q[2], z = q[3];
+  const float tx = 2.f * (y * v[2] - z * v[1]), ty = 2.f * (z * v[0] - x * v[2]), tz = 2.f * (x * v[1] - y * v[0]);
+  o[0] = (v[0] - w * tx) + (y * tz - z * ty);
+  o[1] = (v[1] - w * ty) + (z * tx - x * tz);
+  o[2] = (v[2] - w * tz) + (x * ty - y * tx);
+}
+
+// ---- masked reductions (one workgroup; fixed summation order) ---------------
+struct ColArgs {
+  float* c[MJH_MAX_TERMS];
+  long long cs[MJH_MAX_TERMS];
+  int ncols;
+};
+
+__global__ void masked_means_kernel(const ColArgs a, const unsigned char* __restrict__ mask, float scale, int zero_rows,
+                                    float* __restrict__ out, long long n) {
+  __shared__ float part[kBlock];
+  __shared__ float cnt_s;
+  float cnt = 0.f;
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) cnt += on(mask, e) ? 1.f : 0.f;
+  part[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cnt_s = fmaxf(part[0], 1.f);
+  __syncthreads();
+  const float denom = cnt_s;
+  for (int t = 0; t < a.ncols; t++) {
+    float* col = a.c[t];
+    float s = 0.f;
+    for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+      if (on(mask, e)) {
+        s += col[e * a.cs[t]];
+        if (zero_rows) col[e * a.cs[t]] = 0.f;
+      }
+    }
+    __syncthreads();
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[t] = part[0] / denom * scale;
+  }
+}
+
+struct FlagArgs {
+  const unsigned char* f[MJH_MAX_TERMS];
+  int nflags;
+};
+
+__global__ void masked_counts_kernel(const FlagArgs a, const unsigned char* __restrict__ mask, mjh_i64* __restrict__ out,
+                                     long long n) {
+  __shared__ int part[kBlock];
+  for (int t = 0; t < a.nflags; t++) {
+    int c = 0;
+    for (long long e = threadIdx.x; e < n; e += blockDim.x) c += (on(mask, e) && a.f[t][e]) ? 1 : 0;
+    __syncthreads();
+    part[threadIdx.x] = c;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[t] = part[0];
+  }
+}
+
+// ---- masked draws -------------------------------------------------------------
+__global__ void uniform_draws_kernel(float* __restrict__ out, long long n, unsigned long long seed,
+                                     unsigned long long key, const mjh_i64* ctr) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = Rng(seed, key, ctr).u01(i);
+}
+
+__global__ void uniform_where_kernel(float* __restrict__ t, const unsigned char* __restrict__ mask, float lo, float hi,
+                                     unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  if (on(mask, e)) t[e] = Rng(seed, key, ctr).u01(e) * (hi - lo) + lo;
+}
+
+// interval event timers (event_manager.py:120-145): t -= dt; due = t < 1e-6;
+// due timers are redrawn from U[lo, hi)
+__global__ void interval_tick_kernel(float* __restrict__ t, float dt, float lo, float hi, unsigned char* __restrict__ due,
+                                     unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float v = t[e] - dt;
+  const bool d = v < 1e-6f;
+  t[e] = d ? Rng(seed, key, ctr).u01(e) * (hi - lo) + lo : v;
+  due[e] = d ? 1 : 0;
+}
+
+// ---- event terms ----------------------------------------------------------------
+struct Range6 {
+  float lo[6], hi[6];
+};
+
+// reset_root_state_uniform (envs/mdp/events.py:45-84): draws u[e, 0:6] for the
+// pose, u[e, 6:12] for the velocity (element index e * 12 + j)
+__global__ void reset_root_uniform_kernel(float* __restrict__ qpos, long long qs, int qadr, float* __restrict__ qvel,
+                                          long long vs, int vadr, const unsigned char* __restrict__ mask,
+                                          const float* __restrict__ rs, long long rss, const float* __restrict__ org,
+                                          long long os, const Range6 pose, const Range6 vel, int pose_rand, int vel_rand,
+                                          unsigned long long seed, unsigned long long key, const mjh_i64* ctr,
+                                          long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n || !on(mask, e)) return;
+  const Rng rng(seed, key, ctr);
+  const float* r = rs + e * rss;
+  float p6[6], v6[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    p6[j] = pose_rand ? rng.u01(e * 12 + j) * (pose.hi[j] - pose.lo[j]) + pose.lo[j] : 0.f;
+    v6[j] = vel_rand ? rng.u01(e * 12 + 6 + j) * (vel.hi[j] - vel.lo[j]) + vel.lo[j] : 0.f;
+  }
+  float qe[4], q[4];
+  qeuler(qe, p6[3], p6[4], p6[5]);
+  const float q0[4] = {r[3], r[4], r[5], r[6]};
+  qmul(q, q0, qe);
+  float* qp = qpos + e * qs + qadr;
+  const float* o = org + e * os;
+  qp[0] = r[0] + p6[0] + o[0];
+  qp[1] = r[1] + p6[1] + o[1];
+  qp[2] = r[2] + p6[2] + o[2];
+  qp[3] = q[0]; qp[4] = q[1]; qp[5] = q[2]; qp[6] = q[3];
+  // write_root_link_velocity: linear in the world frame, angular in the new body frame
+  const float w[3] = {r[10] + v6[3], r[11] + v6[4], r[12] + v6[5]};
+  float wb[3];
+  qrot_inv(wb, q, w);
+  float* qv = qvel + e * vs + vadr;
+  qv[0] = r[7] + v6[0]; qv[1] = r[8] + v6[1]; qv[2] = r[9] + v6[2];
+  qv[3] = wb[0]; qv[4] = wb[1]; qv[5] = wb[2];
+}
+
+// reset_joints_by_offset (envs/mdp/events.py:87-121) for k consecutive joints:
+// draws u[e, 0:k] position offsets, u[e, k:2k] velocity offsets
+__global__ void reset_joints_offset_kernel(float* __restrict__ qpos, long long qs, int qadr, float* __restrict__ qvel,
+                                           long long vs, int vadr, int k, const unsigned char* __restrict__ mask,
+                                           const float* __restrict__ dp, long long dps, const float* __restrict__ dv,
+                                           long long dvs, const float* __restrict__ lim, long long ls, float plo,
+                                           float phi, float vlo, float vhi, int prand, int vrand,
+                                           unsigned long long seed, unsigned long long key, const mjh_i64* ctr,
+                                           long long n) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * k) return;
+  const long long e = t / k;
+  const int j = (int)(t - e * k);
+  if (!on(mask, e)) return;
+  const Rng rng(seed, key, ctr);
+  float p = dp[e * dps + j];
+  if (prand) p += rng.u01(e * 2 * k + j) * (phi - plo) + plo;
+  const float* l = lim + e * ls + 2 * j;
+  p = fminf(fmaxf(p, l[0]), l[1]);
+  float v = dv[e * dvs + j];
+  if (vrand) v += rng.u01(e * 2 * k + k + j) * (vhi - vlo) + vlo;
+  qpos[e * qs + qadr + j] = p;
+  qvel[e * vs + vadr + j] = v;
+}
+
+// push_by_setting_velocity (envs/mdp/events.py:124-137): root_link_vel_w + U6,
+// written as the free joint's qvel (angular part into the body frame)
+__global__ void push_velocity_kernel(const float* __restrict__ qpos, long long qs, int qadr, float* __restrict__ qvel,
+                                     long long vs, int vadr, const unsigned char* __restrict__ mask,
+                                     const float* __restrict__ vw, long long vws, const Range6 r,
+                                     unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n || !on(mask, e)) return;
+  const Rng rng(seed, key, ctr);
+  const float* v = vw + e * vws;
+  float u[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) u[j] = v[j] + (rng.u01(e * 6 + j) * (r.hi[j] - r.lo[j]) + r.lo[j]);
+  const float* qp = qpos + e * qs + qadr;
+  const float q[4] = {qp[3], qp[4], qp[5], qp[6]};
+  float wb[3];
+  qrot_inv(wb, q, u + 3);
+  float* qv = qvel + e * vs + vadr;
+  qv[0] = u[0]; qv[1] = u[1]; qv[2] = u[2];
+  qv[3] = wb[0]; qv[4] = wb[1]; qv[5] = wb[2];
+}
+
+// ---- command terms --------------------------------------------------------------
+// CommandTerm.reset + UniformVelocityCommand._resample_command for the masked
+// envs (command_manager.py:34-47, velocity_command.py:103-123): draws per env
+// u[e, 0] timer, u[e, 1:5] lin_x / lin_y / ang_z / heading, u[e, 5] heading env,
+// u[e, 6] standing env (element e * 8 + j). `reset` != 0: the counter restarts
+// (masked_fill 0, then += 1), else it is incremented.
+__global__ void velocity_resample_kernel(const unsigned char* __restrict__ mask, const float* __restrict__ ranges,
+                                         float t_lo, float t_hi, float rel_heading, float rel_standing,
+                                         int heading_command, int reset, float* __restrict__ cmd,
+                                         float* __restrict__ heading_target, unsigned char* __restrict__ is_heading,
+                                         unsigned char* __restrict__ is_standing, float* __restrict__ time_left,
+                                         mjh_i64* __restrict__ counter, unsigned long long seed, unsigned long long key,
+                                         const mjh_i64* ctr, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n || !on(mask, e)) return;
+  const Rng rng(seed, key, ctr);
+  const long long b = e * 8;
+  time_left[e] = rng.u01(b) * (t_hi - t_lo) + t_lo;
+#pragma unroll
+  for (int j = 0; j < 3; j++) cmd[e * 3 + j] = rng.u01(b + 1 + j) * (ranges[2 * j + 1] - ranges[2 * j]) + ranges[2 * j];
+  if (heading_command) {
+    heading_target[e] = rng.u01(b + 4) * (ranges[7] - ranges[6]) + ranges[6];
+    is_heading[e] = rng.u01(b + 5) <= rel_heading ? 1 : 0;
+  }
+  is_standing[e] = rng.u01(b + 6) <= rel_standing ? 1 : 0;
+  counter[e] = reset ? 1 : counter[e] + 1;
+}
+
+// EventManager reset bookkeeping (event_manager.py:146-156): last = step, once = 1
+__global__ void event_mark_kernel(int* __restrict__ last, unsigned char* __restrict__ once,
+                                  const unsigned char* __restrict__ mask, const mjh_i64* __restrict__ step, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n || !on(mask, e)) return;
+  last[e] = step ? (int)*step : 0;
+  once[e] = 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mjh_masked_means(float* const* cols, const long long* strides, int ncols, const unsigned char* mask, float scale,
+                     int zero_rows, float* out, long long n, void* stream) {
+  if (ncols <= 0) return 0;
+  if (ncols > MJH_MAX_TERMS) return 1;
+  ColArgs a{};
+  for (int t = 0; t < ncols; t++) {
+    a.c[t] = cols[t];
+    a.cs[t] = strides[t];
+  }
+  a.ncols = ncols;
+  hipLaunchKernelGGL(masked_means_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, a, mask, scale, zero_rows, out, n);
+  return finish();
+}
+
+int mjh_masked_counts(const unsigned char* const* flags, int nflags, const unsigned char* mask, mjh_i64* out, long long n,
+                      void* stream) {
+  if (nflags <= 0) return 0;
+  if (nflags > MJH_MAX_TERMS) return 1;
+  FlagArgs a{};
+  for (int t = 0; t < nflags; t++) a.f[t] = flags[t];
+  a.nflags = nflags;
+  hipLaunchKernelGGL(masked_counts_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, a, mask, out, n);
+  return finish();
+}
+
+int mjh_uniform_draws(float* out, long long n, unsigned long long seed, unsigned long long key, const mjh_i64* ctr,
+                      void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(uniform_draws_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, out, n, seed, key, ctr);
+  return finish();
+}
+
+int mjh_uniform_where(float* t, const unsigned char* mask, float lo, float hi, unsigned long long seed,
+                      unsigned long long key, const mjh_i64* ctr, long long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(uniform_where_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, t, mask, lo, hi, seed, key,
+                     ctr, n);
+  return finish();
+}
+
+int mjh_interval_tick(float* t, float dt, float lo, float hi, unsigned char* due, unsigned long long seed,
+                      unsigned long long key, const mjh_i64* ctr, long long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(interval_tick_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, t, dt, lo, hi, due, seed,
+                     key, ctr, n);
+  return finish();
+}
+
+int mjh_reset_root_uniform(float* qpos, long long qs, int qadr, float* qvel, long long vs, int vadr,
+                           const unsigned char* mask, const float* root_state, long long rss, const float* origins,
+                           long long os, const float* pose_lo, const float* pose_hi, const float* vel_lo,
+                           const float* vel_hi, int pose_rand, int vel_rand, unsigned long long seed,
+                           unsigned long long key, const mjh_i64* ctr, long long n, void* stream) {
+  if (n <= 0) return 0;
+  Range6 p{}, v{};
+  for (int j = 0; j < 6; j++) {
+    p.lo[j] = pose_lo[j]; p.hi[j] = pose_hi[j];
+    v.lo[j] = vel_lo[j]; v.hi[j] = vel_hi[j];
+  }
+  hipLaunchKernelGGL(reset_root_uniform_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, qpos, qs, qadr, qvel,
+                     vs, vadr, mask, root_state, rss, origins, os, p, v, pose_rand, vel_rand, seed, key, ctr, n);
+  return finish();
+}
+
+int mjh_reset_joints_offset(float* qpos, long long qs, int qadr, float* qvel, long long vs, int vadr, int k,
+                            const unsigned char* mask, const float* def_pos, long long dps, const float* def_vel,
+                            long long dvs, const float* lim, long long ls, float pos_lo, float pos_hi, float vel_lo,
+                            float vel_hi, int pos_rand, int vel_rand, unsigned long long seed, unsigned long long key,
+                            const mjh_i64* ctr, long long n, void* stream) {
+  if (n <= 0 || k <= 0) return 0;
+  hipLaunchKernelGGL(reset_joints_offset_kernel, dim3(grid(n * k)), dim3(kBlock), 0, (hipStream_t)stream, qpos, qs, qadr,
+                     qvel, vs, vadr, k, mask, def_pos, dps, def_vel, dvs, lim, ls, pos_lo, pos_hi, vel_lo, vel_hi,
+                     pos_rand, vel_rand, seed, key, ctr, n);
+  return finish();
+}
+
+int mjh_push_velocity(const float* qpos, long long qs, int qadr, float* qvel, long long vs, int vadr,
+                      const unsigned char* mask, const float* vel_w, long long vws, const float* lo, const float* hi,
+                      unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n, void* stream) {
+  if (n <= 0) return 0;
+  Range6 r{};
+  for (int j = 0; j < 6; j++) {
+    r.lo[j] = lo[j];
+    r.hi[j] = hi[j];
+  }
+  hipLaunchKernelGGL(push_velocity_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, qpos, qs, qadr, qvel, vs,
+                     vadr, mask, vel_w, vws, r, seed, key, ctr, n);
+  return finish();
+}
+
+int mjh_velocity_resample(const unsigned char* mask, const float* ranges, float t_lo, float t_hi, float rel_heading,
+                          float rel_standing, int heading_command, int reset, float* cmd, float* heading_target,
+                          unsigned char* is_heading, unsigned char* is_standing, float* time_left, mjh_i64* counter,
+                          unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n,
+                          void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(velocity_resample_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, mask, ranges, t_lo,
+                     t_hi, rel_heading, rel_standing, heading_command, reset, cmd, heading_target, is_heading,
+                     is_standing, time_left, counter, seed, key, ctr, n);
+  return finish();
+}
+
+int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, const mjh_i64* step, long long n,
+                   void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(event_mark_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, last, once, mask, step, n);
+  return finish();
+}
+
+}  // extern "C"

@@ -371,3 +371,145 @@ def reward_combine(vals: list, weights: torch.Tensor, dt: float, reward: torch.T
   native.check(native.lib().mjh_reward_combine(ptrs, strides, T, _ptr(weights), float(dt), _ptr(reward),
                                                _ptr(step_reward), _ptr(sums), n, _stream()), "mjh_reward_combine")
   return True
+
+
+# ---- reset path, events and commands (csrc/mjh_fuse.hip) -----------------------
+def _bool_mask(m) -> bool:
+  return m is None or (isinstance(m, torch.Tensor) and m.is_cuda and m.dtype == torch.bool and m.dim() == 1
+                       and m.is_contiguous())
+
+
+def _mptr(m):
+  return _ptr(m) if m is not None else None
+
+
+def _site_hash(site: str) -> int:
+  h = 1469598103934665603
+  for ch in site.encode():
+    h = ((h ^ ch) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+  return h
+
+
+def rng_args(env, site: str):
+  """(seed, key, step-counter pointer) of the device random stream for one call
+  site: draws differ per site, per env step (the counter is a device tensor the
+  env step increments, so graph replays draw anew) and per host call."""
+  salt = env.__dict__.get("_rng_calls", 0) + 1
+  env.__dict__["_rng_calls"] = salt
+  key = (_site_hash(site) ^ (salt * 0x9E3779B97F4A7C15)) & 0xFFFFFFFFFFFFFFFF
+  return ctypes.c_ulonglong(env._rng_seed), ctypes.c_ulonglong(key), _ptr(env._rng_ctr)
+
+
+def uniform_draws(seed, key, ctr: torch.Tensor | None, n: int, device) -> torch.Tensor:
+  """The U[0,1) stream the fused kernels draw from (tests reconstruct them with it)."""
+  out = torch.empty(n, dtype=torch.float32, device=device)
+  native.check(native.lib().mjh_uniform_draws(_ptr(out), n, ctypes.c_ulonglong(seed), ctypes.c_ulonglong(key),
+                                              _ptr(ctr) if ctr is not None else None, _stream()), "mjh_uniform_draws")
+  return out
+
+
+def masked_means(cols: list, mask, scale: float, zero_rows: bool, out: torch.Tensor) -> bool:
+  """out[t] = scale * mean over masked rows of cols[t] (and clear them) in one launch."""
+  T = len(cols)
+  if T == 0 or T > MAX_TERMS or not _bool_mask(mask) or not out.is_cuda or out.numel() < T:
+    return False
+  n = cols[0].shape[0]
+  ptrs = (ctypes.c_void_p * T)()
+  strides = (ctypes.c_longlong * T)()
+  for i, c in enumerate(cols):
+    if not (c.is_cuda and c.dtype == torch.float32 and c.dim() == 1 and c.shape[0] == n):
+      return False
+    ptrs[i], strides[i] = c.data_ptr(), c.stride(0)
+  if mask is not None and mask.shape[0] != n:
+    return False
+  native.check(native.lib().mjh_masked_means(ptrs, strides, T, _mptr(mask), float(scale), int(zero_rows), _ptr(out), n,
+                                             _stream()), "mjh_masked_means")
+  return True
+
+
+def masked_counts(flags: list, mask, out: torch.Tensor) -> bool:
+  """out[t] = count(flags[t] & mask) (int64) in one launch."""
+  T = len(flags)
+  if T == 0 or T > MAX_TERMS or not _bool_mask(mask) or out.dtype != torch.int64 or not out.is_cuda:
+    return False
+  if not all(_bool_mask(f) and f is not None for f in flags):
+    return False
+  ptrs = (ctypes.c_void_p * T)(*[f.data_ptr() for f in flags])
+  native.check(native.lib().mjh_masked_counts(ptrs, T, _mptr(mask), _ptr(out), flags[0].shape[0], _stream()),
+               "mjh_masked_counts")
+  return True
+
+
+def uniform_where(env, site: str, t: torch.Tensor, mask, lo: float, hi: float) -> bool:
+  """t[mask] = U[lo, hi) in one launch (draws from the device stream)."""
+  if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 1 and t.is_contiguous() and _bool_mask(mask)):
+    return False
+  seed, key, ctr = rng_args(env, site)
+  native.check(native.lib().mjh_uniform_where(_ptr(t), _mptr(mask), float(lo), float(hi), seed, key, ctr, t.shape[0],
+                                              _stream()), "mjh_uniform_where")
+  return True
+
+
+def interval_tick(env, site: str, t: torch.Tensor, dt: float, lo: float, hi: float, due: torch.Tensor) -> bool:
+  if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 1 and t.is_contiguous() and _bool_mask(due)):
+    return False
+  seed, key, ctr = rng_args(env, site)
+  native.check(native.lib().mjh_interval_tick(_ptr(t), float(dt), float(lo), float(hi), _ptr(due), seed, key, ctr,
+                                              t.shape[0], _stream()), "mjh_interval_tick")
+  return True
+
+
+def _f6(v) -> ctypes.Array:
+  return (ctypes.c_float * 6)(*[float(x) for x in v])
+
+
+def reset_root_uniform(env, site: str, qpos, qadr: int, qvel, vadr: int, mask, root_state, origins, lo6, hi6, vlo6, vhi6,
+                       pose_rand: bool, vel_rand: bool) -> bool:
+  ok = all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 for t in (qpos, qvel, root_state, origins))
+  if not ok or not _bool_mask(mask) or root_state.shape[1] != 13 or origins.shape[1] != 3:
+    return False
+  n = qpos.shape[0]
+  if root_state.shape[0] != n or origins.shape[0] != n:
+    return False
+  seed, key, ctr = rng_args(env, site)
+  native.check(native.lib().mjh_reset_root_uniform(
+    _ptr(qpos), qpos.stride(0), int(qadr), _ptr(qvel), qvel.stride(0), int(vadr), _mptr(mask), _ptr(root_state),
+    root_state.stride(0), _ptr(origins), origins.stride(0), _f6(lo6), _f6(hi6), _f6(vlo6), _f6(vhi6), int(pose_rand),
+    int(vel_rand), seed, key, ctr, n, _stream()), "mjh_reset_root_uniform")
+  return True
+
+
+def reset_joints_offset(env, site: str, qpos, qadr: int, qvel, vadr: int, mask, def_pos, def_vel, lim, prange, vrange) -> bool:
+  ok = all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 for t in (qpos, qvel, def_pos, def_vel))
+  if not ok or not _bool_mask(mask) or lim.dim() != 3 or lim.stride(2) != 1 or lim.stride(1) != 2:
+    return False
+  n, k = def_pos.shape
+  if def_vel.shape != (n, k) or lim.shape[:2] != (n, k) or qpos.shape[0] != n or lim.dtype != torch.float32:
+    return False
+  seed, key, ctr = rng_args(env, site)
+  pr, vr = tuple(prange) != (0.0, 0.0), tuple(vrange) != (0.0, 0.0)
+  native.check(native.lib().mjh_reset_joints_offset(
+    _ptr(qpos), qpos.stride(0), int(qadr), _ptr(qvel), qvel.stride(0), int(vadr), k, _mptr(mask), _ptr(def_pos),
+    def_pos.stride(0), _ptr(def_vel), def_vel.stride(0), _ptr(lim), lim.stride(0), float(prange[0]), float(prange[1]),
+    float(vrange[0]), float(vrange[1]), int(pr), int(vr), seed, key, ctr, n, _stream()), "mjh_reset_joints_offset")
+  return True
+
+
+def push_velocity(env, site: str, qpos, qadr: int, qvel, vadr: int, mask, vel_w, lo6, hi6) -> bool:
+  ok = all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 for t in (qpos, qvel, vel_w))
+  if not ok or not _bool_mask(mask) or vel_w.shape != (qpos.shape[0], 6):
+    return False
+  seed, key, ctr = rng_args(env, site)
+  native.check(native.lib().mjh_push_velocity(
+    _ptr(qpos), qpos.stride(0), int(qadr), _ptr(qvel), qvel.stride(0), int(vadr), _mptr(mask), _ptr(vel_w), vel_w.stride(0),
+    _f6(lo6), _f6(hi6), seed, key, ctr, qpos.shape[0], _stream()), "mjh_push_velocity")
+  return True
+
+
+def event_mark(last: torch.Tensor, once: torch.Tensor, mask, step: torch.Tensor) -> bool:
+  if not (last.is_cuda and last.dtype == torch.int32 and once.dtype == torch.bool and _bool_mask(mask)
+          and isinstance(step, torch.Tensor) and step.is_cuda and step.dtype == torch.int64 and step.numel() == 1):
+    return False
+  native.check(native.lib().mjh_event_mark(_ptr(last), _ptr(once), _mptr(mask), _ptr(step), last.shape[0], _stream()),
+               "mjh_event_mark")
+  return True

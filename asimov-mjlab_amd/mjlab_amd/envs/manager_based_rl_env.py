@@ -89,6 +89,10 @@ class ManagerBasedEnv:
     if cfg.seed is not None:
       cfg.seed = self.seed(cfg.seed)
     self._sim_step_counter = 0
+    # device random stream of the fused reset/event/command kernels (envops.rng_args):
+    # seed from torch's generator (seeded above), counter = env steps taken
+    self._rng_seed = int(torch.randint(0, 2**62, (1,)).item())
+    self._rng_ctr = torch.zeros((), dtype=torch.long, device=device)
     self.extras: dict = {"log": {}}
     self.obs_buf: dict = {}
     self.scene = Scene(cfg.scene, device=device)
@@ -130,6 +134,7 @@ class ManagerBasedEnv:
     return self.obs_buf, self.extras
 
   def step(self, action: torch.Tensor):
+    self._rng_ctr += 1
     self.action_manager.process_action(action.to(self.device))
     for _ in range(self.cfg.decimation):
       self._sim_step_counter += 1
@@ -172,7 +177,7 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     self.reset_time_outs = self.termination_manager._truncated_buf
     self.reward_buf = self.reward_manager._reward_buf
     self._any_reset = torch.zeros(1, dtype=torch.bool, device=self.device)
-    self._env_step_t = torch.zeros((), dtype=torch.long, device=self.device)
+    self._env_step_t = self._rng_ctr  # env steps taken (device), also the random stream's counter
     # device counters [envs reset, env steps that ran the gated forward], accumulated
     # inside the graph (no host sync); read with step_stats()
     self._stats = torch.zeros(2, dtype=torch.long, device=self.device)

@@ -32,6 +32,11 @@ def _ranges6(env, r: dict | None) -> tuple[torch.Tensor, torch.Tensor]:
   return cache[key]
 
 
+def _ranges6_host(r: dict | None) -> tuple[list[float], list[float]]:
+  rl = [(r or {}).get(k, (0.0, 0.0)) for k in _AXES6]
+  return [float(a) for a, _ in rl], [float(b) for _, b in rl]
+
+
 def _uniform6(env, n, ranges, lo, hi):
   """U(lo, hi) draws for the 6 pose/velocity axes, or None when every range is
   (0, 0): the offsets are then exactly zero and no random kernel is launched."""
@@ -51,16 +56,34 @@ def reset_scene_to_default(env, env_ids) -> None:
       ent.write_joint_state_to_sim(ent.data.default_joint_pos.clone(), ent.data.default_joint_vel.clone(), env_ids=m)
 
 
+def _slice_start(cols):
+  """First column of a contiguous column set (EntityData keeps those as slices), else None."""
+  return cols.start if isinstance(cols, slice) and cols.step in (None, 1) else None
+
+
+def _all_range(r) -> bool:
+  return bool(r) and not all(tuple(v) == (0.0, 0.0) for v in r.values())
+
+
 def reset_root_state_uniform(env, env_ids, pose_range: dict, velocity_range: dict | None = None,
                              asset_cfg: SceneEntityCfg = _DEFAULT) -> None:
   m = as_mask(env_ids, env.num_envs, env.device)
   a = env.scene[asset_cfg.name]
   n = env.num_envs
   lo, hi = _ranges6(env, pose_range)
-  pose = _uniform6(env, n, pose_range, lo, hi)
   rs = a.data.default_root_state
   if a.is_fixed_base:
     raise ValueError(f"Cannot reset root state for fixed-base entity '{asset_cfg.name}'.")
+  # one launch on the GPU: draws, pose composition and the root pose/velocity
+  # writes of EntityData (csrc/mjh_fuse.hip); the torch path below is its reference
+  d = a.data
+  qa, va = _slice_start(d._cols["free_joint_q_adr"]), _slice_start(d._cols["free_joint_v_adr"])
+  if qa is not None and va is not None:
+    (plo, phi), (vlo, vhi) = _ranges6_host(pose_range), _ranges6_host(velocity_range)
+    if envops.reset_root_uniform(env, f"reset_root_state_uniform.{asset_cfg.name}", d.data.qpos, qa, d.data.qvel, va, m, rs,
+                                 env.scene.env_origins, plo, phi, vlo, vhi, _all_range(pose_range), _all_range(velocity_range)):
+      return
+  pose = _uniform6(env, n, pose_range, lo, hi)
   if pose is None:
     pose = torch.zeros(n, 6, device=env.device)
   pos = rs[:, 0:3] + pose[:, 0:3] + env.scene.env_origins
@@ -77,6 +100,13 @@ def reset_joints_by_offset(env, env_ids, position_range: tuple[float, float], ve
   m = as_mask(env_ids, env.num_envs, env.device)
   a = env.scene[asset_cfg.name]
   j = asset_cfg.joint_idx
+  d = a.data
+  if isinstance(j, slice) and j == slice(None):  # all joints: one fused launch on the GPU
+    qa, va = _slice_start(d._cols["joint_q_adr"]), _slice_start(d._cols["joint_v_adr"])
+    if qa is not None and va is not None and envops.reset_joints_offset(
+        env, f"reset_joints_by_offset.{asset_cfg.name}", d.data.qpos, qa, d.data.qvel, va, m, d.default_joint_pos,
+        d.default_joint_vel, d.soft_joint_pos_limits, position_range, velocity_range):
+      return
   jp = a.data.default_joint_pos[:, j].clone()
   if tuple(position_range) != (0.0, 0.0):  # (0, 0): exact zero offset, no draw
     jp += torch.rand_like(jp) * (position_range[1] - position_range[0]) + position_range[0]
@@ -92,6 +122,12 @@ def push_by_setting_velocity(env, env_ids, velocity_range: dict, asset_cfg: Scen
   m = as_mask(env_ids, env.num_envs, env.device)
   a = env.scene[asset_cfg.name]
   lo, hi = _ranges6(env, velocity_range)
+  d = a.data
+  qa, va = _slice_start(d._cols["free_joint_q_adr"]), _slice_start(d._cols["free_joint_v_adr"])
+  if qa is not None and va is not None and envops.push_velocity(
+      env, f"push_by_setting_velocity.{asset_cfg.name}", d.data.qpos, qa, d.data.qvel, va, m, d.root_link_vel_w,
+      *_ranges6_host(velocity_range)):
+    return
   vel = a.data.root_link_vel_w + torch.rand(env.num_envs, 6, device=env.device) * (hi - lo) + lo
   a.write_root_link_velocity_to_sim(vel, env_ids=m)
 

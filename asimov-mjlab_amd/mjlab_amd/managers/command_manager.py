@@ -14,6 +14,7 @@ class CommandTerm(ManagerTermBase):
     self.metrics: dict[str, torch.Tensor] = {}
     self.time_left = torch.zeros(self.num_envs, device=self.device)
     self.command_counter = torch.zeros(self.num_envs, device=self.device, dtype=torch.long)
+    self._reset_means = torch.zeros(8, device=self.device)
 
   @property
   def command(self) -> torch.Tensor:
@@ -23,15 +24,30 @@ class CommandTerm(ManagerTermBase):
     m = as_mask(env_ids, self.num_envs, self.device)
     extras = {}
     if self.metrics:
-      w = m.float()
-      vals = torch.stack(list(self.metrics.values()), dim=1)
-      means = (vals * w[:, None]).sum(0) / w.sum().clamp(min=1.0)
-      for i, (k, v) in enumerate(self.metrics.items()):
-        extras[k] = means[i]
-        v.masked_fill_(m, 0.0)
-    self.command_counter.masked_fill_(m, 0)
-    self._resample(m)
+      from mjlab_amd import envops
+
+      if len(self.metrics) > self._reset_means.numel():
+        self._reset_means = torch.zeros(len(self.metrics), device=self.device)
+      if envops.masked_means(list(self.metrics.values()), m, 1.0, True, self._reset_means):
+        for i, k in enumerate(self.metrics):  # one launch: masked means, then the metrics cleared
+          extras[k] = self._reset_means[i]
+      else:
+        w = m.float()
+        vals = torch.stack(list(self.metrics.values()), dim=1)
+        means = (vals * w[:, None]).sum(0) / w.sum().clamp(min=1.0)
+        for i, (k, v) in enumerate(self.metrics.items()):
+          extras[k] = means[i]
+          v.masked_fill_(m, 0.0)
+    if not self._reset_resample(m):
+      self.command_counter.masked_fill_(m, 0)
+      self._resample(m)
     return extras
+
+  def _reset_resample(self, mask: torch.Tensor) -> bool:
+    """Fused counter restart + resampling of the masked envs (terms override);
+    False: run the generic masked_fill + _resample."""
+    del mask
+    return False
 
   def compute(self, dt: float) -> None:
     self._update_metrics()

@@ -31,6 +31,7 @@ class RewardManager:
     self._step_reward = torch.zeros(n, t, device=env.device)
     # weights live on the device, refreshed on the host before each (graph) step
     self._w = torch.zeros(t, device=env.device)
+    self._reset_means = torch.zeros(max(t, 1), device=env.device)
     self._w_host: tuple | None = None
     self.sync_weights()
 
@@ -51,10 +52,16 @@ class RewardManager:
 
   def reset(self, env_ids=None) -> dict:
     m = as_mask(env_ids, self._env.num_envs, self._env.device)
-    w = m.float()
-    means = (self._sums * w[:, None]).sum(0) / (w.sum().clamp(min=1.0) * self._env.max_episode_length_s)
+    from mjlab_amd import envops
+
+    cols = [self._sums[:, i] for i in range(len(self._term_names))]
+    if envops.masked_means(cols, m, 1.0 / self._env.max_episode_length_s, True, self._reset_means):
+      means = self._reset_means  # one launch: masked means of the episode sums, then cleared
+    else:
+      w = m.float()
+      means = (self._sums * w[:, None]).sum(0) / (w.sum().clamp(min=1.0) * self._env.max_episode_length_s)
+      self._sums.masked_fill_(m[:, None], 0.0)
     extras = {"Episode_Reward/" + k: means[i] for i, k in enumerate(self._term_names)}
-    self._sums.masked_fill_(m[:, None], 0.0)
     for tcfg in self._class_term_cfgs:
       if hasattr(tcfg.func, "reset"):
         tcfg.func.reset(env_ids=env_ids)

@@ -26,6 +26,7 @@ class TerminationManager:
     self._truncated_buf = torch.zeros(n, dtype=torch.bool, device=env.device)
     self._terminated_buf = torch.zeros_like(self._truncated_buf)
     self._dones_buf = torch.zeros_like(self._truncated_buf)
+    self._reset_counts = torch.zeros(max(len(self._term_names), 1), dtype=torch.long, device=env.device)
 
   @property
   def active_terms(self) -> list[str]:
@@ -45,7 +46,12 @@ class TerminationManager:
 
   def reset(self, env_ids=None) -> dict:
     m = as_mask(env_ids, self._env.num_envs, self._env.device)
-    extras = {"Episode_Termination/" + k: (v & m).sum() for k, v in self._term_dones.items()}
+    from mjlab_amd import envops
+
+    if envops.masked_counts(list(self._term_dones.values()), m, self._reset_counts):
+      extras = {"Episode_Termination/" + k: self._reset_counts[i] for i, k in enumerate(self._term_dones)}
+    else:
+      extras = {"Episode_Termination/" + k: (v & m).sum() for k, v in self._term_dones.items()}
     for tcfg in self._class_term_cfgs:
       if hasattr(tcfg.func, "reset"):
         tcfg.func.reset(env_ids=env_ids)

@@ -61,6 +61,16 @@ EXPORTS = (
   "mjh_obs_group",
   "mjh_reward_combine",
   "mjh_flag_stats",
+  "mjh_masked_means",
+  "mjh_masked_counts",
+  "mjh_uniform_draws",
+  "mjh_uniform_where",
+  "mjh_interval_tick",
+  "mjh_reset_root_uniform",
+  "mjh_reset_joints_offset",
+  "mjh_push_velocity",
+  "mjh_velocity_resample",
+  "mjh_event_mark",
 )
 
 
@@ -125,6 +135,19 @@ def lib() -> ctypes.CDLL:
   L.mjh_obs_group.argtypes = [vp, ci, vp, ll, vp, ll, ll, vp]
   L.mjh_reward_combine.argtypes = [vp, vp, ci, vp, cf, vp, vp, vp, ll, vp]
   L.mjh_flag_stats.argtypes = [vp, ll, vp, vp]
+  u64 = ctypes.c_ulonglong
+  L.mjh_masked_means.argtypes = [vp, vp, ci, vp, cf, ci, vp, ll, vp]
+  L.mjh_masked_counts.argtypes = [vp, ci, vp, vp, ll, vp]
+  L.mjh_uniform_draws.argtypes = [vp, ll, u64, u64, vp, vp]
+  L.mjh_uniform_where.argtypes = [vp, vp, cf, cf, u64, u64, vp, ll, vp]
+  L.mjh_interval_tick.argtypes = [vp, cf, cf, cf, vp, u64, u64, vp, ll, vp]
+  L.mjh_reset_root_uniform.argtypes = [vp, ll, ci, vp, ll, ci, vp, vp, ll, vp, ll, vp, vp, vp, vp, ci, ci, u64, u64, vp, ll,
+                                       vp]
+  L.mjh_reset_joints_offset.argtypes = [vp, ll, ci, vp, ll, ci, ci, vp, vp, ll, vp, ll, vp, ll, cf, cf, cf, cf, ci, ci, u64,
+                                        u64, vp, ll, vp]
+  L.mjh_push_velocity.argtypes = [vp, ll, ci, vp, ll, ci, vp, vp, ll, vp, vp, u64, u64, vp, ll, vp]
+  L.mjh_velocity_resample.argtypes = [vp, vp, cf, cf, cf, cf, ci, ci, vp, vp, vp, vp, vp, vp, u64, u64, vp, ll, vp]
+  L.mjh_event_mark.argtypes = [vp, vp, vp, vp, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

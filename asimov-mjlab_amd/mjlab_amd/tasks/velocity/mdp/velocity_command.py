@@ -105,6 +105,29 @@ class UniformVelocityCommand(CommandTerm):
     self.command_counter += mask.long()
     self._update_command()
 
+  def _resample_fused(self, mask: torch.Tensor, reset: bool) -> bool:
+    """CommandTerm._resample (+ the counter restart of reset) in one launch
+    (csrc/mjh_fuse.hip), draws from the env's device stream."""
+    if self.cfg.init_velocity_prob != 0.0 or not self.vel_command_b.is_cuda or mask.dtype != torch.bool:
+      return False
+    import ctypes
+
+    from mjlab_amd import envops
+    from mjlab_amd.sim import native
+
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    lo, hi = self.cfg.resampling_time_range
+    seed, key, ctr = envops.rng_args(self._env, "velocity_command.resample")
+    native.check(native.lib().mjh_velocity_resample(
+      P(mask), P(self._ranges_t), float(lo), float(hi), float(self.cfg.rel_heading_envs), float(self.cfg.rel_standing_envs),
+      int(self.cfg.heading_command), int(reset), P(self.vel_command_b), P(self.heading_target), P(self.is_heading_env),
+      P(self.is_standing_env), P(self.time_left), P(self.command_counter), seed, key, ctr, self.num_envs,
+      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "mjh_velocity_resample")
+    return True
+
+  def _reset_resample(self, mask: torch.Tensor) -> bool:
+    return self._resample_fused(mask, reset=True)
+
   def _update_metrics(self) -> None:
     max_command_step = self.cfg.resampling_time_range[1] / self._env.step_dt
     d = self.robot.data

@@ -275,6 +275,83 @@ int mjh_reward_combine(const float* const* values, const long long* strides, int
  * += the same (running totals); flags_acc is cleared. */
 int mjh_flag_stats(int* flags_acc, long long nworld, mjh_i64* stats, void* stream);
 
+
+/* ---- reset path, events and commands (mjh_fuse.hip) ----
+ * Masks are torch.bool (1 byte per env; NULL = every env). Random draws are
+ * U[0,1) from a counter-based generator keyed (seed, key, *ctr, element index):
+ * ctr is a device step counter (NULL = 0), so a captured graph draws anew at
+ * every replay; mjh_uniform_draws exposes the same stream (tests). */
+
+/* out[t] = scale * sum_{mask} cols[t][e] / max(count(mask), 1); zero_rows != 0
+ * also clears the masked entries (RewardManager.reset, reward_manager.py:55-70;
+ * CommandTerm.reset metrics, command_manager.py:34-47). One workgroup. */
+int mjh_masked_means(float* const* cols, const long long* strides, int ncols, const unsigned char* mask, float scale,
+                     int zero_rows, float* out, long long n, void* stream);
+
+/* out[t] = count(flags[t] & mask) (TerminationManager.reset episode logs,
+ * termination_manager.py:84-96). One workgroup. */
+int mjh_masked_counts(const unsigned char* const* flags, int nflags, const unsigned char* mask, mjh_i64* out, long long n,
+                      void* stream);
+
+/* out[i] = U[0,1) element i of the (seed, key, *ctr) stream. */
+int mjh_uniform_draws(float* out, long long n, unsigned long long seed, unsigned long long key, const mjh_i64* ctr,
+                      void* stream);
+
+/* t[e] = U[lo, hi) (element e) where mask[e] (command / interval-event timers,
+ * command_manager.py:40-47, event_manager.py:95-108). */
+int mjh_uniform_where(float* t, const unsigned char* mask, float lo, float hi, unsigned long long seed,
+                      unsigned long long key, const mjh_i64* ctr, long long n, void* stream);
+
+/* Interval-event timers (event_manager.py:120-145): t -= dt; due = t < 1e-6;
+ * due timers redrawn from U[lo, hi) (element e); due written as bool. */
+int mjh_interval_tick(float* t, float dt, float lo, float hi, unsigned char* due, unsigned long long seed,
+                      unsigned long long key, const mjh_i64* ctr, long long n, void* stream);
+
+/* reset_root_state_uniform (envs/mdp/events.py:45-84) with EntityData's root
+ * pose / velocity writes (entity/data.py:112-151) for the masked envs: pose
+ * offsets U[pose_lo, pose_hi) (elements e*12 + 0..5, if pose_rand), velocity
+ * offsets U[vel_lo, vel_hi) (e*12 + 6..11, if vel_rand); root_state rows are
+ * [pos 3, quat 4, lin vel 3, ang vel 3] (world frame); qpos[qadr..+7] = pos +
+ * offset + origin, quat (x) euler(offset); qvel[vadr..+6] = [lin, ang in the new
+ * body frame]. */
+int mjh_reset_root_uniform(float* qpos, long long qs, int qadr, float* qvel, long long vs, int vadr,
+                           const unsigned char* mask, const float* root_state, long long rss, const float* origins,
+                           long long os, const float* pose_lo, const float* pose_hi, const float* vel_lo,
+                           const float* vel_hi, int pose_rand, int vel_rand, unsigned long long seed,
+                           unsigned long long key, const mjh_i64* ctr, long long n, void* stream);
+
+/* reset_joints_by_offset (envs/mdp/events.py:87-121) for k consecutive joints
+ * (qpos columns qadr.., qvel columns vadr..): default + U[pos_lo, pos_hi)
+ * (elements e*2k + j) clamped to lim (N, k, 2), default velocity + U[vel_lo,
+ * vel_hi) (e*2k + k + j), written for the masked envs. */
+int mjh_reset_joints_offset(float* qpos, long long qs, int qadr, float* qvel, long long vs, int vadr, int k,
+                            const unsigned char* mask, const float* def_pos, long long dps, const float* def_vel,
+                            long long dvs, const float* lim, long long ls, float pos_lo, float pos_hi, float vel_lo,
+                            float vel_hi, int pos_rand, int vel_rand, unsigned long long seed, unsigned long long key,
+                            const mjh_i64* ctr, long long n, void* stream);
+
+/* push_by_setting_velocity (envs/mdp/events.py:124-137): vel_w + U[lo, hi)
+ * (elements e*6 + j) written as the free joint's qvel for the masked envs. */
+int mjh_push_velocity(const float* qpos, long long qs, int qadr, float* qvel, long long vs, int vadr,
+                      const unsigned char* mask, const float* vel_w, long long vws, const float* lo, const float* hi,
+                      unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n, void* stream);
+
+/* UniformVelocityCommand resampling of the masked envs (command_manager.py:40-47,
+ * velocity_command.py:103-123): timer U[t_lo, t_hi) (element e*8), command
+ * over ranges (4 x [lo, hi]: lin_x, lin_y, ang_z, heading) from e*8 + 1..4,
+ * heading env (e*8 + 5 <= rel_heading), standing env (e*8 + 6 <= rel_standing);
+ * the counter restarts at 1 when reset != 0, else increments. */
+int mjh_velocity_resample(const unsigned char* mask, const float* ranges, float t_lo, float t_hi, float rel_heading,
+                          float rel_standing, int heading_command, int reset, float* cmd, float* heading_target,
+                          unsigned char* is_heading, unsigned char* is_standing, float* time_left, mjh_i64* counter,
+                          unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n,
+                          void* stream);
+
+/* EventManager reset bookkeeping (event_manager.py:146-156): last[e] = *step,
+ * once[e] = 1 for the masked envs. */
+int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, const mjh_i64* step, long long n,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

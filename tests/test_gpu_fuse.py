@@ -1,0 +1,240 @@
+"""Fused reset-path / event / command kernels (csrc/mjh_fuse.hip) vs the torch
+formulas they replace (managers/*.py, envs/mdp/events.py, velocity_command.py),
+fed the same U[0,1) draws (reconstructed from the device stream with
+envops.uniform_draws)."""
+
+import ctypes
+
+import pytest
+import torch
+
+from mjlab_amd import envops
+from mjlab_amd.sim import native
+from mjlab_amd.utils import math as M
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+SEED, KEY = 1234567, 987654321
+
+
+def _ctr(v: int) -> torch.Tensor:
+  return torch.full((), v, dtype=torch.long, device=DEV)
+
+
+def _args(ctr):
+  return ctypes.c_ulonglong(SEED), ctypes.c_ulonglong(KEY), envops._ptr(ctr)
+
+
+def _s():
+  return envops._stream()
+
+
+def test_draws_are_uniform_and_keyed():
+  c0, c1 = _ctr(5), _ctr(6)
+  a = envops.uniform_draws(SEED, KEY, c0, 1 << 20, DEV)
+  b = envops.uniform_draws(SEED, KEY, c1, 1 << 20, DEV)
+  c = envops.uniform_draws(SEED, KEY + 1, c0, 1 << 20, DEV)
+  assert 0.0 <= a.min().item() and a.max().item() < 1.0
+  assert abs(a.mean().item() - 0.5) < 2e-3 and abs(a.var().item() - 1 / 12) < 2e-3
+  # different step counter / key: a different stream
+  assert (a == b).float().mean().item() < 1e-3 and (a == c).float().mean().item() < 1e-3
+  assert torch.equal(a, envops.uniform_draws(SEED, KEY, c0, 1 << 20, DEV))
+  # consecutive draws uncorrelated
+  x = a.view(-1, 2)
+  assert abs(torch.corrcoef(x.T)[0, 1].item()) < 5e-3
+
+
+def test_masked_means_and_counts_match_torch():
+  g = torch.Generator(device=DEV).manual_seed(0)
+  n, t = 4096, 12
+  sums = torch.randn(n, t, device=DEV, generator=g)
+  m = torch.rand(n, device=DEV, generator=g) < 0.1
+  ref_means = (sums * m.float()[:, None]).sum(0) / (m.float().sum().clamp(min=1.0) * 20.0)
+  ref_sums = sums.masked_fill(m[:, None], 0.0)
+  out = torch.zeros(t, device=DEV)
+  assert envops.masked_means([sums[:, i] for i in range(t)], m, 1 / 20.0, True, out)
+  torch.testing.assert_close(out, ref_means, rtol=1e-5, atol=1e-6)
+  assert torch.equal(sums, ref_sums)
+  # empty mask: means are 0 (count clamped to 1), nothing cleared
+  z = torch.zeros(n, dtype=torch.bool, device=DEV)
+  v = torch.randn(n, device=DEV, generator=g)
+  v0 = v.clone()
+  assert envops.masked_means([v], z, 1.0, True, out)
+  assert out[0].item() == 0.0 and torch.equal(v, v0)
+  flags = [torch.rand(n, device=DEV, generator=g) < p for p in (0.01, 0.5, 0.0, 1.0)]
+  cnt = torch.zeros(4, dtype=torch.long, device=DEV)
+  assert envops.masked_counts(flags, m, cnt)
+  assert cnt.tolist() == [int((f & m).sum()) for f in flags]
+
+
+def test_uniform_where_and_interval_tick():
+  n = 4096
+  g = torch.Generator(device=DEV).manual_seed(1)
+  ctr = _ctr(3)
+  u = envops.uniform_draws(SEED, KEY, ctr, n, DEV)
+  t = torch.rand(n, device=DEV, generator=g)
+  m = torch.rand(n, device=DEV, generator=g) < 0.3
+  ref = torch.where(m, u * (5.0 - 2.0) + 2.0, t)
+  native.check(native.lib().mjh_uniform_where(envops._ptr(t), envops._ptr(m), 2.0, 5.0, *_args(ctr), n, _s()), "uw")
+  torch.testing.assert_close(t, ref, rtol=0, atol=1e-6)
+  # interval events: t -= dt; due = t < 1e-6; redraw (event_manager.py:120-145)
+  t = torch.rand(n, device=DEV, generator=g) * 0.05
+  due = torch.zeros(n, dtype=torch.bool, device=DEV)
+  tt = t - 0.02
+  ref_due = tt < 1e-6
+  ref = torch.where(ref_due, u * (15.0 - 10.0) + 10.0, tt)
+  native.check(native.lib().mjh_interval_tick(envops._ptr(t), 0.02, 10.0, 15.0, envops._ptr(due), *_args(ctr), n, _s()), "it")
+  assert torch.equal(due, ref_due)
+  torch.testing.assert_close(t, ref, rtol=0, atol=1e-6)
+
+
+def _rows(n, k, g):
+  return torch.randn(n, k, device=DEV, generator=g)
+
+
+def test_reset_root_uniform_matches_events_formula():
+  n = 2048
+  g = torch.Generator(device=DEV).manual_seed(2)
+  ctr = _ctr(7)
+  nq, nv, qa, va = 40, 38, 2, 1
+  qpos, qvel = _rows(n, nq, g), _rows(n, nv, g)
+  q0 = qpos.clone()
+  v0 = qvel.clone()
+  rs = _rows(n, 13, g)
+  rs[:, 3:7] = rs[:, 3:7] / rs[:, 3:7].norm(dim=1, keepdim=True)
+  org = _rows(n, 3, g)
+  m = torch.rand(n, device=DEV, generator=g) < 0.4
+  plo, phi = [-0.5, -0.5, 0.0, -0.1, -0.2, -3.14], [0.5, 0.5, 0.0, 0.1, 0.2, 3.14]
+  vlo, vhi = [-0.5] * 6, [0.5] * 6
+  u = envops.uniform_draws(SEED, KEY, ctr, n * 12, DEV).view(n, 12)
+  pose = u[:, :6] * (torch.tensor(phi, device=DEV) - torch.tensor(plo, device=DEV)) + torch.tensor(plo, device=DEV)
+  dv = u[:, 6:] * (torch.tensor(vhi, device=DEV) - torch.tensor(vlo, device=DEV)) + torch.tensor(vlo, device=DEV)
+  pos = rs[:, 0:3] + pose[:, 0:3] + org
+  quat = M.quat_mul(rs[:, 3:7], M.quat_from_euler_xyz(pose[:, 3], pose[:, 4], pose[:, 5]))
+  vel = rs[:, 7:13] + dv
+  ref_q, ref_v = q0.clone(), v0.clone()
+  ref_q[:, qa:qa + 7] = torch.where(m[:, None], torch.cat([pos, quat], 1), q0[:, qa:qa + 7])
+  qv = torch.cat([vel[:, :3], M.quat_apply_inverse(quat, vel[:, 3:])], 1)
+  ref_v[:, va:va + 6] = torch.where(m[:, None], qv, v0[:, va:va + 6])
+  F = (ctypes.c_float * 6)
+  native.check(native.lib().mjh_reset_root_uniform(
+    envops._ptr(qpos), nq, qa, envops._ptr(qvel), nv, va, envops._ptr(m), envops._ptr(rs), 13, envops._ptr(org), 3,
+    F(*plo), F(*phi), F(*vlo), F(*vhi), 1, 1, *_args(ctr), n, _s()), "rr")
+  torch.testing.assert_close(qpos, ref_q, rtol=1e-5, atol=2e-6)
+  torch.testing.assert_close(qvel, ref_v, rtol=1e-5, atol=2e-6)
+
+
+def test_reset_joints_offset_matches_events_formula():
+  n, k = 2048, 29
+  g = torch.Generator(device=DEV).manual_seed(3)
+  ctr = _ctr(9)
+  qpos, qvel = _rows(n, 36, g), _rows(n, 35, g)
+  q0, v0 = qpos.clone(), qvel.clone()
+  dp, dv = _rows(n, k, g), _rows(n, k, g)
+  lo = _rows(n, k, g) - 1.0
+  lim = torch.stack([lo, lo + 1.5], dim=-1)
+  m = torch.rand(n, device=DEV, generator=g) < 0.5
+  u = envops.uniform_draws(SEED, KEY, ctr, n * 2 * k, DEV).view(n, 2 * k)
+  jp = (dp + u[:, :k] * (0.3 + 0.2) - 0.2).clamp(lim[..., 0], lim[..., 1])
+  jv = dv + u[:, k:] * (0.1 + 0.1) - 0.1
+  ref_q, ref_v = q0.clone(), v0.clone()
+  ref_q[:, 7:] = torch.where(m[:, None], jp, q0[:, 7:])
+  ref_v[:, 6:] = torch.where(m[:, None], jv, v0[:, 6:])
+  native.check(native.lib().mjh_reset_joints_offset(
+    envops._ptr(qpos), 36, 7, envops._ptr(qvel), 35, 6, k, envops._ptr(m), envops._ptr(dp), k, envops._ptr(dv), k,
+    envops._ptr(lim), 2 * k, -0.2, 0.3, -0.1, 0.1, 1, 1, *_args(ctr), n, _s()), "rj")
+  torch.testing.assert_close(qpos, ref_q, rtol=1e-6, atol=1e-6)
+  torch.testing.assert_close(qvel, ref_v, rtol=1e-6, atol=1e-6)
+
+
+def test_push_velocity_matches_events_formula():
+  n = 2048
+  g = torch.Generator(device=DEV).manual_seed(4)
+  ctr = _ctr(11)
+  qpos, qvel = _rows(n, 36, g), _rows(n, 35, g)
+  qpos[:, 3:7] = qpos[:, 3:7] / qpos[:, 3:7].norm(dim=1, keepdim=True)
+  v0 = qvel.clone()
+  vw = _rows(n, 6, g)
+  m = torch.rand(n, device=DEV, generator=g) < 0.2
+  lo, hi = [-0.5, -0.5, 0.0, 0.0, 0.0, 0.0], [0.5, 0.5, 0.0, 0.0, 0.0, 0.0]
+  u = envops.uniform_draws(SEED, KEY, ctr, n * 6, DEV).view(n, 6)
+  vel = vw + u * (torch.tensor(hi, device=DEV) - torch.tensor(lo, device=DEV)) + torch.tensor(lo, device=DEV)
+  qv = torch.cat([vel[:, :3], M.quat_apply_inverse(qpos[:, 3:7], vel[:, 3:])], 1)
+  ref_v = v0.clone()
+  ref_v[:, 0:6] = torch.where(m[:, None], qv, v0[:, 0:6])
+  F = (ctypes.c_float * 6)
+  native.check(native.lib().mjh_push_velocity(envops._ptr(qpos), 36, 0, envops._ptr(qvel), 35, 0, envops._ptr(m),
+                                              envops._ptr(vw), 6, F(*lo), F(*hi), *_args(ctr), n, _s()), "pv")
+  torch.testing.assert_close(qvel, ref_v, rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("reset", [0, 1])
+def test_velocity_resample_matches_command_formula(reset):
+  n = 4096
+  g = torch.Generator(device=DEV).manual_seed(5)
+  ctr = _ctr(13)
+  ranges = torch.tensor([[-1.0, 1.0], [-0.5, 0.5], [-1.0, 1.0], [-3.14, 3.14]], device=DEV)
+  cmd, ht = _rows(n, 3, g), _rows(n, 1, g)[:, 0].contiguous()
+  ih = torch.rand(n, device=DEV, generator=g) < 0.5
+  isd = torch.rand(n, device=DEV, generator=g) < 0.5
+  tl = torch.rand(n, device=DEV, generator=g)
+  cnt = torch.randint(0, 5, (n,), device=DEV, generator=g)
+  m = torch.rand(n, device=DEV, generator=g) < 0.3
+  u = envops.uniform_draws(SEED, KEY, ctr, n * 8, DEV).view(n, 8)
+  r_tl = torch.where(m, u[:, 0] * (10.0 - 3.0) + 3.0, tl)
+  new = u[:, 1:5] * (ranges[:, 1] - ranges[:, 0]) + ranges[:, 0]
+  r_cmd = torch.where(m[:, None], new[:, :3], cmd)
+  r_ht = torch.where(m, new[:, 3], ht)
+  r_ih = torch.where(m, u[:, 5] <= 1.0, ih)
+  r_isd = torch.where(m, u[:, 6] <= 0.1, isd)
+  r_cnt = torch.where(m, torch.ones_like(cnt) if reset else cnt + 1, cnt)
+  P = envops._ptr
+  native.check(native.lib().mjh_velocity_resample(P(m), P(ranges), 3.0, 10.0, 1.0, 0.1, 1, reset, P(cmd), P(ht), P(ih),
+                                                  P(isd), P(tl), P(cnt), *_args(ctr), n, _s()), "vr")
+  torch.testing.assert_close(tl, r_tl, rtol=0, atol=1e-6)
+  torch.testing.assert_close(cmd, r_cmd, rtol=0, atol=1e-6)
+  torch.testing.assert_close(ht, r_ht, rtol=0, atol=1e-6)
+  assert torch.equal(ih, r_ih) and torch.equal(isd, r_isd) and torch.equal(cnt, r_cnt)
+
+
+def test_event_mark():
+  n = 1000
+  g = torch.Generator(device=DEV).manual_seed(6)
+  last = torch.randint(0, 50, (n,), dtype=torch.int32, device=DEV, generator=g)
+  once = torch.rand(n, device=DEV, generator=g) < 0.5
+  m = torch.rand(n, device=DEV, generator=g) < 0.5
+  step = _ctr(77)
+  r_last = torch.where(m, torch.full_like(last, 77), last)
+  r_once = once | m
+  assert envops.event_mark(last, once, m, step)
+  assert torch.equal(last, r_last) and torch.equal(once, r_once)
+
+
+def test_env_reset_path_uses_fused_kernels():
+  """A captured velocity-task env step runs the fused reset path (C-ABI tally)
+  and keeps its invariants: reset envs restart at step 0 with fresh commands."""
+  from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
+  from mjlab_amd.tasks import load_env_cfg
+
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = 256
+  env = ManagerBasedRlEnv(cfg, device=DEV)
+  env.reset()
+  native.CALLS.clear()
+  a = torch.zeros(256, env.action_manager.total_action_dim, device=DEV)
+  env.step(a)  # eager
+  for name in ("mjh_masked_means", "mjh_masked_counts", "mjh_reset_root_uniform", "mjh_reset_joints_offset",
+               "mjh_velocity_resample", "mjh_event_mark", "mjh_interval_tick"):
+    assert native.CALLS[name] >= 1, name
+  env.episode_length_buf.fill_(int(env.max_episode_length) - 1)  # every env times out at the next step
+  cmd_before = env.command_manager.get_command("twist").clone()
+  _, _, _, trunc, _ = env.step(a)
+  torch.cuda.synchronize()
+  assert trunc.all() and (env.episode_length_buf == 0).all()
+  assert not torch.equal(env.command_manager.get_command("twist"), cmd_before)
+  t = env.command_manager.get_term("twist")
+  assert (t.command_counter == 1).all()
+  lo, hi = t.cfg.resampling_time_range
+  assert ((t.time_left >= lo - env.step_dt) & (t.time_left <= hi)).all()
+  q = env.sim.data.qpos
+  assert torch.isfinite(q).all() and torch.allclose(q[:, 3:7].norm(dim=1), torch.ones(256, device=DEV), atol=1e-5)

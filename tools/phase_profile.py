@@ -59,7 +59,7 @@ print(f"  rne: cvel {seg(2,21):.0f} cdof_dot {seg(21,22):.0f} rne {seg(22,23):.0
 niter = sim.data.solver_niter.cpu().numpy()
 nefc = sim.data.nefc.cpu().numpy()
 wg = tot[: (N // 8) * 8].reshape(-1, 8)
-print(f"  hessian+factor recomputations per world-step: {p[:, 29].mean():.2f}")
+print(f"  hessian+factor recomputations per world-step: {p[:, 29].mean():.2f}  rank-1 factor updates: {p[:, 30].mean():.0f} cycles")
 print(f"  workgroup (8 worlds) max/mean: {wg.max(1).mean():.0f} / {tot.mean():.0f}; "
       f"p50 {np.percentile(tot, 50):.0f} p90 {np.percentile(tot, 90):.0f} p99 {np.percentile(tot, 99):.0f}")
 for nm, x in (("nefc", nefc), ("niter", niter)):
