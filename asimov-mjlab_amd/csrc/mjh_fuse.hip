@@ -88,38 +88,54 @@ struct ColArgs {
   int ncols;
 };
 
-__global__ void masked_means_kernel(const ColArgs a, const unsigned char* __restrict__ mask, float scale, int zero_rows,
-                                    float* __restrict__ out, long long n) {
-  __shared__ float part[kBlock];
-  __shared__ float cnt_s;
-  float cnt = 0.f;
-  for (long long e = threadIdx.x; e < n; e += blockDim.x) cnt += on(mask, e) ? 1.f : 0.f;
-  part[threadIdx.x] = cnt;
-  __syncthreads();
-  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) cnt_s = fmaxf(part[0], 1.f);
-  __syncthreads();
-  const float denom = cnt_s;
-  for (int t = 0; t < a.ncols; t++) {
-    float* col = a.c[t];
-    float s = 0.f;
-    for (long long e = threadIdx.x; e < n; e += blockDim.x) {
-      if (on(mask, e)) {
-        s += col[e * a.cs[t]];
-        if (zero_rows) col[e * a.cs[t]] = 0.f;
+// wave64 sum (all lanes get the total)
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+constexpr int kRedBlock = 1024;  // one workgroup of 16 waves: 16 rows in flight per column pass
+
+// Each thread accumulates its rows' entries of every column in registers
+// (rows e = tid, tid + 1024, ...; a row's columns share cache lines), then one
+// wave + LDS reduction per column.
+__global__ __launch_bounds__(kRedBlock) void masked_means_kernel(const ColArgs a, const unsigned char* __restrict__ mask,
+                                                                  float scale, int zero_rows, float* __restrict__ out,
+                                                                  long long n) {
+  __shared__ float part[MJH_MAX_TERMS + 1][kRedBlock / 64];
+  float acc[MJH_MAX_TERMS + 1];
+#pragma unroll
+  for (int t = 0; t <= MJH_MAX_TERMS; t++) acc[t] = 0.f;
+  for (long long e = threadIdx.x; e < n; e += kRedBlock) {
+    if (!on(mask, e)) continue;
+    acc[MJH_MAX_TERMS] += 1.f;
+#pragma unroll
+    for (int t = 0; t < MJH_MAX_TERMS; t++) {
+      if (t < a.ncols) {
+        float* p = a.c[t] + e * a.cs[t];
+        acc[t] += *p;
+        if (zero_rows) *p = 0.f;
       }
     }
-    __syncthreads();
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
-      __syncthreads();
+  }
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t <= MJH_MAX_TERMS; t++) {
+    if (t < a.ncols || t == MJH_MAX_TERMS) {
+      const float v = wsum(acc[t]);
+      if (lane == 0) part[t][wv] = v;
     }
-    if (threadIdx.x == 0) out[t] = part[0] / denom * scale;
+  }
+  __syncthreads();
+  if (threadIdx.x < (unsigned)a.ncols) {
+    float cnt = 0.f, s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kRedBlock / 64; w++) {
+      cnt += part[MJH_MAX_TERMS][w];
+      s += part[threadIdx.x][w];
+    }
+    out[threadIdx.x] = s / fmaxf(cnt, 1.f) * scale;
   }
 }
 
@@ -128,20 +144,34 @@ struct FlagArgs {
   int nflags;
 };
 
-__global__ void masked_counts_kernel(const FlagArgs a, const unsigned char* __restrict__ mask, mjh_i64* __restrict__ out,
-                                     long long n) {
-  __shared__ int part[kBlock];
-  for (int t = 0; t < a.nflags; t++) {
-    int c = 0;
-    for (long long e = threadIdx.x; e < n; e += blockDim.x) c += (on(mask, e) && a.f[t][e]) ? 1 : 0;
-    __syncthreads();
-    part[threadIdx.x] = c;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
-      __syncthreads();
+__global__ __launch_bounds__(kRedBlock) void masked_counts_kernel(const FlagArgs a, const unsigned char* __restrict__ mask,
+                                                                   mjh_i64* __restrict__ out, long long n) {
+  __shared__ int part[MJH_MAX_TERMS][kRedBlock / 64];
+  int acc[MJH_MAX_TERMS];
+#pragma unroll
+  for (int t = 0; t < MJH_MAX_TERMS; t++) acc[t] = 0;
+  for (long long e = threadIdx.x; e < n; e += kRedBlock) {
+    if (!on(mask, e)) continue;
+#pragma unroll
+    for (int t = 0; t < MJH_MAX_TERMS; t++)
+      if (t < a.nflags) acc[t] += a.f[t][e] ? 1 : 0;
+  }
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < MJH_MAX_TERMS; t++) {
+    if (t < a.nflags) {
+      int v = acc[t];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) part[t][wv] = v;
     }
-    if (threadIdx.x == 0) out[t] = part[0];
+  }
+  __syncthreads();
+  if (threadIdx.x < (unsigned)a.nflags) {
+    long long s = 0;
+#pragma unroll
+    for (int w = 0; w < kRedBlock / 64; w++) s += part[threadIdx.x][w];
+    out[threadIdx.x] = s;
   }
 }
 
@@ -298,6 +328,35 @@ __global__ void event_mark_kernel(int* __restrict__ last, unsigned char* __restr
   once[e] = 1;
 }
 
+// TerminationManager.compute's combination (termination_manager.py:54-82):
+// per-term done flags copied out, OR-ed into truncated (time-out terms) or
+// terminated, dones = truncated | terminated
+struct TermArgs {
+  const unsigned char* v[MJH_MAX_TERMS];
+  unsigned char* d[MJH_MAX_TERMS];
+  int time_out[MJH_MAX_TERMS];
+  int nterms;
+};
+
+__global__ void term_combine_kernel(const TermArgs a, unsigned char* __restrict__ truncated,
+                                    unsigned char* __restrict__ terminated, unsigned char* __restrict__ dones, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  unsigned char tr = 0, te = 0;
+#pragma unroll
+  for (int t = 0; t < MJH_MAX_TERMS; t++) {
+    if (t < a.nterms) {
+      const unsigned char v = a.v[t][e] ? 1 : 0;
+      a.d[t][e] = v;
+      if (a.time_out[t]) tr |= v;
+      else te |= v;
+    }
+  }
+  truncated[e] = tr;
+  terminated[e] = te;
+  dones[e] = tr | te;
+}
+
 }  // namespace
 
 extern "C" {
@@ -312,7 +371,7 @@ int mjh_masked_means(float* const* cols, const long long* strides, int ncols, co
     a.cs[t] = strides[t];
   }
   a.ncols = ncols;
-  hipLaunchKernelGGL(masked_means_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, a, mask, scale, zero_rows, out, n);
+  hipLaunchKernelGGL(masked_means_kernel, dim3(1), dim3(kRedBlock), 0, (hipStream_t)stream, a, mask, scale, zero_rows, out, n);
   return finish();
 }
 
@@ -323,7 +382,7 @@ int mjh_masked_counts(const unsigned char* const* flags, int nflags, const unsig
   FlagArgs a{};
   for (int t = 0; t < nflags; t++) a.f[t] = flags[t];
   a.nflags = nflags;
-  hipLaunchKernelGGL(masked_counts_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, a, mask, out, n);
+  hipLaunchKernelGGL(masked_counts_kernel, dim3(1), dim3(kRedBlock), 0, (hipStream_t)stream, a, mask, out, n);
   return finish();
 }
 
@@ -408,6 +467,23 @@ int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, co
                    void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(event_mark_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, last, once, mask, step, n);
+  return finish();
+}
+
+int mjh_term_combine(const unsigned char* const* values, unsigned char* const* term_dones, const int* time_out, int nterms,
+                     unsigned char* truncated, unsigned char* terminated, unsigned char* dones, long long n,
+                     void* stream) {
+  if (n <= 0) return 0;
+  if (nterms > MJH_MAX_TERMS) return 1;
+  TermArgs a{};
+  for (int t = 0; t < nterms; t++) {
+    a.v[t] = values[t];
+    a.d[t] = term_dones[t];
+    a.time_out[t] = time_out[t];
+  }
+  a.nterms = nterms;
+  hipLaunchKernelGGL(term_combine_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, a, truncated, terminated,
+                     dones, n);
   return finish();
 }
 

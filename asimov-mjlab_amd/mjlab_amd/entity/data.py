@@ -200,8 +200,24 @@ class EntityData:
   def write_ctrl(self, ctrl: torch.Tensor, ctrl_ids=None, env_ids=None) -> None:
     if not self.is_actuated:
       raise ValueError("Cannot write control for non-actuated entity.")
-    cols = self._cols["ctrl_ids"] if ctrl_ids is None else self._ix["ctrl_ids"][ctrl_ids]
+    cols = self._cols["ctrl_ids"] if ctrl_ids is None else self._sub_cols("ctrl_ids", ctrl_ids)
     _masked_write(self.data.ctrl, cols, ctrl, env_ids)
+
+  def _sub_cols(self, key: str, ids):
+    """Columns self._ix[key][ids], as a slice when contiguous. Resolved once per
+    ids object outside graph capture (the action terms pass the same ids every
+    step), so a per-step write is one copy instead of a gather + scatter."""
+    cache = self.__dict__.setdefault("_sub_cols_cache", {})
+    ck = (key, id(ids)) if isinstance(ids, torch.Tensor) else (key, repr(ids))
+    hit = cache.get(ck)
+    if hit is not None and (hit[0] is ids or not isinstance(ids, torch.Tensor)):
+      return hit[1]
+    cols = self._ix[key][ids]
+    capturing = cols.is_cuda and torch.cuda.is_current_stream_capturing()
+    if not capturing and cols.dim() == 1:
+      cols = _as_slice(cols)
+      cache[ck] = (ids, cols)
+    return cols
 
   def clear_state(self, env_ids=None) -> None:
     """Zero applied generalized forces on the free joint, applied body wrenches

@@ -513,3 +513,21 @@ def event_mark(last: torch.Tensor, once: torch.Tensor, mask, step: torch.Tensor)
   native.check(native.lib().mjh_event_mark(_ptr(last), _ptr(once), _mptr(mask), _ptr(step), last.shape[0], _stream()),
                "mjh_event_mark")
   return True
+
+
+def term_combine(values: list, term_dones: list, time_out: list, truncated, terminated, dones) -> bool:
+  """TerminationManager's copy / OR / dones chain over bool term vectors in one launch."""
+  T = len(values)
+  if T == 0 or T > MAX_TERMS:
+    return False
+  n = dones.shape[0]
+  for v in values + term_dones + [truncated, terminated, dones]:
+    if not (isinstance(v, torch.Tensor) and v.is_cuda and v.dtype == torch.bool and v.dim() == 1 and v.shape[0] == n
+            and v.stride(0) == 1):
+      return False
+  vp = (ctypes.c_void_p * T)(*[v.data_ptr() for v in values])
+  dp = (ctypes.c_void_p * T)(*[d.data_ptr() for d in term_dones])
+  to = (ctypes.c_int * T)(*[int(bool(x)) for x in time_out])
+  native.check(native.lib().mjh_term_combine(vp, dp, to, T, _ptr(truncated), _ptr(terminated), _ptr(dones), n, _stream()),
+               "mjh_term_combine")
+  return True

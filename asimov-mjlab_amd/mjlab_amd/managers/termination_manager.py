@@ -58,10 +58,15 @@ class TerminationManager:
     return extras
 
   def compute(self) -> torch.Tensor:
+    from mjlab_amd import envops
+
+    values = [tcfg.func(self._env, **tcfg.params) for tcfg in self._term_cfgs]
+    if envops.term_combine(values, list(self._term_dones.values()), [c.time_out for c in self._term_cfgs],
+                           self._truncated_buf, self._terminated_buf, self._dones_buf):
+      return self._dones_buf  # one launch: copies, ORs and dones
     self._truncated_buf.zero_()
     self._terminated_buf.zero_()
-    for name, tcfg in zip(self._term_names, self._term_cfgs):
-      value = tcfg.func(self._env, **tcfg.params)
+    for name, tcfg, value in zip(self._term_names, self._term_cfgs, values):
       if tcfg.time_out:
         self._truncated_buf |= value
       else:

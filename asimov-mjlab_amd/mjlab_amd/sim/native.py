@@ -71,6 +71,7 @@ EXPORTS = (
   "mjh_push_velocity",
   "mjh_velocity_resample",
   "mjh_event_mark",
+  "mjh_term_combine",
 )
 
 
@@ -148,6 +149,7 @@ def lib() -> ctypes.CDLL:
   L.mjh_push_velocity.argtypes = [vp, ll, ci, vp, ll, ci, vp, vp, ll, vp, vp, u64, u64, vp, ll, vp]
   L.mjh_velocity_resample.argtypes = [vp, vp, cf, cf, cf, cf, ci, ci, vp, vp, vp, vp, vp, vp, u64, u64, vp, ll, vp]
   L.mjh_event_mark.argtypes = [vp, vp, vp, vp, ll, vp]
+  L.mjh_term_combine.argtypes = [vp, vp, vp, ci, vp, vp, vp, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

@@ -347,6 +347,13 @@ int mjh_velocity_resample(const unsigned char* mask, const float* ranges, float 
                           unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n,
                           void* stream);
 
+/* TerminationManager.compute's combination (termination_manager.py:54-82) for
+ * nterms bool term vectors: term_dones[t] = values[t]; truncated = OR of the
+ * time-out terms, terminated = OR of the others, dones = truncated | terminated. */
+int mjh_term_combine(const unsigned char* const* values, unsigned char* const* term_dones, const int* time_out, int nterms,
+                     unsigned char* truncated, unsigned char* terminated, unsigned char* dones, long long n,
+                     void* stream);
+
 /* EventManager reset bookkeeping (event_manager.py:146-156): last[e] = *step,
  * once[e] = 1 for the masked envs. */
 int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, const mjh_i64* step, long long n,

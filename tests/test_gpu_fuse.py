@@ -210,6 +210,20 @@ def test_event_mark():
   assert torch.equal(last, r_last) and torch.equal(once, r_once)
 
 
+def test_term_combine_matches_manager_formula():
+  n = 4096
+  g = torch.Generator(device=DEV).manual_seed(7)
+  vals = [torch.rand(n, device=DEV, generator=g) < p for p in (0.02, 0.3, 0.0, 0.5)]
+  time_out = [True, False, False, True]
+  dones = [torch.zeros(n, dtype=torch.bool, device=DEV) for _ in vals]
+  tr, te, dn = (torch.ones(n, dtype=torch.bool, device=DEV) for _ in range(3))
+  assert envops.term_combine(vals, dones, time_out, tr, te, dn)
+  r_tr = vals[0] | vals[3]
+  r_te = vals[1] | vals[2]
+  assert torch.equal(tr, r_tr) and torch.equal(te, r_te) and torch.equal(dn, r_tr | r_te)
+  assert all(torch.equal(d, v) for d, v in zip(dones, vals))
+
+
 def test_env_reset_path_uses_fused_kernels():
   """A captured velocity-task env step runs the fused reset path (C-ABI tally)
   and keeps its invariants: reset envs restart at step 0 with fresh commands."""
@@ -224,7 +238,7 @@ def test_env_reset_path_uses_fused_kernels():
   a = torch.zeros(256, env.action_manager.total_action_dim, device=DEV)
   env.step(a)  # eager
   for name in ("mjh_masked_means", "mjh_masked_counts", "mjh_reset_root_uniform", "mjh_reset_joints_offset",
-               "mjh_velocity_resample", "mjh_event_mark", "mjh_interval_tick"):
+               "mjh_velocity_resample", "mjh_event_mark", "mjh_interval_tick", "mjh_term_combine"):
     assert native.CALLS[name] >= 1, name
   env.episode_length_buf.fill_(int(env.max_episode_length) - 1)  # every env times out at the next step
   cmd_before = env.command_manager.get_command("twist").clone()
