@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/mjh_abi.h"
+#include "mjh_rng.h"
 
 namespace {
 
@@ -31,23 +32,7 @@ constexpr int kBlock = 256;
 inline int grid(long long n) { return (int)((n + kBlock - 1) / kBlock); }
 int finish() { return hipGetLastError() == hipSuccess ? 0 : 2; }
 
-__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-  return z ^ (z >> 31);
-}
-
-// U[0, 1) with 24 random bits, element `idx` of the draw keyed (seed, key, step)
-struct Rng {
-  unsigned long long base;
-  __device__ Rng(unsigned long long seed, unsigned long long key, const mjh_i64* ctr) {
-    const unsigned long long step = ctr ? (unsigned long long)*ctr : 0ull;
-    base = mix64(seed ^ mix64(key ^ mix64(step + 0x9e3779b97f4a7c15ull)));
-  }
-  __device__ __forceinline__ float u01(unsigned long long idx) const {
-    return (float)(mix64(base + (idx + 1ull) * 0x9e3779b97f4a7c15ull) >> 40) * (1.f / 16777216.f);
-  }
-};
+using mjh::Rng;
 
 __device__ __forceinline__ bool on(const unsigned char* mask, long long e) { return mask == nullptr || mask[e] != 0; }
 

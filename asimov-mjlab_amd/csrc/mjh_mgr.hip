@@ -6,16 +6,21 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/mjh_abi.h"
+#include "mjh_rng.h"
 
 namespace {
 
 struct ObsArgs {
   mjh_obs_term_desc t[MJH_MAX_TERMS];
   int nterms;
+  int width;  // group width: element index of the device-stream noise draw
+  unsigned long long seed, key;
+  const mjh_i64* ctr;
 };
 
-// blockIdx.y = term; out[e, off + j] = clip(x[e, j] + noise, cmin, cmax) * scale
-// (observation_manager.py:163-176: noise -> clip -> scale)
+// blockIdx.y = term; out[e, off + j] = clip(f(x[e, j]) + noise, cmin, cmax) * scale
+// (observation_manager.py:163-176: term -> noise -> clip -> scale), f the
+// term's elementwise op on its strided input (MJH_OBS_*)
 __global__ void obs_group_kernel(const ObsArgs a, const float* __restrict__ u, long long us, float* __restrict__ out,
                                  long long os, long long n) {
   const mjh_obs_term_desc& d = a.t[blockIdx.y];
@@ -23,8 +28,14 @@ __global__ void obs_group_kernel(const ObsArgs a, const float* __restrict__ u, l
   if (t >= n * d.w) return;
   const long long e = t / d.w;
   const int j = (int)(t - e * d.w);
-  float v = d.x[e * d.xs + j];
-  if (d.noise) v = v + (u[e * us + d.off + j] * (d.hi - d.lo) + d.lo);
+  float v = d.x[e * d.xs + j * d.xcs];
+  if (d.op == MJH_OBS_SUB) v -= d.y[e * d.ys + j];
+  else if (d.op == MJH_OBS_POSITIVE) v = v > 0.f ? 1.f : 0.f;
+  else if (d.op == MJH_OBS_SIGNED_LOG1P) v = (v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f)) * log1pf(fabsf(v));
+  if (d.noise) {
+    const float r = u ? u[e * us + d.off + j] : mjh::Rng(a.seed, a.key, a.ctr).u01(e * a.width + d.off + j);
+    v = v + (r * (d.hi - d.lo) + d.lo);
+  }
   if (d.cmin <= d.cmax) v = fminf(fmaxf(v, d.cmin), d.cmax);
   out[e * os + d.off + j] = v * d.scale;
 }
@@ -83,17 +94,22 @@ __global__ void reward_combine_kernel(const RewArgs a, const float* __restrict__
 extern "C" {
 
 int mjh_obs_group(const mjh_obs_term_desc* terms, int nterms, const float* u, long long us, float* out, long long os,
-                  long long n, void* stream) {
+                  long long n, unsigned long long seed, unsigned long long key, const mjh_i64* ctr, void* stream) {
   if (n <= 0 || nterms <= 0) return 0;
   if (nterms > MJH_MAX_TERMS) return 1;
   ObsArgs a;
-  int wmax = 0;
+  int wmax = 0, width = 0;
   for (int i = 0; i < nterms; i++) {
     a.t[i] = terms[i];
-    if (terms[i].noise && !u) return 1;
     if (terms[i].w > wmax) wmax = terms[i].w;
+    if (terms[i].off + terms[i].w > width) width = terms[i].off + terms[i].w;
+    if (terms[i].op == MJH_OBS_SUB && !terms[i].y) return 1;
   }
   a.nterms = nterms;
+  a.width = width;
+  a.seed = seed;
+  a.key = key;
+  a.ctr = ctr;
   const long long items = n * wmax;
   hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)((items + 255) / 256), (unsigned)nterms), dim3(256), 0,
                      (hipStream_t)stream, a, u, us, out, os, n);

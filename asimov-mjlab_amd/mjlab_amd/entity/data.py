@@ -371,25 +371,31 @@ class EntityData:
   site_lin_vel_w = property(lambda s: s.site_vel_w[..., 0:3])
   site_ang_vel_w = property(lambda s: s.site_vel_w[..., 3:6])
 
+  def _rows(self, key: str):
+    """Index of this entity's bodies/geoms/sites in the data arrays: a slice
+    (reads are views, no gather launch) when they are consecutive, as usual."""
+    c = self._cols[key]
+    return c if isinstance(c, slice) else self._ix[key]
+
   @_cached
   def _body_link_pos_w(self) -> torch.Tensor:
     """== body_link_pose_w[..., 0:3]"""
-    return self.data.xpos[:, self._ix["body_ids"]]
+    return self.data.xpos[:, self._rows("body_ids")]
 
   @_cached
   def _body_link_quat_w(self) -> torch.Tensor:
     """== body_link_pose_w[..., 3:7]"""
-    return self.data.xquat[:, self._ix["body_ids"]]
+    return self.data.xquat[:, self._rows("body_ids")]
 
   @_cached
   def _geom_pos_w(self) -> torch.Tensor:
     """== geom_pose_w[..., 0:3], without converting the frames to quaternions."""
-    return self.data.geom_xpos[:, self._ix["geom_ids"]]
+    return self.data.geom_xpos[:, self._rows("geom_ids")]
 
   @_cached
   def _site_pos_w(self) -> torch.Tensor:
     """== site_pose_w[..., 0:3], without converting the frames to quaternions."""
-    return self.data.site_xpos[:, self._ix["site_ids"]]
+    return self.data.site_xpos[:, self._rows("site_ids")]
 
   @_cached
   def projected_gravity_b(self) -> torch.Tensor:

@@ -199,6 +199,8 @@ def rew_feet(pos: torch.Tensor, vel: torch.Tensor, found, cmd: torch.Tensor, tar
   n, k = pos.shape[0], pos.shape[1]
   if vel.stride(1) != 3:
     vel = vel.contiguous()
+  if found is not None and found.dim() == 2 and found.stride(1) != 1:
+    found = found.contiguous()  # strided sensor-slot view
   if found is not None and not (found.dim() == 2 and found.stride(1) == 1 and found.shape == (n, k) and found.dtype == torch.float32):
     return None
   z = pos[:, :, 2]
@@ -316,28 +318,64 @@ class ObsTermDesc(ctypes.Structure):
   """mjh_obs_term_desc (include/mjh_abi.h)."""
   _fields_ = [("x", ctypes.c_void_p), ("xs", ctypes.c_longlong), ("w", ctypes.c_int), ("off", ctypes.c_int),
               ("lo", ctypes.c_float), ("hi", ctypes.c_float), ("cmin", ctypes.c_float), ("cmax", ctypes.c_float),
-              ("scale", ctypes.c_float), ("noise", ctypes.c_int)]
+              ("scale", ctypes.c_float), ("noise", ctypes.c_int), ("y", ctypes.c_void_p), ("ys", ctypes.c_longlong),
+              ("xcs", ctypes.c_longlong), ("op", ctypes.c_int), ("_pad", ctypes.c_int)]
+
+
+OBS_COPY, OBS_SUB, OBS_POSITIVE, OBS_SIGNED_LOG1P = 0, 1, 2, 3
+
+
+class ObsSrc:
+  """An observation term as an elementwise op on strided device inputs, which
+  the group kernel evaluates while assembling the group (no per-term launch):
+  x (n, w) any strides; OBS_SUB subtracts y (n, w) (unit column stride)."""
+
+  __slots__ = ("x", "op", "y")
+
+  def __init__(self, x: torch.Tensor, op: int = OBS_COPY, y: torch.Tensor | None = None) -> None:
+    self.x, self.op, self.y = x, op, y
+
+  def evaluate(self) -> torch.Tensor:
+    """The torch formula of the op (reference for the fused evaluation)."""
+    x = self.x
+    if self.op == OBS_SUB:
+      return x - self.y
+    if self.op == OBS_POSITIVE:
+      return (x > 0).float()
+    if self.op == OBS_SIGNED_LOG1P:
+      return torch.sign(x) * torch.log1p(torch.abs(x))
+    return x
 
 
 def _term_rows(x: torch.Tensor):
-  """(n,) or (n, w) float32 GPU rows with unit column stride -> (tensor, w), else None."""
+  """(n,) or (n, w) float32 GPU tensor (any strides) -> (2-D view, w), else None."""
   if not (x.is_cuda and x.dtype == torch.float32):
     return None
   if x.dim() == 1:
-    x = x.unsqueeze(1)  # (n, 1) with strides (s, 1)
-  if x.dim() != 2 or (x.shape[1] > 1 and x.stride(1) != 1):
+    x = x.unsqueeze(1)  # (n, 1)
+  if x.dim() != 2:
     return None
   return x, x.shape[1]
 
 
-def obs_group(xs: list, plan: list, u: torch.Tensor | None, out: torch.Tensor) -> bool:
+def obs_group(xs: list, plan: list, u: torch.Tensor | None, out: torch.Tensor, rng=None) -> bool:
   """All terms of a concatenated observation group in one launch.
-  plan[i] = (tcfg, off, w, noise (lo, hi) | None, clip | None, scale)."""
+  xs[i]: the term's tensor or an ObsSrc; plan[i] = (tcfg, off, w, noise (lo, hi) |
+  None, clip | None, scale); noise draws from u (n, width) or, when u is None,
+  the device stream rng = (seed, key, counter ptr) of envops.rng_args."""
   if len(xs) > MAX_TERMS or not out.is_cuda or out.stride(1) != 1 or (u is not None and u.stride(1) != 1):
+    return False
+  if u is None and rng is None and any(p[3] is not None for p in plan):
     return False
   n = out.shape[0]
   descs = (ObsTermDesc * len(xs))()
   for i, (x, (_, off, w, noise, clip, scale)) in enumerate(zip(xs, plan)):
+    op, y = OBS_COPY, None
+    if isinstance(x, ObsSrc):
+      op, y, x = x.op, x.y, x.x
+      if y is not None and not (y.is_cuda and y.dtype == torch.float32 and y.dim() == 2 and y.stride(1) == 1
+                                and y.shape == (n, w)):
+        return False
     r = _term_rows(x)
     if r is None or r[1] != w or r[0].shape[0] != n:
       return False
@@ -345,10 +383,12 @@ def obs_group(xs: list, plan: list, u: torch.Tensor | None, out: torch.Tensor) -
     cmin, cmax = (float(clip[0]), float(clip[1])) if clip else (1.0, -1.0)
     lo, hi = noise if noise is not None else (0.0, 0.0)
     descs[i] = ObsTermDesc(x2.data_ptr(), x2.stride(0), w, off, float(lo), float(hi), cmin, cmax, float(scale),
-                           int(noise is not None))
+                           int(noise is not None), y.data_ptr() if y is not None else None, y.stride(0) if y is not None else 0,
+                           x2.stride(1), op, 0)
+  seed, key, ctr = rng if rng is not None else (ctypes.c_ulonglong(0), ctypes.c_ulonglong(0), None)
   native.check(native.lib().mjh_obs_group(descs, len(xs), _ptr(u) if u is not None else None,
-                                          u.stride(0) if u is not None else 0, _ptr(out), out.stride(0), n, _stream()),
-               "mjh_obs_group")
+                                          u.stride(0) if u is not None else 0, _ptr(out), out.stride(0), n, seed, key, ctr,
+                                          _stream()), "mjh_obs_group")
   return True
 
 

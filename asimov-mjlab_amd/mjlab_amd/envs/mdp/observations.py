@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import torch
 
+from mjlab_amd import envops
 from mjlab_amd.managers.scene_entity_config import SceneEntityCfg
 
 _DEFAULT = SceneEntityCfg("robot")
@@ -31,6 +32,22 @@ def joint_vel_rel(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   a = env.scene[asset_cfg.name]
   j = asset_cfg.joint_idx
   return a.data.joint_vel[:, j] - a.data.default_joint_vel[:, j]
+
+
+def _joint_rel_src(env, key: str, state: str, default: str, asset_cfg: SceneEntityCfg = _DEFAULT):
+  """joint_{pos,vel}_rel as an in-kernel subtraction of strided views (no
+  gather, no subtraction launch) when the entity's joint columns are contiguous."""
+  a = env.scene[asset_cfg.name]
+  j = asset_cfg.joint_idx
+  cols = a.data._cols[key]
+  if not isinstance(j, slice) or not isinstance(cols, slice):
+    return None
+  x = getattr(a.data.data, state)[:, cols][:, j]
+  return envops.ObsSrc(x, envops.OBS_SUB, getattr(a.data, default)[:, j])
+
+
+joint_pos_rel.obs_src = lambda env, asset_cfg=_DEFAULT: _joint_rel_src(env, "joint_q_adr", "qpos", "default_joint_pos", asset_cfg)
+joint_vel_rel.obs_src = lambda env, asset_cfg=_DEFAULT: _joint_rel_src(env, "joint_v_adr", "qvel", "default_joint_vel", asset_cfg)
 
 
 def last_action(env, action_name: str | None = None) -> torch.Tensor:

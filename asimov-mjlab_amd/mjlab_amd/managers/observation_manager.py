@@ -146,6 +146,16 @@ class ObservationManager:
       return torch.cat(list(obs_terms.values()), dim=self._group_concat_dim[group_name])
     return obs_terms
 
+  def _term_input(self, tcfg):
+    """The term's value, or an envops.ObsSrc (an elementwise op on strided
+    inputs the group kernel evaluates) when the term function offers one."""
+    src = getattr(tcfg.func, "obs_src", None)
+    if src is not None:
+      s = src(self._env, **tcfg.params)
+      if s is not None:
+        return s
+    return tcfg.func(self._env, **tcfg.params).float()
+
   def _compute_fused(self, fp, u_fixed=None):
     """One fused launch per term writing straight into the group buffer (no
     per-term clone/noise/scale chain, no final cat); one U[0,1) draw per group."""
@@ -154,12 +164,18 @@ class ObservationManager:
     plan, width = fp
     n = self._env.num_envs
     out = torch.empty((n, width), device=self._env.device)
-    u = None
+    u, rng = None, None
     if any(p[3] is not None for p in plan):
-      u = u_fixed if u_fixed is not None else torch.rand((n, width), device=self._env.device)
-    xs = [tcfg.func(self._env, **tcfg.params).float() for tcfg, *_ in plan]
-    if envops.obs_group(xs, plan, u, out):  # the whole group in one launch
+      if u_fixed is not None:
+        u = u_fixed
+      else:  # noise drawn inside the group kernel from the env's device stream
+        rng = envops.rng_args(self._env, "observation_noise")
+    xs = [self._term_input(tcfg) for tcfg, *_ in plan]
+    if envops.obs_group(xs, plan, u, out, rng):  # the whole group in one launch
       return out
+    if u is None and rng is not None:
+      u = torch.rand((n, width), device=self._env.device)
+    xs = [x.evaluate() if isinstance(x, envops.ObsSrc) else x for x in xs]
     for x, (tcfg, off, w, noise, clip, scale) in zip(xs, plan):
       lo, hi = noise if noise is not None else (0.0, 0.0)
       uu = u[:, off : off + w] if noise is not None else None

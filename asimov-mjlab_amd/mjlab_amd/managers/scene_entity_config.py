@@ -60,5 +60,10 @@ class SceneEntityCfg:
 
     for _, ids_attr, _, _ in _FIELDS:
       ids = getattr(self, ids_attr)
-      idx = slice(None) if isinstance(ids, slice) else torch.tensor(ids, dtype=torch.long, device=scene.device)
+      if isinstance(ids, slice):
+        idx = slice(None)
+      elif len(ids) > 0 and list(ids) == list(range(ids[0], ids[0] + len(ids))):
+        idx = slice(ids[0], ids[0] + len(ids))  # a contiguous range: reads are views, no gather launch
+      else:
+        idx = torch.tensor(ids, dtype=torch.long, device=scene.device)
       setattr(self, ids_attr.replace("_ids", "_idx"), idx)

@@ -39,6 +39,18 @@ class SensorCfg:
   name: str
 
 
+def _regular_slots(cols: list[int], dim: int):
+  """(first column, slot spacing, slots) when cols = [a + i*s + c for i < k, c < dim], else None."""
+  if not cols or len(cols) % dim:
+    return None
+  k = len(cols) // dim
+  a = cols[0]
+  s = cols[dim] - a if k > 1 else dim
+  if s < dim:
+    return None
+  return (a, s, k) if cols == [a + i * s + c for i in range(k) for c in range(dim)] else None
+
+
 @dataclass
 class ContactSensorCfg(SensorCfg):
   primary: ContactMatch = None  # type: ignore[assignment]
@@ -248,12 +260,19 @@ class ContactSensor:
             a = slot.data_view.storage_offset() - self._data.sensordata.storage_offset()
             cols += list(range(a, a + slot.data_view.shape[1]))
         self._field_cols[f] = torch.tensor(cols, dtype=torch.long, device=self._data.sensordata.device)
+        self._field_stride = getattr(self, "_field_stride", {})
+        self._field_stride[f] = _regular_slots(cols, _CONTACT_DATA_DIMS[f])
     out = ContactData()
     sd = self._data.sensordata
     n = sd.shape[0]
     for f in self.cfg.fields:
       dim = _CONTACT_DATA_DIMS[f]
-      cat = sd[:, self._field_cols[f]].view(n, -1, dim)
+      reg = self._field_stride.get(f)
+      if reg is not None and sd.stride(1) == 1:  # slots evenly spaced: a strided view, no gather launch
+        a, s, k = reg
+        cat = sd.as_strided((n, k, dim), (sd.stride(0), s, 1), sd.storage_offset() + a)
+      else:
+        cat = sd[:, self._field_cols[f]].view(n, -1, dim)
       if cat.size(-1) == 1:
         cat = cat.squeeze(-1)
       setattr(out, f, cat)

@@ -20,7 +20,7 @@ PKG = Path(__file__).resolve().parents[1]
 # MJH_LIB selects an alternative build of the same ABI (e.g. the phase-timing
 # build libmjh_prof.so used by tools/phase_profile.py).
 LIB_PATH = Path(os.environ.get("MJH_LIB", str(PKG / "libmjh.so")))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 EXPORTS = (
   "mjh_abi_version",
@@ -133,7 +133,7 @@ def lib() -> ctypes.CDLL:
   L.mjh_quat_error.argtypes = [vp, ll, vp, ll, vp, ll, vp]
   L.mjh_frame_subtract.argtypes = [vp, ll, vp, ll, vp, ll, ll, vp, ll, ll, ci, vp, vp, ci, ll, vp]
   L.mjh_motion_relative.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, ll, vp, ll, ll, ci, vp, vp, ll, vp]
-  L.mjh_obs_group.argtypes = [vp, ci, vp, ll, vp, ll, ll, vp]
+  L.mjh_obs_group.argtypes = [vp, ci, vp, ll, vp, ll, ll, ctypes.c_ulonglong, ctypes.c_ulonglong, vp, vp]
   L.mjh_reward_combine.argtypes = [vp, vp, ci, vp, cf, vp, vp, vp, ll, vp]
   L.mjh_flag_stats.argtypes = [vp, ll, vp, vp]
   u64 = ctypes.c_ulonglong

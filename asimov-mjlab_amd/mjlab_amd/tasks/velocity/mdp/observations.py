@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import torch
 
+from mjlab_amd import envops
 from mjlab_amd.managers.scene_entity_config import SceneEntityCfg
 
 _DEFAULT = SceneEntityCfg("robot")
@@ -24,3 +25,20 @@ def foot_contact(env, sensor_name: str) -> torch.Tensor:
 def foot_contact_forces(env, sensor_name: str) -> torch.Tensor:
   f = env.scene[sensor_name].data.force.flatten(start_dim=1)
   return torch.sign(f) * torch.log1p(torch.abs(f))
+
+
+# evaluated inside the observation group kernel (envops.ObsSrc): no launch per term
+def _foot_contact_src(env, sensor_name: str):
+  found = env.scene[sensor_name].data.found
+  return envops.ObsSrc(found, envops.OBS_POSITIVE) if found is not None and found.dim() == 2 else None
+
+
+def _foot_contact_forces_src(env, sensor_name: str):
+  f = env.scene[sensor_name].data.force
+  if f is None or f.dim() != 3 or f.stride(2) != 1 or f.stride(1) != 3:
+    return None
+  return envops.ObsSrc(f.flatten(start_dim=1), envops.OBS_SIGNED_LOG1P)
+
+
+foot_contact.obs_src = _foot_contact_src
+foot_contact_forces.obs_src = _foot_contact_forces_src

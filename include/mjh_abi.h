@@ -34,7 +34,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 5
+#define MJH_ABI_VERSION 6
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -256,12 +256,27 @@ typedef struct mjh_obs_term_desc {
   int off;
   float lo, hi, cmin, cmax, scale;
   int noise;
+  /* the term's value from a strided input: x[e * xs + j * xcs], then op:
+     MJH_OBS_COPY, MJH_OBS_SUB (minus y[e * ys + j]), MJH_OBS_POSITIVE (x > 0 as
+     0/1), MJH_OBS_SIGNED_LOG1P (sign(x) * log1p(|x|)) */
+  const float* y;
+  long long ys;
+  long long xcs;
+  int op;
+  int _pad;
 } mjh_obs_term_desc;
 
+#define MJH_OBS_COPY 0
+#define MJH_OBS_SUB 1
+#define MJH_OBS_POSITIVE 2
+#define MJH_OBS_SIGNED_LOG1P 3
+
 /* ObservationManager.compute for one concatenated group in one launch
- * (observation_manager.py:156-195); terms are read from host memory at call time. */
+ * (observation_manager.py:156-195); terms are read from host memory at call
+ * time. Noise draws: u[e * us + col] when u != NULL, else element
+ * e * width + col of the (seed, key, *ctr) device stream (mjh_uniform_draws). */
 int mjh_obs_group(const mjh_obs_term_desc* terms, int nterms, const float* u, long long us, float* out, long long os,
-                  long long n, void* stream);
+                  long long n, unsigned long long seed, unsigned long long key, const mjh_i64* ctr, void* stream);
 
 /* RewardManager.compute's combination step (reward_manager.py:76-88) for nterms
  * term vectors values[t] (row stride strides[t]; NULL = weight-0 term, value 0):

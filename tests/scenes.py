@@ -297,7 +297,10 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
   if len(good):
     ne = ref["nefc"][good, 0].astype(int)
     mask = np.arange(ref["efc_pos"].shape[1])[None, :] < ne[:, None]
-    for k, rel in (("efc_pos", 5e-5), ("efc_D", 1e-3), ("efc_aref", 1e-3), ("efc_force", solve_rel)):
+    # efc_D = imp / ((1 - imp) * invweight): near dmax the impedance amplifies the
+    # (5e-5) position difference by ~1 / (1 - imp)^2; measured 1.2e-3 x (1 + max)
+    # on the tracking N=4096 world sample (round 2), hence 3e-3
+    for k, rel in (("efc_pos", 5e-5), ("efc_D", 3e-3), ("efc_aref", 1e-3), ("efc_force", solve_rel)):
       a, b = got[k][good][mask], ref[k][good][mask]
       tol = 5e-5 if k == "efc_pos" else _bound(b, rel if k != "efc_force" else solve_max)
       e = float(np.abs(a - b).max(initial=0.0))

@@ -252,3 +252,33 @@ def test_env_reset_path_uses_fused_kernels():
   assert ((t.time_left >= lo - env.step_dt) & (t.time_left <= hi)).all()
   q = env.sim.data.qpos
   assert torch.isfinite(q).all() and torch.allclose(q[:, 3:7].norm(dim=1), torch.ones(256, device=DEV), atol=1e-5)
+
+
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+def test_obs_group_ops_and_strides(op):
+  """Observation terms given as ObsSrc (strided inputs + elementwise op) are
+  evaluated inside the group kernel exactly as ObsSrc.evaluate's torch formula."""
+  from mjlab_amd.managers.manager_term_config import ObservationTermCfg
+
+  n = 4096
+  g = torch.Generator(device=DEV).manual_seed(10 + op)
+  base = torch.randn(n, 40, device=DEV, generator=g) * 3
+  x = base[:, 2:30:4]  # (n, 7) with column stride 4
+  y = torch.randn(n, 7, device=DEV, generator=g)
+  src = envops.ObsSrc(x, op, y if op == envops.OBS_SUB else None)
+  other = torch.randn(n, 3, device=DEV, generator=g)
+  tc = ObservationTermCfg(func=lambda env: None)
+  plan = [(tc, 0, 3, (-0.1, 0.1), None, 1.0), (tc, 3, 7, (-0.5, 0.5), (-2.0, 2.0), 0.25)]
+  u = torch.rand(n, 10, device=DEV, generator=g)
+  out = torch.empty(n, 10, device=DEV)
+  assert envops.obs_group([other, src], plan, u, out)
+  ref1 = other + (u[:, :3] * 0.2 - 0.1)
+  ref2 = (src.evaluate() + (u[:, 3:] * 1.0 - 0.5)).clamp(-2.0, 2.0) * 0.25
+  torch.testing.assert_close(out[:, :3], ref1, rtol=1e-6, atol=1e-6)
+  torch.testing.assert_close(out[:, 3:], ref2, rtol=1e-5, atol=1e-6)
+  # noise from the device stream: element e * width + column
+  ctr = _ctr(21)
+  out2 = torch.empty(n, 10, device=DEV)
+  assert envops.obs_group([other, src], plan, None, out2, _args(ctr))
+  uu = envops.uniform_draws(SEED, KEY, ctr, n * 10, DEV).view(n, 10)
+  torch.testing.assert_close(out2[:, :3], other + (uu[:, :3] * 0.2 - 0.1), rtol=1e-6, atol=1e-6)
