@@ -342,6 +342,173 @@ __global__ void term_combine_kernel(const TermArgs a, unsigned char* __restrict_
   dones[e] = tr | te;
 }
 
+// compute_velocity_from_cvel (entity/data.py:25-30 of the reference restated)
+// for k rows per env read in place: point j of env e at pos + e*pes + j*prs,
+// its body's cvel at cvel + e*ves + 6*body[j], the root subtree com at
+// com + e*cs; out (n*k, 6) = [lin - ang x (com - pos), ang]
+__global__ void velocity_rows_kernel(const float* __restrict__ pos, long long pes, long long prs,
+                                     const float* __restrict__ com, long long cs, const float* __restrict__ cvel,
+                                     long long ves, const int* __restrict__ body, float* __restrict__ out, int k,
+                                     long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * k) return;
+  const long long e = i / k;
+  const int j = (int)(i - e * k);
+  const float* p = pos + e * pes + j * prs;
+  const float* c = com + e * cs;
+  const float* v = cvel + e * ves + 6ll * body[j];
+  const float ox = c[0] - p[0], oy = c[1] - p[1], oz = c[2] - p[2];
+  const float ax = v[0], ay = v[1], az = v[2];
+  float* o = out + 6 * i;
+  o[0] = v[3] - (ay * oz - az * oy);
+  o[1] = v[4] - (az * ox - ax * oz);
+  o[2] = v[5] - (ax * oy - ay * ox);
+  o[3] = ax; o[4] = ay; o[5] = az;
+}
+
+// zero the rows of several float tensors where mask (one launch for a
+// manager's masked_fill_(mask, 0) chain): tensor t holds w[t] floats per row
+struct ZeroArgs {
+  float* p[MJH_MAX_TERMS];
+  long long rs[MJH_MAX_TERMS];
+  int w[MJH_MAX_TERMS];
+  int ntensors, wmax;
+};
+
+__global__ void masked_zero_kernel(const ZeroArgs a, const unsigned char* __restrict__ mask, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = blockIdx.y;
+  if (i >= n * a.wmax || t >= a.ntensors) return;
+  const long long e = i / a.wmax;
+  const int j = (int)(i - e * a.wmax);
+  if (j < a.w[t] && on(mask, e)) a.p[t][e * a.rs[t] + j] = 0.f;
+}
+
+// sum(num[t]) / max(sum(den[t]), 1) over all envs (the per-step metric logs of
+// the reward terms, e.g. rewards.py Metrics/*_mean); one workgroup
+struct RatioArgs {
+  const float* num[MJH_MAX_TERMS];
+  const float* den[MJH_MAX_TERMS];
+  int nterms;
+};
+
+__global__ __launch_bounds__(1024) void sum_ratios_kernel(const RatioArgs a, float* __restrict__ out, long long n) {
+  __shared__ float part[2 * MJH_MAX_TERMS][16];
+  float sn[MJH_MAX_TERMS], sd[MJH_MAX_TERMS];
+#pragma unroll
+  for (int t = 0; t < MJH_MAX_TERMS; t++) sn[t] = sd[t] = 0.f;
+  for (long long e = threadIdx.x; e < n; e += 1024) {
+#pragma unroll
+    for (int t = 0; t < MJH_MAX_TERMS; t++)
+      if (t < a.nterms) {
+        sn[t] += a.num[t][e];
+        sd[t] += a.den[t][e];
+      }
+  }
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < MJH_MAX_TERMS; t++) {
+    if (t < a.nterms) {
+      float x = sn[t], y = sd[t];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        x += __shfl_xor(x, o, 64);
+        y += __shfl_xor(y, o, 64);
+      }
+      if (lane == 0) {
+        part[2 * t][wv] = x;
+        part[2 * t + 1][wv] = y;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < (unsigned)a.nterms) {
+    float x = 0.f, y = 0.f;
+    for (int w = 0; w < 16; w++) {
+      x += part[2 * threadIdx.x][w];
+      y += part[2 * threadIdx.x + 1][w];
+    }
+    out[threadIdx.x] = x / fmaxf(y, 1.f);
+  }
+}
+
+// ---- contact-timing rewards of the velocity task (tasks/velocity/mdp/rewards.py)
+// One thread per env over its k feet; `cmd` NULL = no command gating, else the
+// term is multiplied by (|cmd_xy| + |cmd_yaw| > cmd_thr). num/den: per-env
+// parts of the term's metric log (sum(num) / max(sum(den), 1), mjh_sum_ratios).
+__device__ __forceinline__ float cmd_active(const float* cmd, long long cs, long long e, float thr) {
+  if (!cmd) return 1.f;
+  const float* c = cmd + e * cs;
+  return (sqrtf(c[0] * c[0] + c[1] * c[1]) + fabsf(c[2])) > thr ? 1.f : 0.f;
+}
+
+// feet_air_time: sum((t > tmin) & (t < tmax)) * active; log air_time_mean
+__global__ void rew_air_time_kernel(const float* __restrict__ t, long long ts, const float* __restrict__ cmd, long long cs,
+                                    float tmin, float tmax, float cmd_thr, float* __restrict__ out,
+                                    float* __restrict__ num, float* __restrict__ den, int k, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  float r = 0.f, a = 0.f, b = 0.f;
+  for (int j = 0; j < k; j++) {
+    const float x = t[e * ts + j];
+    r += (x > tmin && x < tmax) ? 1.f : 0.f;
+    const float in_air = x > 0.f ? 1.f : 0.f;
+    a += x * in_air;
+    b += in_air;
+  }
+  out[e] = r * cmd_active(cmd, cs, e, cmd_thr);
+  num[e] = a;
+  den[e] = b;
+}
+
+// feet_swing_height: peak = in_air ? max(peak, h) : peak; first contact =
+// 0 < contact_time < first_lim; cost = sum((peak / target - 1)^2 * first) *
+// active; log peak_height_mean; peak cleared where first
+__global__ void rew_swing_height_kernel(float* __restrict__ peak, const float* __restrict__ h, long long hes,
+                                        long long hcs, const float* __restrict__ found, long long fes, long long fcs,
+                                        const float* __restrict__ cct, long long cts, const float* __restrict__ cmd,
+                                        long long cs, float first_lim, float target, float cmd_thr,
+                                        float* __restrict__ out, float* __restrict__ num, float* __restrict__ den, int k,
+                                        long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  float c = 0.f, a = 0.f, b = 0.f;
+  for (int j = 0; j < k; j++) {
+    float p = peak[e * k + j];
+    if (found[e * fes + j * fcs] == 0.f) p = fmaxf(p, h[e * hes + j * hcs]);
+    const float ct = cct[e * cts + j];
+    const float first = (ct > 0.f && ct < first_lim) ? 1.f : 0.f;
+    const float err = p / target - 1.f;
+    c += err * err * first;
+    a += p * first;
+    b += first;
+    peak[e * k + j] = first != 0.f ? 0.f : p;
+  }
+  out[e] = c * cmd_active(cmd, cs, e, cmd_thr);
+  num[e] = a;
+  den[e] = b;
+}
+
+// soft_landing: sum(|force| * first) * active; log landing_force_mean
+__global__ void rew_soft_landing_kernel(const float* __restrict__ f, long long fes, long long fss,
+                                        const float* __restrict__ cct, long long cts, const float* __restrict__ cmd,
+                                        long long cs, float first_lim, float cmd_thr, float* __restrict__ out,
+                                        float* __restrict__ num, float* __restrict__ den, int k, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  float c = 0.f, b = 0.f;
+  for (int j = 0; j < k; j++) {
+    const float* v = f + e * fes + j * fss;
+    const float ct = cct[e * cts + j];
+    const float first = (ct > 0.f && ct < first_lim) ? 1.f : 0.f;
+    c += sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]) * first;
+    b += first;
+  }
+  out[e] = c * cmd_active(cmd, cs, e, cmd_thr);
+  num[e] = c;
+  den[e] = b;
+}
+
 }  // namespace
 
 extern "C" {
@@ -469,6 +636,71 @@ int mjh_term_combine(const unsigned char* const* values, unsigned char* const* t
   a.nterms = nterms;
   hipLaunchKernelGGL(term_combine_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, a, truncated, terminated,
                      dones, n);
+  return finish();
+}
+
+int mjh_velocity_rows(const float* pos, long long pes, long long prs, const float* com, long long cs, const float* cvel,
+                      long long ves, const int* body, float* out, int k, long long n, void* stream) {
+  if (n <= 0 || k <= 0) return 0;
+  hipLaunchKernelGGL(velocity_rows_kernel, dim3(grid(n * k)), dim3(kBlock), 0, (hipStream_t)stream, pos, pes, prs, com, cs,
+                     cvel, ves, body, out, k, n);
+  return finish();
+}
+
+int mjh_masked_zero(float* const* ptrs, const long long* row_strides, const int* widths, int ntensors,
+                    const unsigned char* mask, long long n, void* stream) {
+  if (n <= 0 || ntensors <= 0) return 0;
+  if (ntensors > MJH_MAX_TERMS) return 1;
+  ZeroArgs a{};
+  a.wmax = 0;
+  for (int t = 0; t < ntensors; t++) {
+    a.p[t] = ptrs[t];
+    a.rs[t] = row_strides[t];
+    a.w[t] = widths[t];
+    if (widths[t] > a.wmax) a.wmax = widths[t];
+  }
+  a.ntensors = ntensors;
+  hipLaunchKernelGGL(masked_zero_kernel, dim3(grid(n * a.wmax), ntensors), dim3(kBlock), 0, (hipStream_t)stream, a, mask, n);
+  return finish();
+}
+
+int mjh_sum_ratios(const float* const* num, const float* const* den, int nterms, float* out, long long n, void* stream) {
+  if (n <= 0 || nterms <= 0) return 0;
+  if (nterms > MJH_MAX_TERMS) return 1;
+  RatioArgs a{};
+  for (int t = 0; t < nterms; t++) {
+    a.num[t] = num[t];
+    a.den[t] = den[t];
+  }
+  a.nterms = nterms;
+  hipLaunchKernelGGL(sum_ratios_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a, out, n);
+  return finish();
+}
+
+int mjh_rew_air_time(const float* t, long long ts, const float* cmd, long long cs, float tmin, float tmax, float cmd_thr,
+                     float* out, float* num, float* den, int k, long long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rew_air_time_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, t, ts, cmd, cs, tmin, tmax,
+                     cmd_thr, out, num, den, k, n);
+  return finish();
+}
+
+int mjh_rew_swing_height(float* peak, const float* h, long long hes, long long hcs, const float* found, long long fes,
+                         long long fcs, const float* cct, long long cts, const float* cmd, long long cs, float first_lim,
+                         float target, float cmd_thr, float* out, float* num, float* den, int k, long long n,
+                         void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rew_swing_height_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, peak, h, hes, hcs, found,
+                     fes, fcs, cct, cts, cmd, cs, first_lim, target, cmd_thr, out, num, den, k, n);
+  return finish();
+}
+
+int mjh_rew_soft_landing(const float* f, long long fes, long long fss, const float* cct, long long cts, const float* cmd,
+                         long long cs, float first_lim, float cmd_thr, float* out, float* num, float* den, int k,
+                         long long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rew_soft_landing_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, f, fes, fss, cct, cts, cmd,
+                     cs, first_lim, cmd_thr, out, num, den, k, n);
   return finish();
 }
 

@@ -226,6 +226,12 @@ class EntityData:
     if env_ids is not None and not isinstance(env_ids, slice) and env_ids.dtype == torch.bool:
       m = env_ids[:, None]
       xf = self.data.xfrc_applied.view(n, -1)
+      views = [self.data.qfrc_applied[:, self._cols["free_joint_v_adr"]], xf[:, self._cols["xfrc_all"]]]
+      if self.is_actuated:
+        views.append(self.data.ctrl[:, self._cols["ctrl_ids"]])
+      if all(isinstance(self._cols[k], slice) for k in ("free_joint_v_adr", "xfrc_all", "ctrl_ids")) and envops.masked_zero(
+          [v for v in views if v.shape[1] > 0], env_ids):
+        return  # one launch for the applied forces, wrenches and controls
       for dst, key in ((self.data.qfrc_applied, "free_joint_v_adr"), (xf, "xfrc_all"), (self.data.ctrl, "ctrl_ids")):
         cols = self._cols[key]
         if key == "ctrl_ids" and not self.is_actuated:
@@ -276,8 +282,22 @@ class EntityData:
     ids = self._ix["body_ids"]
     return torch.cat([self.data.xpos[:, ids], self.data.xquat[:, ids]], dim=-1)
 
+  def _vel_rows(self, arr, key: str, body_key: str):
+    """compute_velocity_from_cvel of this entity's rows of `arr` in one launch
+    (strided reads, no gathers), or None when the layout is unsupported."""
+    if not arr.is_cuda:
+      return None
+    b32 = self.__dict__.setdefault("_ix32", {})
+    if body_key not in b32:
+      b32[body_key] = self._ix[body_key].to(torch.int32).contiguous()
+    return envops.velocity_rows(arr[:, self._rows(key)], self.data.subtree_com[:, self._root], self.data.cvel,
+                                b32[body_key])
+
   @_cached
   def body_link_vel_w(self) -> torch.Tensor:
+    v = self._vel_rows(self.data.xpos, "body_ids", "body_ids")
+    if v is not None:
+      return v
     ids = self._ix["body_ids"]
     com = self.data.subtree_com[:, self._root].unsqueeze(1)
     return compute_velocity_from_cvel(self.data.xpos[:, ids], com, self.data.cvel[:, ids])
@@ -290,6 +310,9 @@ class EntityData:
 
   @_cached
   def body_com_vel_w(self) -> torch.Tensor:
+    v = self._vel_rows(self.data.xipos, "body_ids", "body_ids")
+    if v is not None:
+      return v
     ids = self._ix["body_ids"]
     com = self.data.subtree_com[:, self._root].unsqueeze(1)
     return compute_velocity_from_cvel(self.data.xipos[:, ids], com, self.data.cvel[:, ids])
@@ -305,6 +328,9 @@ class EntityData:
 
   @_cached
   def geom_vel_w(self) -> torch.Tensor:
+    v = self._vel_rows(self.data.geom_xpos, "geom_ids", "geom_bodyid")
+    if v is not None:
+      return v
     ids = self._ix["geom_ids"]
     bids = self._ix["geom_bodyid"]
     com = self.data.subtree_com[:, self._root].unsqueeze(1)
@@ -317,6 +343,9 @@ class EntityData:
 
   @_cached
   def site_vel_w(self) -> torch.Tensor:
+    v = self._vel_rows(self.data.site_xpos, "site_ids", "site_bodyid")
+    if v is not None:
+      return v
     ids = self._ix["site_ids"]
     bids = self._ix["site_bodyid"]
     com = self.data.subtree_com[:, self._root].unsqueeze(1)

@@ -571,3 +571,116 @@ def term_combine(values: list, term_dones: list, time_out: list, truncated, term
   native.check(native.lib().mjh_term_combine(vp, dp, to, T, _ptr(truncated), _ptr(terminated), _ptr(dones), n, _stream()),
                "mjh_term_combine")
   return True
+
+
+def velocity_rows(pos: torch.Tensor, com: torch.Tensor, cvel: torch.Tensor, body: torch.Tensor) -> torch.Tensor | None:
+  """compute_velocity_from_cvel(pos (N, k, 3) strided view, com (N, 3), cvel[:, body] of
+  cvel (N, nbody, 6)) without the gathers, or None if the layout is unsupported."""
+  ok = all(t.is_cuda and t.dtype == torch.float32 for t in (pos, com, cvel)) and body.is_cuda and body.dtype == torch.int32
+  if not ok or pos.dim() != 3 or pos.stride(2) != 1 or com.dim() != 2 or com.stride(1) != 1 or cvel.dim() != 3:
+    return None
+  if cvel.stride(2) != 1 or cvel.stride(1) != 6 or body.numel() != pos.shape[1] or not body.is_contiguous():
+    return None
+  n, k = pos.shape[0], pos.shape[1]
+  out = torch.empty((n, k, 6), dtype=torch.float32, device=pos.device)
+  native.check(native.lib().mjh_velocity_rows(_ptr(pos), pos.stride(0), pos.stride(1), _ptr(com), com.stride(0), _ptr(cvel),
+                                              cvel.stride(0), _ptr(body), _ptr(out), k, n, _stream()), "mjh_velocity_rows")
+  return out
+
+
+def masked_zero(tensors: list, mask) -> bool:
+  """t[mask] = 0 for several float tensors (rows of unit column stride) in one launch."""
+  T = len(tensors)
+  if T == 0 or T > MAX_TERMS or not _bool_mask(mask) or mask is None:
+    return False
+  n = mask.shape[0]
+  ptrs = (ctypes.c_void_p * T)()
+  rs = (ctypes.c_longlong * T)()
+  ws = (ctypes.c_int * T)()
+  for i, t in enumerate(tensors):
+    t2 = t.unsqueeze(1) if t.dim() == 1 else (t.reshape(t.shape[0], -1) if t.dim() > 2 and t.is_contiguous() else t)
+    if not (t2.is_cuda and t2.dtype == torch.float32 and t2.dim() == 2 and t2.shape[0] == n and (t2.shape[1] == 1 or t2.stride(1) == 1)):
+      return False
+    ptrs[i], rs[i], ws[i] = t2.data_ptr(), t2.stride(0), t2.shape[1]
+  native.check(native.lib().mjh_masked_zero(ptrs, rs, ws, T, _ptr(mask), n, _stream()), "mjh_masked_zero")
+  return True
+
+
+def sum_ratios(pairs: list, out: torch.Tensor) -> bool:
+  """out[t] = sum(num_t) / max(sum(den_t), 1) for (num_t, den_t) (N,) float vectors, one launch."""
+  T = len(pairs)
+  if T == 0 or T > MAX_TERMS or not out.is_cuda or out.numel() < T:
+    return False
+  for a, b in pairs:
+    if not all(x.is_cuda and x.dtype == torch.float32 and x.dim() == 1 and x.is_contiguous() for x in (a, b)):
+      return False
+  num = (ctypes.c_void_p * T)(*[a.data_ptr() for a, _ in pairs])
+  den = (ctypes.c_void_p * T)(*[b.data_ptr() for _, b in pairs])
+  native.check(native.lib().mjh_sum_ratios(num, den, T, _ptr(out), pairs[0][0].shape[0], _stream()), "mjh_sum_ratios")
+  return True
+
+
+def _col_strides(t: torch.Tensor, n: int, k: int):
+  """(env stride, column stride) of a float32 (n, k) GPU view, else None."""
+  if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.shape == (n, k)):
+    return None
+  return t.stride(0), t.stride(1)
+
+
+def _cmd_args(cmd):
+  if cmd is None:
+    return None, 0
+  return _ptr(cmd), cmd.stride(0)
+
+
+def rew_air_time(t, cmd, tmin: float, tmax: float, cmd_thr: float):
+  """feet_air_time in one launch -> (reward, log num, log den), or None."""
+  n, k = t.shape
+  st = _col_strides(t, n, k)
+  if st is None or st[1] != 1 or (cmd is not None and not _rows(cmd, 3)):
+    return None
+  out, num, den = (_vec_out(n, t.device) for _ in range(3))
+  cp, cs = _cmd_args(cmd)
+  native.check(native.lib().mjh_rew_air_time(_ptr(t), st[0], cp, cs, float(tmin), float(tmax), float(cmd_thr), _ptr(out),
+                                             _ptr(num), _ptr(den), k, n, _stream()), "mjh_rew_air_time")
+  return out, num, den
+
+
+def rew_swing_height(peak, h, found, cct, cmd, first_lim: float, target: float, cmd_thr: float):
+  """feet_swing_height (peak-height state updated in place) in one launch -> (cost, num, den), or None."""
+  n, k = peak.shape
+  sh, sf, sc = _col_strides(h, n, k), _col_strides(found, n, k), _col_strides(cct, n, k)
+  if None in (sh, sf, sc) or not peak.is_contiguous() or sc[1] != 1 or (cmd is not None and not _rows(cmd, 3)):
+    return None
+  out, num, den = (_vec_out(n, peak.device) for _ in range(3))
+  cp, cs = _cmd_args(cmd)
+  native.check(native.lib().mjh_rew_swing_height(
+    _ptr(peak), _ptr(h), sh[0], sh[1], _ptr(found), sf[0], sf[1], _ptr(cct), sc[0], cp, cs, float(first_lim), float(target),
+    float(cmd_thr), _ptr(out), _ptr(num), _ptr(den), k, n, _stream()), "mjh_rew_swing_height")
+  return out, num, den
+
+
+def rew_soft_landing(force, cct, cmd, first_lim: float, cmd_thr: float):
+  """soft_landing in one launch -> (cost, num, den), or None."""
+  if not (force.is_cuda and force.dtype == torch.float32 and force.dim() == 3 and force.shape[2] == 3 and force.stride(2) == 1):
+    return None
+  n, k = force.shape[:2]
+  sc = _col_strides(cct, n, k)
+  if sc is None or sc[1] != 1 or (cmd is not None and not _rows(cmd, 3)):
+    return None
+  out, num, den = (_vec_out(n, force.device) for _ in range(3))
+  cp, cs = _cmd_args(cmd)
+  native.check(native.lib().mjh_rew_soft_landing(
+    _ptr(force), force.stride(0), force.stride(1), _ptr(cct), sc[0], cp, cs, float(first_lim), float(cmd_thr), _ptr(out),
+    _ptr(num), _ptr(den), k, n, _stream()), "mjh_rew_soft_landing")
+  return out, num, den
+
+
+def log_ratio(env, key: str, num: torch.Tensor, den: torch.Tensor) -> None:
+  """extras['log'][key] = sum(num) / max(sum(den), 1). Inside a reward pass the
+  reward manager evaluates every such log of the pass in one launch."""
+  pending = env.__dict__.get("_reward_log_ratios")
+  if pending is not None:
+    pending.append((key, num, den))
+    return
+  env.extras["log"][key] = torch.sum(num) / torch.clamp(torch.sum(den), min=1)

@@ -32,6 +32,7 @@ class RewardManager:
     # weights live on the device, refreshed on the host before each (graph) step
     self._w = torch.zeros(t, device=env.device)
     self._reset_means = torch.zeros(max(t, 1), device=env.device)
+    self._log_buf = torch.zeros(8, device=env.device)
     self._w_host: tuple | None = None
     self.sync_weights()
 
@@ -71,6 +72,7 @@ class RewardManager:
     """sum_i term_i * weight_i * dt (reward_manager.py:76-88); zero-weight terms
     are skipped and report 0, as in the reference."""
     self._env.__dict__["_command_active_cache"] = {}  # shared command-activity masks, this pass only
+    self._env.__dict__["_reward_log_ratios"] = []  # the terms' metric logs, evaluated together below
     try:
       vals = [
         tcfg.func(self._env, **tcfg.params).float() if tcfg.weight != 0.0 else None
@@ -78,7 +80,19 @@ class RewardManager:
       ]
     finally:
       self._env.__dict__.pop("_command_active_cache", None)
+      pending = self._env.__dict__.pop("_reward_log_ratios", [])
     from mjlab_amd import envops
+
+    if pending:
+      if self._log_buf.numel() < len(pending):
+        self._log_buf = torch.zeros(len(pending), device=self._env.device)
+      log = self._env.extras.setdefault("log", {})
+      if envops.sum_ratios([(a, b) for _, a, b in pending], self._log_buf):
+        for i, (key, _, _) in enumerate(pending):
+          log[key] = self._log_buf[i]
+      else:
+        for key, a, b in pending:
+          log[key] = torch.sum(a) / torch.clamp(torch.sum(b), min=1)
 
     if envops.reward_combine(vals, self._w, dt, self._reward_buf, self._step_reward, self._sums):
       return self._reward_buf

@@ -216,8 +216,10 @@ class ContactSensor:
       return
     if env_ids is not None and isinstance(env_ids, torch.Tensor) and env_ids.dtype == torch.bool:
       m = env_ids[:, None]
-      for t in (st.current_air_time, st.last_air_time, st.current_contact_time, st.last_contact_time):
-        t.masked_fill_(m, 0.0)
+      timers = (st.current_air_time, st.last_air_time, st.current_contact_time, st.last_contact_time)
+      if not envops.masked_zero(list(timers), env_ids):  # one launch for the four timers
+        for t in timers:
+          t.masked_fill_(m, 0.0)
       torch.where(env_ids, self._data.time, st.last_time, out=st.last_time)
       return
     ids = slice(None) if env_ids is None else env_ids

@@ -72,6 +72,12 @@ EXPORTS = (
   "mjh_velocity_resample",
   "mjh_event_mark",
   "mjh_term_combine",
+  "mjh_velocity_rows",
+  "mjh_masked_zero",
+  "mjh_sum_ratios",
+  "mjh_rew_air_time",
+  "mjh_rew_swing_height",
+  "mjh_rew_soft_landing",
 )
 
 
@@ -150,6 +156,12 @@ def lib() -> ctypes.CDLL:
   L.mjh_velocity_resample.argtypes = [vp, vp, cf, cf, cf, cf, ci, ci, vp, vp, vp, vp, vp, vp, u64, u64, vp, ll, vp]
   L.mjh_event_mark.argtypes = [vp, vp, vp, vp, ll, vp]
   L.mjh_term_combine.argtypes = [vp, vp, vp, ci, vp, vp, vp, ll, vp]
+  L.mjh_velocity_rows.argtypes = [vp, ll, ll, vp, ll, vp, ll, vp, vp, ci, ll, vp]
+  L.mjh_masked_zero.argtypes = [vp, vp, vp, ci, vp, ll, vp]
+  L.mjh_sum_ratios.argtypes = [vp, vp, ci, vp, ll, vp]
+  L.mjh_rew_air_time.argtypes = [vp, ll, vp, ll, cf, cf, cf, vp, vp, vp, ci, ll, vp]
+  L.mjh_rew_swing_height.argtypes = [vp, vp, ll, ll, vp, ll, ll, vp, ll, vp, ll, cf, cf, cf, vp, vp, vp, ci, ll, vp]
+  L.mjh_rew_soft_landing.argtypes = [vp, ll, ll, vp, ll, vp, ll, cf, cf, vp, vp, vp, ci, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

@@ -88,9 +88,18 @@ def angular_momentum_penalty(env, sensor_name: str) -> torch.Tensor:
   return sq
 
 
+def _cmd(env, command_name):
+  return env.command_manager.get_command(command_name) if command_name is not None else None
+
+
 def feet_air_time(env, sensor_name: str, threshold_min: float = 0.05, threshold_max: float = 0.5,
                   command_name: str | None = None, command_threshold: float = 0.5) -> torch.Tensor:
   t = env.scene[sensor_name].data.current_air_time
+  fused = envops.rew_air_time(t, _cmd(env, command_name), threshold_min, threshold_max, command_threshold)
+  if fused is not None:
+    out, num, den = fused
+    envops.log_ratio(env, "Metrics/air_time_mean", num, den)
+    return out
   reward = torch.sum(((t > threshold_min) & (t < threshold_max)).float(), dim=1)
   in_air = (t > 0).float()
   env.extras["log"]["Metrics/air_time_mean"] = torch.sum(t * in_air) / torch.clamp(torch.sum(in_air), min=1)
@@ -125,6 +134,13 @@ class feet_swing_height:
     a = env.scene[asset_cfg.name]
     cs = env.scene[sensor_name]
     h = a.data.site_pos_w[:, asset_cfg.site_idx, 2]
+    d = cs.data
+    fused = envops.rew_swing_height(self.peak_heights, h, d.found, d.current_contact_time, _cmd(env, command_name),
+                                    self.step_dt + 1.0e-8, target_height, command_threshold)
+    if fused is not None:
+      cost, num, den = fused
+      envops.log_ratio(env, "Metrics/peak_height_mean", num, den)
+      return cost
     in_air = cs.data.found == 0
     torch.where(in_air, torch.maximum(self.peak_heights, h), self.peak_heights, out=self.peak_heights)
     first = cs.compute_first_contact(dt=self.step_dt)
@@ -146,7 +162,7 @@ def feet_slip(env, sensor_name: str, command_name: str, command_threshold: float
                           found, env.command_manager.get_command(command_name), 0.0, 0.0, command_threshold, "slip")
   if fused is not None:
     cost, vsum, cnt = fused
-    env.extras["log"]["Metrics/slip_velocity_mean"] = torch.sum(vsum) / torch.clamp(torch.sum(cnt), min=1)
+    envops.log_ratio(env, "Metrics/slip_velocity_mean", vsum, cnt)
     return cost
   active = _command_active(env, command_name, command_threshold)
   in_contact = (found > 0).float()
@@ -158,6 +174,13 @@ def feet_slip(env, sensor_name: str, command_name: str, command_threshold: float
 
 def soft_landing(env, sensor_name: str, command_name: str | None = None, command_threshold: float = 0.05) -> torch.Tensor:
   cs = env.scene[sensor_name]
+  d = cs.data
+  fused = envops.rew_soft_landing(d.force, d.current_contact_time, _cmd(env, command_name), env.step_dt + 1.0e-8,
+                                  command_threshold)
+  if fused is not None:
+    cost, num, den = fused
+    envops.log_ratio(env, "Metrics/landing_force_mean", num, den)
+    return cost
   fm = torch.norm(cs.data.force, dim=-1)
   first = cs.compute_first_contact(dt=env.step_dt)
   impact = fm * first.float()

@@ -369,6 +369,37 @@ int mjh_term_combine(const unsigned char* const* values, unsigned char* const* t
                      unsigned char* truncated, unsigned char* terminated, unsigned char* dones, long long n,
                      void* stream);
 
+/* compute_velocity_from_cvel for k rows per env read in place (EntityData
+ * body/site/geom velocities, entity/data.py:200-260): row j of env e at pos +
+ * e*pes + j*prs, its body's cvel at cvel + e*ves + 6*body[j], root subtree com
+ * at com + e*cs; out (n*k, 6) = [lin - ang x (com - pos), ang]. */
+int mjh_velocity_rows(const float* pos, long long pes, long long prs, const float* com, long long cs, const float* cvel,
+                      long long ves, const int* body, float* out, int k, long long n, void* stream);
+
+/* Zero the masked rows of ntensors float tensors (row t: widths[t] floats at
+ * ptrs[t] + e * row_strides[t]) in one launch (managers' masked_fill_ chains). */
+int mjh_masked_zero(float* const* ptrs, const long long* row_strides, const int* widths, int ntensors,
+                    const unsigned char* mask, long long n, void* stream);
+
+/* out[t] = sum(num[t]) / max(sum(den[t]), 1) over n envs (reward-term metric
+ * logs, tasks/velocity/mdp/rewards.py). One workgroup. */
+int mjh_sum_ratios(const float* const* num, const float* const* den, int nterms, float* out, long long n, void* stream);
+
+/* Contact-timing rewards of the velocity task (tasks/velocity/mdp/rewards.py),
+ * one launch each, per env over its k feet; cmd NULL = no command gating, else
+ * x (|cmd_xy| + |cmd_yaw| > cmd_thr). num/den receive the per-env parts of the
+ * term's metric log (sum(num) / max(sum(den), 1), see mjh_sum_ratios).
+ * Strides: *es per env, *cs / *ss per foot. first contact: 0 < contact time < first_lim. */
+int mjh_rew_air_time(const float* t, long long ts, const float* cmd, long long cs, float tmin, float tmax, float cmd_thr,
+                     float* out, float* num, float* den, int k, long long n, void* stream);
+int mjh_rew_swing_height(float* peak, const float* h, long long hes, long long hcs, const float* found, long long fes,
+                         long long fcs, const float* cct, long long cts, const float* cmd, long long cs, float first_lim,
+                         float target, float cmd_thr, float* out, float* num, float* den, int k, long long n,
+                         void* stream);
+int mjh_rew_soft_landing(const float* f, long long fes, long long fss, const float* cct, long long cts, const float* cmd,
+                         long long cs, float first_lim, float cmd_thr, float* out, float* num, float* den, int k,
+                         long long n, void* stream);
+
 /* EventManager reset bookkeeping (event_manager.py:146-156): last[e] = *step,
  * once[e] = 1 for the masked envs. */
 int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, const mjh_i64* step, long long n,

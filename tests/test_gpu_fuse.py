@@ -282,3 +282,74 @@ def test_obs_group_ops_and_strides(op):
   assert envops.obs_group([other, src], plan, None, out2, _args(ctr))
   uu = envops.uniform_draws(SEED, KEY, ctr, n * 10, DEV).view(n, 10)
   torch.testing.assert_close(out2[:, :3], other + (uu[:, :3] * 0.2 - 0.1), rtol=1e-6, atol=1e-6)
+
+
+def test_velocity_rows_masked_zero_sum_ratios():
+  from mjlab_amd.entity.data import compute_velocity_from_cvel
+
+  n, nb = 2048, 30
+  g = torch.Generator(device=DEV).manual_seed(30)
+  xpos = torch.randn(n, nb, 3, device=DEV, generator=g)
+  cvel = torch.randn(n, nb, 6, device=DEV, generator=g)
+  com = torch.randn(n, nb, 3, device=DEV, generator=g)
+  rows = slice(1, 8)
+  body = torch.tensor([1, 4, 4, 9, 2, 29, 0], dtype=torch.int32, device=DEV)
+  got = envops.velocity_rows(xpos[:, rows], com[:, 0], cvel, body)
+  ref = compute_velocity_from_cvel(xpos[:, rows], com[:, 0].unsqueeze(1), cvel[:, body.long()])
+  torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+  a, b = torch.randn(n, 5, device=DEV, generator=g), torch.randn(n, device=DEV, generator=g)
+  big = torch.randn(n, 20, device=DEV, generator=g)
+  c = big[:, 4:10]  # column slice of a wider tensor
+  m = torch.rand(n, device=DEV, generator=g) < 0.3
+  ra, rb, rbig = a.masked_fill(m[:, None], 0.0), b.masked_fill(m, 0.0), big.clone()
+  rbig[:, 4:10] = rbig[:, 4:10].masked_fill(m[:, None], 0.0)
+  assert envops.masked_zero([a, b, c], m)
+  assert torch.equal(a, ra) and torch.equal(b, rb) and torch.equal(big, rbig)
+  nums = [torch.rand(n, device=DEV, generator=g) for _ in range(3)]
+  dens = [torch.rand(n, device=DEV, generator=g) > 0.5, torch.zeros(n, device=DEV), torch.rand(n, device=DEV, generator=g)]
+  dens = [d.float() for d in dens]
+  out = torch.zeros(3, device=DEV)
+  assert envops.sum_ratios(list(zip(nums, dens)), out)
+  ref = torch.stack([x.sum() / torch.clamp(y.sum(), min=1) for x, y in zip(nums, dens)])
+  torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-6)
+
+
+def test_contact_timing_rewards_match_formulas():
+  """feet_air_time / feet_swing_height / soft_landing kernels vs the torch
+  formulas of tasks/velocity/mdp/rewards.py (sensor slots as strided views)."""
+  n, k = 4096, 2
+  g = torch.Generator(device=DEV).manual_seed(31)
+  cmd = torch.randn(n, 3, device=DEV, generator=g) * 0.3
+  t = torch.rand(n, k, device=DEV, generator=g) * 0.6 * (torch.rand(n, k, device=DEV, generator=g) > 0.3)
+  total = torch.norm(cmd[:, :2], dim=1) + torch.abs(cmd[:, 2])
+  out, num, den = envops.rew_air_time(t, cmd, 0.05, 0.5, 0.5)
+  act = (total > 0.5).float()
+  torch.testing.assert_close(out, torch.sum(((t > 0.05) & (t < 0.5)).float(), 1) * act)
+  in_air = (t > 0).float()
+  torch.testing.assert_close(num, (t * in_air).sum(1))
+  torch.testing.assert_close(den, in_air.sum(1))
+  # sensordata-like slots: [found, fx, fy, fz] per foot -> strided views
+  sd = torch.randn(n, 4 * k + 3, device=DEV, generator=g)
+  sd[:, 0:4 * k:4] = (torch.rand(n, k, device=DEV, generator=g) > 0.5).float() * 2
+  found = sd[:, 0:4 * k:4]
+  force = sd.as_strided((n, k, 3), (sd.stride(0), 4, 1), sd.storage_offset() + 1)
+  cct = torch.rand(n, k, device=DEV, generator=g) * 0.04 * (torch.rand(n, k, device=DEV, generator=g) > 0.4)
+  site = torch.randn(n, 6, 3, device=DEV, generator=g).abs()
+  h = site[:, 2:4, 2]
+  peak = torch.rand(n, k, device=DEV, generator=g) * 0.2
+  peak_ref = peak.clone()
+  lim = 0.02 + 1e-8
+  cost, pn, pd = envops.rew_swing_height(peak, h, found, cct, cmd, lim, 0.1, 0.05)
+  a2 = (total > 0.05).float()
+  peak_ref = torch.where(found == 0, torch.maximum(peak_ref, h), peak_ref)
+  first = (cct > 0) & (cct < lim)
+  ref_cost = torch.sum(torch.square(peak_ref / 0.1 - 1.0) * first.float(), dim=1) * a2
+  torch.testing.assert_close(cost, ref_cost, rtol=1e-5, atol=1e-6)
+  torch.testing.assert_close(pn, (peak_ref * first.float()).sum(1), rtol=1e-5, atol=1e-6)
+  torch.testing.assert_close(pd, first.float().sum(1))
+  assert torch.equal(peak, peak_ref.masked_fill(first, 0.0))
+  lc, ln, ld = envops.rew_soft_landing(force, cct, cmd, lim, 0.05)
+  impact = torch.norm(force, dim=-1) * first.float()
+  torch.testing.assert_close(lc, impact.sum(1) * a2, rtol=1e-5, atol=1e-5)
+  torch.testing.assert_close(ln, impact.sum(1), rtol=1e-5, atol=1e-5)
+  torch.testing.assert_close(ld, first.float().sum(1))
