@@ -68,28 +68,25 @@ __global__ void velocity_from_cvel_kernel(const float* __restrict__ pos, long lo
   o[3] = wx; o[4] = wy; o[5] = wz;
 }
 
+// one thread per env: its k slots, then the env's last_time (read before, so
+// every slot sees the pre-update value)
 __global__ void air_time_kernel(const float* __restrict__ sensordata, long long sds, const int* __restrict__ cols, int k,
                                 const float* __restrict__ time, float* last_time, float* cur_air, float* last_air,
                                 float* cur_con, float* last_con, long long n) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n * k) return;
-  const long long e = t / k;
-  const int j = (int)(t - e * k);
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
   const float now = time[e];
   const float el = now - last_time[e];
-  const bool is_c = sensordata[e * sds + cols[j]] > 0.f;
-  const float ca = cur_air[t], cc = cur_con[t];
-  if (ca > 0.f && is_c) last_air[t] = ca + el;
-  cur_air[t] = is_c ? 0.f : ca + el;
-  if (cc > 0.f && !is_c) last_con[t] = cc + el;
-  cur_con[t] = is_c ? cc + el : 0.f;
-}
-
-// last_time is written by a second launch so every (env, slot) thread above
-// reads the pre-update value
-__global__ void copy_kernel(const float* __restrict__ src, float* __restrict__ dst, long long n) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) dst[i] = src[i];
+  for (int j = 0; j < k; j++) {
+    const long long t = e * k + j;
+    const bool is_c = sensordata[e * sds + cols[j]] > 0.f;
+    const float ca = cur_air[t], cc = cur_con[t];
+    if (ca > 0.f && is_c) last_air[t] = ca + el;
+    cur_air[t] = is_c ? 0.f : ca + el;
+    if (cc > 0.f && !is_c) last_con[t] = cc + el;
+    cur_con[t] = is_c ? cc + el : 0.f;
+  }
+  last_time[e] = now;
 }
 
 inline int grid(long long n) { return (int)((n + 255) / 256); }
@@ -127,9 +124,8 @@ int mjh_air_time_update(const float* sensordata, long long sds, const int* cols,
                         void* stream) {
   if (n <= 0 || k <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(air_time_kernel, dim3(grid(n * k)), dim3(256), 0, s, sensordata, sds, cols, k, time, last_time,
+  hipLaunchKernelGGL(air_time_kernel, dim3(grid(n)), dim3(256), 0, s, sensordata, sds, cols, k, time, last_time,
                      cur_air, last_air, cur_con, last_con, n);
-  hipLaunchKernelGGL(copy_kernel, dim3(grid(n)), dim3(256), 0, s, time, last_time, n);
   return finish();
 }
 

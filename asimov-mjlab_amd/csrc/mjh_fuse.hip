@@ -80,47 +80,41 @@ __device__ __forceinline__ float wsum(float v) {
   return v;
 }
 
-constexpr int kRedBlock = 1024;  // one workgroup of 16 waves: 16 rows in flight per column pass
+constexpr int kRedBlock = 1024;  // one workgroup of 16 waves per column
 
-// Each thread accumulates its rows' entries of every column in registers
-// (rows e = tid, tid + 1024, ...; a row's columns share cache lines), then one
-// wave + LDS reduction per column.
+// blockIdx.x = column: masked row count and masked column sum (each thread
+// accumulates rows tid, tid + 1024, ...), wave + LDS reduction; the column's
+// masked rows are cleared when zero_rows
 __global__ __launch_bounds__(kRedBlock) void masked_means_kernel(const ColArgs a, const unsigned char* __restrict__ mask,
                                                                   float scale, int zero_rows, float* __restrict__ out,
                                                                   long long n) {
-  __shared__ float part[MJH_MAX_TERMS + 1][kRedBlock / 64];
-  float acc[MJH_MAX_TERMS + 1];
-#pragma unroll
-  for (int t = 0; t <= MJH_MAX_TERMS; t++) acc[t] = 0.f;
+  __shared__ float part[2][kRedBlock / 64];
+  const int t = blockIdx.x;
+  float* const col = a.c[t];
+  const long long cs = a.cs[t];
+  float s = 0.f, cnt = 0.f;
   for (long long e = threadIdx.x; e < n; e += kRedBlock) {
     if (!on(mask, e)) continue;
-    acc[MJH_MAX_TERMS] += 1.f;
-#pragma unroll
-    for (int t = 0; t < MJH_MAX_TERMS; t++) {
-      if (t < a.ncols) {
-        float* p = a.c[t] + e * a.cs[t];
-        acc[t] += *p;
-        if (zero_rows) *p = 0.f;
-      }
-    }
+    cnt += 1.f;
+    s += col[e * cs];
+    if (zero_rows) col[e * cs] = 0.f;
   }
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-  for (int t = 0; t <= MJH_MAX_TERMS; t++) {
-    if (t < a.ncols || t == MJH_MAX_TERMS) {
-      const float v = wsum(acc[t]);
-      if (lane == 0) part[t][wv] = v;
-    }
+  s = wsum(s);
+  cnt = wsum(cnt);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    part[0][wv] = s;
+    part[1][wv] = cnt;
   }
   __syncthreads();
-  if (threadIdx.x < (unsigned)a.ncols) {
-    float cnt = 0.f, s = 0.f;
+  if (threadIdx.x == 0) {
+    float ts = 0.f, tc = 0.f;
 #pragma unroll
     for (int w = 0; w < kRedBlock / 64; w++) {
-      cnt += part[MJH_MAX_TERMS][w];
-      s += part[threadIdx.x][w];
+      ts += part[0][w];
+      tc += part[1][w];
     }
-    out[threadIdx.x] = s / fmaxf(cnt, 1.f) * scale;
+    out[t] = ts / fmaxf(tc, 1.f) * scale;
   }
 }
 
@@ -392,43 +386,30 @@ struct RatioArgs {
   int nterms;
 };
 
+// blockIdx.x = term
 __global__ __launch_bounds__(1024) void sum_ratios_kernel(const RatioArgs a, float* __restrict__ out, long long n) {
-  __shared__ float part[2 * MJH_MAX_TERMS][16];
-  float sn[MJH_MAX_TERMS], sd[MJH_MAX_TERMS];
-#pragma unroll
-  for (int t = 0; t < MJH_MAX_TERMS; t++) sn[t] = sd[t] = 0.f;
+  __shared__ float part[2][16];
+  const int t = blockIdx.x;
+  float x = 0.f, y = 0.f;
   for (long long e = threadIdx.x; e < n; e += 1024) {
-#pragma unroll
-    for (int t = 0; t < MJH_MAX_TERMS; t++)
-      if (t < a.nterms) {
-        sn[t] += a.num[t][e];
-        sd[t] += a.den[t][e];
-      }
+    x += a.num[t][e];
+    y += a.den[t][e];
   }
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-  for (int t = 0; t < MJH_MAX_TERMS; t++) {
-    if (t < a.nterms) {
-      float x = sn[t], y = sd[t];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        x += __shfl_xor(x, o, 64);
-        y += __shfl_xor(y, o, 64);
-      }
-      if (lane == 0) {
-        part[2 * t][wv] = x;
-        part[2 * t + 1][wv] = y;
-      }
-    }
+  x = wsum(x);
+  y = wsum(y);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    part[0][wv] = x;
+    part[1][wv] = y;
   }
   __syncthreads();
-  if (threadIdx.x < (unsigned)a.nterms) {
-    float x = 0.f, y = 0.f;
+  if (threadIdx.x == 0) {
+    float sx = 0.f, sy = 0.f;
     for (int w = 0; w < 16; w++) {
-      x += part[2 * threadIdx.x][w];
-      y += part[2 * threadIdx.x + 1][w];
+      sx += part[0][w];
+      sy += part[1][w];
     }
-    out[threadIdx.x] = x / fmaxf(y, 1.f);
+    out[t] = sx / fmaxf(sy, 1.f);
   }
 }
 
@@ -509,6 +490,65 @@ __global__ void rew_soft_landing_kernel(const float* __restrict__ f, long long f
   den[e] = b;
 }
 
+// ActionManager.process_action with one JointAction term (action_manager.py:
+// 107-116, joint_actions.py:90-108): prev = action; action = raw = input;
+// processed = raw * scale + offset (scale / offset: per-column rows, or the
+// scalars when the pointer is NULL)
+__global__ void joint_action_kernel(const float* __restrict__ input, long long is, float* __restrict__ action,
+                                    float* __restrict__ prev, float* __restrict__ raw, float* __restrict__ processed,
+                                    const float* __restrict__ scale, long long ss, float scale0,
+                                    const float* __restrict__ offset, long long os, float offset0, int d, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * d) return;
+  const long long e = i / d;
+  const int j = (int)(i - e * d);
+  const float a = input[e * is + j];
+  prev[i] = action[i];
+  action[i] = a;
+  raw[i] = a;
+  const float sc = scale ? scale[e * ss + j] : scale0;
+  const float of = offset ? offset[e * os + j] : offset0;
+  processed[i] = fmaf(a, sc, of);
+}
+
+// The root body's frame quantities EntityData derives from one forward pass
+// (entity/data.py): out[e] = [root_link_vel_w (lin, ang) 6 | lin_vel_b 3 |
+// ang_vel_b 3 | projected_gravity_b 3 | heading_w 1]; quaternion rotations as
+// quat_apply(_inverse) (utils/math.py), velocity as compute_velocity_from_cvel
+__device__ __forceinline__ void qrot(float o[3], const float q[4], const float v[3], float sgn) {
+  const float w = q[0], x = q[1], y = q[2], z = q[3];
+  const float tx = 2.f * (y * v[2] - z * v[1]), ty = 2.f * (z * v[0] - x * v[2]), tz = 2.f * (x * v[1] - y * v[0]);
+  o[0] = (v[0] + sgn * w * tx) + (y * tz - z * ty);
+  o[1] = (v[1] + sgn * w * ty) + (z * tx - x * tz);
+  o[2] = (v[2] + sgn * w * tz) + (x * ty - y * tx);
+}
+
+__global__ void root_frame_kernel(const float* __restrict__ xpos, long long ps, const float* __restrict__ xquat,
+                                  long long qs, const float* __restrict__ com, long long cs, const float* __restrict__ cvel,
+                                  long long vs, const float* __restrict__ grav, long long gs, const float* __restrict__ fwd,
+                                  long long fs, float* __restrict__ out, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float* p = xpos + e * ps;
+  const float* c = com + e * cs;
+  const float* v = cvel + e * vs;
+  const float q[4] = {xquat[e * qs], xquat[e * qs + 1], xquat[e * qs + 2], xquat[e * qs + 3]};
+  const float ox = c[0] - p[0], oy = c[1] - p[1], oz = c[2] - p[2];
+  const float ang[3] = {v[0], v[1], v[2]};
+  const float lin[3] = {v[3] - (ang[1] * oz - ang[2] * oy), v[4] - (ang[2] * ox - ang[0] * oz), v[5] - (ang[0] * oy - ang[1] * ox)};
+  float* o = out + 16 * e;
+  o[0] = lin[0]; o[1] = lin[1]; o[2] = lin[2];
+  o[3] = ang[0]; o[4] = ang[1]; o[5] = ang[2];
+  qrot(o + 6, q, lin, -1.f);
+  qrot(o + 9, q, ang, -1.f);
+  const float g[3] = {grav[e * gs], grav[e * gs + 1], grav[e * gs + 2]};
+  qrot(o + 12, q, g, -1.f);
+  const float f0[3] = {fwd[e * fs], fwd[e * fs + 1], fwd[e * fs + 2]};
+  float f[3];
+  qrot(f, q, f0, 1.f);
+  o[15] = atan2f(f[1], f[0]);
+}
+
 }  // namespace
 
 extern "C" {
@@ -523,7 +563,7 @@ int mjh_masked_means(float* const* cols, const long long* strides, int ncols, co
     a.cs[t] = strides[t];
   }
   a.ncols = ncols;
-  hipLaunchKernelGGL(masked_means_kernel, dim3(1), dim3(kRedBlock), 0, (hipStream_t)stream, a, mask, scale, zero_rows, out, n);
+  hipLaunchKernelGGL(masked_means_kernel, dim3(ncols), dim3(kRedBlock), 0, (hipStream_t)stream, a, mask, scale, zero_rows, out, n);
   return finish();
 }
 
@@ -673,7 +713,7 @@ int mjh_sum_ratios(const float* const* num, const float* const* den, int nterms,
     a.den[t] = den[t];
   }
   a.nterms = nterms;
-  hipLaunchKernelGGL(sum_ratios_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a, out, n);
+  hipLaunchKernelGGL(sum_ratios_kernel, dim3(nterms), dim3(1024), 0, (hipStream_t)stream, a, out, n);
   return finish();
 }
 
@@ -701,6 +741,24 @@ int mjh_rew_soft_landing(const float* f, long long fes, long long fss, const flo
   if (n <= 0) return 0;
   hipLaunchKernelGGL(rew_soft_landing_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, f, fes, fss, cct, cts, cmd,
                      cs, first_lim, cmd_thr, out, num, den, k, n);
+  return finish();
+}
+
+int mjh_joint_action(const float* input, long long is, float* action, float* prev, float* raw, float* processed,
+                     const float* scale, long long ss, float scale0, const float* offset, long long os, float offset0,
+                     int d, long long n, void* stream) {
+  if (n <= 0 || d <= 0) return 0;
+  hipLaunchKernelGGL(joint_action_kernel, dim3(grid(n * d)), dim3(kBlock), 0, (hipStream_t)stream, input, is, action, prev,
+                     raw, processed, scale, ss, scale0, offset, os, offset0, d, n);
+  return finish();
+}
+
+int mjh_root_frame(const float* xpos, long long ps, const float* xquat, long long qs, const float* com, long long cs,
+                   const float* cvel, long long vs, const float* grav, long long gs, const float* fwd, long long fs,
+                   float* out, long long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(root_frame_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, xpos, ps, xquat, qs, com, cs,
+                     cvel, vs, grav, gs, fwd, fs, out, n);
   return finish();
 }
 

@@ -262,7 +262,18 @@ class EntityData:
     return torch.cat([self.data.xpos[:, self._root], self.data.xquat[:, self._root]], dim=-1)
 
   @_cached
+  def _root_frame(self):
+    """[root_link_vel_w 6 | lin_vel_b 3 | ang_vel_b 3 | projected_gravity_b 3 |
+    heading_w 1] per env from one launch (csrc/mjh_fuse.hip), or None (CPU)."""
+    r = self._root
+    return envops.root_frame(self.data.xpos[:, r], self.data.xquat[:, r], self.data.subtree_com[:, r], self.data.cvel[:, r],
+                             self.gravity_vec_w, self.forward_vec_b)
+
+  @_cached
   def root_link_vel_w(self) -> torch.Tensor:
+    f = self._root_frame
+    if f is not None:
+      return f[:, 0:6]
     r = self._root
     return envops.velocity_from_cvel(self.data.xpos[:, r], self.data.subtree_com[:, r], self.data.cvel[:, r], compute_velocity_from_cvel)
 
@@ -428,19 +439,31 @@ class EntityData:
 
   @_cached
   def projected_gravity_b(self) -> torch.Tensor:
+    rf = self._root_frame
+    if rf is not None:
+      return rf[:, 12:15]
     return quat_apply_inverse(self.root_link_quat_w, self.gravity_vec_w)
 
   @_cached
   def heading_w(self) -> torch.Tensor:
+    rf = self._root_frame
+    if rf is not None:
+      return rf[:, 15]
     f = quat_apply(self.root_link_quat_w, self.forward_vec_b)
     return torch.atan2(f[:, 1], f[:, 0])
 
   @_cached
   def root_link_lin_vel_b(self) -> torch.Tensor:
+    rf = self._root_frame
+    if rf is not None:
+      return rf[:, 6:9]
     return quat_apply_inverse(self.root_link_quat_w, self.root_link_lin_vel_w)
 
   @_cached
   def root_link_ang_vel_b(self) -> torch.Tensor:
+    rf = self._root_frame
+    if rf is not None:
+      return rf[:, 9:12]
     return quat_apply_inverse(self.root_link_quat_w, self.root_link_ang_vel_w)
 
   @_cached

@@ -684,3 +684,42 @@ def log_ratio(env, key: str, num: torch.Tensor, den: torch.Tensor) -> None:
     pending.append((key, num, den))
     return
   env.extras["log"][key] = torch.sum(num) / torch.clamp(torch.sum(den), min=1)
+
+
+def root_frame(xpos, xquat, com, cvel, grav, fwd) -> torch.Tensor | None:
+  """(N, 16) [root_link_vel_w | lin_vel_b | ang_vel_b | projected_gravity_b | heading_w]
+  of the root body in one launch, or None when the layout is unsupported (CPU)."""
+  ts = (xpos, xquat, com, cvel, grav, fwd)
+  widths = (3, 4, 3, 6, 3, 3)
+  if not all(_rowsN(t, w) for t, w in zip(ts, widths)):
+    return None
+  n = xpos.shape[0]
+  if not all(t.shape[0] == n for t in ts):
+    return None
+  out = torch.empty((n, 16), dtype=torch.float32, device=xpos.device)
+  native.check(native.lib().mjh_root_frame(_ptr(xpos), xpos.stride(0), _ptr(xquat), xquat.stride(0), _ptr(com), com.stride(0),
+                                           _ptr(cvel), cvel.stride(0), _ptr(grav), grav.stride(0), _ptr(fwd), fwd.stride(0),
+                                           _ptr(out), n, _stream()), "mjh_root_frame")
+  return out
+
+
+def joint_action(inp, action, prev, raw, processed, scale, offset) -> bool:
+  """ActionManager.process_action for one JointAction term in one launch."""
+  n, d = action.shape
+  bufs = (action, prev, raw, processed)
+  if not all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.shape == (n, d) for t in bufs):
+    return False
+  if not (_rowsN(inp, d) and inp.shape[0] == n):
+    return False
+  def arg(x):
+    if isinstance(x, torch.Tensor):
+      if not (_rowsN(x, d) and x.shape[0] == n):
+        return None
+      return _ptr(x), x.stride(0), 0.0
+    return None, 0, float(x)
+  sa, oa = arg(scale), arg(offset)
+  if sa is None or oa is None:
+    return False
+  native.check(native.lib().mjh_joint_action(_ptr(inp), inp.stride(0), _ptr(action), _ptr(prev), _ptr(raw), _ptr(processed),
+                                             *sa, *oa, d, n, _stream()), "mjh_joint_action")
+  return True

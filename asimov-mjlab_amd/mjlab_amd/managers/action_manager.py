@@ -80,6 +80,14 @@ class ActionManager:
   def process_action(self, action: torch.Tensor) -> None:
     if action.shape[1] != self.total_action_dim:
       raise ValueError(f"Invalid action shape, expected: {self.total_action_dim}, received: {action.shape[1]}.")
+    if len(self._terms) == 1:
+      from mjlab_amd import envops
+      from mjlab_amd.envs.mdp.actions import JointAction
+
+      (t,) = self._terms.values()
+      if type(t).process_actions is JointAction.process_actions and envops.joint_action(
+          action, self._action, self._prev_action, t._raw_actions, t._processed_actions, t._scale, t._offset):
+        return  # one launch: previous / last / raw actions and the processed targets
     self._prev_action.copy_(self._action)
     self._action.copy_(action)
     idx = 0

@@ -78,6 +78,8 @@ EXPORTS = (
   "mjh_rew_air_time",
   "mjh_rew_swing_height",
   "mjh_rew_soft_landing",
+  "mjh_joint_action",
+  "mjh_root_frame",
 )
 
 
@@ -162,6 +164,8 @@ def lib() -> ctypes.CDLL:
   L.mjh_rew_air_time.argtypes = [vp, ll, vp, ll, cf, cf, cf, vp, vp, vp, ci, ll, vp]
   L.mjh_rew_swing_height.argtypes = [vp, vp, ll, ll, vp, ll, ll, vp, ll, vp, ll, cf, cf, cf, vp, vp, vp, ci, ll, vp]
   L.mjh_rew_soft_landing.argtypes = [vp, ll, ll, vp, ll, vp, ll, cf, cf, vp, vp, vp, ci, ll, vp]
+  L.mjh_joint_action.argtypes = [vp, ll, vp, vp, vp, vp, vp, ll, cf, vp, ll, cf, ci, ll, vp]
+  L.mjh_root_frame.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

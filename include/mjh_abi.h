@@ -400,6 +400,22 @@ int mjh_rew_soft_landing(const float* f, long long fes, long long fss, const flo
                          long long cs, float first_lim, float cmd_thr, float* out, float* num, float* den, int k,
                          long long n, void* stream);
 
+/* ActionManager.process_action with one JointAction term (action_manager.py:
+ * 107-116, joint_actions.py:90-108), contiguous (n, d) buffers: prev = action;
+ * action = raw = input; processed = raw * scale + offset, scale / offset from
+ * rows (stride ss / os) or the scalars scale0 / offset0 when NULL. */
+int mjh_joint_action(const float* input, long long is, float* action, float* prev, float* raw, float* processed,
+                     const float* scale, long long ss, float scale0, const float* offset, long long os, float offset0,
+                     int d, long long n, void* stream);
+
+/* The root body's EntityData frame reads from one forward pass, out (n, 16) =
+ * [root_link_vel_w 6 | root_link_lin_vel_b 3 | root_link_ang_vel_b 3 |
+ * projected_gravity_b 3 | heading_w 1] (entity/data.py; quat_apply(_inverse),
+ * compute_velocity_from_cvel of utils/math.py / data.py). Row strides *s. */
+int mjh_root_frame(const float* xpos, long long ps, const float* xquat, long long qs, const float* com, long long cs,
+                   const float* cvel, long long vs, const float* grav, long long gs, const float* fwd, long long fs,
+                   float* out, long long n, void* stream);
+
 /* EventManager reset bookkeeping (event_manager.py:146-156): last[e] = *step,
  * once[e] = 1 for the masked envs. */
 int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, const mjh_i64* step, long long n,

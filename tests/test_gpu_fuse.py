@@ -353,3 +353,35 @@ def test_contact_timing_rewards_match_formulas():
   torch.testing.assert_close(lc, impact.sum(1) * a2, rtol=1e-5, atol=1e-5)
   torch.testing.assert_close(ln, impact.sum(1), rtol=1e-5, atol=1e-5)
   torch.testing.assert_close(ld, first.float().sum(1))
+
+
+def test_root_frame_and_joint_action_match_formulas():
+  from mjlab_amd.entity.data import compute_velocity_from_cvel
+
+  n = 4096
+  g = torch.Generator(device=DEV).manual_seed(40)
+  xpos, com = torch.randn(n, 5, 3, device=DEV, generator=g), torch.randn(n, 5, 3, device=DEV, generator=g)
+  xquat = torch.randn(n, 5, 4, device=DEV, generator=g)
+  xquat = xquat / xquat.norm(dim=-1, keepdim=True)
+  cvel = torch.randn(n, 5, 6, device=DEV, generator=g)
+  grav = torch.tensor([0.0, 0.0, -1.0], device=DEV).repeat(n, 1)
+  fwd = torch.tensor([1.0, 0.0, 0.0], device=DEV).repeat(n, 1)
+  r = 1
+  out = envops.root_frame(xpos[:, r], xquat[:, r], com[:, r], cvel[:, r], grav, fwd)
+  q = xquat[:, r]
+  v = compute_velocity_from_cvel(xpos[:, r], com[:, r], cvel[:, r])
+  f = M.quat_apply(q, fwd)
+  ref = torch.cat([v, M.quat_apply_inverse(q, v[:, :3]), M.quat_apply_inverse(q, v[:, 3:]), M.quat_apply_inverse(q, grav),
+                   torch.atan2(f[:, 1], f[:, 0])[:, None]], dim=1)
+  torch.testing.assert_close(out, ref, rtol=1e-5, atol=2e-5)
+  d = 29
+  inp = torch.randn(n, d, device=DEV, generator=g)
+  action, raw, proc = torch.randn(n, d, device=DEV, generator=g), torch.zeros(n, d, device=DEV), torch.zeros(n, d, device=DEV)
+  prev = torch.zeros(n, d, device=DEV)
+  a0 = action.clone()
+  scale, offset = torch.rand(n, d, device=DEV, generator=g), torch.randn(n, d, device=DEV, generator=g)
+  assert envops.joint_action(inp, action, prev, raw, proc, scale, offset)
+  assert torch.equal(prev, a0) and torch.equal(action, inp) and torch.equal(raw, inp)
+  torch.testing.assert_close(proc, torch.addcmul(offset, inp, scale), rtol=1e-6, atol=1e-6)
+  assert envops.joint_action(inp, action, prev, raw, proc, 0.5, offset)
+  torch.testing.assert_close(proc, offset + inp * 0.5, rtol=1e-6, atol=1e-6)
