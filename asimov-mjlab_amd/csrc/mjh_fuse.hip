@@ -549,6 +549,40 @@ __global__ void root_frame_kernel(const float* __restrict__ xpos, long long ps, 
   o[15] = atan2f(f[1], f[0]);
 }
 
+// World order for the step kernel's workgroups (mjh_data.world_order): worlds
+// bucketed by their previous step's cost (solver_niter + 2) * nefc, most
+// expensive first (counting sort, one workgroup), so the 8 worlds sharing a
+// workgroup's LDS take similar time. Within a bucket the order is arbitrary:
+// results do not depend on it.
+constexpr int kOrderBuckets = 256;
+
+__global__ __launch_bounds__(1024) void order_worlds_kernel(const int* __restrict__ niter, const int* __restrict__ nefc,
+                                                           long long* __restrict__ order, long long n) {
+  __shared__ int cnt[kOrderBuckets];
+  __shared__ int base[kOrderBuckets];
+  for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+    const int key = (niter[e] + 2) * nefc[e];
+    const int b = kOrderBuckets - 1 - min(key >> 4, kOrderBuckets - 1);  // descending cost
+    atomicAdd(&cnt[b], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = 0; b < kOrderBuckets; b++) {
+      base[b] = acc;
+      acc += cnt[b];
+    }
+  }
+  __syncthreads();
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+    const int key = (niter[e] + 2) * nefc[e];
+    const int b = kOrderBuckets - 1 - min(key >> 4, kOrderBuckets - 1);
+    order[atomicAdd(&base[b], 1)] = e;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -759,6 +793,12 @@ int mjh_root_frame(const float* xpos, long long ps, const float* xquat, long lon
   if (n <= 0) return 0;
   hipLaunchKernelGGL(root_frame_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, xpos, ps, xquat, qs, com, cs,
                      cvel, vs, grav, gs, fwd, fs, out, n);
+  return finish();
+}
+
+int mjh_order_worlds(const int* solver_niter, const int* nefc, long long* order, long long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(order_worlds_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, solver_niter, nefc, order, n);
   return finish();
 }
 

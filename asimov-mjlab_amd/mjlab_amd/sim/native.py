@@ -80,6 +80,7 @@ EXPORTS = (
   "mjh_rew_soft_landing",
   "mjh_joint_action",
   "mjh_root_frame",
+  "mjh_order_worlds",
 )
 
 
@@ -166,6 +167,7 @@ def lib() -> ctypes.CDLL:
   L.mjh_rew_soft_landing.argtypes = [vp, ll, ll, vp, ll, vp, ll, cf, cf, vp, vp, vp, ci, ll, vp]
   L.mjh_joint_action.argtypes = [vp, ll, vp, vp, vp, vp, vp, ll, cf, vp, ll, cf, ci, ll, vp]
   L.mjh_root_frame.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp]
+  L.mjh_order_worlds.argtypes = [vp, vp, vp, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

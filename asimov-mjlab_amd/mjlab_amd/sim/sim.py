@@ -173,7 +173,9 @@ class SimulationCfg:
   njmax: int | None = None
   ls_parallel: bool = True
   contact_sensor_maxmatch: int = 64
-  balance_worlds: bool = False  # cost-sorted wave assignment (measured: no gain on G1)
+  # worlds handed to workgroups in order of their previous step's cost (one counting-sort
+  # launch before each physics launch): G1 4096 0.741 -> 0.700 ms per step launch
+  balance_worlds: bool = True
   mujoco: MujocoCfg = field(default_factory=MujocoCfg)
   nan_guard: NanGuardCfg = field(default_factory=NanGuardCfg)
 
@@ -390,10 +392,11 @@ class Simulation:
   def _refresh_order(self) -> None:
     if self.cfg.balance_worlds and self.num_envs > 1:
       # expected cost of a world ~ (solver iterations + 2) x constraint rows of
-      # its previous step; most expensive first (longest-processing-time order)
-      torch.add(self.data.solver_niter.view(-1), 2, out=self._order_cost)
-      self._order_cost.mul_(self.data.nefc.view(-1))
-      torch.sort(self._order_cost, descending=True, stable=False, out=(self._order_keys, self._order))
+      # its previous step; most expensive first (one counting-sort launch)
+      native.check(native.lib().mjh_order_worlds(ctypes.c_void_p(self.data.solver_niter.data_ptr()),
+                                                 ctypes.c_void_p(self.data.nefc.data_ptr()),
+                                                 ctypes.c_void_p(self._order.data_ptr()), self.num_envs, self._stream()),
+                   "mjh_order_worlds")
 
   def _launch_step(self) -> None:
     self._refresh_order()

@@ -416,6 +416,11 @@ int mjh_root_frame(const float* xpos, long long ps, const float* xquat, long lon
                    const float* cvel, long long vs, const float* grav, long long gs, const float* fwd, long long fs,
                    float* out, long long n, void* stream);
 
+/* A permutation of the worlds for mjh_data.world_order: most expensive first by
+ * the previous step's (solver_niter + 2) * nefc (counting sort in 256 buckets,
+ * one workgroup), so the worlds sharing a workgroup take similar time. */
+int mjh_order_worlds(const int* solver_niter, const int* nefc, long long* order, long long n, void* stream);
+
 /* EventManager reset bookkeeping (event_manager.py:146-156): last[e] = *step,
  * once[e] = 1 for the masked envs. */
 int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, const mjh_i64* step, long long n,

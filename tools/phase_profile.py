@@ -67,3 +67,22 @@ for nm, x in (("nefc", nefc), ("niter", niter)):
 srt = np.sort(tot)[: (N // 8) * 8].reshape(-1, 8)
 print(f"  if sorted by true cost: workgroup max mean {srt.max(1).mean():.0f}")
 print(f"  niter mean {niter.mean():.2f}  nefc mean {nefc.mean():.1f}  ncon mean {sim.data.ncon.float().mean().item():.1f}")
+
+# cost predictability for load balancing: one more step, per-world cycles of
+# step t+1 against predictors from step t
+tot1 = tot.copy()
+key1 = ((niter.reshape(-1).astype(np.int64) + 2) * nefc.reshape(-1).astype(np.int64))
+sim.step()
+torch.cuda.synchronize()
+p2 = buf.view(N, 32).cpu().numpy().astype(np.int64)
+tot2 = p2[:, 9] - p2[:, 0]
+M8 = (N // 8) * 8
+
+
+def wg_max(order):
+  return tot2[order][:M8].reshape(-1, 8).max(1).mean()
+
+
+print(f"  next step: corr(cycles_t, cycles_t+1) = {np.corrcoef(tot1, tot2)[0, 1]:.2f}; "
+      f"workgroup max mean: identity {wg_max(np.arange(N)):.0f}, by prev cycles {wg_max(np.argsort(-tot1)):.0f}, "
+      f"by prev (niter+2)*nefc {wg_max(np.argsort(-key1, kind='stable')):.0f}, by true cost {wg_max(np.argsort(-tot2)):.0f}")
