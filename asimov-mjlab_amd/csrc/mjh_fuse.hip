@@ -583,6 +583,159 @@ __global__ __launch_bounds__(1024) void order_worlds_kernel(const int* __restric
   }
 }
 
+// ---- motion tracking command (tasks/tracking/mdp/commands.py) -------------------
+constexpr int kMaxBins = 4096;
+
+// MotionCommand._adaptive_sampling for the envs in mask, one workgroup:
+// failed-bin histogram (kept only when some resampled env failed), sampling
+// probabilities p = smooth(bin_failed + ratio / B) / sum, time steps drawn by
+// inverse CDF (draws e*2, e*2+1 of the stream), and the sampling metrics
+// (entropy, top-1 probability, top-1 bin) written to every env when some env
+// resampled (commands.py:258-307)
+__global__ __launch_bounds__(1024) void motion_adaptive_kernel(
+    const unsigned char* __restrict__ mask, const unsigned char* __restrict__ terminated, long long* __restrict__ ts,
+    const float* __restrict__ bin_failed, float* __restrict__ cur_failed, const float* __restrict__ kern, int B, int K,
+    long long T, float ratio, float* __restrict__ m_entropy, float* __restrict__ m_top1p, float* __restrict__ m_top1b,
+    unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n) {
+  __shared__ float p[kMaxBins];
+  __shared__ float cdf[kMaxBins];
+  __shared__ int hist[kMaxBins];
+  __shared__ int anyfail, anymask;
+  __shared__ float H, pmax, imax;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) hist[b] = 0;
+  if (threadIdx.x == 0) anyfail = anymask = 0;
+  __syncthreads();
+  const long long Tc = T > 1 ? T : 1;
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+    const bool m = mask[e] != 0;
+    if (m) anymask = 1;
+    if (m && terminated[e]) {
+      long long b = (ts[e] * B) / Tc;
+      b = b < 0 ? 0 : (b > B - 1 ? B - 1 : b);
+      atomicAdd(&hist[b], 1);
+      anyfail = 1;
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    if (anyfail) cur_failed[b] = (float)hist[b];
+    p[b] = bin_failed[b] + ratio / (float)B;
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    float v = 0.f;
+    for (int k = 0; k < K; k++) v += p[min(b + k, B - 1)] * kern[k];
+    cdf[b] = v;  // smoothed, unnormalised
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int b = 0; b < B; b++) s += cdf[b];
+    float c = 0.f, h = 0.f, mx = -1.f;
+    int im = 0;
+    for (int b = 0; b < B; b++) {
+      const float q = cdf[b] / s;
+      p[b] = q;
+      c += q;
+      cdf[b] = c;
+      h -= q * logf(q + 1e-12f);
+      if (q > mx) { mx = q; im = b; }
+    }
+    H = h;
+    pmax = mx;
+    imax = (float)im;
+  }
+  __syncthreads();
+  const Rng rng(seed, key, ctr);
+  const float total = cdf[B - 1];
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+    if (mask[e]) {
+      const float target = rng.u01(2 * e) * total;
+      int lo = 0, hi = B;  // first b with cdf[b] > target (searchsorted right)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cdf[mid] <= target) lo = mid + 1; else hi = mid;
+      }
+      const int bin = lo > B - 1 ? B - 1 : lo;
+      ts[e] = (long long)(((float)bin + rng.u01(2 * e + 1)) / (float)B * (float)(T - 1));
+    }
+    if (anymask) {
+      m_entropy[e] = H / logf((float)B);
+      m_top1p[e] = pmax;
+      m_top1b[e] = imax / (float)B;
+    }
+  }
+}
+
+// MotionCommand._refresh_frame: frame[e] = table[ts[e]]; body_pos_w = the
+// frame's body positions + env origin (commands.py:134-181)
+__global__ void motion_frame_kernel(const float* __restrict__ table, const long long* __restrict__ ts,
+                                    float* __restrict__ frame, int W, int pos_off, int nb, float* __restrict__ body_pos_w,
+                                    const float* __restrict__ org, long long os, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * W) return;
+  const long long e = i / W;
+  const int c = (int)(i - e * W);
+  const float v = table[ts[e] * W + c];
+  frame[i] = v;
+  const int r = c - pos_off;
+  if (r >= 0 && r < 3 * nb) body_pos_w[e * 3 * nb + r] = v + org[e * os + r % 3];
+}
+
+// MotionCommand._resample_command's state write for the masked envs
+// (commands.py:309-375): root = reference root + pose offsets (U[pose], draws
+// e*S + 0..5; quat = euler(offset) (x) reference quat), velocity + U[vel] (e*S +
+// 6..11), joints = reference + U[jlo, jhi) (e*S + 12 + j) clipped to the soft
+// limits, joint velocities = reference; written as EntityData root/joint state
+// (angular velocity into the new body frame); S = 12 + nj
+__global__ void motion_reset_kernel(const float* __restrict__ frame, long long fs, int nj, int pos_off, int quat_off,
+                                    int lin_off, int ang_off, const float* __restrict__ body_pos_w, long long bps,
+                                    const unsigned char* __restrict__ mask, const Range6 pose, const Range6 vel,
+                                    int pose_any, int vel_any, float jlo, float jhi, const float* __restrict__ lim,
+                                    long long ls, float* __restrict__ qpos, long long qs, int rq, int jq,
+                                    float* __restrict__ qvel, long long vs, int rv, int jv, unsigned long long seed,
+                                    unsigned long long key, const mjh_i64* ctr, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n || !mask[e]) return;
+  const Rng rng(seed, key, ctr);
+  const long long S = 12 + nj;
+  const float* f = frame + e * fs;
+  float pos[3] = {body_pos_w[e * bps], body_pos_w[e * bps + 1], body_pos_w[e * bps + 2]};
+  float q[4] = {f[quat_off], f[quat_off + 1], f[quat_off + 2], f[quat_off + 3]};
+  float lin[3] = {f[lin_off], f[lin_off + 1], f[lin_off + 2]};
+  float ang[3] = {f[ang_off], f[ang_off + 1], f[ang_off + 2]};
+  if (pose_any) {
+    float r[6];
+    for (int j = 0; j < 6; j++) r[j] = rng.u01(e * S + j) * (pose.hi[j] - pose.lo[j]) + pose.lo[j];
+    pos[0] += r[0]; pos[1] += r[1]; pos[2] += r[2];
+    float qe[4], q2[4];
+    qeuler(qe, r[3], r[4], r[5]);
+    qmul(q2, qe, q);
+    q[0] = q2[0]; q[1] = q2[1]; q[2] = q2[2]; q[3] = q2[3];
+  }
+  if (vel_any) {
+    float r[6];
+    for (int j = 0; j < 6; j++) r[j] = rng.u01(e * S + 6 + j) * (vel.hi[j] - vel.lo[j]) + vel.lo[j];
+    lin[0] += r[0]; lin[1] += r[1]; lin[2] += r[2];
+    ang[0] += r[3]; ang[1] += r[4]; ang[2] += r[5];
+  }
+  float* qp = qpos + e * qs;
+  float* qv = qvel + e * vs;
+  for (int j = 0; j < nj; j++) {
+    float v = f[j] + (rng.u01(e * S + 12 + j) * (jhi - jlo) + jlo);
+    const float* l = lim + e * ls + 2 * j;
+    v = fminf(fmaxf(v, l[0]), l[1]);
+    qp[jq + j] = v;
+    qv[jv + j] = f[nj + j];
+  }
+  qp[rq] = pos[0]; qp[rq + 1] = pos[1]; qp[rq + 2] = pos[2];
+  qp[rq + 3] = q[0]; qp[rq + 4] = q[1]; qp[rq + 5] = q[2]; qp[rq + 6] = q[3];
+  float wb[3];
+  qrot_inv(wb, q, ang);
+  qv[rv] = lin[0]; qv[rv + 1] = lin[1]; qv[rv + 2] = lin[2];
+  qv[rv + 3] = wb[0]; qv[rv + 4] = wb[1]; qv[rv + 5] = wb[2];
+}
+
 }  // namespace
 
 extern "C" {
@@ -799,6 +952,43 @@ int mjh_root_frame(const float* xpos, long long ps, const float* xquat, long lon
 int mjh_order_worlds(const int* solver_niter, const int* nefc, long long* order, long long n, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(order_worlds_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, solver_niter, nefc, order, n);
+  return finish();
+}
+
+int mjh_motion_adaptive(const unsigned char* mask, const unsigned char* terminated, long long* time_steps,
+                        const float* bin_failed, float* cur_failed, const float* kern, int nbins, int ksize,
+                        long long T, float ratio, float* m_entropy, float* m_top1p, float* m_top1b,
+                        unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n, void* stream) {
+  if (n <= 0) return 0;
+  if (nbins <= 0 || nbins > kMaxBins || ksize <= 0) return 1;
+  hipLaunchKernelGGL(motion_adaptive_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, mask, terminated, time_steps,
+                     bin_failed, cur_failed, kern, nbins, ksize, T, ratio, m_entropy, m_top1p, m_top1b, seed, key, ctr, n);
+  return finish();
+}
+
+int mjh_motion_frame(const float* table, const long long* time_steps, float* frame, int width, int pos_off, int nb,
+                     float* body_pos_w, const float* origins, long long os, long long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(motion_frame_kernel, dim3(grid(n * width)), dim3(kBlock), 0, (hipStream_t)stream, table, time_steps,
+                     frame, width, pos_off, nb, body_pos_w, origins, os, n);
+  return finish();
+}
+
+int mjh_motion_reset(const float* frame, long long fs, int nj, int pos_off, int quat_off, int lin_off, int ang_off,
+                     const float* body_pos_w, long long bps, const unsigned char* mask, const float* pose_lo,
+                     const float* pose_hi, const float* vel_lo, const float* vel_hi, int pose_any, int vel_any, float jlo,
+                     float jhi, const float* lim, long long ls, float* qpos, long long qs, int root_q, int joint_q,
+                     float* qvel, long long vs, int root_v, int joint_v, unsigned long long seed,
+                     unsigned long long key, const mjh_i64* ctr, long long n, void* stream) {
+  if (n <= 0) return 0;
+  Range6 p{}, v{};
+  for (int j = 0; j < 6; j++) {
+    p.lo[j] = pose_lo[j]; p.hi[j] = pose_hi[j];
+    v.lo[j] = vel_lo[j]; v.hi[j] = vel_hi[j];
+  }
+  hipLaunchKernelGGL(motion_reset_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, frame, fs, nj, pos_off,
+                     quat_off, lin_off, ang_off, body_pos_w, bps, mask, p, v, pose_any, vel_any, jlo, jhi, lim, ls, qpos,
+                     qs, root_q, joint_q, qvel, vs, root_v, joint_v, seed, key, ctr, n);
   return finish();
 }
 

@@ -81,6 +81,9 @@ EXPORTS = (
   "mjh_joint_action",
   "mjh_root_frame",
   "mjh_order_worlds",
+  "mjh_motion_adaptive",
+  "mjh_motion_frame",
+  "mjh_motion_reset",
 )
 
 
@@ -168,6 +171,10 @@ def lib() -> ctypes.CDLL:
   L.mjh_joint_action.argtypes = [vp, ll, vp, vp, vp, vp, vp, ll, cf, vp, ll, cf, ci, ll, vp]
   L.mjh_root_frame.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp]
   L.mjh_order_worlds.argtypes = [vp, vp, vp, ll, vp]
+  L.mjh_motion_adaptive.argtypes = [vp, vp, vp, vp, vp, vp, ci, ci, ll, cf, vp, vp, vp, u64, u64, vp, ll, vp]
+  L.mjh_motion_frame.argtypes = [vp, vp, vp, ci, ci, ci, vp, vp, ll, ll, vp]
+  L.mjh_motion_reset.argtypes = [vp, ll, ci, ci, ci, ci, ci, vp, ll, vp, vp, vp, vp, vp, ci, ci, cf, cf, vp, ll, vp, ll, ci, ci,
+                                 vp, ll, ci, ci, u64, u64, vp, ll, vp]
   if L.mjh_abi_version() != ABI_VERSION:
     raise NativeLibraryError(f"libmjh ABI {L.mjh_abi_version()} != {ABI_VERSION}")
   if L.mjh_sizeof_model() != ctypes.sizeof(abi.model_struct()):

@@ -24,6 +24,7 @@ The RNG stream differs from the reference (draws are taken for all envs).
 
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass, field
 from typing import Literal
@@ -34,6 +35,7 @@ from mjlab_amd import envops
 from mjlab_amd.managers.command_manager import CommandTerm
 from mjlab_amd.managers.manager_term_config import CommandTermCfg
 from mjlab_amd.motion import load_motion
+from mjlab_amd.sim import native
 from mjlab_amd.envops import quat_error_magnitude
 from mjlab_amd.utils.math import quat_inv, yaw_quat
 
@@ -148,6 +150,8 @@ class MotionCommand(CommandTerm):
 
     self._pose_lo, self._pose_hi, self._pose_any = rng6(cfg.pose_range)
     self._vel_lo, self._vel_hi, self._vel_any = rng6(cfg.velocity_range)
+    self._ranges_host = [[float(r.get(a, (0.0, 0.0))[i]) for a in _AXES6] for r in (cfg.pose_range, cfg.velocity_range)
+                         for i in (0, 1)]
 
     for name in ("error_anchor_pos", "error_anchor_rot", "error_anchor_lin_vel", "error_anchor_ang_vel",
                  "error_body_pos", "error_body_rot", "error_body_lin_vel", "error_body_ang_vel",
@@ -174,6 +178,12 @@ class MotionCommand(CommandTerm):
   anchor_ang_vel_w = property(lambda s: s._f_body_ang_vel[:, s.motion_anchor_body_index])
 
   def _refresh_frame(self) -> None:
+    if self._frame.is_cuda and self._origins.stride(1) == 1:  # one launch (csrc/mjh_fuse.hip)
+      P = envops._ptr
+      native.check(native.lib().mjh_motion_frame(
+        P(self.motion.frame_table), P(self.time_steps), P(self._frame), self._frame.shape[1], 2 * self._nj, self._nb,
+        P(self._body_pos_w), P(self._origins), self._origins.stride(0), self.num_envs, envops._stream()), "mjh_motion_frame")
+      return
     torch.index_select(self.motion.frame_table, 0, self.time_steps, out=self._frame)
     torch.add(self._f_body_pos, self._origins[:, None, :], out=self._body_pos_w)
 
@@ -230,7 +240,23 @@ class MotionCommand(CommandTerm):
     p = (p[self._smooth_idx] * self.kernel[None]).sum(-1)
     return p / p.sum()
 
+  def _adaptive_sampling_fused(self, mask: torch.Tensor) -> bool:
+    if not (mask.is_cuda and mask.dtype == torch.bool and self.bin_count <= 4096):
+      return False
+    term = self._env.termination_manager.terminated
+    P = envops._ptr
+    seed, key, ctr = envops.rng_args(self._env, "motion_command.adaptive_sampling")
+    m = self.metrics
+    native.check(native.lib().mjh_motion_adaptive(
+      P(mask), P(term), P(self.time_steps), P(self.bin_failed_count), P(self._current_bin_failed), P(self.kernel),
+      self.bin_count, self.kernel.numel(), self.motion.time_step_total, float(self.cfg.adaptive_uniform_ratio),
+      P(m["sampling_entropy"]), P(m["sampling_top1_prob"]), P(m["sampling_top1_bin"]), seed, key, ctr, self.num_envs,
+      envops._stream()), "mjh_motion_adaptive")
+    return True
+
   def _adaptive_sampling(self, mask: torch.Tensor) -> None:
+    if self._adaptive_sampling_fused(mask):
+      return
     T = self.motion.time_step_total
     failed = mask & self._env.termination_manager.terminated
     cur_bin = torch.clamp((self.time_steps * self.bin_count) // max(T, 1), 0, self.bin_count - 1)
@@ -274,6 +300,8 @@ class MotionCommand(CommandTerm):
     else:
       raise ValueError(f"unknown sampling_mode '{mode}'")
     self._refresh_frame()
+    if self._write_state_fused(mask):
+      return
 
     n = self.num_envs
     root_pos = self.body_pos_w[:, 0]
@@ -296,6 +324,34 @@ class MotionCommand(CommandTerm):
     self.robot.write_joint_state_to_sim(joint_pos, self.joint_vel, env_ids=mask)
     self.robot.write_root_state_to_sim(torch.cat([root_pos, root_ori, root_lin_vel, root_ang_vel], dim=-1), env_ids=mask)
     self.robot.clear_state(env_ids=mask)
+
+  def _write_state_fused(self, mask: torch.Tensor) -> bool:
+    """The resampled envs' robot state (reference root +- pose/velocity offsets,
+    joints + offsets clipped) written in one launch, plus clear_state."""
+    d = self.robot.data
+    c = d._cols
+    keys = ("free_joint_q_adr", "free_joint_v_adr", "joint_q_adr", "joint_v_adr")
+    if not (mask.is_cuda and mask.dtype == torch.bool and all(isinstance(c[k], slice) for k in keys)):
+      return False
+    lim = d.soft_joint_pos_limits
+    qpos, qvel = d.data.qpos, d.data.qvel
+    if not (lim.is_contiguous() and lim.shape[1] == self._nj and qpos.stride(1) == 1 and qvel.stride(1) == 1):
+      return False
+    nj, nb = self._nj, self._nb
+    pos_off = 2 * nj
+    F6 = ctypes.c_float * 6
+    plo, phi, vlo, vhi = (F6(*r) for r in self._ranges_host)
+    lo, hi = self.cfg.joint_position_range
+    seed, key, ctr = envops.rng_args(self._env, "motion_command.resample_state")
+    P = envops._ptr
+    native.check(native.lib().mjh_motion_reset(
+      P(self._frame), self._frame.stride(0), nj, pos_off, pos_off + 3 * nb, pos_off + 7 * nb, pos_off + 10 * nb,
+      P(self._body_pos_w), self._body_pos_w.stride(0), P(mask), plo, phi, vlo, vhi, int(self._pose_any), int(self._vel_any),
+      float(lo), float(hi), P(lim), lim.stride(0), P(qpos), qpos.stride(0), c["free_joint_q_adr"].start, c["joint_q_adr"].start,
+      P(qvel), qvel.stride(0), c["free_joint_v_adr"].start, c["joint_v_adr"].start, seed, key, ctr, self.num_envs,
+      envops._stream()), "mjh_motion_reset")
+    self.robot.clear_state(env_ids=mask)
+    return True
 
   # ---- per-step update (commands.py:377-412) ----
   def _update_command(self) -> None:

@@ -421,6 +421,35 @@ int mjh_root_frame(const float* xpos, long long ps, const float* xquat, long lon
  * one workgroup), so the worlds sharing a workgroup take similar time. */
 int mjh_order_worlds(const int* solver_niter, const int* nefc, long long* order, long long n, void* stream);
 
+/* ---- motion tracking command (tasks/tracking/mdp/commands.py), mjh_fuse.hip ---- */
+
+/* MotionCommand._adaptive_sampling (commands.py:258-307) for the masked envs in
+ * one workgroup: failed-bin histogram into cur_failed (when some masked env
+ * terminated), p = smooth(bin_failed + ratio / nbins, kern[ksize]) / sum,
+ * time steps by inverse CDF (draws 2e, 2e + 1), metrics when any env resampled.
+ * nbins <= 4096. */
+int mjh_motion_adaptive(const unsigned char* mask, const unsigned char* terminated, long long* time_steps,
+                        const float* bin_failed, float* cur_failed, const float* kern, int nbins, int ksize,
+                        long long T, float ratio, float* m_entropy, float* m_top1p, float* m_top1b,
+                        unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n, void* stream);
+
+/* MotionCommand._refresh_frame: frame[e] = table[time_steps[e]] (width floats);
+ * body_pos_w (n, nb, 3) = the frame's body positions (columns pos_off..) + origins. */
+int mjh_motion_frame(const float* table, const long long* time_steps, float* frame, int width, int pos_off, int nb,
+                     float* body_pos_w, const float* origins, long long os, long long n, void* stream);
+
+/* MotionCommand._resample_command's robot state write for the masked envs
+ * (commands.py:309-375): reference root pose/velocity + U offsets (draws e*S +
+ * 0..11), joints + U[jlo, jhi) (e*S + 12 + j) clipped to lim (n, nj, 2), S = 12
+ * + nj; written into qpos/qvel (root free joint at root_q/root_v, joints at
+ * joint_q/joint_v; angular velocity into the new body frame). */
+int mjh_motion_reset(const float* frame, long long fs, int nj, int pos_off, int quat_off, int lin_off, int ang_off,
+                     const float* body_pos_w, long long bps, const unsigned char* mask, const float* pose_lo,
+                     const float* pose_hi, const float* vel_lo, const float* vel_hi, int pose_any, int vel_any, float jlo,
+                     float jhi, const float* lim, long long ls, float* qpos, long long qs, int root_q, int joint_q,
+                     float* qvel, long long vs, int root_v, int joint_v, unsigned long long seed,
+                     unsigned long long key, const mjh_i64* ctr, long long n, void* stream);
+
 /* EventManager reset bookkeeping (event_manager.py:146-156): last[e] = *step,
  * once[e] = 1 for the masked envs. */
 int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, const mjh_i64* step, long long n,

@@ -385,3 +385,84 @@ def test_root_frame_and_joint_action_match_formulas():
   torch.testing.assert_close(proc, torch.addcmul(offset, inp, scale), rtol=1e-6, atol=1e-6)
   assert envops.joint_action(inp, action, prev, raw, proc, 0.5, offset)
   torch.testing.assert_close(proc, offset + inp * 0.5, rtol=1e-6, atol=1e-6)
+
+
+def test_motion_command_kernels_match_formulas():
+  """Tracking MotionCommand: adaptive sampling, frame refresh and the resampled
+  robot state vs the torch formulas of tasks/tracking/mdp/commands.py fed the
+  same device-stream draws."""
+  import math
+
+  n, B, K, T = 4096, 11, 3, 500
+  g = torch.Generator(device=DEV).manual_seed(50)
+  ctr = _ctr(61)
+  mask = torch.rand(n, device=DEV, generator=g) < 0.2
+  term = torch.rand(n, device=DEV, generator=g) < 0.5
+  ts = torch.randint(0, T, (n,), device=DEV, generator=g)
+  ts0 = ts.clone()
+  bin_failed = torch.rand(B, device=DEV, generator=g)
+  cur = torch.zeros(B, device=DEV)
+  kern = torch.tensor([0.8 ** i for i in range(K)], device=DEV)
+  kern = kern / kern.sum()
+  met = [torch.zeros(n, device=DEV) for _ in range(3)]
+  P = envops._ptr
+  native.check(native.lib().mjh_motion_adaptive(P(mask), P(term), P(ts), P(bin_failed), P(cur), P(kern), B, K, T, 0.1,
+                                                *[P(x) for x in met], *_args(ctr), n, _s()), "ma")
+  failed = mask & term
+  cb = torch.clamp((ts0 * B) // T, 0, B - 1)
+  ref_cur = torch.zeros(B, device=DEV).scatter_add_(0, cb, failed.float())
+  torch.testing.assert_close(cur, ref_cur)
+  p = bin_failed + 0.1 / B
+  idx = torch.clamp(torch.arange(B, device=DEV)[:, None] + torch.arange(K, device=DEV)[None], max=B - 1)
+  p = (p[idx] * kern[None]).sum(-1)
+  p = p / p.sum()
+  cdf = torch.cumsum(p.double(), 0)
+  u = envops.uniform_draws(SEED, KEY, ctr, 2 * n, DEV).view(n, 2)
+  bins = torch.searchsorted(cdf, (u[:, 0].double() * cdf[-1]).contiguous(), right=True).clamp_(max=B - 1)
+  new = ((bins.float() + u[:, 1]) / B * (T - 1)).long()
+  ref_ts = torch.where(mask, new, ts0)
+  assert (ts != ref_ts).float().mean().item() < 1e-3  # bin boundaries: float32 vs float64 CDF
+  H = -(p * (p + 1e-12).log()).sum()
+  torch.testing.assert_close(met[0], (H / math.log(B)).expand(n), rtol=1e-5, atol=1e-6)
+  torch.testing.assert_close(met[1], p.max().expand(n), rtol=1e-5, atol=1e-6)
+  torch.testing.assert_close(met[2], (p.argmax().float() / B).expand(n))
+  # frame refresh
+  nj, nb = 29, 14
+  W = 2 * nj + 13 * nb
+  table = torch.randn(T, W, device=DEV, generator=g)
+  frame = torch.zeros(n, W, device=DEV)
+  bpw = torch.zeros(n, nb, 3, device=DEV)
+  org = torch.randn(n, 3, device=DEV, generator=g)
+  native.check(native.lib().mjh_motion_frame(P(table), P(ts), P(frame), W, 2 * nj, nb, P(bpw), P(org), 3, n, _s()), "mf")
+  ref_frame = table[ts]
+  assert torch.equal(frame, ref_frame)
+  torch.testing.assert_close(bpw, ref_frame[:, 2 * nj:2 * nj + 3 * nb].view(n, nb, 3) + org[:, None, :])
+  # resampled robot state
+  q = frame[:, 2 * nj + 3 * nb:2 * nj + 7 * nb].view(n, nb, 4)
+  q /= q.norm(dim=-1, keepdim=True)
+  qpos, qvel = torch.zeros(n, 7 + nj, device=DEV), torch.zeros(n, 6 + nj, device=DEV)
+  lo = torch.rand(n, nj, device=DEV, generator=g) - 1.5
+  lim = torch.stack([lo, lo + 2.0], -1).contiguous()
+  F6 = ctypes.c_float * 6
+  pr = ([-0.05, -0.05, -0.01, -0.1, -0.1, -0.2], [0.05, 0.05, 0.01, 0.1, 0.1, 0.2])
+  vr = ([-0.5, -0.5, -0.2, -0.52, -0.52, -0.78], [0.5, 0.5, 0.2, 0.52, 0.52, 0.78])
+  ctr2 = _ctr(62)
+  native.check(native.lib().mjh_motion_reset(
+    P(frame), W, nj, 2 * nj, 2 * nj + 3 * nb, 2 * nj + 7 * nb, 2 * nj + 10 * nb, P(bpw), 3 * nb, P(mask), F6(*pr[0]),
+    F6(*pr[1]), F6(*vr[0]), F6(*vr[1]), 1, 1, -0.52, 0.52, P(lim), 2 * nj, P(qpos), 7 + nj, 0, 7, P(qvel), 6 + nj, 0, 6,
+    *_args(ctr2), n, _s()), "mr")
+  S = 12 + nj
+  uu = envops.uniform_draws(SEED, KEY, ctr2, n * S, DEV).view(n, S)
+  T6 = lambda v: torch.tensor(v, device=DEV)  # noqa: E731
+  rp = uu[:, 0:6] * (T6(pr[1]) - T6(pr[0])) + T6(pr[0])
+  rv = uu[:, 6:12] * (T6(vr[1]) - T6(vr[0])) + T6(vr[0])
+  root_pos = bpw[:, 0] + rp[:, 0:3]
+  root_q = M.quat_mul(M.quat_from_euler_xyz(rp[:, 3], rp[:, 4], rp[:, 5]), q[:, 0])
+  lin = frame[:, 2 * nj + 7 * nb:2 * nj + 7 * nb + 3] + rv[:, 0:3]
+  ang = frame[:, 2 * nj + 10 * nb:2 * nj + 10 * nb + 3] + rv[:, 3:6]
+  jp = torch.clip(frame[:, :nj] + (uu[:, 12:] * 1.04 - 0.52), lim[:, :, 0], lim[:, :, 1])
+  ref_q = torch.cat([root_pos, root_q, jp], 1)
+  ref_v = torch.cat([lin, M.quat_apply_inverse(root_q, ang), frame[:, nj:2 * nj]], 1)
+  m2 = mask[:, None]
+  torch.testing.assert_close(qpos, torch.where(m2, ref_q, 0.0), rtol=1e-5, atol=1e-5)
+  torch.testing.assert_close(qvel, torch.where(m2, ref_v, 0.0), rtol=1e-5, atol=1e-5)

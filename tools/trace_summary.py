@@ -34,9 +34,18 @@ for i, (s, e, n) in enumerate(win):
   if i + 1 < len(win):
     gaps += max(0, win[i + 1][0] - e)
 print(f"{K} env steps: {tot / K / 1e3:.3f} us/step wall, {len(win) / K:.1f} dispatches/step")
+gl = defaultdict(lambda: [0, 0.0])
+for i in range(len(win) - 1):
+  g = win[i + 1][0] - win[i][1]
+  if g > 2000:  # > 2 us: attribute the idle time to the (previous -> next) kernel pair
+    gl[(win[i][2][:60], win[i + 1][2][:60])][0] += 1
+    gl[(win[i][2][:60], win[i + 1][2][:60])][1] += g
+big = sorted(gl.items(), key=lambda x: -x[1][1])[:6]
 for c, v in sorted(cat.items(), key=lambda x: -x[1]):
   print(f"  {c:8s} {v / K / 1e3:9.1f} us/step")
 print(f"  gaps     {gaps / K / 1e3:9.1f} us/step")
+for (a, b), (c, g) in big:
+  print(f"    gap {g / K / 1e3:7.1f} us/step ({c / K:.1f}/step): {a} -> {b}")
 print("env kernels (per step: count, us):")
 for n, (c, d) in sorted(names.items(), key=lambda x: -x[1][1])[:40]:
   print(f"  {c / K:5.1f} {d / K / 1e3:8.1f}  {n}")
