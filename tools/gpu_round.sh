@@ -25,6 +25,11 @@ if [ "${PMC:-1}" = 1 ]; then
   timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcw -o w -- python tools/kernel_bench.py 4096 40 > $O/pmcw.log 2>&1
   python tools/pmc_traffic.py $(find $O/pmcf -name '*counter_collection.csv') $(find $O/pmcw -name '*counter_collection.csv') 4096 > $O/step_kernel_traffic.json
   cat $O/step_kernel_traffic.json
+  # keep the per-dispatch counter rows of the step kernel (the JSON's evidence)
+  for P in pmcf pmcw; do
+    F=$(find $O/$P -name '*counter_collection.csv' | head -1)
+    { head -1 $F; grep 'step_kernel' $F || true; } > $O/${P}_step_kernel_rows.csv
+  done
   find $O/pmcf $O/pmcw -name '*.csv' -delete
 fi
 du -sh $O
