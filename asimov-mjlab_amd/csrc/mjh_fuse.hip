@@ -736,6 +736,45 @@ __global__ void motion_reset_kernel(const float* __restrict__ frame, long long f
   qv[rv + 3] = wb[0]; qv[rv + 4] = wb[1]; qv[rv + 5] = wb[2];
 }
 
+// |axis_angle_from_quat(a (x) conj(b))| (quat_error_magnitude, utils/math.py;
+// the formula of mjh_envops.hip)
+__device__ __forceinline__ float quat_err(const float* a, const float* b) {
+  const float bc[4] = {b[0], -b[1], -b[2], -b[3]};
+  float q[4];
+  qmul(q, a, bc);
+  const float sg = q[0] < 0.f ? -1.f : 1.f;
+  const float w = q[0] * sg, x = q[1] * sg, y = q[2] * sg, z = q[3] * sg;
+  const float mag = sqrtf(x * x + y * y + z * z);
+  const float half = atan2f(mag, w);
+  const float ang = 2.f * half;
+  const float s = fabsf(ang) > 1e-6f ? sinf(half) / ang : 0.5f - ang * ang / 48.f;
+  const float ax = x / s, ay = y / s, az = z / s;
+  return sqrtf(ax * ax + ay * ay + az * az);
+}
+
+// Gaussian tracking rewards (tasks/tracking/mdp/rewards.py): out[e] =
+// exp(-mean_j err_j * inv_std2) over k rows, row j of a at a + e*aes +
+// ra[j]*ars (ra NULL: j), likewise b; err_j = sum_c (a - b)^2 over d columns
+// (quat = 0), or quat_error_magnitude(a_j, b_j)^2 (quat != 0)
+__global__ void rew_exp_err_kernel(const float* __restrict__ a, long long aes, long long ars, const int* __restrict__ ra,
+                                   const float* __restrict__ b, long long bes, long long brs, const int* __restrict__ rb,
+                                   int k, int d, int quat, float inv_std2, float* __restrict__ out, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  float s = 0.f;
+  for (int j = 0; j < k; j++) {
+    const float* x = a + e * aes + (long long)(ra ? ra[j] : j) * ars;
+    const float* y = b + e * bes + (long long)(rb ? rb[j] : j) * brs;
+    if (quat) {
+      const float q = quat_err(x, y);
+      s += q * q;
+    } else {
+      for (int c = 0; c < d; c++) s += (x[c] - y[c]) * (x[c] - y[c]);
+    }
+  }
+  out[e] = expf(-(s / (float)k) * inv_std2);
+}
+
 }  // namespace
 
 extern "C" {
@@ -989,6 +1028,15 @@ int mjh_motion_reset(const float* frame, long long fs, int nj, int pos_off, int 
   hipLaunchKernelGGL(motion_reset_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, frame, fs, nj, pos_off,
                      quat_off, lin_off, ang_off, body_pos_w, bps, mask, p, v, pose_any, vel_any, jlo, jhi, lim, ls, qpos,
                      qs, root_q, joint_q, qvel, vs, root_v, joint_v, seed, key, ctr, n);
+  return finish();
+}
+
+int mjh_rew_exp_err(const float* a, long long aes, long long ars, const int* ra, const float* b, long long bes,
+                    long long brs, const int* rb, int k, int d, int quat, float inv_std2, float* out, long long n,
+                    void* stream) {
+  if (n <= 0 || k <= 0) return 0;
+  hipLaunchKernelGGL(rew_exp_err_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, a, aes, ars, ra, b, bes, brs, rb,
+                     k, d, quat, inv_std2, out, n);
   return finish();
 }
 

@@ -723,3 +723,36 @@ def joint_action(inp, action, prev, raw, processed, scale, offset) -> bool:
   native.check(native.lib().mjh_joint_action(_ptr(inp), inp.stride(0), _ptr(action), _ptr(prev), _ptr(raw), _ptr(processed),
                                              *sa, *oa, d, n, _stream()), "mjh_joint_action")
   return True
+
+
+def _row_view(t: torch.Tensor, d: int):
+  """(N, d) or (N, k, d) float32 GPU view with unit last stride -> (ptr, env stride, row stride, k), else None."""
+  if not (t.is_cuda and t.dtype == torch.float32 and t.shape[-1] == d and t.stride(-1) == 1):
+    return None
+  if t.dim() == 2:
+    return t.data_ptr(), t.stride(0), 0, 1
+  if t.dim() == 3:
+    return t.data_ptr(), t.stride(0), t.stride(1), t.shape[1]
+  return None
+
+
+def rew_exp_err(a: torch.Tensor, b: torch.Tensor, std: float, quat: bool = False, rows_a=None, rows_b=None):
+  """exp(-mean_j err_j / std^2) of rows of a and b (rows_*: int32 row indices or None) in one launch, or None."""
+  d = 4 if quat else a.shape[-1]
+  va, vb = _row_view(a, d), _row_view(b, d)
+  if va is None or vb is None or a.shape[0] != b.shape[0]:
+    return None
+  k = rows_a.numel() if rows_a is not None else va[3]
+  kb = rows_b.numel() if rows_b is not None else vb[3]
+  if k != kb or k == 0:
+    return None
+  for r in (rows_a, rows_b):
+    if r is not None and not (r.is_cuda and r.dtype == torch.int32 and r.is_contiguous()):
+      return None
+  n = a.shape[0]
+  out = _vec_out(n, a.device)
+  native.check(native.lib().mjh_rew_exp_err(
+    ctypes.c_void_p(va[0]), va[1], va[2], _ptr(rows_a) if rows_a is not None else None, ctypes.c_void_p(vb[0]), vb[1], vb[2],
+    _ptr(rows_b) if rows_b is not None else None, k, d, int(quat), 1.0 / (std * std), _ptr(out), n, _stream()),
+    "mjh_rew_exp_err")
+  return out

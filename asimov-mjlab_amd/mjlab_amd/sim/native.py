@@ -84,6 +84,7 @@ EXPORTS = (
   "mjh_motion_adaptive",
   "mjh_motion_frame",
   "mjh_motion_reset",
+  "mjh_rew_exp_err",
 )
 
 
@@ -172,6 +173,7 @@ def lib() -> ctypes.CDLL:
   L.mjh_root_frame.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp]
   L.mjh_order_worlds.argtypes = [vp, vp, vp, ll, vp]
   L.mjh_motion_adaptive.argtypes = [vp, vp, vp, vp, vp, vp, ci, ci, ll, cf, vp, vp, vp, u64, u64, vp, ll, vp]
+  L.mjh_rew_exp_err.argtypes = [vp, ll, ll, vp, vp, ll, ll, vp, ci, ci, ci, cf, vp, ll, vp]
   L.mjh_motion_frame.argtypes = [vp, vp, vp, ci, ci, ci, vp, vp, ll, ll, vp]
   L.mjh_motion_reset.argtypes = [vp, ll, ci, ci, ci, ci, ci, vp, ll, vp, vp, vp, vp, vp, ci, ci, cf, cf, vp, ll, vp, ll, ci, ci,
                                  vp, ll, ci, ci, u64, u64, vp, ll, vp]

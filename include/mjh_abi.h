@@ -450,6 +450,14 @@ int mjh_motion_reset(const float* frame, long long fs, int nj, int pos_off, int 
                      float* qvel, long long vs, int root_v, int joint_v, unsigned long long seed,
                      unsigned long long key, const mjh_i64* ctr, long long n, void* stream);
 
+/* Gaussian tracking rewards (tasks/tracking/mdp/rewards.py): out[e] =
+ * exp(-mean_j err_j * inv_std2) over k rows; row j of a at a + e*aes + ra[j]*ars
+ * (ra NULL: j), likewise b; err_j = sum of squared differences over d columns,
+ * or quat_error_magnitude(a_j, b_j)^2 when quat != 0. */
+int mjh_rew_exp_err(const float* a, long long aes, long long ars, const int* ra, const float* b, long long bes,
+                    long long brs, const int* rb, int k, int d, int quat, float inv_std2, float* out, long long n,
+                    void* stream);
+
 /* EventManager reset bookkeeping (event_manager.py:146-156): last[e] = *step,
  * once[e] = 1 for the masked envs. */
 int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, const mjh_i64* step, long long n,

@@ -466,3 +466,21 @@ def test_motion_command_kernels_match_formulas():
   m2 = mask[:, None]
   torch.testing.assert_close(qpos, torch.where(m2, ref_q, 0.0), rtol=1e-5, atol=1e-5)
   torch.testing.assert_close(qvel, torch.where(m2, ref_v, 0.0), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("quat", [False, True])
+def test_rew_exp_err_matches_tracking_formula(quat):
+  n, nb, nbe = 4096, 14, 30
+  d = 4 if quat else 3
+  g = torch.Generator(device=DEV).manual_seed(70 + quat)
+  a = torch.randn(n, nb, d, device=DEV, generator=g)
+  big = torch.randn(n, nbe, 6 if not quat else 4, device=DEV, generator=g)
+  b = big[..., :d]
+  if quat:
+    a, b = a / a.norm(dim=-1, keepdim=True), b / b.norm(dim=-1, keepdim=True)
+  ra = torch.tensor([0, 3, 5, 13], dtype=torch.int32, device=DEV)
+  rb = torch.tensor([1, 7, 2, 29], dtype=torch.int32, device=DEV)
+  out = envops.rew_exp_err(a, b, 0.3, quat, ra, rb)
+  x, y = a[:, ra.long()], b[:, rb.long()]
+  err = M.quat_error_magnitude(x, y) ** 2 if quat else torch.sum(torch.square(x - y), dim=-1)
+  torch.testing.assert_close(out, torch.exp(-err.mean(-1) / 0.09), rtol=2e-5, atol=1e-6)
