@@ -983,6 +983,15 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     for (int c = 0; c < cn; c++) {
       const int k = IMG_I(body_chain)[ca + c];
       const int ja = IMG_I(body_jntadr)[k], jn = IMG_I(body_jntnum)[k];
+      const int mid = Z.nmocap > 0 ? IMG_I(body_mocapid)[k] : -1;
+      if (mid >= 0) {  // mocap body (a child of the world): pose from mocap_pos / mocap_quat
+        const float* mp = DP(mocap_pos) + (W * Z.nmocap + mid) * 3;
+        const float* mq = DP(mocap_quat) + (W * Z.nmocap + mid) * 4;
+        p[0] = mp[0]; p[1] = mp[1]; p[2] = mp[2];
+        q[0] = mq[0]; q[1] = mq[1]; q[2] = mq[2]; q[3] = mq[3];
+        quat_normalize(q);
+        continue;
+      }
       if (jn == 1 && IMG_I(jnt_type)[ja] == 0) {
         const int qa = IMG_I(jnt_qposadr)[ja];
         p[0] = qpos[qa]; p[1] = qpos[qa + 1]; p[2] = qpos[qa + 2];

@@ -165,6 +165,16 @@ class EntityData:
     qv = torch.cat([velocity[:, :3], ang_b], dim=-1)
     _masked_write(self.data.qvel, self._cols["free_joint_v_adr"], qv, env_ids)
 
+  def write_mocap_pose(self, pose: torch.Tensor, env_ids=None) -> None:
+    """Mocap body pose (pos 3, quat 4) of a mocap entity (data.py:178-187)."""
+    mid = self.indexing.mocap_id
+    if mid is None:
+      raise ValueError("Cannot write mocap pose for non-mocap entity.")
+    assert pose.shape[-1] == 7
+    n = self.data.qpos.shape[0]
+    _masked_write(self.data.mocap_pos.view(n, -1), slice(3 * mid, 3 * mid + 3), pose[:, 0:3], env_ids)
+    _masked_write(self.data.mocap_quat.view(n, -1), slice(4 * mid, 4 * mid + 4), pose[:, 3:7], env_ids)
+
   def write_joint_state(self, position, velocity, joint_ids=None, env_ids=None) -> None:
     if not self.is_articulated:
       raise ValueError("Cannot write joint state for non-articulated entity.")

@@ -283,7 +283,8 @@ class Entity:
       site_ids=T(site_ids),
       ctrl_ids=T(ctrl_ids),
       joint_ids=T(joint_ids),
-      mocap_id=None,
+      mocap_id=(int(model.body_mocapid[body_ids[0]]) if self.is_fixed_base and self.is_mocap
+                and int(model.body_mocapid[body_ids[0]]) >= 0 else None),
       joint_q_adr=T(jq),
       joint_v_adr=T(jv),
       free_joint_q_adr=T(fq),
@@ -325,6 +326,10 @@ class Entity:
 
   def write_joint_position_target_to_sim(self, position_target, joint_ids=None, env_ids=None) -> None:
     self._data.write_ctrl(position_target, joint_ids, env_ids)
+
+  def write_mocap_pose_to_sim(self, mocap_pose: torch.Tensor, env_ids=None) -> None:
+    """(N, 7) [pos, quat] of this mocap entity's root body (entity.py:582-595)."""
+    self._data.write_mocap_pose(mocap_pose, env_ids)
 
   def write_external_wrench_to_sim(self, forces, torques, env_ids=None, body_ids: Sequence[int] | slice | None = None) -> None:
     self._data.write_external_wrench(forces, torques, body_ids, env_ids)

@@ -222,6 +222,10 @@ class Simulation:
       self._data_flat[f.name] = v if _TORCH_DT[f.ctype] == torch.float32 else v.view(_TORCH_DT[f.ctype])
       off += c
     self._data_flat["qpos"][:] = torch.as_tensor(model.qpos0, dtype=torch.float32, device=device)
+    if int(model.nmocap) > 0:  # mj_resetData: mocap poses start at the bodies' model poses
+      mb = np.argsort(np.where(model.body_mocapid >= 0, model.body_mocapid, np.iinfo(np.int32).max))[: int(model.nmocap)]
+      self._data_flat["mocap_pos"][:] = torch.as_tensor(np.asarray(model.body_pos)[mb].reshape(-1), dtype=torch.float32)
+      self._data_flat["mocap_quat"][:] = torch.as_tensor(np.asarray(model.body_quat)[mb].reshape(-1), dtype=torch.float32)
     data_views = {n: self._data_view(n) for n in self._data_flat}
     self.epoch = Epoch()
     self._data_bridge = Bridge(data_views, extra={"epoch": self.epoch}, nworld=num_envs)
@@ -484,7 +488,8 @@ class Simulation:
 
   def state_dict(self) -> dict[str, torch.Tensor]:
     """Physics state (qpos, qvel, act, ctrl, qacc_warmstart, time) for checkpoint/resume."""
-    return {k: self._data_flat[k].clone() for k in ("qpos", "qvel", "act", "ctrl", "qacc_warmstart", "time")}
+    return {k: self._data_flat[k].clone() for k in ("qpos", "qvel", "act", "ctrl", "qacc_warmstart", "time", "mocap_pos",
+                                                      "mocap_quat")}
 
   def load_state_dict(self, state: dict[str, torch.Tensor]) -> None:
     for k, v in state.items():

@@ -284,9 +284,15 @@ def compile_spec(spec: Spec, nconmax: int = 0, njmax: int = 0) -> Model:
   m.body_pos = np.array([b.pos for b in bodies], np.float64)
   m.body_quat = np.array([np.array(b.quat) / np.linalg.norm(b.quat) for b in bodies])
   m.body_mocapid = np.full(nbody, -1, np.int32)
+  nmocap = 0
   for bi, b in enumerate(bodies):
     if b.mocap:
-      raise NotImplementedError("mocap bodies are not supported on the HIP path")
+      # MuJoCo: mocap bodies are static children of the world (no joints)
+      if parent[bi] != 0 or body_jntnum[bi] != 0:
+        raise ValueError(f"mocap body '{b.name}' must be a child of the world body without joints")
+      m.body_mocapid[bi] = nmocap
+      nmocap += 1
+  m.nmocap = nmocap
   # weld / root ids
   weld = np.zeros(nbody, np.int32)
   root = np.zeros(nbody, np.int32)

@@ -192,7 +192,7 @@ static void ws_free(ws_t* w) {
 }
 
 /* ---------------------------------------------------------------- smooth dynamics */
-static void kinematics(const or_model* m, int wi, ws_t* w) {
+static void kinematics(const or_model* m, const or_data* d, int wi, ws_t* w) {
   const real* bpos = WF(m, body_pos, wi);
   const real* bquat = WF(m, body_quat, wi);
   const real* qpos0 = WF(m, qpos0, wi);
@@ -203,6 +203,16 @@ static void kinematics(const or_model* m, int wi, ws_t* w) {
     real* xp = w->xpos + 3 * b;
     real* xq = w->xquat + 4 * b;
     int ja = m->body_jntadr[b], jn = m->body_jntnum[b];
+    const int mid = m->body_mocapid[b];
+    if (mid >= 0) { /* mocap body (child of the world): pose from mocap_pos / mocap_quat */
+      const real* mp = d->mocap_pos + ((size_t)wi * m->nmocap + mid) * 3;
+      const real* mq = d->mocap_quat + ((size_t)wi * m->nmocap + mid) * 4;
+      xp[0] = mp[0]; xp[1] = mp[1]; xp[2] = mp[2];
+      xq[0] = mq[0]; xq[1] = mq[1]; xq[2] = mq[2]; xq[3] = mq[3];
+      normalize4(xq);
+      quat2mat(w->xmat + 9 * b, xq);
+      continue;
+    }
     if (jn == 1 && m->jnt_type[ja] == 0) {
       const real* q = w->qpos + m->jnt_qposadr[ja];
       xp[0] = q[0]; xp[1] = q[1]; xp[2] = q[2];
@@ -1259,7 +1269,7 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   const real* xfrc = d->xfrc_applied + (size_t)wi * nb * 6;
   w->flags = 0;
 
-  kinematics(m, wi, w);
+  kinematics(m, d, wi, w);
   com_pos(m, wi, w);
   crb(m, wi, w);
   factor_tree(m, w->M, w->LD);

@@ -99,6 +99,33 @@ def go1_scene(num_envs: int) -> Scene:
   return Scene(cfg, "cpu")
 
 
+MOCAP_BALL_XML = (
+  '<mujoco><worldbody><body name="ball" mocap="true" pos="0.3 0 0.8">'
+  '<geom name="ball_geom" type="sphere" size="0.12"/></body></worldbody></mujoco>'
+)
+
+
+def g1_mocap_scene(num_envs: int) -> Scene:
+  """G1 plus a mocap entity (a sphere moved by mocap_pos/mocap_quat) that can
+  collide with the robot (entity.py:101-104, data.py:178-187)."""
+  from mjlab_amd.entity.entity import EntityCfg
+  from mjlab_amd.spec.mjcf import read_mjcf_string
+
+  ball = EntityCfg(spec_fn=lambda: read_mjcf_string(MOCAP_BALL_XML))
+  cfg = SceneCfg(num_envs=num_envs, terrain=TerrainImporterCfg(), entities={"robot": get_g1_robot_cfg(), "ball": ball})
+  return Scene(cfg, "cpu")
+
+
+def mocap_states(m, n: int, rng: np.random.Generator) -> dict:
+  """random_states plus mocap poses around the robot's torso (contacts with arms/torso)."""
+  st = random_states(m, n, rng)
+  pos = np.stack([rng.uniform(-0.35, 0.35, n), rng.uniform(-0.35, 0.35, n), rng.uniform(0.5, 1.1, n)], 1)
+  q = rng.normal(size=(n, 4)) * 3.0  # not normalised: the step normalises mocap quaternions
+  st["mocap_pos"] = np.concatenate([pos] * int(m.nmocap), 1)
+  st["mocap_quat"] = np.concatenate([q] * int(m.nmocap), 1)
+  return st
+
+
 def g1_scene_model(num_envs: int, nconmax: int = 50, njmax: int = 300):
   return g1_scene(num_envs).compile(nconmax, njmax)
 

@@ -7,7 +7,7 @@ import torch
 
 from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg
 from oracle.oracle import INPUTS, Oracle
-from tests.scenes import compare_step, g1_scene_model, g1_sensor_scene, go1_scene_model, random_states
+from tests.scenes import compare_step, g1_mocap_scene, g1_scene_model, g1_sensor_scene, go1_scene_model, mocap_states, random_states
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -280,3 +280,23 @@ def test_known_answers_on_gpu():
       assert a == pytest.approx(g * (np.sin(th) - mu * np.cos(th)), rel=0.05)
     else:
       assert abs(vx[-1]) < 5e-3 and abs(sim.data.qpos[0, 0].item()) < 5e-3
+
+
+@pytest.mark.parametrize("integrate", [True, False])
+def test_mocap_body_parity(integrate):
+  """A mocap sphere (pose from mocap_pos / unnormalised mocap_quat) moved into
+  the robot: kinematics, contacts and the solve against the oracle."""
+  n = 256
+  m = g1_mocap_scene(n).compile(50, 300)
+  st = mocap_states(m, n, np.random.default_rng(5))
+  sim = make_sim(m, n)
+  put(sim, st)
+  sim.step() if integrate else sim.forward()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=integrate)
+  assert_parity(got, ref, n, tag=f" mocap integrate={integrate}")
+  b = int(np.nonzero(m.body_mocapid >= 0)[0][0])
+  np.testing.assert_allclose(got["xpos"].reshape(n, -1, 3)[:, b], st["mocap_pos"][:, :3], atol=1e-6)
+  g = [i for i in range(m.ngeom) if m.geom_bodyid[i] == b][0]
+  hits = (got["contact_geom"].reshape(n, -1) == g).any(1).mean()
+  assert hits > 0.05, hits  # the ball touches the robot in a fair share of worlds
