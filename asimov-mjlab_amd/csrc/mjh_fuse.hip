@@ -775,6 +775,35 @@ __global__ void rew_exp_err_kernel(const float* __restrict__ a, long long aes, l
   out[e] = expf(-(s / (float)k) * inv_std2);
 }
 
+// env-step bookkeeping (manager_based_rl_env.py:111-152): every episode
+// length += 1 and the env-step counter += 1 (the device random stream's counter)
+__global__ void step_counters_kernel(mjh_i64* __restrict__ episode_length, mjh_i64* __restrict__ step, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) episode_length[e] += 1;
+  if (e == 0 && step) *step += 1;
+}
+
+// after the terminations: any_reset = any(reset); stats[0] += count(reset),
+// stats[1] += any_reset (the gated forward's decision and its counters); one workgroup
+__global__ __launch_bounds__(1024) void reset_stats_kernel(const unsigned char* __restrict__ reset,
+                                                          unsigned char* __restrict__ any_reset, mjh_i64* __restrict__ stats,
+                                                          long long n) {
+  __shared__ int part[16];
+  int c = 0;
+  for (long long e = threadIdx.x; e < n; e += 1024) c += reset[e] ? 1 : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long t = 0;
+    for (int w = 0; w < 16; w++) t += part[w];
+    any_reset[0] = t > 0 ? 1 : 0;
+    stats[0] += t;
+    stats[1] += t > 0 ? 1 : 0;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1037,6 +1066,18 @@ int mjh_rew_exp_err(const float* a, long long aes, long long ars, const int* ra,
   if (n <= 0 || k <= 0) return 0;
   hipLaunchKernelGGL(rew_exp_err_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, a, aes, ars, ra, b, bes, brs, rb,
                      k, d, quat, inv_std2, out, n);
+  return finish();
+}
+
+int mjh_step_counters(mjh_i64* episode_length, mjh_i64* step, long long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(step_counters_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, episode_length, step, n);
+  return finish();
+}
+
+int mjh_reset_stats(const unsigned char* reset, unsigned char* any_reset, mjh_i64* stats, long long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(reset_stats_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, reset, any_reset, stats, n);
   return finish();
 }
 

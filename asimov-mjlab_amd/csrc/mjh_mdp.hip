@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/mjh_abi.h"
+#include "mjh_rng.h"
 
 namespace {
 
@@ -209,7 +210,8 @@ __global__ void velocity_command_kernel(const float* lin_b, long long ls, const 
                                         float rel_heading, float rel_standing, float stiffness, int heading_command,
                                         float* cmd, float* heading_target, float* heading_error, bool* is_heading,
                                         bool* is_standing, float* time_left, long long* counter, float* err_xy,
-                                        float* err_yaw, long long n) {
+                                        float* err_yaw, unsigned long long seed, unsigned long long key,
+                                        const mjh_i64* ctr, long long n) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   float* c = cmd + 3 * e;
@@ -221,8 +223,14 @@ __global__ void velocity_command_kernel(const float* lin_b, long long ls, const 
   err_yaw[e] += fabsf(c[2] - av[2]) * inv_max_step;
   // countdown + resample
   float tl = time_left[e] - dt;
-  const float* ue = u + e * us;
+  float ud[8];
+  const float* ue = u ? u + e * us : ud;
   if (tl <= 0.f) {
+    if (!u) {  // draws e*8 + j of the env's device stream (mjh_rng.h)
+      const mjh::Rng rng(seed, key, ctr);
+#pragma unroll
+      for (int j = 0; j < 8; j++) ud[j] = rng.u01(8 * e + j);
+    }
     tl = ue[0] * (t_hi - t_lo) + t_lo;
 #pragma unroll
     for (int k = 0; k < 3; k++) c[k] = ue[1 + k] * (ranges[2 * k + 1] - ranges[2 * k]) + ranges[2 * k];
@@ -255,12 +263,13 @@ extern "C" int mjh_velocity_command(const float* lin_b, long long ls, const floa
                                     float inv_max_step, float t_lo, float t_hi, float rel_heading, float rel_standing,
                                     float stiffness, int heading_command, float* cmd, float* heading_target,
                                     float* heading_error, unsigned char* is_heading, unsigned char* is_standing,
-                                    float* time_left, long long* counter, float* err_xy, float* err_yaw, long long n,
+                                    float* time_left, long long* counter, float* err_xy, float* err_yaw,
+                                    unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n,
                                     void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(velocity_command_kernel, dim3(grid(n)), dim3(256), 0, (hipStream_t)stream, lin_b, ls, ang_b, as, root_q,
                      qs, u, us, ranges, dt, inv_max_step, t_lo, t_hi, rel_heading, rel_standing, stiffness, heading_command,
                      cmd, heading_target, heading_error, reinterpret_cast<bool*>(is_heading),
-                     reinterpret_cast<bool*>(is_standing), time_left, counter, err_xy, err_yaw, n);
+                     reinterpret_cast<bool*>(is_standing), time_left, counter, err_xy, err_yaw, seed, key, ctr, n);
   return finish();
 }

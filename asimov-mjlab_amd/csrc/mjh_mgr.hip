@@ -28,7 +28,7 @@ __global__ void obs_group_kernel(const ObsArgs a, const float* __restrict__ u, l
   if (t >= n * d.w) return;
   const long long e = t / d.w;
   const int j = (int)(t - e * d.w);
-  float v = d.x[e * d.xs + j * d.xcs];
+  float v = d.xd > 1 ? d.x[e * d.xs + (j / d.xd) * d.xcs + j % d.xd] : d.x[e * d.xs + j * d.xcs];
   if (d.op == MJH_OBS_SUB) v -= d.y[e * d.ys + j];
   else if (d.op == MJH_OBS_POSITIVE) v = v > 0.f ? 1.f : 0.f;
   else if (d.op == MJH_OBS_SIGNED_LOG1P) v = (v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f)) * log1pf(fabsf(v));

@@ -319,7 +319,7 @@ class ObsTermDesc(ctypes.Structure):
   _fields_ = [("x", ctypes.c_void_p), ("xs", ctypes.c_longlong), ("w", ctypes.c_int), ("off", ctypes.c_int),
               ("lo", ctypes.c_float), ("hi", ctypes.c_float), ("cmin", ctypes.c_float), ("cmax", ctypes.c_float),
               ("scale", ctypes.c_float), ("noise", ctypes.c_int), ("y", ctypes.c_void_p), ("ys", ctypes.c_longlong),
-              ("xcs", ctypes.c_longlong), ("op", ctypes.c_int), ("_pad", ctypes.c_int)]
+              ("xcs", ctypes.c_longlong), ("op", ctypes.c_int), ("xd", ctypes.c_int)]
 
 
 OBS_COPY, OBS_SUB, OBS_POSITIVE, OBS_SIGNED_LOG1P = 0, 1, 2, 3
@@ -328,7 +328,8 @@ OBS_COPY, OBS_SUB, OBS_POSITIVE, OBS_SIGNED_LOG1P = 0, 1, 2, 3
 class ObsSrc:
   """An observation term as an elementwise op on strided device inputs, which
   the group kernel evaluates while assembling the group (no per-term launch):
-  x (n, w) any strides; OBS_SUB subtracts y (n, w) (unit column stride)."""
+  x (n, w) any strides, or (n, k, d) rows of d contiguous floats (columns
+  flattened row-major); OBS_SUB subtracts y (n, w) (unit column stride)."""
 
   __slots__ = ("x", "op", "y")
 
@@ -337,7 +338,7 @@ class ObsSrc:
 
   def evaluate(self) -> torch.Tensor:
     """The torch formula of the op (reference for the fused evaluation)."""
-    x = self.x
+    x = self.x if self.x.dim() < 3 else self.x.reshape(self.x.shape[0], -1)
     if self.op == OBS_SUB:
       return x - self.y
     if self.op == OBS_POSITIVE:
@@ -370,13 +371,22 @@ def obs_group(xs: list, plan: list, u: torch.Tensor | None, out: torch.Tensor, r
   n = out.shape[0]
   descs = (ObsTermDesc * len(xs))()
   for i, (x, (_, off, w, noise, clip, scale)) in enumerate(zip(xs, plan)):
-    op, y = OBS_COPY, None
+    op, y, xd = OBS_COPY, None, 1
     if isinstance(x, ObsSrc):
       op, y, x = x.op, x.y, x.x
       if y is not None and not (y.is_cuda and y.dtype == torch.float32 and y.dim() == 2 and y.stride(1) == 1
                                 and y.shape == (n, w)):
         return False
-    r = _term_rows(x)
+      if x.dim() == 3:  # rows of d contiguous floats at a row stride
+        if not (x.is_cuda and x.dtype == torch.float32 and x.stride(2) == 1 and x.shape[1] * x.shape[2] == w):
+          return False
+        xd = x.shape[2]
+        x = x.as_strided((x.shape[0], x.shape[1]), (x.stride(0), x.stride(1)))
+        r = (x, w)
+      else:
+        r = _term_rows(x)
+    else:
+      r = _term_rows(x)
     if r is None or r[1] != w or r[0].shape[0] != n:
       return False
     x2 = r[0]
@@ -384,7 +394,7 @@ def obs_group(xs: list, plan: list, u: torch.Tensor | None, out: torch.Tensor, r
     lo, hi = noise if noise is not None else (0.0, 0.0)
     descs[i] = ObsTermDesc(x2.data_ptr(), x2.stride(0), w, off, float(lo), float(hi), cmin, cmax, float(scale),
                            int(noise is not None), y.data_ptr() if y is not None else None, y.stride(0) if y is not None else 0,
-                           x2.stride(1), op, 0)
+                           x2.stride(1), op, xd)
   seed, key, ctr = rng if rng is not None else (ctypes.c_ulonglong(0), ctypes.c_ulonglong(0), None)
   native.check(native.lib().mjh_obs_group(descs, len(xs), _ptr(u) if u is not None else None,
                                           u.stride(0) if u is not None else 0, _ptr(out), out.stride(0), n, seed, key, ctr,
@@ -756,3 +766,15 @@ def rew_exp_err(a: torch.Tensor, b: torch.Tensor, std: float, quat: bool = False
     _ptr(rows_b) if rows_b is not None else None, k, d, int(quat), 1.0 / (std * std), _ptr(out), n, _stream()),
     "mjh_rew_exp_err")
   return out
+
+
+def step_counters(episode_length: torch.Tensor, step: torch.Tensor) -> None:
+  """episode_length += 1; step += 1 (int64 device tensors) in one launch."""
+  native.check(native.lib().mjh_step_counters(_ptr(episode_length), _ptr(step), episode_length.shape[0], _stream()),
+               "mjh_step_counters")
+
+
+def reset_stats(reset: torch.Tensor, any_reset: torch.Tensor, stats: torch.Tensor) -> None:
+  """any_reset = any(reset); stats += [count, any] in one launch."""
+  native.check(native.lib().mjh_reset_stats(_ptr(reset), _ptr(any_reset), _ptr(stats), reset.shape[0], _stream()),
+               "mjh_reset_stats")

@@ -276,15 +276,25 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
       self.scene.write_data_to_sim()
       self.sim.step()
       self.scene.update(dt=self.physics_dt)
-    self.episode_length_buf += 1
-    self._env_step_t += 1
+    if self.episode_length_buf.is_cuda:
+      from mjlab_amd import envops
+
+      envops.step_counters(self.episode_length_buf, self._env_step_t)
+    else:
+      self.episode_length_buf += 1
+      self._env_step_t += 1
     self.termination_manager.compute()  # -> reset_buf / reset_terminated / reset_time_outs
     self.reward_manager.compute(dt=self.step_dt)  # -> reward_buf
     self._reset_idx(self.reset_buf)
     self.scene.write_data_to_sim()
-    torch.any(self.reset_buf, dim=0, keepdim=True, out=self._any_reset)
-    self._stats[0] += self.reset_buf.sum()
-    self._stats[1:] += self._any_reset
+    if self.reset_buf.is_cuda:
+      from mjlab_amd import envops
+
+      envops.reset_stats(self.reset_buf, self._any_reset, self._stats)
+    else:
+      torch.any(self.reset_buf, dim=0, keepdim=True, out=self._any_reset)
+      self._stats[0] += self.reset_buf.sum()
+      self._stats[1:] += self._any_reset
     self.sim.forward_gated(self._any_reset)
     # capacity / NaN statistics of this env step's physics passes (device
     # counters, no sync): worlds that dropped contacts or constraint rows

@@ -85,6 +85,8 @@ EXPORTS = (
   "mjh_motion_frame",
   "mjh_motion_reset",
   "mjh_rew_exp_err",
+  "mjh_step_counters",
+  "mjh_reset_stats",
 )
 
 
@@ -140,7 +142,7 @@ def lib() -> ctypes.CDLL:
   L.mjh_rew_pos_limits.argtypes = [vp, ll, vp, ll, ci, vp, ll, vp]
   L.mjh_rew_posture.argtypes = [vp, ll, vp, ll, vp, vp, vp, vp, ll, cf, cf, ci, vp, ll, vp]
   L.mjh_velocity_command.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, cf, cf, cf, cf, cf, cf, cf, ci, vp, vp, vp, vp, vp,
-                                     vp, vp, vp, vp, ll, vp]
+                                     vp, vp, vp, vp, ctypes.c_ulonglong, ctypes.c_ulonglong, vp, ll, vp]
   L.mjh_rew_feet.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, cf, cf, cf, ci, vp, vp, vp, vp, ll, vp]
   L.mjh_quat_from_euler.argtypes = [vp, ll, vp, ll, vp]
   L.mjh_quat_error.argtypes = [vp, ll, vp, ll, vp, ll, vp]
@@ -173,6 +175,8 @@ def lib() -> ctypes.CDLL:
   L.mjh_root_frame.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp, ll, vp]
   L.mjh_order_worlds.argtypes = [vp, vp, vp, ll, vp]
   L.mjh_motion_adaptive.argtypes = [vp, vp, vp, vp, vp, vp, ci, ci, ll, cf, vp, vp, vp, u64, u64, vp, ll, vp]
+  L.mjh_step_counters.argtypes = [vp, vp, ll, vp]
+  L.mjh_reset_stats.argtypes = [vp, vp, vp, ll, vp]
   L.mjh_rew_exp_err.argtypes = [vp, ll, ll, vp, vp, ll, ll, vp, ci, ci, ci, cf, vp, ll, vp]
   L.mjh_motion_frame.argtypes = [vp, vp, vp, ci, ci, ci, vp, vp, ll, ll, vp]
   L.mjh_motion_reset.argtypes = [vp, ll, ci, ci, ci, ci, ci, vp, ll, vp, vp, vp, vp, vp, ci, ci, cf, cf, vp, ll, vp, ll, ci, ci,

@@ -35,9 +35,9 @@ def _foot_contact_src(env, sensor_name: str):
 
 def _foot_contact_forces_src(env, sensor_name: str):
   f = env.scene[sensor_name].data.force
-  if f is None or f.dim() != 3 or f.stride(2) != 1 or f.stride(1) != 3:
+  if f is None or f.dim() != 3 or f.stride(2) != 1:
     return None
-  return envops.ObsSrc(f.flatten(start_dim=1), envops.OBS_SIGNED_LOG1P)
+  return envops.ObsSrc(f, envops.OBS_SIGNED_LOG1P)  # (n, slots, 3) read in place
 
 
 foot_contact.obs_src = _foot_contact_src

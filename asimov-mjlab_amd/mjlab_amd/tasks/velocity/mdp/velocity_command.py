@@ -59,12 +59,12 @@ class UniformVelocityCommand(CommandTerm):
     draw per step: [timer, lin_x, lin_y, ang_z, heading, heading-env,
     standing-env, init-velocity]. On the GPU the whole update is one fused
     kernel (csrc/mjh_mdp.hip); the torch path below is its reference."""
+    if self.cfg.init_velocity_prob == 0.0 and self._compute_fused(dt, None):
+      return  # draws from the env's device stream inside the kernel
     u = torch.rand(self.num_envs, 8, device=self.device)
-    if self.cfg.init_velocity_prob == 0.0 and self._compute_fused(dt, u):
-      return
     self._compute_torch(dt, u)
 
-  def _compute_fused(self, dt: float, u: torch.Tensor) -> bool:
+  def _compute_fused(self, dt: float, u: torch.Tensor | None) -> bool:
     if not self.vel_command_b.is_cuda:
       return False
     import ctypes
@@ -75,15 +75,20 @@ class UniformVelocityCommand(CommandTerm):
     lin, ang, q = d.root_link_lin_vel_b, d.root_link_ang_vel_b, d.root_link_quat_w
     if not all(t.dim() == 2 and t.stride(1) == 1 for t in (lin, ang, q)):
       return False
+    from mjlab_amd import envops
+
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     lo, hi = self.cfg.resampling_time_range
     max_step = self.cfg.resampling_time_range[1] / self._env.step_dt
+    seed, key, ctr = envops.rng_args(self._env, "velocity_command.compute") if u is None else (
+      ctypes.c_ulonglong(0), ctypes.c_ulonglong(0), None)
     native.check(native.lib().mjh_velocity_command(
-      P(lin), lin.stride(0), P(ang), ang.stride(0), P(q), q.stride(0), P(u), u.stride(0), P(self._ranges_t),
+      P(lin), lin.stride(0), P(ang), ang.stride(0), P(q), q.stride(0), P(u) if u is not None else None,
+      u.stride(0) if u is not None else 0, P(self._ranges_t),
       float(dt), 1.0 / max_step, float(lo), float(hi), float(self.cfg.rel_heading_envs), float(self.cfg.rel_standing_envs),
       float(self.cfg.heading_control_stiffness), int(self.cfg.heading_command), P(self.vel_command_b),
       P(self.heading_target), P(self.heading_error), P(self.is_heading_env), P(self.is_standing_env), P(self.time_left),
-      P(self.command_counter), P(self.metrics["error_vel_xy"]), P(self.metrics["error_vel_yaw"]), self.num_envs,
+      P(self.command_counter), P(self.metrics["error_vel_xy"]), P(self.metrics["error_vel_yaw"]), seed, key, ctr, self.num_envs,
       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "mjh_velocity_command")
     return True
 

@@ -207,14 +207,16 @@ int mjh_rew_feet(const float* z, long long zs, const float* vel, long long vs, c
                  float* slip, float* slip_vsum, float* slip_cnt, long long n, void* stream);
 
 /* UniformVelocityCommand.compute for all envs (velocity_command.py:65-101):
- * metrics, timers, masked resampling from u (N, 8) uniform draws, heading
- * control, standing override. Boolean buffers are torch.bool (1 byte). */
+ * metrics, timers, masked resampling from u (N, 8) uniform draws (u NULL:
+ * draws e*8 + j of the (seed, key, *ctr) device stream), heading control,
+ * standing override. Boolean buffers are torch.bool (1 byte). */
 int mjh_velocity_command(const float* lin_b, long long ls, const float* ang_b, long long as, const float* root_q,
                          long long qs, const float* u, long long us, const float* ranges, float dt, float inv_max_step,
                          float t_lo, float t_hi, float rel_heading, float rel_standing, float stiffness,
                          int heading_command, float* cmd, float* heading_target, float* heading_error,
                          unsigned char* is_heading, unsigned char* is_standing, float* time_left, long long* counter,
-                         float* err_xy, float* err_yaw, long long n, void* stream);
+                         float* err_xy, float* err_yaw, unsigned long long seed, unsigned long long key,
+                         const mjh_i64* ctr, long long n, void* stream);
 
 /* ---- rotations for resets and motion tracking (mjh_envops.hip) ----
  * Formulas of isaaclab/utils/math.py as restated in mjlab_amd/utils/math.py. */
@@ -256,14 +258,15 @@ typedef struct mjh_obs_term_desc {
   int off;
   float lo, hi, cmin, cmax, scale;
   int noise;
-  /* the term's value from a strided input: x[e * xs + j * xcs], then op:
+  /* the term's value from a strided input: x[e * xs + j * xcs] (xd > 1: rows
+     of xd contiguous floats, x[e * xs + (j / xd) * xcs + j % xd]), then op:
      MJH_OBS_COPY, MJH_OBS_SUB (minus y[e * ys + j]), MJH_OBS_POSITIVE (x > 0 as
      0/1), MJH_OBS_SIGNED_LOG1P (sign(x) * log1p(|x|)) */
   const float* y;
   long long ys;
   long long xcs;
   int op;
-  int _pad;
+  int xd;
 } mjh_obs_term_desc;
 
 #define MJH_OBS_COPY 0
@@ -457,6 +460,14 @@ int mjh_motion_reset(const float* frame, long long fs, int nj, int pos_off, int 
 int mjh_rew_exp_err(const float* a, long long aes, long long ars, const int* ra, const float* b, long long bes,
                     long long brs, const int* rb, int k, int d, int quat, float inv_std2, float* out, long long n,
                     void* stream);
+
+/* Env-step bookkeeping (manager_based_rl_env.py:111-152): episode_length[e] +=
+ * 1 for all n envs and *step += 1 (step may be NULL). */
+int mjh_step_counters(mjh_i64* episode_length, mjh_i64* step, long long n, void* stream);
+
+/* any_reset[0] = any(reset); stats[0] += count(reset); stats[1] += any_reset
+ * (the gated forward's decision and the env's device counters). One workgroup. */
+int mjh_reset_stats(const unsigned char* reset, unsigned char* any_reset, mjh_i64* stats, long long n, void* stream);
 
 /* EventManager reset bookkeeping (event_manager.py:146-156): last[e] = *step,
  * once[e] = 1 for the masked envs. */

@@ -224,6 +224,24 @@ def test_term_combine_matches_manager_formula():
   assert all(torch.equal(d, v) for d, v in zip(dones, vals))
 
 
+@pytest.mark.parametrize("n", [1, 1000, 5000])
+def test_step_counters_and_reset_stats(n):
+  g = torch.Generator(device=DEV).manual_seed(8)
+  ep = torch.randint(0, 900, (n,), dtype=torch.long, device=DEV, generator=g)
+  r_ep = ep + 1
+  step = _ctr(41)
+  envops.step_counters(ep, step)
+  assert torch.equal(ep, r_ep) and int(step) == 42
+  for p in (0.0, 0.01, 1.0):
+    reset = torch.rand(n, device=DEV, generator=g) < p
+    anyr = torch.ones(1, dtype=torch.bool, device=DEV)
+    stats = torch.tensor([5, 3], dtype=torch.long, device=DEV)
+    envops.reset_stats(reset, anyr, stats)
+    c = int(reset.sum())
+    assert bool(anyr) == (c > 0)
+    assert stats.tolist() == [5 + c, 3 + (1 if c > 0 else 0)]
+
+
 def test_env_reset_path_uses_fused_kernels():
   """A captured velocity-task env step runs the fused reset path (C-ABI tally)
   and keeps its invariants: reset envs restart at step 0 with fresh commands."""
@@ -484,3 +502,20 @@ def test_rew_exp_err_matches_tracking_formula(quat):
   x, y = a[:, ra.long()], b[:, rb.long()]
   err = M.quat_error_magnitude(x, y) ** 2 if quat else torch.sum(torch.square(x - y), dim=-1)
   torch.testing.assert_close(out, torch.exp(-err.mean(-1) / 0.09), rtol=2e-5, atol=1e-6)
+
+
+
+def test_obs_src_rows_of_slot_records():
+  """(n, k, 3) force slots at a row stride of 4 (sensordata records) flattened in-kernel."""
+  from mjlab_amd.managers.manager_term_config import ObservationTermCfg
+
+  n, k = 2048, 2
+  g = torch.Generator(device=DEV).manual_seed(80)
+  sd = torch.randn(n, 4 * k + 1, device=DEV, generator=g) * 50
+  f = sd.as_strided((n, k, 3), (sd.stride(0), 4, 1), sd.storage_offset() + 1)
+  src = envops.ObsSrc(f, envops.OBS_SIGNED_LOG1P)
+  tc = ObservationTermCfg(func=lambda env: None)
+  out = torch.empty(n, 3 * k, device=DEV)
+  assert envops.obs_group([src], [(tc, 0, 3 * k, None, None, 1.0)], None, out)
+  ff = f.reshape(n, -1)
+  torch.testing.assert_close(out, torch.sign(ff) * torch.log1p(torch.abs(ff)), rtol=1e-6, atol=1e-6)
