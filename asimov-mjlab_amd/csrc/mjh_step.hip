@@ -165,6 +165,10 @@ struct ImgOff {
 __device__ __forceinline__ float rl(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
+__device__ __forceinline__ unsigned long long rl64(unsigned long long v, int k) {
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)v, k), hi = __builtin_amdgcn_readlane((int)(unsigned)(v >> 32), k);
+  return ((unsigned long long)hi << 32) | lo;
+}
 // lane src's value (src per lane): ds_bpermute; call with every lane active
 __device__ __forceinline__ float shfl(float v, int src) { return __shfl(v, src, 64); }
 
@@ -406,24 +410,38 @@ __device__ void ldl_solve_fast(const float* A, int n, int ld, float* x) {
 
 // H (lower triangle of Hout) = M + sum_k ash[k]^2 J[arow[k]] J[arow[k]]^T over the
 // nact compacted active rows, on the f32 matrix cores (v_mfma_f32_16x16x4_f32:
-// exact fp32 FMA chains). Tiles of 16x16 on the lower block triangle.
-template <int NT>
+// exact fp32 FMA chains). Tiles of 16x16 on the lower block triangle; at most
+// NB = NVP/16 (rounded up) tile rows. The accumulators start from M's lower
+// triangle (its loads overlap the first J loads instead of trailing the loop).
+template <int NT, int NVP>
 __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const float* J, int ldj, const int* arow, const float* ash,
                              int nact, int n, float* Hout) {
   typedef float v4f __attribute__((ext_vector_type(4)));
+  constexpr int NB = (NVP + 15) / 16;
+  constexpr int NTILE = NB * (NB + 1) / 2;
   const int lane = threadIdx.x & 63;
-  const int nb = (n + 15) >> 4;  // <= 4 (n <= 63)
+  const int nb = (n + 15) >> 4;  // <= NB
   const int ci = lane & 15, kq = lane >> 4;
-  v4f acc[10];
+  v4f acc[NTILE];
+  {
+    int t = 0;
 #pragma unroll
-  for (int t = 0; t < 10; t++) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int I = 0; I < NB; I++)
+#pragma unroll
+      for (int Jb = 0; Jb <= I; Jb++, t++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int i = I * 16 + kq * 4 + q, j = Jb * 16 + ci;
+          acc[t][q] = (i < n && j <= i) ? M[i * ldm + j] : 0.f;
+        }
+  }
   // software pipeline: the next k-step's J values are loaded (J may live in
   // L2) while this step's MFMAs run
-  auto load = [&](int k, float (&v)[4]) {
+  auto load = [&](int k, float (&v)[NB]) {
     const int r = k < nact ? arow[k] : 0;
     const float sc = k < nact ? ash[k] : 0.f;
 #pragma unroll
-    for (int b = 0; b < 4; b++) {
+    for (int b = 0; b < NB; b++) {
       const int c = b * 16 + ci;
       v[b] = (b < nb && c < n) ? J[r * ldj + c] * sc : 0.f;
     }
@@ -431,7 +449,7 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
   // PF k-steps of J loads in flight (a ring unrolled by PF so every register
   // index is static); same k order as a plain loop, so the sums are unchanged
   constexpr int PF = 4;
-  float v[PF][4];
+  float v[PF][NB];
 #pragma unroll
   for (int s = 0; s < PF; s++) load(4 * s + kq, v[s]);
   for (int k0 = 0; k0 < nact; k0 += 4 * PF) {
@@ -440,7 +458,7 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
       if (k0 + 4 * s < nact) {
         int t = 0;
 #pragma unroll
-        for (int I = 0; I < 4; I++)
+        for (int I = 0; I < NB; I++)
 #pragma unroll
           for (int Jb = 0; Jb <= I; Jb++, t++)
             if (I < nb) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[s][I], v[s][Jb], acc[t], 0, 0, 0);
@@ -450,14 +468,14 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
   }
   int t = 0;
 #pragma unroll
-  for (int I = 0; I < 4; I++)
+  for (int I = 0; I < NB; I++)
 #pragma unroll
     for (int Jb = 0; Jb <= I; Jb++, t++) {
       if (I >= nb) continue;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int i = I * 16 + kq * 4 + q, j = Jb * 16 + ci;
-        if (i < n && j <= i) Hout[i * ldm + j] = M[i * ldm + j] + acc[t][q];
+        if (i < n && j <= i) Hout[i * ldm + j] = acc[t][q];
       }
     }
 }
@@ -523,16 +541,15 @@ __device__ __forceinline__ void load_row_lower(const float* A, int n, int ld, fl
   }
 }
 
+// factor of the rows already in registers (lane i: row i, identity rows for
+// lanes >= n); the factored rows are stored to A
 template <int NVP>
-__device__ MJH_SOLVER_INLINE void ldl_factor_reg(float* A, int n, int ld) {
+__device__ __forceinline__ void ldl_factor_rows(float (&a)[NVP], float* A, int n, int ld) {
   // Branch-free: lane i updates its whole row each step; entries right of the
   // diagonal are scratch never read back (only rdlane(a[k], j) with k < j, i.e.
   // lower-triangle values, crosses lanes), and rows >= n are identity rows, so
   // the padded steps k >= n are exact no-ops for rows < n.
   const int lane = threadIdx.x & 63;
-  float a[NVP];
-  wsync();
-  load_row_lower<NVP>(A, n, ld, a);
 #pragma unroll
   for (int k = 0; k < NVP; k++) {
     float piv = rdlane_f(a[k], k);
@@ -548,6 +565,14 @@ __device__ MJH_SOLVER_INLINE void ldl_factor_reg(float* A, int n, int ld) {
     for (int k = 0; k < NVP; k += 4) *reinterpret_cast<float4*>(r + k) = make_float4(a[k], a[k + 1], a[k + 2], a[k + 3]);
   }
   wsync();
+}
+
+template <int NVP>
+__device__ MJH_SOLVER_INLINE void ldl_factor_reg(float* A, int n, int ld) {
+  float a[NVP];
+  wsync();
+  load_row_lower<NVP>(A, n, ld, a);
+  ldl_factor_rows<NVP>(a, A, n, ld);
 }
 
 // (L D L^T) x = b with the factor from ldl_factor_reg; x in LDS (in place).
@@ -1089,17 +1114,21 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   PROF(1);
   const unsigned long long* tmk = reinterpret_cast<const unsigned long long*>(IMG_L(body_treemask));
   const unsigned long long* dmk = reinterpret_cast<const unsigned long long*>(IMG_L(body_dofmask));
+  // lane b holds body b's chain mask; the subtree loops read it by readlane
+  // (no LDS load per body on their dependency chain)
+  const unsigned long long r_tmk = bl ? tmk[tid] : 0ull;
   // subtree com: lane b sums the bodies k whose chain contains b (ascending k)
   float r_sc[3];
   {
     const float bm = bl ? body_mass[tid] : 0.f;
     float ms = 0.f, mp0 = 0.f, mp1 = 0.f, mp2 = 0.f;
     for (int k = 0; k < nb; k++) {
-      const float mk = rl(bm, k), x0 = rl(r_xipos[0], k), x1 = rl(r_xipos[1], k), x2 = rl(r_xipos[2], k);
-      if (tid == 0 || ((tmk[k] >> tid) & 1ull)) {
-        ms += mk;
-        mp0 += mk * x0; mp1 += mk * x1; mp2 += mk * x2;
-      }
+      // masked accumulation as a multiply by 0/1 (no select per term): adds
+      // exactly 0 for bodies outside the subtree
+      const float mk = (tid == 0 || ((rl64(r_tmk, k) >> tid) & 1ull)) ? rl(bm, k) : 0.f;
+      const float x0 = rl(r_xipos[0], k), x1 = rl(r_xipos[1], k), x2 = rl(r_xipos[2], k);
+      ms += mk;
+      mp0 += mk * x0; mp1 += mk * x1; mp2 += mk * x2;
     }
     if (ms < MJH_MINVAL) {
       r_sc[0] = r_xipos[0]; r_sc[1] = r_xipos[1]; r_sc[2] = r_xipos[2];
@@ -1177,19 +1206,21 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   }
   // crb (lane b) = sum of cinert over b's subtree, ascending k
   float r_crb[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // not unrolled: a fully unrolled body loop hoists every readlane and spills
+  // the scalar results into VGPR lanes
+#pragma nounroll
   for (int k = 1; k < nb; k++) {
-    const bool in = tid > 0 && ((tmk[k] >> tid) & 1ull);
+    const float in = (tid > 0 && ((rl64(r_tmk, k) >> tid) & 1ull)) ? 1.f : 0.f;
 #pragma unroll
-    for (int c = 0; c < 10; c++) {
-      const float x = rl(r_cin[c], k);
-      if (in) r_crb[c] += x;
-    }
+    for (int c = 0; c < 10; c++) r_crb[c] = fmaf(rl(r_cin[c], k), in, r_crb[c]);  // exact: x*1 + r, or r + 0
   }
   PROF(20);
-  for (int i = tid; i < nv * ldm; i += NT) { Mm[i] = 0.f; Lm[i] = 0.f; }
-  wsync();
   {
-    // lane i: row/column i of M over the dofs j <= i of i's ancestor chain
+    // lane i builds row i of M in registers: the entries j <= i over i's
+    // ancestor chain (cdof_j . crb_b(i) cdof_i), then the entries j > i from the
+    // rows the other lanes stored (M is symmetric). Whole-row stores only (no
+    // zero fill, no column scatter), and the factorisation starts from the
+    // registers. Rows of lanes >= nv are inert identity rows (never stored).
     const int bi = tid < nv ? IMG_I(dof_bodyid)[tid] : 0;
     float cb[10], buf[6];
 #pragma unroll
@@ -1197,23 +1228,37 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     inert_vec(buf, cb, r_cdof);
     unsigned long long mask = tid < nv ? dmk[bi] : 0ull;
     mask &= (tid == 63) ? ~0ull : ((2ull << tid) - 1ull);
-    for (int j = 0; j < nv; j++) {
+    const float arm = tid < nv ? dof_armature[tid] : 0.f;
+    float a[NVP];
+#pragma unroll
+    for (int j = 0; j < NVP; j++) {
       float cj[6];
 #pragma unroll
       for (int c = 0; c < 6; c++) cj[c] = rl(r_cdof[c], j);
-      if ((mask >> j) & 1ull) {
-        float v = cj[0] * buf[0] + cj[1] * buf[1] + cj[2] * buf[2] + cj[3] * buf[3] + cj[4] * buf[4] + cj[5] * buf[5];
-        if (j == tid) v += dof_armature[tid];
-        Mm[tid * ldm + j] = v;
-        Mm[j * ldm + tid] = v;  // full symmetric storage: contiguous row reads in M*v
-        Lm[tid * ldm + j] = v;
-        Lm[j * ldm + tid] = v;
-      }
+      float v = cj[0] * buf[0] + cj[1] * buf[1] + cj[2] * buf[2] + cj[3] * buf[3] + cj[4] * buf[4] + cj[5] * buf[5];
+      if (j == tid) v += arm;
+      a[j] = ((mask >> j) & 1ull) ? v : 0.f;
     }
+    if (tid < nv) {
+      float* r = Lm + tid * ldm;
+#pragma unroll
+      for (int k = 0; k < NVP; k += 4) *reinterpret_cast<float4*>(r + k) = make_float4(a[k], a[k + 1], a[k + 2], a[k + 3]);
+    }
+    wsync();
+    if (tid < nv) {
+#pragma unroll
+      for (int j = 1; j < NVP; j++)
+        if (j > tid && j < nv) a[j] = Lm[j * ldm + tid];
+      float* r = Mm + tid * ldm;
+#pragma unroll
+      for (int k = 0; k < NVP; k += 4) *reinterpret_cast<float4*>(r + k) = make_float4(a[k], a[k + 1], a[k + 2], a[k + 3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NVP; j++) a[j] = j == tid ? 1.f : 0.f;
+    }
+    PROF(10);
+    ldl_factor_rows<NVP>(a, Lm, nv, ldm);
   }
-  wsync();
-  PROF(10);
-  ldl_factor_reg<NVP>(Lm, nv, ldm);
   PROF(2);
 
   // ---------------------------------------------------------------- com_vel / rne (bias)
@@ -1221,13 +1266,9 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   const unsigned long long r_dm = bl ? dmk[tid] : 0ull;
   float r_cvel[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j = 0; j < nv; j++) {
-    const float q = rl(r_qv, j);
-    const bool in = (r_dm >> j) & 1ull;
+    const float q = ((r_dm >> j) & 1ull) ? rl(r_qv, j) : 0.f;  // 0 outside the chain: adds exactly 0
 #pragma unroll
-    for (int c = 0; c < 6; c++) {
-      const float x = rl(r_cdof[c], j);
-      if (in) r_cvel[c] += x * q;
-    }
+    for (int c = 0; c < 6; c++) r_cvel[c] += rl(r_cdof[c], j) * q;
   }
   if (bl) {
 #pragma unroll
@@ -1244,16 +1285,18 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     float v[6];
 #pragma unroll
     for (int c = 0; c < 6; c++) v[c] = shfl(r_cvel[c], p);
-    // earlier dofs of this body: other joints fully, own free joint translations only
-    for (int k = 0; k < nv; k++) {
-      const float q = rl(r_qv, k);
+    // earlier dofs of this body: other joints fully, own free joint translations
+    // only. Only bodies with several dofs have any, so the loop ends at the
+    // wave's largest such dof (G1/Go1: the free joint's, k < 5)
+    int kend = (tid < nv && d0 < i) ? i : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) kend = max(kend, __shfl_xor(kend, o, 64));
+    for (int k = 0; k < kend; k++) {
       const int jk = IMG_I(dof_jntid)[k];
       const bool use = k >= d0 && k < i && !(jk == jnt && !(freej && k - da < 3));
+      const float q = use ? rl(r_qv, k) : 0.f;  // adds exactly 0 when unused
 #pragma unroll
-      for (int c = 0; c < 6; c++) {
-        const float x = rl(r_cdof[c], k);
-        if (use) v[c] += x * q;
-      }
+      for (int c = 0; c < 6; c++) v[c] += rl(r_cdof[c], k) * q;
     }
     if (tid < nv && !(freej && i - da < 3)) cross_motion(r_cdd, v, r_cdof);
     if (tid < nv) {
@@ -1268,13 +1311,9 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     const float g0 = -m.gravity_x, g1 = -m.gravity_y, g2 = -m.gravity_z;
     float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
     for (int j = 0; j < nv; j++) {
-      const float q = rl(r_qv, j);
-      const bool in = (r_dm >> j) & 1ull;
+      const float q = ((r_dm >> j) & 1ull) ? rl(r_qv, j) : 0.f;
 #pragma unroll
-      for (int c = 0; c < 6; c++) {
-        const float x = rl(r_cdd[c], j);
-        if (in) a[c] += x * q;
-      }
+      for (int c = 0; c < 6; c++) a[c] += rl(r_cdd[c], j) * q;
     }
     float f1[6], f2[6], f3[6];
     inert_vec(f1, r_cin, a);
@@ -1286,13 +1325,11 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   PROF(23);
   // subtree sums of cfrc (lane b), ascending k
   float r_bf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma nounroll
   for (int k = 1; k < nb; k++) {
-    const bool in = tid > 0 && ((tmk[k] >> tid) & 1ull);
+    const float in = (tid > 0 && ((rl64(r_tmk, k) >> tid) & 1ull)) ? 1.f : 0.f;
 #pragma unroll
-    for (int c = 0; c < 6; c++) {
-      const float x = rl(r_cfrc[c], k);
-      if (in) r_bf[c] += x;
-    }
+    for (int c = 0; c < 6; c++) r_bf[c] = fmaf(rl(r_cfrc[c], k), in, r_bf[c]);
   }
   if (bl) {
 #pragma unroll
@@ -1720,7 +1757,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
             Lm[i * ldm + j] = hs;
           }
 #else
-        hessian_mfma<NT>(Mm, ldm, J, ldj, arow, ash, nact, nv, Lm);
+        hessian_mfma<NT, NVP>(Mm, ldm, J, ldj, arow, ash, nact, nv, Lm);
 #endif
         PROF_ACC(15, th);
         unsigned long long tf = PROF_NOW();
@@ -1848,12 +1885,12 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     const unsigned long long dm = bl ? dmk[tid] : 0ull;
     float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
     for (int j = 0; j < nv; j++) {
-      const float qv = rl(qv_l, j), qa = rl(qa_l, j);
       const bool in = (dm >> j) & 1ull;
+      const float qv = in ? rl(qv_l, j) : 0.f, qa = in ? rl(qa_l, j) : 0.f;
 #pragma unroll
       for (int c = 0; c < 6; c++) {
         const float x = rl(cdd[c], j), y = rl(cd[c], j);
-        if (in) a[c] += x * qv + y * qa;
+        a[c] += x * qv + y * qa;
       }
     }
     if (bl) {

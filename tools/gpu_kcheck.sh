@@ -7,7 +7,7 @@ TAG=${1:-kc}
 cd "${GRAFT_REPO_ROOT:-.}"
 O=gpurun_out/$TAG
 mkdir -p $O
-bash tools/gpu_kb.sh $TAG
+bash tools/gpu_kb.sh $TAG "${@:2}"
 if [ -f asimov-mjlab_amd/mjlab_amd/libmjh_prof.so ]; then
   timeout -k 10 120 python tools/phase_profile.py 4096 > $O/phase.log 2>&1 || { tail -20 $O/phase.log; exit 1; }
   cat $O/phase.log
