@@ -408,6 +408,9 @@ __device__ void ldl_solve_fast(const float* A, int n, int ld, float* x) {
   }
 }
 
+#ifndef MJH_HESS_PF
+#define MJH_HESS_PF 4  // k-steps of J loads in flight in the Hessian
+#endif
 // H (lower triangle of Hout) = M + sum_k ash[k]^2 J[arow[k]] J[arow[k]]^T over the
 // nact compacted active rows, on the f32 matrix cores (v_mfma_f32_16x16x4_f32:
 // exact fp32 FMA chains). Tiles of 16x16 on the lower block triangle; at most
@@ -448,7 +451,7 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
   };
   // PF k-steps of J loads in flight (a ring unrolled by PF so every register
   // index is static); same k order as a plain loop, so the sums are unchanged
-  constexpr int PF = 4;
+  constexpr int PF = MJH_HESS_PF;
   float v[PF][NB];
 #pragma unroll
   for (int s = 0; s < PF; s++) load(4 * s + kq, v[s]);
@@ -523,6 +526,9 @@ __device__ __forceinline__ float rowdot(const float* r, const float* x, int n) {
 }
 
 // ---- register-resident LDL^T (lane i owns row i; NVP = padded size) ---------
+#ifndef MJH_PK_FACTOR
+#define MJH_PK_FACTOR 1
+#endif
 // Right-looking LDL^T fully unrolled over compile-time column indices: the
 // entries of other rows come from v_readlane, so the factorisation never
 // touches LDS between columns. Rows >= n are inert identity rows.
@@ -550,13 +556,30 @@ __device__ __forceinline__ void ldl_factor_rows(float (&a)[NVP], float* A, int n
   // lower-triangle values, crosses lanes), and rows >= n are identity rows, so
   // the padded steps k >= n are exact no-ops for rows < n.
   const int lane = threadIdx.x & 63;
+  // the row update runs on pairs (v_pk_fma_f32: two entries per VALU issue);
+  // a pair that starts at k only writes scratch a[k] (overwritten below for
+  // rows >= k, right of the diagonal for rows < k)
+  typedef float v2f __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (int k = 0; k < NVP; k++) {
-    float piv = rdlane_f(a[k], k);
+    const float ak = a[k];
+    float piv = rdlane_f(ak, k);
     piv = piv < MJH_MINVAL ? MJH_MINVAL : piv;
-    const float lik = a[k] * (1.f / piv);
+    const float lik = ak * __builtin_amdgcn_rcpf(piv);  // v_rcp_f32 (1 ulp), not the IEEE division sequence
+#if MJH_PK_FACTOR
+    const v2f l2 = {lik, lik};
 #pragma unroll
-    for (int j = k + 1; j < NVP; j++) a[j] -= lik * rdlane_f(a[k], j);
+    for (int j = (k + 1) & ~1; j < NVP; j += 2) {
+      const v2f r = {rdlane_f(ak, j), rdlane_f(ak, j + 1)};
+      v2f x = {a[j], a[j + 1]};
+      x -= l2 * r;
+      a[j] = x.x;
+      a[j + 1] = x.y;
+    }
+#else
+#pragma unroll
+    for (int j = k + 1; j < NVP; j++) a[j] -= lik * rdlane_f(ak, j);
+#endif
     a[k] = lane > k ? lik : (lane == k ? piv : a[k]);
   }
   if (lane < n) {
@@ -955,8 +978,8 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   unsigned long long* efc_mask = reinterpret_cast<unsigned long long*>(SP(efc_mask));
   float* efc_h = SP(efc_h);
   int* arow = SPI(arow);
-  int* arow_prev = SPI(arow_prev);
   float* ash = SP(ash);
+  int* arow_prev = SPI(arow_prev);
   int* sidx = SPI(sidx);
   float* red = S + Lo.red;
   int* redi = SI + Lo.red + 2 * (NT / 64) + 2;
