@@ -505,6 +505,28 @@ __device__ __forceinline__ float rowdot_u(const float* r, const float* x, int n)
   return s0 + s1;
 }
 
+// two dots of one row (the row's loads shared): ox = r.x, oy = r.y
+template <int NVP>
+__device__ __forceinline__ void rowdot2_u(const float* r, const float* x, const float* y, int n, float& ox, float& oy) {
+  float s0 = 0.f, s1 = 0.f, t0 = 0.f, t1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < NVP; j += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(r + j);
+    float4 b = *reinterpret_cast<const float4*>(x + j);
+    float4 c = *reinterpret_cast<const float4*>(y + j);
+    if (j + 4 > n) {
+      b.x = j < n ? b.x : 0.f; b.y = j + 1 < n ? b.y : 0.f; b.z = j + 2 < n ? b.z : 0.f; b.w = j + 3 < n ? b.w : 0.f;
+      c.x = j < n ? c.x : 0.f; c.y = j + 1 < n ? c.y : 0.f; c.z = j + 2 < n ? c.z : 0.f; c.w = j + 3 < n ? c.w : 0.f;
+    }
+    s0 += a.x * b.x + a.y * b.y;
+    s1 += a.z * b.z + a.w * b.w;
+    t0 += a.x * c.x + a.y * c.y;
+    t1 += a.z * c.z + a.w * c.w;
+  }
+  ox = s0 + s1;
+  oy = t0 + t1;
+}
+
 // y = A x for the full symmetric (zero-padded) A, one row per lane
 template <int NT, int NVP>
 __device__ __forceinline__ void symv_u(const float* A, int n, int ld, const float* x, float* y) {
@@ -1696,14 +1718,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     }
     wsync();
   } else {
-    // jaref = J x - aref ; Ma = M x ; forces, qfrc_constraint, cost
-    auto eval_point = [&](const float* x) {
-      symv_u<NT, NVP>(Mm, nv, ldm, x, Ma);
-      for (int r = tid; r < nefc; r += NT) {
-        jaref[r] = rowdot_u<NVP>(J + r * ldj, x, nv) - efc_aref[r];
-      }
-      wsync();
-    };
+    // forces, qfrc_constraint and cost at the point whose jaref / Ma are set
     auto update_constraint = [&]() -> float {
       float c = 0.f;
       for (int r = tid; r < nefc; r += NT) {
@@ -1799,23 +1814,34 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
       wsync();
     };
 
-    // warm start: the cheaper of qacc_warmstart and qacc_smooth
+    // warm start: the cheaper of qacc_warmstart and qacc_smooth, both
+    // evaluated in one pass over M's and J's rows (each row loaded once; the
+    // qacc_smooth values wait in Mv / jv in case they win)
     for (int i = tid; i < nv; i += NT) qacc[i] = DP(qacc_warmstart)[W * nv + i];
     wsync();
-    eval_point(qacc);
+    for (int i = tid; i < nv; i += NT) rowdot2_u<NVP>(Mm + i * ldm, qacc, qacc_smooth, nv, Ma[i], Mv[i]);
+    for (int r = tid; r < nefc; r += NT) {
+      float a, b;
+      rowdot2_u<NVP>(J + r * ldj, qacc, qacc_smooth, nv, a, b);
+      jaref[r] = a - efc_aref[r];
+      jv[r] = b - efc_aref[r];
+    }
+    wsync();
     float cost = update_constraint();
     float cs = 0.f;
     for (int r = tid; r < nefc; r += NT) {
-      const float s = rowdot_u<NVP>(J + r * ldj, qacc_smooth, nv);
       float f, cr;
-      row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], s - efc_aref[r], &f, &cr);
+      row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], jv[r], &f, &cr);
       cs += cr;
     }
     const float cost_smooth = bsum<NT>(cs, red);
     if (cost > cost_smooth) {
-      for (int i = tid; i < nv; i += NT) qacc[i] = qacc_smooth[i];
+      for (int i = tid; i < nv; i += NT) {
+        qacc[i] = qacc_smooth[i];
+        Ma[i] = Mv[i];
+      }
+      for (int r = tid; r < nefc; r += NT) jaref[r] = jv[r];
       wsync();
-      eval_point(qacc);
       cost = update_constraint();
     }
     wsync();
