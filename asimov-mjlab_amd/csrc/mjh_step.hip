@@ -2202,56 +2202,117 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
 
   // ---------------------------------------------------------------- forward outputs
   PROF(7);
-  for (int i = tid; i < nb * 3; i += NT) {
-    DP(xpos)[W * nb * 3 + i] = xpos[i];
-    DP(xipos)[W * nb * 3 + i] = xipos[i];
-    DP(subtree_com)[W * nb * 3 + i] = subtree_com[i];
+  // Each lane loads everything it copies before its first store: the data
+  // arrays may alias the scratch as far as the compiler knows, and a load
+  // issued after a store waits for the store too (one memory latency per
+  // array otherwise). Lane = body / joint / site / dof / contact / row.
+  if (tid < nb) {
+    const int b = tid;
+    float v[43];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { v[k] = xpos[3 * b + k]; v[3 + k] = xipos[3 * b + k]; v[6 + k] = subtree_com[3 * b + k]; }
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[9 + k] = xquat[4 * b + k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) { v[13 + k] = xmat[9 * b + k]; v[22 + k] = ximat[9 * b + k]; }
+#pragma unroll
+    for (int k = 0; k < 6; k++) { v[31 + k] = cvel[6 * b + k]; v[37 + k] = cacc[6 * b + k]; }
+    const long long o = (long long)W * nb + b;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      DP(xpos)[3 * o + k] = v[k];
+      DP(xipos)[3 * o + k] = v[3 + k];
+      DP(subtree_com)[3 * o + k] = v[6 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) DP(xquat)[4 * o + k] = v[9 + k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      DP(xmat)[9 * o + k] = v[13 + k];
+      DP(ximat)[9 * o + k] = v[22 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      DP(cvel)[6 * o + k] = v[31 + k];
+      DP(cacc)[6 * o + k] = v[37 + k];
+    }
   }
-  for (int i = tid; i < nb * 4; i += NT) DP(xquat)[W * nb * 4 + i] = xquat[i];
-  for (int i = tid; i < nb * 9; i += NT) {
-    DP(xmat)[W * nb * 9 + i] = xmat[i];
-    DP(ximat)[W * nb * 9 + i] = ximat[i];
-  }
-  for (int i = tid; i < nb * 6; i += NT) {
-    DP(cvel)[W * nb * 6 + i] = cvel[i];
-    DP(cacc)[W * nb * 6 + i] = cacc[i];
-  }
-  for (int i = tid; i < nj * 3; i += NT) {
-    DP(xanchor)[W * nj * 3 + i] = xanchor[i];
-    DP(xaxis)[W * nj * 3 + i] = xaxis[i];
-  }
-  for (int i = tid; i < Z.nsite * 3; i += NT) DP(site_xpos)[W * Z.nsite * 3 + i] = sxpos[i];
-  for (int i = tid; i < Z.nsite * 9; i += NT) DP(site_xmat)[W * Z.nsite * 9 + i] = sxmat[i];
-  for (int i = tid; i < nv; i += NT) {
-    DP(qfrc_bias)[W * nv + i] = qfrc_bias[i];
-    DP(qfrc_passive)[W * nv + i] = qfrc_passive[i];
-    DP(qfrc_actuator)[W * nv + i] = qfrc_act[i];
-    DP(qfrc_smooth)[W * nv + i] = qfrc_smooth[i];
-    DP(qfrc_constraint)[W * nv + i] = qfrc_con[i];
-    DP(qacc_smooth)[W * nv + i] = qacc_smooth[i];
-    DP(qacc)[W * nv + i] = qacc[i];
-    DP(qacc_warmstart)[W * nv + i] = qacc[i];
+  {
+    float vj[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, vs[12], vd[8];
+    const bool jl = tid < nj, sl = tid < Z.nsite, dl = tid < nv;  // nj <= nv < 64
+    if (jl) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) { vj[k] = xanchor[3 * tid + k]; vj[3 + k] = xaxis[3 * tid + k]; }
+    }
+    if (sl) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) vs[k] = sxpos[3 * tid + k];
+#pragma unroll
+      for (int k = 0; k < 9; k++) vs[3 + k] = sxmat[9 * tid + k];
+    }
+    if (dl) {
+      vd[0] = qfrc_bias[tid]; vd[1] = qfrc_passive[tid]; vd[2] = qfrc_act[tid]; vd[3] = qfrc_smooth[tid];
+      vd[4] = qfrc_con[tid]; vd[5] = qacc_smooth[tid]; vd[6] = qacc[tid];
+    }
+    if (jl) {
+      const long long o = (long long)W * nj + tid;
+#pragma unroll
+      for (int k = 0; k < 3; k++) { DP(xanchor)[3 * o + k] = vj[k]; DP(xaxis)[3 * o + k] = vj[3 + k]; }
+    }
+    for (int st = tid; sl; st += NT) {  // sites beyond the first 64: one more round each
+      const long long o = (long long)W * Z.nsite + st;
+#pragma unroll
+      for (int k = 0; k < 3; k++) DP(site_xpos)[3 * o + k] = vs[k];
+#pragma unroll
+      for (int k = 0; k < 9; k++) DP(site_xmat)[9 * o + k] = vs[3 + k];
+      if (st + NT >= Z.nsite) break;
+#pragma unroll
+      for (int k = 0; k < 3; k++) vs[k] = sxpos[3 * (st + NT) + k];
+#pragma unroll
+      for (int k = 0; k < 9; k++) vs[3 + k] = sxmat[9 * (st + NT) + k];
+    }
+    if (dl) {
+      const long long o = (long long)W * nv + tid;
+      DP(qfrc_bias)[o] = vd[0]; DP(qfrc_passive)[o] = vd[1]; DP(qfrc_actuator)[o] = vd[2]; DP(qfrc_smooth)[o] = vd[3];
+      DP(qfrc_constraint)[o] = vd[4]; DP(qacc_smooth)[o] = vd[5]; DP(qacc)[o] = vd[6]; DP(qacc_warmstart)[o] = vd[6];
+    }
   }
   for (int ci = tid; ci < ncon; ci += NT) {
+    float c[22];
+    int ic[4];
+    c[0] = con_dist[ci];
+#pragma unroll
+    for (int k = 0; k < 3; k++) c[1 + k] = con_pos[3 * ci + k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) c[4 + k] = con_frame[9 * ci + k];
+#pragma unroll
+    for (int k = 0; k < 5; k++) c[13 + k] = con_fric[5 * ci + k];
+    c[18] = con_imargin[ci];
+    ic[0] = con_dim[ci]; ic[1] = con_geom[2 * ci]; ic[2] = con_geom[2 * ci + 1]; ic[3] = con_efcadr[ci];
     const long long o = W * Z.nconmax + ci;
-    DP(contact_dist)[o] = con_dist[ci];
-    for (int k = 0; k < 3; k++) DP(contact_pos)[3 * o + k] = con_pos[3 * ci + k];
-    for (int k = 0; k < 9; k++) DP(contact_frame)[9 * o + k] = con_frame[9 * ci + k];
-    for (int k = 0; k < 5; k++) DP(contact_friction)[5 * o + k] = con_fric[5 * ci + k];
-    DP(contact_includemargin)[o] = con_imargin[ci];
-    DP(contact_dim)[o] = con_dim[ci];
-    DP(contact_geom)[2 * o] = con_geom[2 * ci];
-    DP(contact_geom)[2 * o + 1] = con_geom[2 * ci + 1];
-    DP(contact_efc_address)[o] = con_efcadr[ci];
+    DP(contact_dist)[o] = c[0];
+#pragma unroll
+    for (int k = 0; k < 3; k++) DP(contact_pos)[3 * o + k] = c[1 + k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) DP(contact_frame)[9 * o + k] = c[4 + k];
+#pragma unroll
+    for (int k = 0; k < 5; k++) DP(contact_friction)[5 * o + k] = c[13 + k];
+    DP(contact_includemargin)[o] = c[18];
+    DP(contact_dim)[o] = ic[0];
+    DP(contact_geom)[2 * o] = ic[1];
+    DP(contact_geom)[2 * o + 1] = ic[2];
+    DP(contact_efc_address)[o] = ic[3];
   }
   for (int r = tid; r < nefc; r += NT) {
+    const int ty = efc_type[r], id = efc_id[r];
+    const float ps = efc_pos[r], dd = efc_D[r], ar = efc_aref[r], fo = efc_force[r];
     const long long o = W * Z.njmax + r;
-    DP(efc_type)[o] = efc_type[r];
-    DP(efc_id)[o] = efc_id[r];
-    DP(efc_pos)[o] = efc_pos[r];
-    DP(efc_D)[o] = efc_D[r];
-    DP(efc_aref)[o] = efc_aref[r];
-    DP(efc_force)[o] = efc_force[r];
+    DP(efc_type)[o] = ty;
+    DP(efc_id)[o] = id;
+    DP(efc_pos)[o] = ps;
+    DP(efc_D)[o] = dd;
+    DP(efc_aref)[o] = ar;
+    DP(efc_force)[o] = fo;
   }
   if (tid == 0) {
     DP(ncon)[W] = ncon;

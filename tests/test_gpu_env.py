@@ -76,3 +76,23 @@ def test_tracking_graph_rollout(tmp_path):
   delta_ori = M.yaw_quat(M.quat_mul(c.robot_anchor_quat_w[:, None].repeat(1, nb, 1), M.quat_inv(c.anchor_quat_w[:, None].repeat(1, nb, 1))))
   torch.testing.assert_close(c.body_pos_relative_w, delta_pos + M.quat_apply(delta_ori, c.body_pos_w - a_pos), rtol=1e-5, atol=1e-5)
   torch.testing.assert_close(c.body_quat_relative_w, M.quat_mul(delta_ori, c.body_quat_w), rtol=1e-5, atol=1e-5)
+
+
+def test_vecenv_obs_survive_the_next_graph_replay():
+  """RSL-RL stores a step's observations only after the NEXT env.step:
+  the wrapper must hand out tensors that the graph replay does not overwrite."""
+  from mjlab_amd.rl import RslRlVecEnvWrapper
+
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = 64
+  cfg.seed = 0
+  env = ManagerBasedRlEnv(cfg, device="cuda:0")
+  w = RslRlVecEnvWrapper(env, clip_actions=1.0)
+  w.get_observations()
+  g = torch.Generator(device="cuda:0").manual_seed(3)
+  o1, r1, _, _ = w.step(2 * torch.rand(64, 29, device="cuda:0", generator=g) - 1)
+  o1c, r1c = o1["policy"].clone(), r1.clone()
+  o2, r2, _, _ = w.step(2 * torch.rand(64, 29, device="cuda:0", generator=g) - 1)
+  assert env._graph is not None  # the second step replays the captured graph
+  assert torch.equal(o1["policy"], o1c) and torch.equal(r1, r1c)
+  assert not torch.equal(o2["policy"], o1c)
