@@ -1962,7 +1962,11 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
         const int otype = IMG_I(sensor_objtype)[s], rtype = IMG_I(sensor_reftype)[s], rid = IMG_I(sensor_refid)[s];
         const int dim = IMG_I(sensor_dim)[s];
         const int cap = min(m.contact_sensor_maxmatch, 64);
-        for (int k = tid; k < dim; k += NT) sd[adr + k] = 0.f;
+        // kept matches in the solver's (now dead) LDS row-index array when it is
+        // large enough (always for the benchmark models), else in global scratch.
+        // The record is zeroed where it is written (below), so no store precedes
+        // this sensor's scratch loads.
+        int* const sx = Lo.rcap + 4 >= 64 ? arow : sidx;
         auto om = [&](int ty, int oid, int g) -> bool {
           if (oid < 0) return true;
           const int gb = IMG_I(geom_bodyid)[g];
@@ -1982,16 +1986,19 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
           }
           int total;
           const int off = bscan<NT>(match, &total, redi);
-          if (match && cnt + off < cap) sidx[cnt + off] = flip ? ~ci : ci;
+          if (match && cnt + off < cap) sx[cnt + off] = flip ? ~ci : ci;
           cnt += total;
         }
         wsync();
         const int nm = min(cnt, cap);
-        if (nm == 0) continue;
+        if (nm == 0) {
+          for (int k = tid; k < dim; k += NT) sd[adr + k] = 0.f;
+          continue;
+        }
         // lane k < nm: match k. F = contact force/torque in the contact frame
         // (mj_contactForce for pyramidal cones), Fw/Tw = on the primary, world frame
         const bool own = tid < nm;
-        const int code = own ? sidx[tid] : 0;
+        const int code = own ? sx[tid] : 0;
         const int ci = code < 0 ? ~code : code;
         const float sgn = code < 0 ? 1.f : -1.f;
         float F[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, Fw[3] = {0.f, 0.f, 0.f}, Tw[3] = {0.f, 0.f, 0.f};
@@ -2072,6 +2079,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
           if (bits & 32) { o[q++] = sg * fr[0]; o[q++] = sg * fr[1]; o[q++] = sg * fr[2]; }
           if (bits & 64) { o[q++] = sg * fr[3]; o[q++] = sg * fr[4]; o[q++] = sg * fr[5]; }
         }
+        for (int k = nm * (dim / nslot) + tid; k < dim; k += NT) sd[adr + k] = 0.f;  // slots without a match
         wsync();
         continue;
       }
