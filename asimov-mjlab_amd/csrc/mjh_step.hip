@@ -1952,6 +1952,28 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   // ---------------------------------------------------------------- sensors
   {
     float* sd = DP(sensordata) + W * Z.nsensordata;
+    // contact tid's force (contact frame, mj_contactForce for pyramidal cones),
+    // frame, position, distance and geoms in registers, loaded once for all
+    // contact sensors when ncon <= 64 (then a sensor's kept matches fetch them
+    // by ds_bpermute instead of a dependent chain of scratch loads)
+    const bool creg = ncon <= 64;
+    bool cloaded = false;
+    float cF[6], cfr[9], cps[3], cds = 0.f;
+    int cg1 = 0, cg2 = 0;
+    auto contact_force = [&](int ci, float (&F)[6]) {
+#pragma unroll
+      for (int k = 0; k < 6; k++) F[k] = 0.f;
+      const int r0 = con_efcadr[ci];
+      if (r0 >= 0) {
+        const int cdm = con_dim[ci];
+        if (cdm == 1) {
+          F[0] = efc_force[r0];
+        } else {
+          for (int e = 0; e < 2 * (cdm - 1); e++) F[0] += efc_force[r0 + e];
+          for (int k = 1; k < cdm && k < 6; k++) F[k] = con_fric[5 * ci + k - 1] * (efc_force[r0 + 2 * k - 2] - efc_force[r0 + 2 * k - 1]);
+        }
+      }
+    };
     for (int s = 0; s < Z.nsensor; s++) {
       const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
       if (type == 40) {
@@ -1975,12 +1997,30 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
           if (ty == 2) return oid == 0 || (((unsigned long long)IMG_L(body_treemask)[gb] >> oid) & 1ull);
           return false;
         };
+        if (creg && !cloaded) {
+          cloaded = true;
+#pragma unroll
+          for (int k = 0; k < 6; k++) cF[k] = 0.f;
+#pragma unroll
+          for (int k = 0; k < 9; k++) cfr[k] = 0.f;
+          cps[0] = cps[1] = cps[2] = 0.f;
+          if (tid < ncon) {
+            cg1 = con_geom[2 * tid];
+            cg2 = con_geom[2 * tid + 1];
+#pragma unroll
+            for (int k = 0; k < 9; k++) cfr[k] = con_frame[9 * tid + k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) cps[k] = con_pos[3 * tid + k];
+            cds = con_dist[tid];
+            contact_force(tid, cF);
+          }
+        }
         int cnt = 0;
         for (int base = 0; base < ncon; base += NT) {
           const int ci = base + tid;
           int match = 0, flip = 0;
           if (ci < ncon) {
-            const int g1 = con_geom[2 * ci], g2 = con_geom[2 * ci + 1];
+            const int g1 = creg ? cg1 : con_geom[2 * ci], g2 = creg ? cg2 : con_geom[2 * ci + 1];
             if (om(otype, id, g1) && om(rtype, rid, g2)) match = 1;
             else if (om(otype, id, g2) && om(rtype, rid, g1)) { match = 1; flip = 1; }
           }
@@ -2002,25 +2042,34 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
         const int ci = code < 0 ? ~code : code;
         const float sgn = code < 0 ? 1.f : -1.f;
         float F[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, Fw[3] = {0.f, 0.f, 0.f}, Tw[3] = {0.f, 0.f, 0.f};
-        float cpos[3] = {0.f, 0.f, 0.f}, cdist = 0.f;
-        const float* fr = con_frame + 9 * ci;
+        float cpos[3] = {0.f, 0.f, 0.f}, cdist = 0.f, fr[9];
+        if (creg) {
+          const int src = own ? ci : 0;  // every lane takes part in the permutes
+#pragma unroll
+          for (int k = 0; k < 6; k++) F[k] = shfl(cF[k], src);
+#pragma unroll
+          for (int k = 0; k < 9; k++) fr[k] = shfl(cfr[k], src);
+#pragma unroll
+          for (int k = 0; k < 3; k++) cpos[k] = shfl(cps[k], src);
+          cdist = shfl(cds, src);
+        } else if (own) {
+          contact_force(ci, F);
+#pragma unroll
+          for (int k = 0; k < 9; k++) fr[k] = con_frame[9 * ci + k];
+#pragma unroll
+          for (int k = 0; k < 3; k++) cpos[k] = con_pos[3 * ci + k];
+          cdist = con_dist[ci];
+        }
         if (own) {
-          const int r0 = con_efcadr[ci];
-          if (r0 >= 0) {
-            const int cdm = con_dim[ci];
-            if (cdm == 1) {
-              F[0] = efc_force[r0];
-            } else {
-              for (int e = 0; e < 2 * (cdm - 1); e++) F[0] += efc_force[r0 + e];
-              for (int k = 1; k < cdm && k < 6; k++) F[k] = con_fric[5 * ci + k - 1] * (efc_force[r0 + 2 * k - 2] - efc_force[r0 + 2 * k - 1]);
-            }
-          }
           for (int a = 0; a < 3; a++) {
             Fw[a] = sgn * (F[0] * fr[a] + F[1] * fr[3 + a] + F[2] * fr[6 + a]);
             Tw[a] = sgn * (F[3] * fr[a] + F[4] * fr[3 + a] + F[5] * fr[6 + a]);
-            cpos[a] = con_pos[3 * ci + a];
           }
-          cdist = con_dist[ci];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 6; k++) F[k] = 0.f;
+          cpos[0] = cpos[1] = cpos[2] = 0.f;
+          cdist = 0.f;
         }
         const float found = (float)nm;
         if (reduce == 3) {
