@@ -1215,28 +1215,41 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   PROF(18);
   wsync();  // subtree_com visible to the per-joint lanes
   for (int j = tid; j < nj; j += NT) {
+    // every input is loaded before the first cdof store (a load behind a store
+    // waits for it)
     const int b = IMG_I(jnt_bodyid)[j], da = IMG_I(jnt_dofadr)[j];
     const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
     float off[3] = {c[0] - xanchor[3 * j], c[1] - xanchor[3 * j + 1], c[2] - xanchor[3 * j + 2]};
     const int t = IMG_I(jnt_type)[j];
     if (t == 0) {
+      float R[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) R[k] = xmat[9 * b + k];
+      float rows[6][6];
+#pragma unroll
       for (int k = 0; k < 3; k++) {
-        float* cd = cdof + 6 * (da + k);
-        cd[0] = cd[1] = cd[2] = cd[3] = cd[4] = cd[5] = 0.f;
-        cd[3 + k] = 1.f;
-        float* cr = cdof + 6 * (da + 3 + k);
-        float ax[3] = {xmat[9 * b + k], xmat[9 * b + 3 + k], xmat[9 * b + 6 + k]};
-        cr[0] = ax[0]; cr[1] = ax[1]; cr[2] = ax[2];
-        cross3(cr + 3, ax, off);
+#pragma unroll
+        for (int e = 0; e < 6; e++) rows[k][e] = e == 3 + k ? 1.f : 0.f;
+        const float ax[3] = {R[k], R[3 + k], R[6 + k]};
+        rows[3 + k][0] = ax[0]; rows[3 + k][1] = ax[1]; rows[3 + k][2] = ax[2];
+        cross3(&rows[3 + k][3], ax, off);
       }
-    } else if (t == 2) {
-      float* cd = cdof + 6 * da;
-      cd[0] = cd[1] = cd[2] = 0.f;
-      cd[3] = xaxis[3 * j]; cd[4] = xaxis[3 * j + 1]; cd[5] = xaxis[3 * j + 2];
+#pragma unroll
+      for (int k = 0; k < 6; k++)
+#pragma unroll
+        for (int e = 0; e < 6; e++) cdof[6 * (da + k) + e] = rows[k][e];
     } else {
+      const float ax[3] = {xaxis[3 * j], xaxis[3 * j + 1], xaxis[3 * j + 2]};
       float* cd = cdof + 6 * da;
-      cd[0] = xaxis[3 * j]; cd[1] = xaxis[3 * j + 1]; cd[2] = xaxis[3 * j + 2];
-      cross3(cd + 3, xaxis + 3 * j, off);
+      if (t == 2) {
+        cd[0] = cd[1] = cd[2] = 0.f;
+        cd[3] = ax[0]; cd[4] = ax[1]; cd[5] = ax[2];
+      } else {
+        float cr[3];
+        cross3(cr, ax, off);
+        cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+        cd[3] = cr[0]; cd[4] = cr[1]; cd[5] = cr[2];
+      }
     }
   }
   wsync();
@@ -1623,47 +1636,99 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
       nefc = max(nsimple, min(rcap, ints[I_MISC]));
     }
     wsync();
-    // zero J rows, write the single-dof rows
-    for (int i = tid; i < nefc * ldj; i += NT) J[i] = 0.f;
-    wsync();
-    for (int r = tid; r < nsimple; r += NT) {
-      const int t = efc_type[r];
-      if (t == MJH_CNSTR_FRICTION_DOF) J[r * ldj + efc_id[r]] = 1.f;
-      else J[r * ldj + IMG_I(jnt_dofadr)[efc_id[r]]] = jv[r];
-    }
-    // contact Jacobian rows: flat over (contact, dof)
-    for (int item = tid; item < ncon * nv; item += NT) {
-      const int ci = item / nv, dof = item - ci * nv;
-      const int r0 = con_efcadr[ci];
-      if (r0 < 0) continue;
-      const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
-      const bool in1 = ((unsigned long long)IMG_L(body_dofmask)[b1] >> dof) & 1ull;
-      const bool in2 = ((unsigned long long)IMG_L(body_dofmask)[b2] >> dof) & 1ull;
-      const int dim = con_dim[ci];
-      const int nr = dim == 1 ? 1 : 2 * (dim - 1);
-      if (in1 == in2) {  // not in either chain, or in both (relative motion cancels)
-        continue;
+    // J rows with lane = column: every entry of every row is stored (zeros
+    // included, so no zero fill) as coalesced row stores, and all of a round's
+    // inputs are loaded before its first store (a load behind a store waits for
+    // it). Single-dof rows first, their (type, column, value) one per lane.
+    for (int base = 0; base < nsimple; base += NT) {
+      int col = -1;
+      float val = 0.f;
+      if (base + tid < nsimple) {
+        const int r = base + tid, t = efc_type[r];
+        col = t == MJH_CNSTR_FRICTION_DOF ? efc_id[r] : IMG_I(jnt_dofadr)[efc_id[r]];
+        val = t == MJH_CNSTR_FRICTION_DOF ? 1.f : jv[r];
       }
-      const float sg = in2 ? 1.f : -1.f;
-      const int bb = in2 ? b2 : b1;
-      const float* cd = cdof + 6 * dof;
-      const float* c = subtree_com + 3 * IMG_I(body_rootid)[bb];
-      const float* cp = con_pos + 3 * ci;
-      float off[3] = {cp[0] - c[0], cp[1] - c[1], cp[2] - c[2]}, t[3];
-      cross3(t, cd, off);
-      float jp[3] = {sg * (cd[3] + t[0]), sg * (cd[4] + t[1]), sg * (cd[5] + t[2])};
-      float jr[3] = {sg * cd[0], sg * cd[1], sg * cd[2]};
-      const float* fr = con_frame + 9 * ci;
-      float jf[6];
-      jf[0] = dot3(fr, jp); jf[1] = dot3(fr + 3, jp); jf[2] = dot3(fr + 6, jp);
-      jf[3] = dot3(fr, jr); jf[4] = dot3(fr + 3, jr); jf[5] = dot3(fr + 6, jr);
-      if (dim == 1) {
-        J[r0 * ldj + dof] = jf[0];
-      } else {
-        for (int e = 0; e < nr; e++) {
-          const int k = e / 2 + 1;
-          const float fk = con_fric[5 * ci + k - 1];
-          J[(r0 + e) * ldj + dof] = jf[0] + ((e & 1) ? -fk : fk) * jf[k];
+      const int cnt = min(NT, nsimple - base);
+      for (int k = 0; k < cnt; k++) {
+        const int ck = __builtin_amdgcn_readlane(col, k);
+        const float vk = rl(val, k);
+        if (tid < ldj) J[(base + k) * ldj + tid] = tid == ck ? vk : 0.f;
+      }
+    }
+    // contact rows: lane = contact loads the contact's data, then per contact
+    // (uniform) lane = dof builds the rows' column entries
+    {
+      float cd[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (tid < nv) {
+#pragma unroll
+        for (int c = 0; c < 6; c++) cd[c] = cdof[6 * tid + c];
+      }
+      for (int base = 0; base < ncon; base += NT) {
+        const int cl = base + tid;
+        int r0 = -1, b1 = 0, b2 = 0, dim = 1;
+        float cp[3] = {0.f, 0.f, 0.f}, fr[9], fk[5], c1[3] = {0.f, 0.f, 0.f}, c2[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 9; k++) fr[k] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 5; k++) fk[k] = 0.f;
+        if (cl < ncon) {
+          r0 = con_efcadr[cl];
+          b1 = IMG_I(geom_bodyid)[con_geom[2 * cl]];
+          b2 = IMG_I(geom_bodyid)[con_geom[2 * cl + 1]];
+          dim = con_dim[cl];
+#pragma unroll
+          for (int k = 0; k < 3; k++) cp[k] = con_pos[3 * cl + k];
+#pragma unroll
+          for (int k = 0; k < 9; k++) fr[k] = con_frame[9 * cl + k];
+#pragma unroll
+          for (int k = 0; k < 5; k++) fk[k] = con_fric[5 * cl + k];
+          const float* s1 = subtree_com + 3 * IMG_I(body_rootid)[b1];
+          const float* s2 = subtree_com + 3 * IMG_I(body_rootid)[b2];
+#pragma unroll
+          for (int k = 0; k < 3; k++) { c1[k] = s1[k]; c2[k] = s2[k]; }
+        }
+        const int cnt = min(NT, ncon - base);
+        for (int k = 0; k < cnt; k++) {
+          const int r0k = __builtin_amdgcn_readlane(r0, k);
+          if (r0k < 0) continue;
+          const int b1k = __builtin_amdgcn_readlane(b1, k), b2k = __builtin_amdgcn_readlane(b2, k);
+          const int dimk = __builtin_amdgcn_readlane(dim, k);
+          const int nr = dimk == 1 ? 1 : 2 * (dimk - 1);
+          const bool in1 = tid < nv && (((unsigned long long)IMG_L(body_dofmask)[b1k] >> tid) & 1ull);
+          const bool in2 = tid < nv && (((unsigned long long)IMG_L(body_dofmask)[b2k] >> tid) & 1ull);
+          // not in either chain, or in both (relative motion cancels): zero column
+          const bool use = in1 != in2;
+          const float sg = in2 ? 1.f : -1.f;
+          float off[3], t[3];
+#pragma unroll
+          for (int q = 0; q < 3; q++) off[q] = rl(cp[q], k) - (in2 ? rl(c2[q], k) : rl(c1[q], k));
+          cross3(t, cd, off);
+          const float jp[3] = {sg * (cd[3] + t[0]), sg * (cd[4] + t[1]), sg * (cd[5] + t[2])};
+          const float jr[3] = {sg * cd[0], sg * cd[1], sg * cd[2]};
+          float f[9];
+#pragma unroll
+          for (int q = 0; q < 9; q++) f[q] = rl(fr[q], k);
+          float jf[6];
+          jf[0] = dot3(f, jp); jf[1] = dot3(f + 3, jp); jf[2] = dot3(f + 6, jp);
+          jf[3] = dot3(f, jr); jf[4] = dot3(f + 3, jr); jf[5] = dot3(f + 6, jr);
+          if (tid < ldj) {
+            if (dimk == 1) {
+              J[r0k * ldj + tid] = use ? jf[0] : 0.f;
+            } else {
+              float fkv[5];
+#pragma unroll
+              for (int q = 0; q < 5; q++) fkv[q] = rl(fk[q], k);
+              // pyramid edges e = 2(kk-1), 2(kk-1)+1 of friction direction kk
+              // (static register indices: no private-memory arrays)
+#pragma unroll
+              for (int kk = 1; kk < 6; kk++) {
+                if (2 * (kk - 1) >= nr) break;
+                const int e = 2 * (kk - 1);
+                J[(r0k + e) * ldj + tid] = use ? jf[0] + fkv[kk - 1] * jf[kk] : 0.f;
+                J[(r0k + e + 1) * ldj + tid] = use ? jf[0] + (-fkv[kk - 1]) * jf[kk] : 0.f;
+              }
+            }
+          }
         }
       }
     }
