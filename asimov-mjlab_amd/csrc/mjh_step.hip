@@ -42,7 +42,7 @@ struct Layout {
   int act_force;
   int con_pos, con_frame, con_dist, con_fric, con_solref, con_solimp, con_imargin, con_dim, con_geom, con_efcadr;
   int J, ldj, efc_D, efc_R, efc_aref, efc_jaref, efc_jv, efc_force, efc_fl, efc_pos, efc_type, efc_id, efc_mask;
-  int efc_h, arow, ash, arow_prev;
+  int efc_h, arow, ash;
   int sidx;  // contact sensor: kept matches (contact index, ~index if flipped)
   int red, ints;
   int total, gtotal;  // per-world words: LDS, global scratch
@@ -77,7 +77,7 @@ enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
   X(con_imargin, 1) X(con_dim, 1) X(con_geom, 1) X(con_efcadr, 1)                                     \
   X(J, 0) X(efc_D, 0) X(efc_R, 0) X(efc_aref, 0) X(efc_jaref, 0) X(efc_jv, 0) X(efc_force, 0)        \
   X(efc_fl, 0) X(efc_pos, 1) X(efc_type, 0) X(efc_id, 1) X(efc_mask, 1) X(efc_h, 0) X(arow, 0)       \
-  X(ash, 0) X(arow_prev, 1) X(sidx, 1)
+  X(ash, 0) X(sidx, 1)
 struct Rg {
 #if MJH_PRESET == 0
 #define X_RG(name, r) static constexpr bool name = false;
@@ -1001,7 +1001,6 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   float* efc_h = SP(efc_h);
   int* arow = SPI(arow);
   float* ash = SP(ash);
-  int* arow_prev = SPI(arow_prev);
   int* sidx = SPI(sidx);
   float* red = S + Lo.red;
   int* redi = SI + Lo.red + 2 * (NT / 64) + 2;
@@ -1823,15 +1822,24 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
       }
       return bsum<NT>(c, red);
     };
-    int nact_prev = -1, nfactor = 0;
+    // active set of the factor in Lm as wave-uniform row masks (no memory: a
+    // global copy of the row list put a store ahead of the next J loads)
+    constexpr int kMaskWords = 5;  // rows beyond 320: always rebuild
+    unsigned long long act_prev[kMaskWords] = {0ull, 0ull, 0ull, 0ull, 0ull};
+    bool have_prev = false;
+    int nfactor = 0;
     auto newton_direction = [&]() {
       for (int i = tid; i < nv; i += NT) grad[i] = Ma[i] - qfrc_smooth[i] - qfrc_con[i];
       // compact the rows in the quadratic zone: H = M + sum h_r J_r J_r^T
       int nact = 0;
+      unsigned long long act[kMaskWords] = {0ull, 0ull, 0ull, 0ull, 0ull};
       for (int base = 0; base < nefc; base += NT) {
         const int r = base + tid;
         const float h = r < nefc ? efc_h[r] : 0.f;
         const int a = h > 0.f ? 1 : 0;
+        const unsigned long long bal = __ballot(a);
+#pragma unroll
+        for (int q = 0; q < kMaskWords; q++) act[q] = q == base / NT ? bal : act[q];
         int total;
         const int off = bscan<NT>(a, &total, redi);
         if (a) {
@@ -1842,10 +1850,10 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
       }
       wsync();
       // same active set as the factor in Lm -> H is identical, keep the factor
-      float diff = (nact != nact_prev) ? 1.f : 0.f;
-      if (diff == 0.f)
-        for (int k = tid; k < nact; k += NT) diff += arow[k] != arow_prev[k] ? 1.f : 0.f;
-      diff = bsum<NT>(diff, red);
+      bool same = have_prev && nefc <= kMaskWords * NT;
+#pragma unroll
+      for (int q = 0; q < kMaskWords; q++) same = same && act[q] == act_prev[q];
+      float diff = same ? 0.f : 1.f;
 #ifdef MJH_DEBUG_ALWAYS_REBUILD
       diff = 1.f;
 #endif
@@ -1866,8 +1874,9 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
         unsigned long long tf = PROF_NOW();
         ldl_factor_reg<NVP>(Lm, nv, ldm);
         PROF_ACC(16, tf);
-        for (int k = tid; k < nact; k += NT) arow_prev[k] = arow[k];
-        nact_prev = nact;
+#pragma unroll
+        for (int q = 0; q < kMaskWords; q++) act_prev[q] = act[q];
+        have_prev = true;
         nfactor++;
         nfactor_total++;
       }
@@ -2629,7 +2638,7 @@ Layout make_layout(const mjh_model* m, int budget) {
   // the 32-word slack below)
   const int per_row_lds = (Rg::J ? 0 : L.ldj) + !Rg::efc_D + !Rg::efc_R + !Rg::efc_aref + !Rg::efc_jaref +
                           !Rg::efc_jv + !Rg::efc_force + !Rg::efc_fl + !Rg::efc_pos + !Rg::efc_type + !Rg::efc_id +
-                          2 * !Rg::efc_mask + !Rg::efc_h + !Rg::arow + !Rg::ash + !Rg::arow_prev;
+                          2 * !Rg::efc_mask + !Rg::efc_h + !Rg::arow + !Rg::ash;
   int rcap = m->njmax;
   if (per_row_lds > 0) {
     const int r = (budget - off - 64) / per_row_lds;
@@ -2642,7 +2651,7 @@ Layout make_layout(const mjh_model* m, int budget) {
   TAKE(efc_jv, rcap); TAKE(efc_force, rcap); TAKE(efc_fl, rcap); TAKE(efc_pos, rcap);
   TAKE(efc_type, rcap); TAKE(efc_id, rcap);
   TAKE(efc_mask, 2 * rcap);
-  TAKE(efc_h, rcap); TAKE(arow, rcap + 4); TAKE(ash, rcap + 4); TAKE(arow_prev, rcap + 4);
+  TAKE(efc_h, rcap); TAKE(arow, rcap + 4); TAKE(ash, rcap + 4);
   TAKE(sidx, 64);
 #undef TAKE
   L.total = al(off);
