@@ -947,7 +947,9 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   float* qfrc_bias = SP(qfrc_bias);
   float* qfrc_con = SP(qfrc_con);
   float* qfrc_passive = SP(qfrc_passive);
-  float* qfrc_act = SP(qfrc_act);
+  // actuator forces per dof accumulate with LDS atomics in tmp2 (otherwise
+  // unused); the global qfrc_act region stays reserved in the layout
+  float* qfrc_act = SP(tmp2);
   float* grad = SP(grad);
   float* search = SP(search);
   float* Ma = SP(Ma);
@@ -1122,34 +1124,54 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   wsync();
 
   PROF(27);
-  // geoms (all written out; collision geoms kept in LDS) and sites
-  for (int g = tid; g < Z.ngeom; g += NT) {
-    const int b = IMG_I(geom_bodyid)[g];
-    float t[3], GR[9], GM[9];
-    mat_vec(t, xmat + 9 * b, geom_pos + 3 * g);
-    float gp[3] = {xpos[3 * b] + t[0], xpos[3 * b + 1] + t[1], xpos[3 * b + 2] + t[2]};
-    quat2mat(GR, geom_quat + 4 * g);
-    mat_mul(GM, xmat + 9 * b, GR);
-    float* og = DP(geom_xpos) + W * Z.ngeom * 3 + 3 * g;
-    og[0] = gp[0]; og[1] = gp[1]; og[2] = gp[2];
-    float* om = DP(geom_xmat) + W * Z.ngeom * 9 + 9 * g;
+  // geoms (all written out; collision geoms kept in LDS) and sites. The next
+  // geom's inputs are loaded before this geom's stores (a load behind a store
+  // waits for it).
+  {
+    int g = tid;
+    float R[9], P[3];
+    auto load_in = [&](int gg, float (&R_)[9], float (&P_)[3]) {
+      const int b = IMG_I(geom_bodyid)[gg];
 #pragma unroll
-    for (int k = 0; k < 9; k++) om[k] = GM[k];
-    const int slot = IMG_I(geom_colslot)[g];
-    if (slot >= 0) {
-      cgpos[3 * slot] = gp[0]; cgpos[3 * slot + 1] = gp[1]; cgpos[3 * slot + 2] = gp[2];
+      for (int k = 0; k < 9; k++) R_[k] = xmat[9 * b + k];
 #pragma unroll
-      for (int k = 0; k < 9; k++) cgmat[9 * slot + k] = GM[k];
+      for (int k = 0; k < 3; k++) P_[k] = xpos[3 * b + k];
+    };
+    if (g < Z.ngeom) load_in(g, R, P);
+    while (g < Z.ngeom) {
+      float t[3], GR[9], GM[9];
+      mat_vec(t, R, geom_pos + 3 * g);
+      const float gp[3] = {P[0] + t[0], P[1] + t[1], P[2] + t[2]};
+      quat2mat(GR, geom_quat + 4 * g);
+      mat_mul(GM, R, GR);
+      const int gn = g + NT;
+      if (gn < Z.ngeom) load_in(gn, R, P);
+      float* og = DP(geom_xpos) + W * Z.ngeom * 3 + 3 * g;
+      og[0] = gp[0]; og[1] = gp[1]; og[2] = gp[2];
+      float* om = DP(geom_xmat) + W * Z.ngeom * 9 + 9 * g;
+#pragma unroll
+      for (int k = 0; k < 9; k++) om[k] = GM[k];
+      const int slot = IMG_I(geom_colslot)[g];
+      if (slot >= 0) {
+        cgpos[3 * slot] = gp[0]; cgpos[3 * slot + 1] = gp[1]; cgpos[3 * slot + 2] = gp[2];
+#pragma unroll
+        for (int k = 0; k < 9; k++) cgmat[9 * slot + k] = GM[k];
+      }
+      g = gn;
     }
   }
   PROF(28);
   for (int s = tid; s < Z.nsite; s += NT) {
     const int b = IMG_I(site_bodyid)[s];
-    float t[3], SR[9], SM[9];
-    mat_vec(t, xmat + 9 * b, site_pos + 3 * s);
+    float R[9], P[3], t[3], SR[9], SM[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = xmat[9 * b + k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) P[k] = xpos[3 * b + k];
+    mat_vec(t, R, site_pos + 3 * s);
     quat2mat(SR, site_quat + 4 * s);
-    mat_mul(SM, xmat + 9 * b, SR);
-    sxpos[3 * s] = xpos[3 * b] + t[0]; sxpos[3 * s + 1] = xpos[3 * b + 1] + t[1]; sxpos[3 * s + 2] = xpos[3 * b + 2] + t[2];
+    mat_mul(SM, R, SR);
+    sxpos[3 * s] = P[0] + t[0]; sxpos[3 * s + 1] = P[1] + t[1]; sxpos[3 * s + 2] = P[2] + t[2];
 #pragma unroll
     for (int k = 0; k < 9; k++) sxmat[9 * s + k] = SM[k];
   }
@@ -1381,7 +1403,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   }
   PROF(23);
   // subtree sums of cfrc (lane b), ascending k
-  float r_bf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float r_bf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, r_bias = 0.f;
 #pragma nounroll
   for (int k = 1; k < nb; k++) {
     const float in = (tid > 0 && ((rl64(r_tmk, k) >> tid) & 1ull)) ? 1.f : 0.f;
@@ -1399,14 +1421,20 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     for (int c = 0; c < 6; c++) f[c] = shfl(r_bf[c], bi);
     if (tid < nv) {
       const float* cd = r_cdof;
-      qfrc_bias[tid] = cd[0] * f[0] + cd[1] * f[1] + cd[2] * f[2] + cd[3] * f[3] + cd[4] * f[4] + cd[5] * f[5];
+      r_bias = cd[0] * f[0] + cd[1] * f[1] + cd[2] * f[2] + cd[3] * f[3] + cd[4] * f[4] + cd[5] * f[5];
+      qfrc_bias[tid] = r_bias;
     }
   }
   wsync();
 
   PROF(24);
   // ---------------------------------------------------------------- passive, actuation, smooth force
-  for (int i = tid; i < nv; i += NT) {
+  // lane i = dof i (nv < 64); passive force and bias stay in registers, the
+  // applied force is loaded before any store
+  const float r_qapp = tid < nv ? DP(qfrc_applied)[W * nv + tid] : 0.f;
+  float r_pas = 0.f;
+  if (tid < nv) {
+    const int i = tid;
     float pas = -dof_damping[i] * qvel[i];
     const int jnt = IMG_I(dof_jntid)[i];
     const int t = IMG_I(jnt_type)[jnt];
@@ -1416,6 +1444,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     }
     qfrc_passive[i] = pas;
     qfrc_act[i] = 0.f;
+    r_pas = pas;
   }
   wsync();
   for (int i = tid; i < nu; i += NT) {
@@ -1448,7 +1477,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     }
     const unsigned long long nzb = __ballot(nzf);
     for (int i = tid; i < nv; i += NT) {
-      float s = qfrc_passive[i] - qfrc_bias[i] + DP(qfrc_applied)[W * nv + i] + qfrc_act[i];
+      float s = r_pas - r_bias + r_qapp + qfrc_act[i];
       // J^T xfrc_applied at each body com
       const float* cd = cdof + 6 * i;
       for (unsigned long long bm = nzb; bm; bm &= bm - 1) {
