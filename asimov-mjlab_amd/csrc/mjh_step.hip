@@ -111,6 +111,7 @@ struct Rg {
 
 thread_local std::string g_err;
 bool g_disable_spec = false;  // mjh_set_specialization(0): always the generic instance
+bool g_auto_order = false;    // mjh_set_world_ordering(1): order the worlds in the pack launch
 
 #ifdef MJH_PROFILE
 __device__ unsigned long long* g_prof;
@@ -2570,7 +2571,41 @@ __global__ void repeat_kernel(float* dst, const float* src, long long nelem, lon
 // One workgroup per model field copies it into the packed image (all fields in
 // parallel, ~µs); launched ahead of every step so in-place edits of shared
 // model fields take effect at the next step, as with MuJoCo Warp.
-__global__ void pack_kernel(const mjh_model m, const ImgOff io) {
+// World visiting order for the step launch that follows (mjh_order_worlds'
+// rule: descending (niter + 2) * nefc of the previous step in 256 buckets of
+// 16), run by one extra workgroup of the pack launch.
+constexpr int kPackOrderBuckets = 256;
+__device__ void order_worlds_block(const int* __restrict__ niter, const int* __restrict__ nefc, long long* __restrict__ order,
+                                   long long n) {
+  __shared__ int cnt[kPackOrderBuckets];
+  __shared__ int base[kPackOrderBuckets];
+  for (int b = threadIdx.x; b < kPackOrderBuckets; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+    const int key = (niter[e] + 2) * nefc[e];
+    atomicAdd(&cnt[kPackOrderBuckets - 1 - min(key >> 4, kPackOrderBuckets - 1)], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = 0; b < kPackOrderBuckets; b++) {
+      base[b] = acc;
+      acc += cnt[b];
+    }
+  }
+  __syncthreads();
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+    const int key = (niter[e] + 2) * nefc[e];
+    order[atomicAdd(&base[kPackOrderBuckets - 1 - min(key >> 4, kPackOrderBuckets - 1)], 1)] = e;
+  }
+}
+
+__global__ __launch_bounds__(1024) void pack_kernel(const mjh_model m, const ImgOff io, const int* niter, const int* nefc_w,
+                                                   long long* order, long long nworld) {
+  if ((int)blockIdx.x == io.nfields) {  // the extra workgroup: world order
+    order_worlds_block(niter, nefc_w, order, nworld);
+    return;
+  }
 #define X_SZ(name) const int name = m.name;
   MJH_MODEL_SIZES(X_SZ)
 #undef X_SZ
@@ -2781,7 +2816,10 @@ int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, voi
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     attr_set[STEP] = true;
   }
-  hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields), dim3(256), 0, s, *m, p.io);
+  const bool order = g_auto_order && d->world_order != nullptr && d->nworld > 1;
+  // 1024 threads: the order workgroup's counting sort is the launch's long pole
+  hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields + (order ? 1 : 0)), dim3(1024), 0, s, *m, p.io, d->solver_niter, d->nefc,
+                     const_cast<long long*>(d->world_order), (long long)d->nworld);
   const int blocks = (d->nworld + kWorldsPerBlock - 1) / kWorldsPerBlock;
   // specialised instances assume the slab data layout (data_is_slab)
   const int k = (g_disable_spec || !data_is_slab(m, d)) ? -1 : find_spec(p, m);
@@ -2830,6 +2868,11 @@ extern const int mjh_layout_ints = kLayoutInts;  // for tools/gen_spec.py
 
 int mjh_set_specialization(int enable) {
   g_disable_spec = enable == 0;
+  return 0;
+}
+
+int mjh_set_world_ordering(int on) {
+  g_auto_order = on != 0;
   return 0;
 }
 

@@ -36,6 +36,7 @@ EXPORTS = (
   "mjh_spec_index",
   "mjh_data_is_slab",
   "mjh_set_specialization",
+  "mjh_set_world_ordering",
   "mjh_scratch_words",
   "mjh_step",
   "mjh_forward",
@@ -116,6 +117,10 @@ def lib() -> ctypes.CDLL:
   L.mjh_spec_index.argtypes = [ctypes.c_void_p]
   L.mjh_data_is_slab.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
   L.mjh_set_specialization.argtypes = [ctypes.c_int]
+  L.mjh_set_world_ordering.argtypes = [ctypes.c_int]
+  # the step launches order the worlds themselves (in the pack launch) unless
+  # MJH_PACK_ORDER=0 (A/B: one mjh_order_worlds launch per step from the host)
+  L.mjh_set_world_ordering(0 if os.environ.get("MJH_PACK_ORDER") == "0" else 1)
   if os.environ.get("MJH_SPEC") == "0":  # A/B timing: generic kernel instance only
     L.mjh_set_specialization(0)
   L.mjh_image_words.argtypes = [ctypes.c_void_p]

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import json
+import os
 from collections import deque
 from contextlib import contextmanager
 from dataclasses import dataclass, field
@@ -394,7 +395,9 @@ class Simulation:
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
   def _refresh_order(self) -> None:
-    if self.cfg.balance_worlds and self.num_envs > 1:
+    # default: the step library rewrites world_order inside its pack launch
+    # (mjh_set_world_ordering, set at load); the separate launch is the A/B path
+    if self.cfg.balance_worlds and self.num_envs > 1 and os.environ.get("MJH_PACK_ORDER") == "0":
       # expected cost of a world ~ (solver iterations + 2) x constraint rows of
       # its previous step; most expensive first (one counting-sort launch)
       native.check(native.lib().mjh_order_worlds(ctypes.c_void_p(self.data.solver_niter.data_ptr()),

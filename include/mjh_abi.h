@@ -138,6 +138,12 @@ int mjh_data_is_slab(const mjh_model* m, const mjh_data* d);
 /* 0: always launch the generic instance (A/B timing, tests); 1: default. */
 int mjh_set_specialization(int enable);
 
+/* 1: mjh_step / mjh_forward / mjh_forward_gated rewrite data.world_order (when
+ * set) on the device before the step, by the same rule as mjh_order_worlds, in
+ * the model-image pack launch (no separate launch); 0 (default): the caller
+ * supplies world_order. */
+int mjh_set_world_ordering(int on);
+
 /* Diagnostic builds only (-DMJH_PROFILE): per-world phase timestamps. */
 int mjh_set_profile_buffer(void* ptr);
 
