@@ -21,6 +21,30 @@ from mjlab_amd.utils import spec_config as spec_cfg
 from mjlab_amd.utils.string import resolve_expr, resolve_matching_names
 
 
+def merge_keyframes(m, entities) -> None:
+  """Entity ``init_state`` keyframes -> ``m.key_qpos`` / ``m.key_ctrl`` at the
+  global addresses (MjSpec.attach merges the per-entity keys the same way)."""
+  key_qpos = m.qpos0.copy()
+  key_ctrl = np.zeros(m.nu)
+  for ent in entities:
+    k = ent.spec.keys[0] if ent.spec.keys else None
+    if k is None:
+      continue
+    p = ent.prefix
+    qa = []
+    if not ent.is_fixed_base:
+      jn = ent.spec.joints[0].name
+      a = int(m.jnt_qposadr[m.names["joint"].index(p + jn)])
+      qa += list(range(a, a + 7))
+    for n in ent.joint_names:
+      qa.append(int(m.jnt_qposadr[m.names["joint"].index(p + n)]))
+    key_qpos[qa] = k.qpos
+    if k.ctrl:
+      ca = [m.names["actuator"].index(p + n) for n in ent.actuator_names]
+      key_ctrl[ca] = k.ctrl
+  m.key_qpos, m.key_ctrl = key_qpos, key_ctrl
+
+
 @dataclass(frozen=True)
 class EntityIndexing:
   body_names: tuple[str, ...]
@@ -187,6 +211,15 @@ class Entity:
       name_keys, site_subset if site_subset is not None else self.site_names, preserve_order
     )
 
+  def compile(self):
+    """Compile this entity's spec on its own (``entity.py:307-309``): the
+    compiled model, with the ``init_state`` keyframe merged as ``key``."""
+    from mjlab_amd.spec.compiler import compile_spec
+
+    m = compile_spec(self._spec)
+    merge_keyframes(m, [self])
+    return m
+
   # --- init ---
   def initialize(self, model, sim_model, data, device: str) -> None:
     """``model`` is the compiled host model, ``sim_model``/``data`` the bridges."""
@@ -254,6 +287,13 @@ class Entity:
     gbody = np.asarray(model.geom_bodyid)
     sbody = np.asarray(model.site_bodyid)
     geom_ids, site_ids = [], []
+    # world-level geoms/sites of the entity come first in spec order; they
+    # share body 0 with every other entity's, so they are found by name
+    for kind, elems, out in (("geom", self._spec.worldbody.geoms, geom_ids), ("site", self._spec.worldbody.sites, site_ids)):
+      for el in elems:
+        if not el.name:
+          raise NotImplementedError(f"unnamed world-level {kind} in entity spec: cannot be indexed")
+        out.append(model.names[kind].index(p + el.name))
     for gb in body_ids:
       geom_ids += [int(i) for i in np.nonzero(gbody == gb)[0]]
       site_ids += [int(i) for i in np.nonzero(sbody == gb)[0]]

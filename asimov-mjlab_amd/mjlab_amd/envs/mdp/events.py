@@ -13,6 +13,7 @@ from typing import Literal
 
 import torch
 
+from mjlab_amd.entity.data import EntityData
 from mjlab_amd.managers.manager_base import as_mask
 from mjlab_amd.managers.scene_entity_config import SceneEntityCfg
 from mjlab_amd import envops
@@ -61,6 +62,14 @@ def _slice_start(cols):
   return cols.start if isinstance(cols, slice) and cols.step in (None, 1) else None
 
 
+def _fused_cols(d, prefix: str):
+  """(qpos, qvel) start columns of an EntityData's contiguous joint block for the
+  fused kernels, else (None, None) (duck-typed entities take the torch path)."""
+  if not isinstance(d, EntityData):
+    return None, None
+  return _slice_start(d._cols[prefix + "_q_adr"]), _slice_start(d._cols[prefix + "_v_adr"])
+
+
 def _all_range(r) -> bool:
   return bool(r) and not all(tuple(v) == (0.0, 0.0) for v in r.values())
 
@@ -77,7 +86,7 @@ def reset_root_state_uniform(env, env_ids, pose_range: dict, velocity_range: dic
   # one launch on the GPU: draws, pose composition and the root pose/velocity
   # writes of EntityData (csrc/mjh_fuse.hip); the torch path below is its reference
   d = a.data
-  qa, va = _slice_start(d._cols["free_joint_q_adr"]), _slice_start(d._cols["free_joint_v_adr"])
+  qa, va = _fused_cols(d, "free_joint")
   if qa is not None and va is not None:
     (plo, phi), (vlo, vhi) = _ranges6_host(pose_range), _ranges6_host(velocity_range)
     if envops.reset_root_uniform(env, f"reset_root_state_uniform.{asset_cfg.name}", d.data.qpos, qa, d.data.qvel, va, m, rs,
@@ -101,7 +110,7 @@ def reset_joints_by_offset(env, env_ids, position_range: tuple[float, float], ve
   a = env.scene[asset_cfg.name]
   j = asset_cfg.joint_idx
   d = a.data
-  if isinstance(j, slice) and j == slice(None):  # all joints: one fused launch on the GPU
+  if isinstance(j, slice) and j == slice(None) and isinstance(d, EntityData):  # all joints: one fused launch
     qa, va = _slice_start(d._cols["joint_q_adr"]), _slice_start(d._cols["joint_v_adr"])
     if qa is not None and va is not None and envops.reset_joints_offset(
         env, f"reset_joints_by_offset.{asset_cfg.name}", d.data.qpos, qa, d.data.qvel, va, m, d.default_joint_pos,
@@ -123,7 +132,7 @@ def push_by_setting_velocity(env, env_ids, velocity_range: dict, asset_cfg: Scen
   a = env.scene[asset_cfg.name]
   lo, hi = _ranges6(env, velocity_range)
   d = a.data
-  qa, va = _slice_start(d._cols["free_joint_q_adr"]), _slice_start(d._cols["free_joint_v_adr"])
+  qa, va = _fused_cols(d, "free_joint")
   if qa is not None and va is not None and envops.push_velocity(
       env, f"push_by_setting_velocity.{asset_cfg.name}", d.data.qpos, qa, d.data.qvel, va, m, d.root_link_vel_w,
       *_ranges6_host(velocity_range)):

@@ -23,6 +23,7 @@ import numpy as np
 import torch
 
 from mjlab_amd.entity import Entity, EntityCfg
+from mjlab_amd.entity.entity import merge_keyframes
 from mjlab_amd.sensor import BuiltinSensor, SensorCfg
 from mjlab_amd.spec.compiler import Model, compile_spec
 from mjlab_amd.spec.spec import BodySpec, GeomSpec, Spec
@@ -90,26 +91,7 @@ class Scene:
 
   def compile(self, nconmax: int | None = None, njmax: int | None = None) -> Model:
     m = compile_spec(self._spec, nconmax or 0, njmax or 0)
-    # Entity keyframes -> model key_qpos / key_ctrl at the global addresses.
-    key_qpos = m.qpos0.copy()
-    key_ctrl = np.zeros(m.nu)
-    for ent in self._entities.values():
-      k = ent.spec.keys[0] if ent.spec.keys else None
-      if k is None:
-        continue
-      p = ent.prefix
-      qa = []
-      if not ent.is_fixed_base:
-        jn = ent.spec.joints[0].name
-        a = int(m.jnt_qposadr[m.names["joint"].index(p + jn)])
-        qa += list(range(a, a + 7))
-      for n in ent.joint_names:
-        qa.append(int(m.jnt_qposadr[m.names["joint"].index(p + n)]))
-      key_qpos[qa] = k.qpos
-      if k.ctrl:
-        ca = [m.names["actuator"].index(p + n) for n in ent.actuator_names]
-        key_ctrl[ca] = k.ctrl
-    m.key_qpos, m.key_ctrl = key_qpos, key_ctrl
+    merge_keyframes(m, self._entities.values())
     return m
 
   @property

@@ -22,6 +22,7 @@ Outputs are numpy arrays named exactly as in ``include/mjh_fields.h``.
 from __future__ import annotations
 
 import math
+import warnings
 from dataclasses import dataclass, field
 from typing import Any
 
@@ -31,6 +32,7 @@ from mjlab_amd.spec.spec import GEOM_TYPES, JOINT_TYPES, Spec
 from mjlab_amd.utils import rot
 
 MINVAL = 1e-15
+SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3)}
 
 # Sensor type codes used by the kernels (order is ours; names follow mjtSensor).
 SENSOR_TYPES = {
@@ -98,7 +100,29 @@ class Model:
 
   def body(self, name: str) -> _Named:
     i = self._index("body", name)
-    return _Named(i, name, {"parentid": self.body_parentid[i : i + 1]})
+    return _Named(i, name, {"parentid": self.body_parentid[i : i + 1], "pos": self.body_pos[i],
+                            "quat": self.body_quat[i], "mass": self.body_mass[i : i + 1],
+                            "mocapid": self.body_mocapid[i : i + 1]})
+
+  @property
+  def nkey(self) -> int:
+    return 0 if getattr(self, "key_qpos", None) is None else 1
+
+  def key(self, name: str) -> _Named:
+    """The entity keyframe (``init_state``) merged at compile time (entity.py:145-166)."""
+    if self.nkey == 0 or name != "init_state":
+      raise KeyError(f"key '{name}' not found")
+    return _Named(0, name, {"qpos": np.asarray(self.key_qpos), "ctrl": np.asarray(self.key_ctrl)})
+
+  @property
+  def opt(self):
+    """``mjModel.opt`` view (mjtIntegrator / mjtSolver / mjtCone codes)."""
+    from types import SimpleNamespace
+
+    return SimpleNamespace(timestep=self.timestep, gravity=np.asarray(self.gravity), impratio=self.impratio,
+                           tolerance=self.tolerance, ls_tolerance=self.ls_tolerance, iterations=self.iterations,
+                           ls_iterations=self.ls_iterations, integrator=self.integrator, solver=self.solver,
+                           cone=self.cone)
 
   def joint(self, name: str) -> _Named:
     i = self._index("joint", name)
@@ -716,6 +740,17 @@ def _compile_pairs(m: Model, spec: Spec) -> None:
       pairs.append((g1_, g2_))
       colgeoms.add(g1)
       colgeoms.add(g2)
+  # geom-type pairs with a narrowphase in the HIP step (and the oracle):
+  # plane-{sphere,capsule,box}, sphere-{sphere,capsule}, capsule-capsule.
+  # Other pairs stay in the table (the kernels return no contact for them)
+  # and are reported here instead of being silently ignored.
+  unsupported = sorted({(int(m.geom_type[a]), int(m.geom_type[b])) for a, b in pairs
+                        if (int(m.geom_type[a]), int(m.geom_type[b])) not in SUPPORTED_PAIRS})
+  m.unsupported_pair_types = unsupported
+  if unsupported:
+    inv = {v: k for k, v in GEOM_TYPES.items()}
+    warnings.warn("collision pairs without a narrowphase on the HIP path (no contacts are generated): "
+                  + ", ".join(f"{inv[a]}-{inv[b]}" for a, b in unsupported), UserWarning, stacklevel=3)
   m.npair = len(pairs)
   m.pair_geom1 = np.array([p[0] for p in pairs] or [0], np.int32)
   m.pair_geom2 = np.array([p[1] for p in pairs] or [0], np.int32)
