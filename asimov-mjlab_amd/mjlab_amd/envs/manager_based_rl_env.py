@@ -91,8 +91,8 @@ class ManagerBasedEnv:
     self._sim_step_counter = 0
     # device random stream of the fused reset/event/command kernels (envops.rng_args):
     # seed from torch's generator (seeded above), counter = env steps taken
-    self._rng_seed = int(torch.randint(0, 2**62, (1,)).item())
     self._rng_ctr = torch.zeros((), dtype=torch.long, device=device)
+    self._reseed_stream()
     self.extras: dict = {"log": {}}
     self.obs_buf: dict = {}
     self.scene = Scene(cfg.scene, device=device)
@@ -116,12 +116,26 @@ class ManagerBasedEnv:
       self.event_manager.apply(mode="startup")
       self.sim.create_graph()
 
-  @staticmethod
-  def seed(seed: int = -1) -> int:
+  def seed(self, seed: int = -1) -> int:
+    """Seed python/numpy/torch (``manager_based_env.py`` ``seed``) and restart the
+    device random stream from that seed, so ``reset(seed=s)`` reproduces the
+    fused kernels' draws exactly as it reproduces the reference's torch draws."""
     if seed == -1:
       seed = int(np.random.randint(0, 10_000))
     seed_rng(seed)
+    if hasattr(self, "_rng_ctr"):
+      self._reseed_stream()
     return seed
+
+  def _reseed_stream(self) -> None:
+    """(seed, call counter, step counter) of the device stream from torch's
+    (freshly seeded) generator. The step counter restarts in place (captured
+    graphs hold its pointer); captured graphs are dropped because they baked
+    the old seed and call keys."""
+    self._rng_seed = int(torch.randint(0, 2**62, (1,)).item())
+    self.__dict__["_rng_calls"] = 0
+    self._rng_ctr.zero_()
+    self.__dict__["_graph"] = None
 
   def reset(self, *, seed: int | None = None, env_ids=None, options=None):
     del options

@@ -229,7 +229,11 @@ def randomize_field(env, env_ids, field: str, ranges, distribution: str = "unifo
     lo, hi = axis_ranges[ax]
     shape = (*data.shape[:-1], 1) if data.dim() > 2 else data.shape
     if distribution == "uniform":
-      vals = torch.rand(shape, device=env.device) * (hi - lo) + lo
+      # bounds as float32 tensors, as the reference (events.py:405-406), so the
+      # range is rounded the same way
+      lo_t = torch.tensor([lo], device=env.device)
+      hi_t = torch.tensor([hi], device=env.device)
+      vals = torch.rand(shape, device=env.device) * (hi_t - lo_t) + lo_t
     elif distribution == "log_uniform":
       vals = torch.exp(torch.rand(shape, device=env.device) * (torch.log(torch.tensor(hi)) - torch.log(torch.tensor(lo))) + torch.log(torch.tensor(lo)))
     elif distribution == "gaussian":

@@ -375,13 +375,14 @@ SIMPLE_ROBOT_XML = """
 </worldbody></mujoco>"""
 
 
-def _scene_with_sensors(xml: str, entity_name: str, sensors: tuple, backend: str, num_envs: int = 2, njmax: int = 50):
+def _scene_with_sensors(xml: str, entity_name: str, sensors: tuple, backend: str, num_envs: int = 2, njmax: int = 50,
+                        skip: tuple[str, ...] = ()):
   """test_contact_sensor.py:102-130 (create_scene_with_sensor)."""
   dev = device_of(backend)
   scene = Scene(SceneCfg(num_envs=num_envs, env_spacing=3.0, entities={entity_name: EntityCfg(
     spec_fn=lambda: read_mjcf_string(xml))}, sensors=sensors), dev)
   model = scene.compile()
-  sim = make_sim(num_envs, SimulationCfg(njmax=njmax), model, backend)
+  sim = make_sim(num_envs, SimulationCfg(njmax=njmax), model, backend, skip=skip)
   scene.initialize(sim.mj_model, sim.model, sim.data)
   return scene, sim
 
@@ -428,9 +429,13 @@ def test_basic_contact_detection(backend):
 
 
 def test_contact_fields(backend):
-  """test_contact_sensor.py:191-231."""
+  """test_contact_sensor.py:191-231. The box rests on four corner contacts
+  carrying near-equal forces, so the maxforce reduction's pick (and with it
+  pos/torque) may differ between float32 and float64 while every force agrees:
+  the shadow skips sensordata here and the test checks what is determined."""
   scene, sim = _scene_with_sensors(
-    FALLING_BOX_XML, "box", (_box_sensor(fields=("found", "force", "torque", "dist", "pos", "normal")),), backend)
+    FALLING_BOX_XML, "box", (_box_sensor(fields=("found", "force", "torque", "dist", "pos", "normal")),), backend,
+    skip=("sensordata",))
   _place(scene["box"], sim, 0.105)
   _settle(sim, 10)
   data = scene["box_contact"].data
