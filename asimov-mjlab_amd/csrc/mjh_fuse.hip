@@ -84,7 +84,10 @@ constexpr int kRedBlock = 1024;  // one workgroup of 16 waves per column
 
 // blockIdx.x = column: masked row count and masked column sum (each thread
 // accumulates rows tid, tid + 1024, ...), wave + LDS reduction; the column's
-// masked rows are cleared when zero_rows
+// masked rows are cleared when zero_rows. With no row masked, out[t] keeps its
+// value: the reference writes its episode logs only from _reset_idx, which runs
+// only when some env resets, so the log holds the last reset's values
+// (manager_based_rl_env.py:133-135, 216-238)
 __global__ __launch_bounds__(kRedBlock) void masked_means_kernel(const ColArgs a, const unsigned char* __restrict__ mask,
                                                                   float scale, int zero_rows, float* __restrict__ out,
                                                                   long long n) {
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(kRedBlock) void masked_means_kernel(const ColArgs a
       ts += part[0][w];
       tc += part[1][w];
     }
-    out[t] = ts / fmaxf(tc, 1.f) * scale;
+    if (tc > 0.f) out[t] = ts / tc * scale;
   }
 }
 
@@ -126,11 +129,15 @@ struct FlagArgs {
 __global__ __launch_bounds__(kRedBlock) void masked_counts_kernel(const FlagArgs a, const unsigned char* __restrict__ mask,
                                                                    mjh_i64* __restrict__ out, long long n) {
   __shared__ int part[MJH_MAX_TERMS][kRedBlock / 64];
+  __shared__ int any_masked;
   int acc[MJH_MAX_TERMS];
 #pragma unroll
   for (int t = 0; t < MJH_MAX_TERMS; t++) acc[t] = 0;
+  if (threadIdx.x == 0) any_masked = 0;
+  __syncthreads();
   for (long long e = threadIdx.x; e < n; e += kRedBlock) {
     if (!on(mask, e)) continue;
+    any_masked = 1;  // benign race: every writer stores 1
 #pragma unroll
     for (int t = 0; t < MJH_MAX_TERMS; t++)
       if (t < a.nflags) acc[t] += a.f[t][e] ? 1 : 0;
@@ -146,7 +153,7 @@ __global__ __launch_bounds__(kRedBlock) void masked_counts_kernel(const FlagArgs
     }
   }
   __syncthreads();
-  if (threadIdx.x < (unsigned)a.nflags) {
+  if (any_masked && threadIdx.x < (unsigned)a.nflags) {  // no env masked: keep the last counts
     long long s = 0;
 #pragma unroll
     for (int w = 0; w < kRedBlock / 64; w++) s += part[threadIdx.x][w];

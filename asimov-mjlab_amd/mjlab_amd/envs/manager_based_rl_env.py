@@ -134,13 +134,26 @@ class ManagerBasedEnv:
     the old seed and call keys."""
     self._rng_seed = int(torch.randint(0, 2**62, (1,)).item())
     self.__dict__["_rng_calls"] = 0
+    self._reset_epoch = 0
     self._rng_ctr.zero_()
     self.__dict__["_graph"] = None
+
+  def _begin_rng_phase(self, outside_step: bool) -> None:
+    """Call keys restart at every env step (draws differ per step through the
+    device step counter), so an eager step and a graph replay of it draw the
+    same numbers; calls made outside the step (``reset()``) take a separate
+    key range per call so they never repeat a step's draws."""
+    if outside_step:
+      self._reset_epoch += 1
+      self.__dict__["_rng_calls"] = self._reset_epoch << 32
+    else:
+      self.__dict__["_rng_calls"] = 0
 
   def reset(self, *, seed: int | None = None, env_ids=None, options=None):
     del options
     if seed is not None:
       self.seed(seed)
+    self._begin_rng_phase(outside_step=True)
     self._reset_idx(as_mask(env_ids, self.num_envs, self.device))
     self.scene.write_data_to_sim()
     self.sim.forward()
@@ -149,6 +162,7 @@ class ManagerBasedEnv:
 
   def step(self, action: torch.Tensor):
     self._rng_ctr += 1
+    self._begin_rng_phase(outside_step=False)
     self.action_manager.process_action(action.to(self.device))
     for _ in range(self.cfg.decimation):
       self._sim_step_counter += 1
@@ -284,6 +298,7 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     self._graph, self._graph_key, self._graph_out = g, key, out
 
   def _step_body(self) -> None:
+    self._begin_rng_phase(outside_step=False)
     self.action_manager.process_action(self._action_in)
     for _ in range(self.cfg.decimation):
       self.action_manager.apply_action()
@@ -326,6 +341,7 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     del options
     if seed is not None:
       self.seed(seed)
+    self._begin_rng_phase(outside_step=True)
     mask = as_mask(env_ids, self.num_envs, self.device)
     self._reset_idx(mask)
     self.scene.write_data_to_sim()

@@ -35,6 +35,9 @@ class CommandTerm(ManagerTermBase):
         w = m.float()
         vals = torch.stack(list(self.metrics.values()), dim=1)
         means = (vals * w[:, None]).sum(0) / w.sum().clamp(min=1.0)
+        # no env masked: the log keeps the last reset's values (as the kernel)
+        means = torch.where(w.sum() > 0, means, self._reset_means[: len(self.metrics)])
+        self._reset_means[: len(self.metrics)] = means
         for i, (k, v) in enumerate(self.metrics.items()):
           extras[k] = means[i]
           v.masked_fill_(m, 0.0)

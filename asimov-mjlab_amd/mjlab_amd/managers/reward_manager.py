@@ -61,6 +61,9 @@ class RewardManager:
     else:
       w = m.float()
       means = (self._sums * w[:, None]).sum(0) / (w.sum().clamp(min=1.0) * self._env.max_episode_length_s)
+      # no env masked: the log keeps the last reset's values (as the kernel)
+      means = torch.where(w.sum() > 0, means, self._reset_means[: len(self._term_names)])
+      self._reset_means[: len(self._term_names)] = means
       self._sums.masked_fill_(m[:, None], 0.0)
     extras = {"Episode_Reward/" + k: means[i] for i, k in enumerate(self._term_names)}
     for tcfg in self._class_term_cfgs:

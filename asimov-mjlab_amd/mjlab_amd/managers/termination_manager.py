@@ -51,7 +51,10 @@ class TerminationManager:
     if envops.masked_counts(list(self._term_dones.values()), m, self._reset_counts):
       extras = {"Episode_Termination/" + k: self._reset_counts[i] for i, k in enumerate(self._term_dones)}
     else:
-      extras = {"Episode_Termination/" + k: (v & m).sum() for k, v in self._term_dones.items()}
+      counts = torch.stack([(v & m).sum() for v in self._term_dones.values()])
+      # no env masked: the log keeps the last reset's counts (as the kernel)
+      self._reset_counts[: len(counts)] = torch.where(m.any(), counts, self._reset_counts[: len(counts)])
+      extras = {"Episode_Termination/" + k: self._reset_counts[i] for i, k in enumerate(self._term_dones)}
     for tcfg in self._class_term_cfgs:
       if hasattr(tcfg.func, "reset"):
         tcfg.func.reset(env_ids=env_ids)

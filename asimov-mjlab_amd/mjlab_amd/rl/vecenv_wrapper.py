@@ -16,6 +16,21 @@ import torch
 from mjlab_amd.envs.manager_based_rl_env import Box, ManagerBasedRlEnv
 
 
+def _fresh_log(log: dict) -> dict:
+  """Copies of the 0-d tensor log values, grouped by dtype/device into one stack each."""
+  out = dict(log)
+  groups: dict = {}
+  for k, v in log.items():
+    if isinstance(v, torch.Tensor) and v.dim() == 0:
+      groups.setdefault((v.dtype, v.device), []).append(k)
+    elif isinstance(v, torch.Tensor):
+      out[k] = v.clone()
+  for keys in groups.values():
+    for k, v in zip(keys, torch.stack([log[k] for k in keys]).unbind(0)):
+      out[k] = v
+  return out
+
+
 class ObsDict(dict):
   def __init__(self, data: dict, batch_size) -> None:
     super().__init__(data)
@@ -94,8 +109,13 @@ class RslRlVecEnvWrapper:
     obs = {k: v.clone() for k, v in obs.items()}
     rew = rew.clone()
     dones = (terminated | truncated).to(dtype=torch.long)
+    # the log values are persistent device buffers too (episode means/counts,
+    # Sim/* flag counts): rsl_rl appends each step's log dict and averages at
+    # log time, so each step gets its own copies (one stack+clone per dtype)
+    extras = dict(extras)
+    extras["log"] = _fresh_log(extras.get("log", {}))
     if not self.cfg.is_finite_horizon:
-      extras["time_outs"] = truncated
+      extras["time_outs"] = truncated.clone()
     if self._gather is not None:
       extras["gathered"] = self._gather(obs, rew, terminated, truncated)
     return ObsDict(obs, [self.num_envs]), rew, dones, extras

@@ -96,3 +96,75 @@ def test_vecenv_obs_survive_the_next_graph_replay():
   assert env._graph is not None  # the second step replays the captured graph
   assert torch.equal(o1["policy"], o1c) and torch.equal(r1, r1c)
   assert not torch.equal(o2["policy"], o1c)
+
+
+def _twin_envs(task: str, n: int, tmp_path=None):
+  envs = []
+  for use_graph in (True, False):
+    cfg = load_env_cfg(task)
+    cfg.scene.num_envs = n
+    cfg.seed = 7
+    if "Tracking" in task:
+      cfg.commands["motion"].motion_file = _gpu_motion(tmp_path)
+    envs.append(ManagerBasedRlEnv(cfg, device="cuda:0", use_graph=use_graph))
+  return envs
+
+
+_STATE = ("qpos", "qvel", "qacc_warmstart", "ctrl", "time", "xpos", "xquat", "cvel", "subtree_com", "sensordata",
+          "qfrc_applied", "xfrc_applied", "actuator_force", "nefc", "ncon", "solver_niter")
+
+
+@pytest.mark.parametrize("task", ["Mjlab-Velocity-Flat-Unitree-G1", "Mjlab-Tracking-Flat-Unitree-G1"])
+def test_graph_replay_equals_eager_step(task, tmp_path):
+  """The benchmarked object — the captured env step — against the same step run
+  eagerly, call by call: from identical state, counters and seeds, every
+  returned tensor, every log value and the simulation state must agree
+  bitwise over K steps, with resets forced on a subset (episode_length_buf at
+  the limit) so the masked reset kernels, the gated forward and the command
+  resampling all run inside the graph."""
+  n, K = 64, 10
+  ge, ee = _twin_envs(task, n, tmp_path)
+  adim = ge.action_manager.total_action_dim
+  for e in (ge, ee):
+    e.reset()
+    e.episode_length_buf[:12] = e.max_episode_length - 1 - torch.arange(12, device="cuda:0") % 4
+  g = torch.Generator(device="cuda:0").manual_seed(11)
+  resets = 0
+  for k in range(K):
+    a = 2 * torch.rand(n, adim, device="cuda:0", generator=g) - 1
+    og, rg, tg, trg, xg = ge.step(a)
+    oe, re_, te, tre, xe = ee.step(a)
+    if k >= 1:
+      assert ge._graph is not None, "graph env must replay from step 2 on"
+    assert ee._graph is None
+    resets += int((tg | trg).sum())
+    for name in ("policy", "critic"):
+      assert torch.equal(og[name], oe[name]), f"step {k}: obs {name}"
+    assert torch.equal(rg, re_), f"step {k}: reward"
+    assert torch.equal(tg, te) and torch.equal(trg, tre), f"step {k}: dones"
+    assert set(xg["log"]) == set(xe["log"])
+    for key, v in xg["log"].items():
+      assert torch.equal(torch.as_tensor(v), torch.as_tensor(xe["log"][key])), f"step {k}: log {key}"
+    for f in _STATE:
+      assert torch.equal(getattr(ge.sim.data, f), getattr(ee.sim.data, f)), f"step {k}: sim.data.{f}"
+    assert torch.equal(ge.episode_length_buf, ee.episode_length_buf)
+  assert resets >= 12
+
+
+def test_reset_with_seed_reproduces_device_draws():
+  """reset(seed=s) restarts the fused kernels' random stream, so two
+  resets with the same seed draw the same reset states and commands."""
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = 64
+  env = ManagerBasedRlEnv(cfg, device="cuda:0")
+  snaps = []
+  for _ in range(2):
+    env.reset(seed=5)
+    cmd = env.command_manager.get_term("twist")
+    snaps.append([env.sim.data.qpos.clone(), env.sim.data.qvel.clone(), cmd.vel_command_b.clone(), cmd.time_left.clone()])
+    for _ in range(3):
+      env.step(torch.rand(64, 29, device="cuda:0"))
+  for a, b in zip(*snaps):
+    assert torch.equal(a, b)
+  env.reset(seed=6)
+  assert not torch.equal(env.sim.data.qpos, snaps[0][0])

@@ -21,3 +21,43 @@ def test_wrapper_contract():
   assert d.dtype == torch.long and r.shape == (4,) and "time_outs" in ex
   assert torch.allclose(env.action_manager.action, torch.ones(4, 29))  # clipped
   assert w.action_space.high == 1.0
+
+
+def test_wrapper_logs_do_not_alias_across_steps():
+  """rsl_rl keeps every step's extras['log']; the env's log values are
+  persistent buffers, so the wrapper must hand out per-step copies."""
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = 4
+  env = ManagerBasedRlEnv(cfg, device="cpu")
+  oracle_sim.attach(env.sim, env.event_manager.domain_randomization_fields)
+  w = RslRlVecEnvWrapper(env)
+  _, _, _, ex1 = w.step(torch.zeros(4, 29))
+  snap = {k: v.clone() for k, v in ex1["log"].items() if isinstance(v, torch.Tensor)}
+  env.episode_length_buf[:] = env.max_episode_length  # every env times out next step: all logs rewritten
+  _, _, _, ex2 = w.step(torch.zeros(4, 29))
+  for k, v in snap.items():
+    assert torch.equal(ex1["log"][k], v), k
+    assert ex1["log"][k].data_ptr() != ex2["log"][k].data_ptr(), k
+  assert int(ex2["log"]["Episode_Termination/time_out"]) == 4
+  assert ex2["time_outs"].data_ptr() != env.termination_manager.time_outs.data_ptr()
+
+
+def test_episode_logs_hold_last_reset_values():
+  """the reference writes Episode_* / metric logs only from _reset_idx,
+  which runs only when some env resets (manager_based_rl_env.py:133-135), so a
+  step without resets keeps the previous values instead of logging zeros
+  (reward-term Metrics/* are written every step and are not held)."""
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = 4
+  env = ManagerBasedRlEnv(cfg, device="cpu")
+  oracle_sim.attach(env.sim, env.event_manager.domain_randomization_fields)
+  env.reset()
+  env.episode_length_buf[:] = env.max_episode_length
+  _, _, _, _, ex = env.step(torch.zeros(4, 29))
+  held = {k: torch.as_tensor(v).clone() for k, v in ex["log"].items() if k.startswith(("Episode_", "Metrics/twist/"))}
+  assert any(k.startswith("Metrics/twist/") for k in held)
+  assert int(held["Episode_Termination/time_out"]) == 4
+  _, _, term, trunc, ex = env.step(torch.zeros(4, 29))
+  assert not bool((term | trunc).any())
+  for k, v in held.items():
+    assert torch.equal(torch.as_tensor(ex["log"][k]), v), k
