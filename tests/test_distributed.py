@@ -33,7 +33,9 @@ def _worker(rank, world, port, q):
   assert (to0 is None) == (rank != 0)
   if rank == 0:
     assert torch.equal(to0, out)  # gather to the learner rank == all-gather there
-  q.put((rank, out.clone(), pack_step_outputs(obs, rew, term, trunc)))
+  # numpy payloads: torch tensors travel as shared-memory handles that die with
+  # the child process (ConnectionResetError if it exits before the parent reads)
+  q.put((rank, out.numpy().copy(), pack_step_outputs(obs, rew, term, trunc).numpy().copy()))
   dist.destroy_process_group()
 
 
@@ -50,6 +52,7 @@ def test_step_gather_world2():
     p.join(timeout=60)
     assert p.exitcode == 0
   res.sort(key=lambda x: x[0])
+  res = [(r, torch.from_numpy(a), torch.from_numpy(b)) for r, a, b in res]
   full = torch.cat([r[2] for r in res], dim=0)
   for _, gathered, _ in res:
     assert gathered.shape == (10, 3 + 4 + 3)
@@ -73,7 +76,7 @@ def _env_worker(rank, world, port, q):
   dist.init_process_group("gloo", rank=rank, world_size=world)
   torch.set_num_threads(1)
   outs = _run_shard(rank, gather=True)
-  q.put((rank, outs))
+  q.put((rank, [(o.numpy().copy(), g.numpy().copy()) for o, g in outs]))
   dist.destroy_process_group()
 
 
@@ -114,7 +117,7 @@ def test_env_shards_world2_match_single_process():
   ps = [ctx.Process(target=_env_worker, args=(r, world, port, q)) for r in range(world)]
   for p in ps:
     p.start()
-  res = dict(q.get(timeout=300) for _ in range(world))
+  res = {r: [(torch.from_numpy(o), torch.from_numpy(g)) for o, g in v] for r, v in (q.get(timeout=300) for _ in range(world))}
   for p in ps:
     p.join(timeout=60)
     assert p.exitcode == 0
