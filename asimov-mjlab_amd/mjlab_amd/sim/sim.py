@@ -439,7 +439,7 @@ class Simulation:
 
     The decision is taken on the device, so the env step can call this inside
     a captured graph where the reference syncs on ``len(reset_env_ids) > 0``
-    (``manager_based_rl_env.py:155-160``)."""
+    (``manager_based_rl_env.py:133-137``)."""
     self._require_gpu()
     self.epoch.bump()
     if gate.dtype not in (torch.bool, torch.uint8) or gate.numel() != 1 or not gate.is_cuda:

@@ -158,7 +158,7 @@ int mjh_forward(const mjh_model* m, const mjh_data* d, void* stream);
 /* mjh_forward, executed only if the device byte *gate is non-zero (read by the
  * kernel, so the decision needs no host sync and can sit inside a captured
  * graph). Replaces the host-side `if len(reset_env_ids) > 0: sim.forward()`
- * of manager_based_rl_env.py:155-160. */
+ * of manager_based_rl_env.py:133-137. */
 int mjh_forward_gated(const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream);
 
 /* Tile src[0:nelem] into dst[w*nelem:(w+1)*nelem] for w < nworld.

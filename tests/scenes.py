@@ -9,12 +9,17 @@ here once and cited by the tests:
   11 levels deep);
 * smooth dynamics (cvel, qfrc_bias, qfrc_actuator, qfrc_smooth, qacc_smooth,
   actuator_force): |d| <= 1e-4 * (1 + max|ref|);
-* constraint solve (qacc, qfrc_constraint): |d| <= 2e-2 * (1 + max|ref|) — the
+* constraint rows: efc_pos |d| <= 5e-5, efc_D <= 3e-3 * (1 + max), efc_aref
+  <= 1e-3 * (1 + max), efc_J <= 1e-4 * (1 + max) (row by row, integer-identical
+  worlds); the mass matrix qM <= 1e-4 * (1 + max) on every world;
+* constraint solve (qacc, qfrc_constraint, efc_force): per world
+  |d| <= SOLVE_REL (2e-3) * (1 + max|ref|) on at least SOLVE_FRAC (99.5 %) of
+  the worlds and <= SOLVE_MAX (3e-2) * (1 + max|ref|) on every world — the
   Newton solver stops on a tolerance test, and a float32 run can take one
   more/fewer iteration than the float64 one (MuJoCo Warp has the same property);
-* integrated state: qvel |d| <= 1e-2 * (1 + max|ref qvel|), qpos |d| <= 1e-4 + dt * (qvel bound)
-  (qpos integrates the new qvel);
-* sensordata: |d| <= 2e-2 * (1 + max|ref|) (contact forces come out of the solve).
+* integrated state: qvel |d| <= SOLVE_REL * 2 dt (1 + max|ref qacc|) + 1e-5,
+  qpos |d| <= SOLVE_REL * 2 dt^2 (1 + max|ref qacc|) + 1e-5 (same world fractions);
+* sensordata: SOLVE_REL / SOLVE_MAX as the solve (contact forces come out of it).
 """
 
 from __future__ import annotations

@@ -55,16 +55,21 @@ def test_masked_means_and_counts_match_torch():
   assert envops.masked_means([sums[:, i] for i in range(t)], m, 1 / 20.0, True, out)
   torch.testing.assert_close(out, ref_means, rtol=1e-5, atol=1e-6)
   assert torch.equal(sums, ref_sums)
-  # empty mask: means are 0 (count clamped to 1), nothing cleared
+  # empty mask: the outputs keep their last values (the reference logs episode
+  # statistics only from _reset_idx, i.e. only when some env resets), nothing cleared
   z = torch.zeros(n, dtype=torch.bool, device=DEV)
   v = torch.randn(n, device=DEV, generator=g)
   v0 = v.clone()
+  held = out.clone()
   assert envops.masked_means([v], z, 1.0, True, out)
-  assert out[0].item() == 0.0 and torch.equal(v, v0)
+  assert torch.equal(out, held) and torch.equal(v, v0)
   flags = [torch.rand(n, device=DEV, generator=g) < p for p in (0.01, 0.5, 0.0, 1.0)]
   cnt = torch.zeros(4, dtype=torch.long, device=DEV)
   assert envops.masked_counts(flags, m, cnt)
   assert cnt.tolist() == [int((f & m).sum()) for f in flags]
+  held = cnt.clone()
+  assert envops.masked_counts(flags, z, cnt)
+  assert torch.equal(cnt, held)
 
 
 def test_uniform_where_and_interval_tick():
