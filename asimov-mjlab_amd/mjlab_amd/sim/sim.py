@@ -88,10 +88,14 @@ class NanGuard:
   writes the buffered states of the first ``max_envs_to_dump`` non-finite
   worlds to ``nan_dump_<timestamp>.npz``. The state layout is MuJoCo's
   mjSTATE_PHYSICS = [qpos (nq), qvel (nv), act (na)] in float64 (the models
-  here have no plugin or history state). Deviations, both because MuJoCo is
-  absent: metadata is stored as a JSON string (loadable without pickle) instead
-  of a pickled dict, and the model is saved as ``model_<timestamp>.npz`` (the
-  compiled model's arrays) instead of an MJB file.
+  here have no plugin or history state). ``_metadata`` is the same dict object
+  array the reference writes (``nan_guard.py:135-150``; read by
+  ``scripts/nan_viz.py:31`` with ``.item()``). MuJoCo is absent, so the model
+  cannot be saved as MJB: it is written as MJCF (``model_<timestamp>.xml``,
+  ``spec.mjcf.model_to_mjcf``), which ``MjModel.from_xml_path`` loads with the
+  same body/dof/geom order; ``mjlab_amd.utils.nan_guard.load_nan_dump`` reads
+  both files (the reference viewer needs ``from_xml_path`` in place of
+  ``from_binary_path`` for this one file).
   """
 
   def __init__(self, cfg: NanGuardCfg, num_envs: int, model) -> None:
@@ -148,19 +152,22 @@ class NanGuard:
     self.output_dir.mkdir(parents=True, exist_ok=True)
     stamp = datetime.now().strftime("%Y%m%d_%H%M%S")
     fname = self.output_dir / f"nan_dump_{stamp}.npz"
-    mname = self.output_dir / f"model_{stamp}.npz"
+    mname = self.output_dir / f"model_{stamp}.xml"
     envs = nan_env_ids[: self.max_envs_to_dump]
     out = {f"states_step_{it['step']:06d}": it["states"][envs] for it in self.buffer}
     meta = {
       "num_envs_total": self.num_envs, "num_envs_dumped": len(envs), "nan_env_ids": nan_env_ids,
       "dumped_env_ids": list(envs), "state_size": self.state_size, "buffer_size": len(self.buffer),
       "detection_step": self.step_counter, "timestamp": stamp, "model_file": mname.name,
-      "note": "States in mjSTATE_PHYSICS layout [qpos, qvel, act] (float64).",
+      "note": "States in mjSTATE_PHYSICS layout [qpos, qvel, act] (float64); use mj_setState to restore. "
+      "Model saved as MJCF (MjModel.from_xml_path).",
     }
-    out["_metadata"] = np.array(json.dumps(meta))
+    out["_metadata"] = np.array(meta, dtype=object)
     np.savez_compressed(fname, **out)
-    np.savez_compressed(mname, **{k: np.asarray(v) for k, v in abi.model_host_arrays(self.model).items()})
-    for link, target in ((self.output_dir / "nan_dump_latest.npz", fname), (self.output_dir / "model_latest.npz", mname)):
+    from mjlab_amd.spec.mjcf import model_to_mjcf
+
+    mname.write_text(model_to_mjcf(self.model))
+    for link, target in ((self.output_dir / "nan_dump_latest.npz", fname), (self.output_dir / "model_latest.xml", mname)):
       link.unlink(missing_ok=True)
       link.symlink_to(target.name)
     print(f"[NanGuard] Detected NaN/Inf at step {self.step_counter}; envs {nan_env_ids[:10]}; "

@@ -709,6 +709,7 @@ def _set_const(m: Model) -> None:
 def _compile_pairs(m: Model, spec: Spec) -> None:
   bid = {n: i for i, n in enumerate(m.names["body"])}
   excl = set()
+  m.excludes = [tuple(e) for e in spec.excludes]
   for a, b in spec.excludes:
     i, j = bid[a], bid[b]
     excl.add((min(i, j), max(i, j)))

@@ -307,7 +307,28 @@ class MjcfReader:
   def _read_sensor(self, node: ET.Element) -> SensorSpec:
     a = node.attrib
     s = SensorSpec(name=a.get("name", ""), type=node.tag)
-    if node.tag in ("gyro", "velocimeter", "accelerometer", "framequat", "framepos"):
+    if node.tag == "contact":
+      # MuJoCo >= 3.3 contact sensor: {geom,body,subtree}{1,2}, data, reduce, num
+      # (mjlab adds these through MjSpec with the same intprm encoding,
+      # contact_sensor.py:472-496)
+      fields = ("found", "force", "torque", "dist", "pos", "normal", "tangent")
+      kinds = {"geom": "geom", "body": "body", "subtree": "xbody"}
+      for side in ("1", "2"):
+        for k, ot in kinds.items():
+          if k + side in a:
+            if side == "1":
+              s.objtype, s.objname = ot, a[k + side]
+            else:
+              s.reftype, s.refname = ot, a[k + side]
+      bits = 0
+      for f in a.get("data", "found").split():
+        bits |= 1 << fields.index(f)
+      reduce = {"none": 0, "mindist": 1, "maxforce": 2, "netforce": 3}[a.get("reduce", "none")]
+      s.intprm = [bits, reduce, int(a.get("num", 1))]
+      return s
+    if node.tag in ("framequat", "framepos") and "objname" in a:
+      s.objtype, s.objname = a.get("objtype", "site"), a["objname"]
+    elif node.tag in ("gyro", "velocimeter", "accelerometer", "framequat", "framepos"):
       s.objtype, s.objname = "site", a["site"]
     elif node.tag in ("subtreeangmom", "subtreecom", "subtreelinvel"):
       s.objtype, s.objname = "body", a["body"]
@@ -333,3 +354,139 @@ def read_mjcf_string(text: str, name: str = "inline.xml") -> Spec:
     return read_mjcf(p)
   finally:
     Path(p).unlink(missing_ok=True)
+
+
+# ---- writer: compiled model -> MJCF (for NaN dumps; MuJoCo's mj_saveModel is absent) ----
+_GEOM_NAMES = {0: "plane", 2: "sphere", 3: "capsule", 4: "ellipsoid", 5: "cylinder", 6: "box", 7: "mesh"}
+_SENSOR_TAGS = {1: "accelerometer", 2: "velocimeter", 3: "gyro", 9: "jointpos", 10: "jointvel", 30: "framepos",
+                31: "framequat", 34: "subtreecom", 35: "subtreelinvel", 36: "subtreeangmom"}
+_OBJ_NAMES = {1: "body", 2: "xbody", 3: "joint", 5: "geom", 6: "site"}
+_CONTACT_OBJ = {1: "body", 2: "subtree", 5: "geom"}
+
+
+def _fmt(v) -> str:
+  return " ".join(f"{float(x):.9g}" for x in np.asarray(v).reshape(-1))
+
+
+def model_to_mjcf(m) -> str:
+  """MJCF of a compiled model (mjlab_amd.spec.compiler.Model) that MuJoCo's
+  ``MjModel.from_xml_string`` compiles to the same bodies, dofs, geoms, sites,
+  actuators and sensors, in the same order (so an mjSTATE_PHYSICS vector of
+  this build restores with ``mj_setState``). Every body gets its compiled
+  inertial explicitly; visual mesh geoms (no mesh data on this path) become
+  massless non-colliding spheres so geom indices are kept. Used by the NaN
+  guard in place of ``mj_saveModel`` (reference utils/nan_guard.py:156)."""
+  names = m.names
+  nb = int(m.nbody)
+  children: dict[int, list[int]] = {i: [] for i in range(nb)}
+  for b in range(1, nb):
+    children[int(m.body_parentid[b])].append(b)
+  geoms_of: dict[int, list[int]] = {i: [] for i in range(nb)}
+  for g in range(int(m.ngeom)):
+    geoms_of[int(m.geom_bodyid[g])].append(g)
+  sites_of: dict[int, list[int]] = {i: [] for i in range(nb)}
+  for s in range(int(m.nsite)):
+    sites_of[int(m.site_bodyid[s])].append(s)
+  out = ['<mujoco model="mjlab_amd export">', '  <compiler angle="radian" autolimits="false" inertiafromgeom="false"/>',
+         f'  <option timestep="{m.timestep:.9g}" gravity="{_fmt(m.gravity)}" impratio="{m.impratio:.9g}" '
+         f'tolerance="{m.tolerance:.9g}" ls_tolerance="{m.ls_tolerance:.9g}" iterations="{int(m.iterations)}" '
+         f'ls_iterations="{int(m.ls_iterations)}" integrator="{ {0: "Euler", 3: "implicitfast"}.get(int(m.integrator), "Euler") }" '
+         f'cone="{ {0: "pyramidal", 1: "elliptic"}[int(m.cone)] }" solver="{ {0: "PGS", 1: "CG", 2: "Newton"}[int(m.solver)] }"/>',
+         "  <worldbody>"]
+
+  def geom_xml(g: int, ind: str) -> str:
+    t = int(m.geom_type[g])
+    nm = f' name="{names["geom"][g]}"' if names["geom"][g] else ""
+    common = (f' pos="{_fmt(m.geom_pos[g])}" quat="{_fmt(m.geom_quat[g])}" group="{int(m.geom_group[g])}" '
+              f'rgba="{_fmt(m.geom_rgba[g])}"')
+    if t == 7:  # visual mesh without mesh data: an inert placeholder keeps the index
+      return f'{ind}<geom{nm} type="sphere" size="0.001" contype="0" conaffinity="0" mass="0"{common}/>'
+    size = np.asarray(m.geom_size[g])
+    sz = {0: size[:3], 2: size[:1], 3: size[:2], 4: size[:3], 5: size[:2], 6: size[:3]}[t]
+    if t == 0:
+      sz = [max(float(size[0]), 0.0), max(float(size[1]), 0.0), max(float(size[2]), 0.01)]
+    return (f'{ind}<geom{nm} type="{_GEOM_NAMES[t]}" size="{_fmt(sz)}"{common} contype="{int(m.geom_contype[g])}" '
+            f'conaffinity="{int(m.geom_conaffinity[g])}" condim="{int(m.geom_condim[g])}" '
+            f'priority="{int(m.geom_priority[g])}" friction="{_fmt(m.geom_friction[g])}" solmix="{float(m.geom_solmix[g]):.9g}" '
+            f'solref="{_fmt(m.geom_solref[g])}" solimp="{_fmt(m.geom_solimp[g])}" margin="{float(m.geom_margin[g]):.9g}" '
+            f'gap="{float(m.geom_gap[g]):.9g}" mass="0"/>')
+
+  def body_xml(b: int, depth: int) -> None:
+    ind = "  " * (depth + 2)
+    if b != 0:
+      moc = ' mocap="true"' if int(m.body_mocapid[b]) >= 0 else ""
+      out.append(f'{ind}<body name="{names["body"][b]}" pos="{_fmt(m.body_pos[b])}" quat="{_fmt(m.body_quat[b])}"{moc}>')
+      if float(m.body_mass[b]) > 0:
+        out.append(f'{ind}  <inertial pos="{_fmt(m.body_ipos[b])}" quat="{_fmt(m.body_iquat[b])}" '
+                   f'mass="{float(m.body_mass[b]):.9g}" diaginertia="{_fmt(np.maximum(m.body_inertia[b], 1e-12))}"/>')
+      ja, jn = int(m.body_jntadr[b]), int(m.body_jntnum[b])
+      for j in range(ja, ja + jn if ja >= 0 else ja):
+        t = int(m.jnt_type[j])
+        if t == 0:
+          out.append(f'{ind}  <freejoint name="{names["joint"][j]}"/>')
+          continue
+        d = int(m.jnt_dofadr[j])
+        lim = "true" if int(m.jnt_limited[j]) else "false"
+        out.append(f'{ind}  <joint name="{names["joint"][j]}" type="{ {2: "slide", 3: "hinge"}[t] }" pos="{_fmt(m.jnt_pos[j])}" '
+                   f'axis="{_fmt(m.jnt_axis[j])}" limited="{lim}" range="{_fmt(m.jnt_range[j])}" '
+                   f'ref="{float(m.qpos0[int(m.jnt_qposadr[j])]):.9g}" springref="{float(m.qpos_spring[int(m.jnt_qposadr[j])]):.9g}" '
+                   f'stiffness="{float(m.jnt_stiffness[j]):.9g}" armature="{float(m.dof_armature[d]):.9g}" '
+                   f'damping="{float(m.dof_damping[d]):.9g}" frictionloss="{float(m.dof_frictionloss[d]):.9g}" '
+                   f'margin="{float(m.jnt_margin[j]):.9g}" solreflimit="{_fmt(m.jnt_solref[j])}" '
+                   f'solimplimit="{_fmt(m.jnt_solimp[j])}" solreffriction="{_fmt(m.dof_solref[d])}" '
+                   f'solimpfriction="{_fmt(m.dof_solimp[d])}"/>')
+    for g in geoms_of[b]:
+      out.append(geom_xml(g, ind + ("  " if b else "")))
+    for s in sites_of[b]:
+      nm = f' name="{names["site"][s]}"' if names["site"][s] else ""
+      out.append(f'{ind}{"  " if b else ""}<site{nm} pos="{_fmt(m.site_pos[s])}" quat="{_fmt(m.site_quat[s])}"/>')
+    for c in children[b]:
+      body_xml(c, depth + (1 if b else 0))
+    if b != 0:
+      out.append(f"{ind}</body>")
+
+  body_xml(0, 0)
+  out.append("  </worldbody>")
+  # the compiled pair table is the authority: parent/weld/contype filters are
+  # recomputed by MuJoCo, the spec's <exclude> pairs are re-emitted
+  excl = getattr(m, "excludes", [])
+  if excl:
+    out.append("  <contact>")
+    out += [f'    <exclude body1="{a}" body2="{b}"/>' for a, b in excl]
+    out.append("  </contact>")
+  if int(m.nu):
+    out.append("  <actuator>")
+    for i in range(int(m.nu)):
+      j = int(m.actuator_trnid[i])
+      out.append(f'    <general name="{names["actuator"][i]}" joint="{names["joint"][j]}" gear="{float(m.actuator_gear[i]):.9g}" '
+                 f'gaintype="fixed" biastype="affine" gainprm="{_fmt(m.actuator_gainprm[i][:3])}" '
+                 f'biasprm="{_fmt(m.actuator_biasprm[i][:3])}" ctrllimited="{"true" if int(m.actuator_ctrllimited[i]) else "false"}" '
+                 f'ctrlrange="{_fmt(m.actuator_ctrlrange[i])}" forcelimited="{"true" if int(m.actuator_forcelimited[i]) else "false"}" '
+                 f'forcerange="{_fmt(m.actuator_forcerange[i])}"/>')
+    out.append("  </actuator>")
+  if int(m.nsensor):
+    out.append("  <sensor>")
+    for s in range(int(m.nsensor)):
+      t, ot, oid = int(m.sensor_type[s]), int(m.sensor_objtype[s]), int(m.sensor_objid[s])
+      nm = names["sensor"][s]
+      cut = float(m.sensor_cutoff[s])
+      cut_a = f' cutoff="{cut:.9g}"' if cut > 0 else ""
+      if t == 40:  # mjSENS_CONTACT (MuJoCo >= 3.3): intprm = [1 << field bits, reduce, num]
+        bits, red, num = (int(x) for x in m.sensor_intprm[s])
+        fields = " ".join(f for k, f in enumerate(("found", "force", "torque", "dist", "pos", "normal", "tangent")) if bits & (1 << k))
+        o1 = f' {_CONTACT_OBJ[ot]}1="{names["geom" if ot == 5 else "body"][oid]}"'
+        rt, rid = int(m.sensor_reftype[s]), int(m.sensor_refid[s])
+        o2 = f' {_CONTACT_OBJ[rt]}2="{names["geom" if rt == 5 else "body"][rid]}"' if rid >= 0 and rt in _CONTACT_OBJ else ""
+        out.append(f'    <contact name="{nm}"{o1}{o2} data="{fields}" '
+                   f'reduce="{ {0: "none", 1: "mindist", 2: "maxforce", 3: "netforce"}[red] }" num="{num}"/>')
+        continue
+      kind = _OBJ_NAMES[ot]
+      attr = {"site": "site", "joint": "joint", "body": "body", "xbody": "body"}[kind]
+      obj = names["site" if kind == "site" else "joint" if kind == "joint" else "body"][oid]
+      if t in (30, 31):
+        out.append(f'    <{_SENSOR_TAGS[t]} name="{nm}" objtype="site" objname="{obj}"{cut_a}/>')
+      else:
+        out.append(f'    <{_SENSOR_TAGS[t]} name="{nm}" {attr}="{obj}"{cut_a}/>')
+    out.append("  </sensor>")
+  out.append("</mujoco>")
+  return "\n".join(out) + "\n"

@@ -48,3 +48,32 @@ def test_g1_keyframe_and_inertia():
   assert (m.body_mass[2:] > 0).all()
   assert 30.0 < m.body_mass.sum() < 40.0  # G1 29-dof total mass ~33 kg
   assert m.meaninertia > 0
+
+
+def test_model_to_mjcf_round_trip():
+  """The NaN guard's model file (spec.mjcf.model_to_mjcf): read back and
+  compiled, it reproduces the compiled model (mesh geoms become inert
+  placeholder spheres, so geom type/size of those are excluded)."""
+  import numpy as np
+
+  from mjlab_amd.spec.compiler import compile_spec
+  from mjlab_amd.spec.mjcf import model_to_mjcf, read_mjcf_string
+  from tests.scenes import g1_sensor_scene, go1_scene
+
+  for scene in (g1_sensor_scene(2), go1_scene(2)):
+    m = scene.compile(50, 300)
+    m2 = compile_spec(read_mjcf_string(model_to_mjcf(m)), 50, 300)
+    assert m2.names == m.names
+    mesh = np.asarray(m.geom_type) == 7
+    for k in ("body_parentid", "body_pos", "body_quat", "body_ipos", "body_iquat", "body_mass", "body_inertia",
+              "jnt_type", "jnt_qposadr", "jnt_dofadr", "jnt_pos", "jnt_axis", "jnt_range", "jnt_limited", "qpos0",
+              "dof_armature", "dof_damping", "dof_invweight0", "body_invweight0", "geom_bodyid", "geom_pos",
+              "geom_quat", "geom_friction", "geom_contype", "geom_conaffinity", "geom_condim", "geom_priority",
+              "site_bodyid", "site_pos", "site_quat", "actuator_trnid", "actuator_gainprm", "actuator_biasprm",
+              "actuator_ctrlrange", "actuator_forcerange", "sensor_type", "sensor_objtype", "sensor_objid",
+              "sensor_reftype", "sensor_refid", "sensor_adr", "sensor_dim", "sensor_intprm", "pair_geom1", "pair_geom2"):
+      a, b = np.asarray(getattr(m, k)), np.asarray(getattr(m2, k))
+      np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7, err_msg=k)
+    np.testing.assert_allclose(np.asarray(m.geom_size)[~mesh], np.asarray(m2.geom_size)[~mesh], rtol=1e-6, err_msg="geom_size")
+    np.testing.assert_array_equal(np.asarray(m.geom_type)[~mesh], np.asarray(m2.geom_type)[~mesh])
+    assert abs(m.meaninertia - m2.meaninertia) < 1e-9 * m.meaninertia

@@ -1,6 +1,7 @@
 """NaN guard (utils/nan_guard.py semantics): rolling mjSTATE_PHYSICS buffer,
 detection over qpos/qvel/qacc/qacc_warmstart, npz dump of the first
-max_envs_to_dump non-finite worlds, loadable without pickle."""
+max_envs_to_dump non-finite worlds with the reference's metadata dict, and the
+model as MJCF that compiles back to the same model."""
 
 import json
 from types import SimpleNamespace
@@ -46,8 +47,11 @@ def test_dump_on_nan_injection(tmp_path):
       pass
     assert guard.check_and_dump(d) is False  # dumps once
   np.testing.assert_array_equal(NanGuard.detect_nans(d).numpy(), [0, 0, 1, 0, 0, 1, 0, 1])
-  z = np.load(tmp_path / "nan_dump_latest.npz")  # no pickle needed
-  meta = json.loads(str(z["_metadata"]))
+  from mjlab_amd.utils.nan_guard import load_nan_dump
+
+  meta, states, model_file = load_nan_dump(tmp_path / "nan_dump_latest.npz")
+  z = np.load(tmp_path / "nan_dump_latest.npz", allow_pickle=True)
+  assert isinstance(z["_metadata"].item(), dict)  # scripts/nan_viz.py:31 reads it with .item()
   assert meta["nan_env_ids"] == [2, 5, 7] and meta["dumped_env_ids"] == [2, 5]
   assert meta["state_size"] == m.nq + m.nv and meta["buffer_size"] == 3 and meta["detection_step"] == 5
   steps = sorted(k for k in z.files if k.startswith("states_step_"))
@@ -55,7 +59,8 @@ def test_dump_on_nan_injection(tmp_path):
   for s in steps:
     k = int(s[-6:])
     np.testing.assert_array_equal(z[s], hist[k][[2, 5]])
-  assert (tmp_path / meta["model_file"]).exists()
+  assert model_file.exists() and model_file.suffix == ".xml"
+  assert sorted(states) == [2, 3, 4]
   assert guard.tripped.tolist() == [2, 5, 7]
 
 
@@ -74,5 +79,5 @@ def test_simulation_step_dumps_on_nan(tmp_path):
   assert not (tmp_path / "nan_dump_latest.npz").exists()
   sim.data.qvel[3, 10] = float("nan")
   sim.step()
-  meta = json.loads(str(np.load(tmp_path / "nan_dump_latest.npz")["_metadata"]))
+  meta = np.load(tmp_path / "nan_dump_latest.npz", allow_pickle=True)["_metadata"].item()
   assert 3 in meta["nan_env_ids"] and meta["num_envs_total"] == n
