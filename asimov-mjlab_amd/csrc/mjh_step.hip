@@ -900,7 +900,13 @@ __host__ __device__ __forceinline__ DataOff data_offsets(const Sizes& Z) {
 template <int K> __device__ __forceinline__ Layout spec_layout(const Layout& a) { return a; }
 template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) { return a; }
 
+// MJH_SPEC_TABLE: an alternative table (A/B builds of kernel variants whose
+// launch plans differ, tools/build_variant.py)
+#ifdef MJH_SPEC_TABLE
+#include MJH_SPEC_TABLE
+#else
 #include "mjh_spec_table.h"
+#endif
 
 // ---- the step kernel --------------------------------------------------------
 #ifndef MJH_MINWAVES

@@ -13,11 +13,21 @@ def shard_seed(base_seed: int, rank: int) -> int:
   return base_seed + rank
 
 
-def pack_step_outputs(obs: dict, reward: torch.Tensor, terminated: torch.Tensor, truncated: torch.Tensor) -> torch.Tensor:
-  """(num_envs, D) float32: [obs groups in key order | reward | terminated | truncated]."""
+def packed_width(obs_dims: dict) -> int:
+  """Columns of the packed step outputs for observation groups of these widths."""
+  return sum(int(obs_dims[k]) for k in sorted(obs_dims)) + 3
+
+
+def pack_step_outputs(obs: dict, reward: torch.Tensor, terminated: torch.Tensor, truncated: torch.Tensor,
+                      out: torch.Tensor | None = None) -> torch.Tensor:
+  """(num_envs, D) float32: [obs groups in key order | reward | terminated | truncated].
+  With ``out`` (preallocated, e.g. the env's graph-resident pack buffer) the
+  result is written in place: no allocation, capturable."""
   parts = [obs[k].reshape(obs[k].shape[0], -1).float() for k in sorted(obs)]
   parts += [reward[:, None].float(), terminated[:, None].float(), truncated[:, None].float()]
-  return torch.cat(parts, dim=1)
+  if out is None:
+    return torch.cat(parts, dim=1)
+  return torch.cat(parts, dim=1, out=out)
 
 
 class StepGather:
@@ -30,13 +40,20 @@ class StepGather:
 
   def __init__(self, group=None, dst: int | None = None) -> None:
     self.group = group
-    self.dst = dst
+    self.dst = dst  # rank within `group`
     self.world = dist.get_world_size(group) if dist.is_initialized() else 1
     self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+    # the collective takes a global rank (a subgroup's ranks need not be 0..k-1)
+    self._dst_global = (dist.get_global_rank(group, dst) if (group is not None and dst is not None) else dst)
     self.buf: torch.Tensor | None = None
 
   def __call__(self, obs, reward, terminated, truncated) -> torch.Tensor:
-    packed = pack_step_outputs(obs, reward, terminated, truncated)
+    return self.gather_packed(pack_step_outputs(obs, reward, terminated, truncated))
+
+  def gather_packed(self, packed: torch.Tensor) -> torch.Tensor | None:
+    """Exchange an already packed (num_envs, D) buffer — the env's graph-resident
+    pack buffer (ManagerBasedRlEnv.enable_step_pack) — stream-ordered after the
+    step, no host sync."""
     if self.world == 1:
       return packed
     if self.buf is None or self.buf.shape != (self.world * packed.shape[0], packed.shape[1]):
@@ -45,7 +62,7 @@ class StepGather:
       dist.all_gather_into_tensor(self.buf, packed.contiguous(), group=self.group)
       return self.buf
     if self.rank == self.dst:
-      dist.gather(packed.contiguous(), list(self.buf.chunk(self.world, dim=0)), dst=self.dst, group=self.group)
+      dist.gather(packed.contiguous(), list(self.buf.chunk(self.world, dim=0)), dst=self._dst_global, group=self.group)
       return self.buf
-    dist.gather(packed.contiguous(), None, dst=self.dst, group=self.group)
+    dist.gather(packed.contiguous(), None, dst=self._dst_global, group=self.group)
     return None

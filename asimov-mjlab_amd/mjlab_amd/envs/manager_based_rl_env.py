@@ -219,7 +219,22 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     self._graph_key = None
     self._graph_out = None
     self._eager_steps = 0
+    self._pack_buf: torch.Tensor | None = None
     self.metadata = dict(self.metadata, render_fps=1.0 / self.step_dt)
+
+  def enable_step_pack(self) -> torch.Tensor:
+    """Learner-facing outputs packed at the end of every env step, inside the
+    captured graph, into one persistent (num_envs, D) float32 buffer
+    [obs groups in key order | reward | terminated | truncated]
+    (mjlab_amd.distributed.pack_step_outputs): the multi-GPU exchange then
+    all-gathers this buffer with no per-step allocation."""
+    from mjlab_amd.distributed import packed_width
+
+    if self._pack_buf is None:
+      dims = {g: int(np.prod(d)) for g, d in self.observation_manager.group_obs_dim.items()}
+      self._pack_buf = torch.empty(self.num_envs, packed_width(dims), device=self.device)
+      self._graph = None  # re-capture with the pack at the end of the step
+    return self._pack_buf
 
   @property
   def max_episode_length_s(self) -> float:
@@ -336,6 +351,10 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     if "interval" in self.event_manager.available_modes:
       self.event_manager.apply(mode="interval", dt=self.step_dt)
     self.obs_buf = self.observation_manager.compute(update_history=True)
+    if self._pack_buf is not None:
+      from mjlab_amd.distributed import pack_step_outputs
+
+      pack_step_outputs(self.obs_buf, self.reward_buf, self.reset_terminated, self.reset_time_outs, out=self._pack_buf)
 
   def reset(self, *, seed: int | None = None, env_ids=None, options=None):
     del options

@@ -71,7 +71,7 @@ def parse() -> argparse.Namespace:
   p.add_argument("--task", default=TASK)
   p.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL all-gather (N > 1)")
   p.add_argument("--no-cpu-baseline", action="store_true")
-  p.add_argument("--cpu-sample-worlds", type=int, default=512)
+  p.add_argument("--cpu-sample-worlds", type=int, default=0, help="0: all of the workload's worlds")
   p.add_argument("--cpu-seconds", type=float, default=8.0, help="per precision")
   p.add_argument("--kernel-launches", type=int, default=50)
   p.add_argument("--motion-file", default="", help="tracking tasks: motion npz (default: synthetic 500-frame clip)")
@@ -110,18 +110,27 @@ def synthetic_motion_file(dev: str, frames: int = 500) -> str:
   return str(path)
 
 
+def _host_threads() -> tuple[int, int]:
+  """(threads used, host cores in this process's affinity). The threads are the
+  affinity's cores unless OMP_NUM_THREADS says otherwise (on the GPU box it is
+  set to the box's CPU share: the machine's other cores belong to other jobs)."""
+  try:
+    host = len(os.sched_getaffinity(0))
+  except AttributeError:
+    host = os.cpu_count() or 1
+  omp = os.environ.get("OMP_NUM_THREADS")
+  return (max(1, min(host, int(omp))) if omp else host), host
+
+
 def cpu_baseline(env, args) -> dict:
   """Time the oracle (CPU restatement of the same physics step, OpenMP over
-  worlds) on a bounded sample of this workload's worlds, float64 then float32."""
+  worlds) on the workload's worlds (all N of them, from the bench's live
+  state), float64 then float32, for a bounded time each."""
   sys.path.insert(0, str(REPO))
   from oracle.oracle import Oracle
 
-  try:
-    cores = len(os.sched_getaffinity(0))
-  except AttributeError:
-    cores = os.cpu_count() or 1
-  cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
-  n = min(args.cpu_sample_worlds, env.num_envs)
+  cores, host = _host_threads()
+  n = min(args.cpu_sample_worlds, env.num_envs) if args.cpu_sample_worlds > 0 else env.num_envs
   d = env.sim.data
   state0 = {k: getattr(d, k)[:n].detach().cpu().numpy() for k in ("qpos", "qvel", "act", "qacc_warmstart", "ctrl", "qfrc_applied", "xfrc_applied", "time")}
   overrides = {}
@@ -150,12 +159,65 @@ def cpu_baseline(env, args) -> dict:
     "value": v64,
     "unit": "env steps/sec (physics only: decimation x mj_step per env step)",
     "cores": cores,
+    "host_cores": host,
     "kind": "port",
     "value_f32": v32,
-    "sample": f"{n} {env.sim.mj_model.nv}-dof worlds from the bench's live state, oracle/oracle.c with OpenMP {cores} threads: "
+    "sample": f"all {n} {env.sim.mj_model.nv}-dof worlds of the workload from the bench's live state, oracle/oracle.c "
+    f"with OpenMP {cores} threads ({host} cores in the affinity, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}): "
     f"float64 {r64} physics steps ({e64:.1f} s) -> value; float32 {r32} steps ({e32:.1f} s) -> value_f32; "
     "env-layer cost excluded; MuJoCo C is not available",
   }
+
+
+def cpu_config1(args) -> dict:
+  """BASELINE.json config 1: Mjlab-Velocity-Flat-Unitree-G1, num_envs=1, zero
+  agent (scripts/play.py:212-215), the whole env step on the CPU: mjlab_amd's
+  env layer on CPU tensors with the oracle's float64 physics standing in for
+  MuJoCo C's mj_step (absent). One thread. Timed for --cpu-seconds."""
+  import torch
+
+  sys.path.insert(0, str(REPO))
+  from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
+  from mjlab_amd.tasks import load_env_cfg
+  from oracle.oracle import INPUTS, Oracle
+
+  nthr = torch.get_num_threads()
+  torch.set_num_threads(1)
+  try:
+    cfg = load_env_cfg(TASK)
+    cfg.scene.num_envs = 1
+    cfg.seed = 42
+    env = ManagerBasedRlEnv(cfg, device="cpu")
+    sim = env.sim
+    ov = {f: getattr(sim.model, f).numpy() for f in env.event_manager.domain_randomization_fields}
+    orc = Oracle(sim.mj_model, "f64", overrides=ov)
+    fields = [f for f in INPUTS if f in sim._data_flat]
+
+    def run(integrate: bool) -> None:
+      sim.epoch.bump()
+      out = orc.run(1, {f: sim._data_flat[f].numpy() for f in fields}, integrate=integrate)
+      for f, t in sim._data_flat.items():
+        if f in out and t.numel():
+          t.copy_(torch.as_tensor(out[f].reshape(1, -1)[:, : t.shape[1]]).to(t.dtype))
+
+    sim._require_gpu = lambda: None
+    sim.step = lambda: run(True)
+    sim.forward = lambda: run(False)
+    sim.forward_gated = lambda gate: run(False) if bool(gate.any()) else None
+    env.reset()
+    zero = torch.zeros(1, env.action_manager.total_action_dim)
+    for _ in range(10):
+      env.step(zero)
+    k, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+      env.step(zero)
+      k += 1
+    el = time.perf_counter() - t0
+  finally:
+    torch.set_num_threads(nthr)
+  return {"value": k / el, "unit": "env steps/s", "cores": 1, "kind": "port", "steps": k,
+          "sample": f"config 1: {TASK}, num_envs=1, zero agent, {k} full env steps in {el:.1f} s on one host thread "
+          "(env layer on CPU tensors + oracle float64 physics; MuJoCo C is not available)"}
 
 
 def main() -> None:
@@ -204,10 +266,13 @@ def main() -> None:
 
   gather = StepGather()
   use_gather = world > 1 and not args.no_gather
+  # learner-facing outputs packed by the env step itself (inside its graph),
+  # then all-gathered over RCCL, stream-ordered after the replay (no host sync)
+  packed = env.enable_step_pack() if use_gather else None
 
   def exchange(obs, rew, term, trunc):
     if use_gather:
-      gather(obs, rew, term, trunc)
+      gather.gather_packed(packed)
 
   # graph capture happens on the 2nd step; settle + warmup steps are untimed
   for _ in range(2 + args.settle + args.warmup):
@@ -215,6 +280,7 @@ def main() -> None:
     exchange(o, r, te, tr)
   torch.cuda.synchronize()
   stats0 = env.step_stats().clone()
+  flags0 = env.sim.flag_stats()[3:].clone()  # running totals of worlds that overflowed / went non-finite
   if world > 1:
     dist.barrier()
   torch.cuda.synchronize()
@@ -231,6 +297,7 @@ def main() -> None:
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
   stats = (env.step_stats() - stats0).double().cpu()
+  flags = (env.sim.flag_stats()[3:] - flags0).cpu().tolist()  # world-passes in the timed window
   resets_per_step = float(stats[0]) / args.steps
   gate_rate = float(stats[1]) / args.steps
   n_total = num_envs * world
@@ -276,12 +343,29 @@ def main() -> None:
   nv = sim.mj_model.nv
   b_solve = niter * 4 * (nefc * nv + nv * nv + 6 * nefc + 4 * nv) + 4 * (nefc + 2 * nv)
 
+  # algorithmic FLOPs per env step (SURVEY §8d / BASELINE.md): smooth dynamics,
+  # collision over the pair table, and per Newton iteration the Hessian
+  # (nefc nv(nv+1)), the factor (nv^3/3), gradient/J products (4 nefc nv) and
+  # the line search (6 ls nefc, ls ~ 3 evaluations), with this run's mean nefc
+  # and iterations; x decimation physics steps (+ the gated forward's pass)
+  npair = int(sim.mj_model.npair)
+  f_phys = 60e3 + 150 * npair + niter * (nefc * nv * (nv + 1) + nv ** 3 / 3 + 4 * nefc * nv + 6 * 3 * nefc)
+  f_env = f_phys * (env.cfg.decimation + gate_rate)
+  flops = {"per_env_step": f_env, "achieved_tflops": f_env * value / 1e12, "fp32_vector_peak_tflops": 157.3,
+           "model": "60k + 150 npair + iters (nefc nv(nv+1) + nv^3/3 + 4 nefc nv + 18 nefc) per physics pass, "
+                    "x (decimation + forward_gate_rate); mean nefc/iters of this run"}
+
   cpu = None
   if rank == 0 and world == 1 and not args.no_cpu_baseline:
     try:
       cpu = cpu_baseline(env, args)
     except Exception as e:  # noqa: BLE001 - a missing oracle build must not void the GPU line
       cpu = {"value": None, "unit": "env steps/sec", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
+    if args.task == TASK:
+      try:
+        cpu["config1"] = cpu_config1(args)
+      except Exception as e:  # noqa: BLE001
+        cpu["config1"] = {"value": None, "sample": f"unavailable: {e}"}
 
   if rank == 0:
     line = {
@@ -312,7 +396,15 @@ def main() -> None:
         "gather_ms_per_step": gather_ms,
         "mean_nefc": nefc,
         "mean_solver_iters": niter,
+        "efc_capacity": sim.efc_capacity(),
+        "njmax": int(sim.mj_model.njmax),
+        "nconmax": int(sim.mj_model.nconmax),
+        "contact_overflow_worlds": int(flags[0]),
+        "efc_overflow_worlds": int(flags[1]),
+        "nonfinite_worlds": int(flags[2]),
+        "overflow_window": f"world-physics-passes flagged over the {args.steps} timed env steps (5 passes each)",
       },
+      "flops": flops,
       "roofline": {
         "bound": "hbm",
         "achieved": achieved,

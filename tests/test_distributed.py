@@ -96,6 +96,7 @@ def _run_shard(rank, gather, n=3, steps=3):
   env = ManagerBasedRlEnv(cfg, device="cpu")
   oracle_sim.attach(env.sim, env.event_manager.domain_randomization_fields)
   env.reset()
+  packed = env.enable_step_pack()  # written by the env step itself (inside the graph on the GPU)
   g = torch.Generator().manual_seed(1234 + rank)
   sg = StepGather() if gather else None
   outs = []
@@ -103,7 +104,8 @@ def _run_shard(rank, gather, n=3, steps=3):
     a = 2 * torch.rand(n, env.action_manager.total_action_dim, generator=g) - 1
     obs, rew, term, trunc, _ = env.step(a)
     own = pack_step_outputs(obs, rew, term, trunc).clone()
-    outs.append((own, sg(obs, rew, term, trunc).clone() if sg else None))
+    assert torch.equal(own, packed)
+    outs.append((own, sg.gather_packed(packed).clone() if sg else None))
   return outs
 
 
@@ -127,3 +129,41 @@ def test_env_shards_world2_match_single_process():
       assert torch.equal(own, single[t][0]), (r, t)
       full = torch.cat([res[k][t][0] for k in range(world)], dim=0)
       assert torch.equal(gathered, full)
+
+
+def _subgroup_worker(rank, world, port, q):
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  sub = dist.new_group([1, 2])  # group ranks 0, 1 = global ranks 1, 2
+  res = None
+  if rank in (1, 2):
+    n = 2
+    obs = {"policy": torch.full((n, 2), float(rank))}
+    rew = torch.full((n,), 10.0 * rank)
+    z = torch.zeros(n, dtype=torch.bool)
+    sg = StepGather(group=sub, dst=0)
+    out = sg(obs, rew, z, z)
+    res = None if out is None else out.numpy().copy()
+  q.put((rank, res))
+  dist.destroy_process_group()
+
+
+def test_step_gather_to_learner_in_a_subgroup():
+  """dst is a group rank; the collective needs its global rank."""
+  world = 3
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  port = _free_port()
+  ps = [ctx.Process(target=_subgroup_worker, args=(r, world, port, q)) for r in range(world)]
+  for p in ps:
+    p.start()
+  res = dict(q.get(timeout=120) for _ in range(world))
+  for p in ps:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  assert res[0] is None and res[2] is None
+  got = torch.from_numpy(res[1])
+  assert got.shape == (4, 2 + 3)
+  assert got[:2, 0].tolist() == [1.0, 1.0] and got[2:, 0].tolist() == [2.0, 2.0]
+  assert got[:2, 2].tolist() == [10.0, 10.0] and got[2:, 2].tolist() == [20.0, 20.0]

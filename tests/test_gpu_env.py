@@ -168,3 +168,24 @@ def test_reset_with_seed_reproduces_device_draws():
     assert torch.equal(a, b)
   env.reset(seed=6)
   assert not torch.equal(env.sim.data.qpos, snaps[0][0])
+
+
+def test_config1_single_env_zero_agent_against_oracle():
+  """BASELINE.json config 1 (G1 flat velocity, num_envs=1, zero agent,
+  scripts/play.py:212-215) on the HIP path: the eager env step with every
+  physics pass shadowed by the float64 oracle (tests/refsim.Shadow tolerances)."""
+  from tests.refsim import Shadow
+
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = 1
+  cfg.seed = 42
+  env = ManagerBasedRlEnv(cfg, device="cuda:0", use_graph=False)
+  sh = Shadow(env.sim)
+  env.reset()
+  zero = torch.zeros(1, 29, device="cuda:0")
+  for _ in range(30):
+    obs, rew, term, trunc, _ = env.step(zero)
+  assert sh.nsteps >= 30 * 4
+  assert torch.isfinite(obs["policy"]).all() and torch.isfinite(rew).all()
+  # the zero agent holds the default pose: still standing after 30 env steps
+  assert not bool(term.any())
