@@ -1185,6 +1185,9 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
 
   // ---------------------------------------------------------------- com_pos
   PROF(1);
+#if MJH_DEBUG_STOP == 1
+  return;
+#endif
   const unsigned long long* tmk = reinterpret_cast<const unsigned long long*>(IMG_L(body_treemask));
   const unsigned long long* dmk = reinterpret_cast<const unsigned long long*>(IMG_L(body_dofmask));
   // lane b holds body b's chain mask; the subtree loops read it by readlane
@@ -1346,6 +1349,9 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     ldl_factor_rows<NVP>(a, Lm, nv, ldm);
   }
   PROF(2);
+#if MJH_DEBUG_STOP == 2
+  return;
+#endif
 
   // ---------------------------------------------------------------- com_vel / rne (bias)
   const float r_qv = tid < nv ? qvel[tid] : 0.f;
@@ -1503,6 +1509,9 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   PROF(25);
   ldl_solve_reg<NVP>(Lm, nv, ldm, qacc_smooth);
   PROF(3);
+#if MJH_DEBUG_STOP == 3
+  return;
+#endif
 
   // ---------------------------------------------------------------- collision
   {
@@ -1591,6 +1600,10 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   }
   const int ncon = ints[I_NCON];
   PROF(4);
+#if MJH_DEBUG_STOP == 4
+  if (tid == 0) DP(ncon)[W] = ncon;
+  return;
+#endif
 
   // ---------------------------------------------------------------- make_constraint
   {
@@ -1807,6 +1820,10 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   }
   const int nefc = ints[I_NEFC];
   PROF(5);
+#if defined(MJH_DEBUG_STOP_AFTER_CONSTRAINTS) || MJH_DEBUG_STOP == 5
+  if (tid == 0) DP(nefc)[W] = nefc;
+  return;
+#endif
 
   // ---------------------------------------------------------------- Newton solver
   const float scale = 1.f / (m.meaninertia * (float)(nv > 1 ? nv : 1));
