@@ -26,6 +26,7 @@
 
 #include "../../include/mjh_abi.h"
 #include "mjh_math.h"
+#include "mjh_rng.h"
 
 using namespace mjh;
 
@@ -47,6 +48,11 @@ struct Layout {
   int red, ints;
   int total, gtotal;  // per-world words: LDS, global scratch
   int ncap, rcap;
+  // split step (MODE 1 position kernel -> MODE 2 velocity/solver kernel): the
+  // position kernel's outputs that the full kernel keeps in LDS go through a
+  // per-world global handoff region, plus the reuse snapshot
+  int h_L, h_type, h_fl, h_D, h_R, h_aref, h_b, h_jv, h_ints, h_snap;
+  int pred, pints, ptotal;  // the position kernel's per-world LDS (qpos + reductions)
 };
 
 enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
@@ -112,6 +118,13 @@ struct Rg {
 thread_local std::string g_err;
 bool g_disable_spec = false;  // mjh_set_specialization(0): always the generic instance
 bool g_auto_order = false;    // mjh_set_world_ordering(1): order the worlds in the pack launch
+bool g_pos_reuse = true;      // mjh_set_position_reuse: split position pass skips unchanged worlds
+#ifndef MJH_SPLIT
+#define MJH_SPLIT 0
+#endif
+#ifndef MJH_PWPB
+#define MJH_PWPB 8
+#endif
 
 #ifdef MJH_PROFILE
 __device__ unsigned long long* g_prof;
@@ -839,6 +852,37 @@ __device__ __forceinline__ void row_params(float timestep, float pos_aref, float
   *aref = -k * imp * pos_aref - b * jqvel;
 }
 
+// The position-dependent part of row_params: D, R, aref_pos = -k imp pos and
+// the damping coefficient b; the velocity stage completes aref = aref_pos - b J qvel
+__device__ __forceinline__ void row_params_pos(float timestep, float pos_aref, float pos_imp, float invweight,
+                                               const float* solref, const float* solimp, float* D, float* R,
+                                               float* arefp, float* bb) {
+  float timeconst = solref[0], dampratio = solref[1];
+  if (solref[0] > 0.f && timeconst < 2.f * timestep) timeconst = 2.f * timestep;
+  float dmin = clampf(solimp[0], MJH_MINIMP, MJH_MAXIMP);
+  float dmax = clampf(solimp[1], MJH_MINIMP, MJH_MAXIMP);
+  float width = fmaxf(solimp[2], MJH_MINVAL);
+  float mid = clampf(solimp[3], MJH_MINIMP, MJH_MAXIMP);
+  float power = fmaxf(solimp[4], 1.f);
+  float k = 1.f / (dmax * dmax * timeconst * timeconst * dampratio * dampratio);
+  float b = 2.f / (dmax * timeconst);
+  if (solref[0] <= 0.f) k = -solref[0] / (dmax * dmax);
+  if (solref[1] <= 0.f) b = -solref[1] / dmax;
+  float x = fabsf(pos_imp) / width, imp;
+  if (x > 1.f) {
+    imp = dmax;
+  } else {
+    float y = x < mid ? powf(x, power) / powf(mid, power - 1.f)
+                      : 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
+    imp = clampf(dmin + y * (dmax - dmin), dmin, dmax);
+  }
+  float r = fmaxf(invweight * (1.f - imp) / imp, MJH_MINVAL);
+  *R = r;
+  *D = 1.f / r;
+  *arefp = -k * imp * pos_aref;
+  *bb = b;
+}
+
 // constraint state at jaref: writes force, returns Hessian weight (0 if inactive/linear)
 __device__ __forceinline__ float row_state(int type, float D, float R, float fl, float jaref, float* force, float* cost) {
   if (type == MJH_CNSTR_FRICTION_DOF) {
@@ -909,12 +953,25 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 #endif
 
 // ---- the step kernel --------------------------------------------------------
+#ifndef MJH_PMINWAVES
+#define MJH_PMINWAVES 1
+#endif
 #ifndef MJH_MINWAVES
 #define MJH_MINWAVES 1
 #endif
-template <int WPB, bool STEP, int NVP, int SPEC = -1, bool SLAB = false>
-__global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo_,
-                                                         const ImgOff Io_, const unsigned char* gate) {
+// MODE 0: the whole step in one launch. MODE 1: the position stage only
+// (kinematics, com, CRB, M and its factor, collision, constraint rows and their
+// position-dependent parameters), results to the global handoff region; a world
+// whose qpos, mocap poses and model are unchanged since its last position pass
+// (reuse != 0) exits at once: the pass's results are still in its scratch.
+// MODE 2: everything else (velocity stage, solver, sensors, outputs,
+// integration), starting from the handoff region. Split, the position stage
+// needs far fewer registers and LDS, so it runs at higher occupancy, and the
+// first physics step after a gated forward skips it.
+template <int WPB, bool STEP, int NVP, int SPEC = -1, bool SLAB = false, int MODE = 0>
+__global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo_,
+                                                         const ImgOff Io_, const unsigned char* gate, int reuse,
+                                                         unsigned long long key) {
   constexpr int NT = 64;  // one wave per world
   const Layout Lo = spec_layout<SPEC>(Lo_);
   const ImgOff Io = spec_imgoff<SPEC>(Io_);
@@ -933,20 +990,37 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   }
   __syncthreads();
   const int wave = threadIdx.x >> 6;
+  // position pass: a hash of the model image this workgroup staged (every
+  // workgroup computes the same value), part of the reuse snapshot
+  unsigned long long img_hash = 0ull;
+  if constexpr (MODE == 1) {
+    __shared__ unsigned long long hpart[WPB];
+    const unsigned* iw = reinterpret_cast<const unsigned*>(smem);
+    unsigned long long h = 0ull;
+    for (int i = threadIdx.x; i < Io.img_words; i += 64 * WPB) h += mix64(((unsigned long long)i << 32) | iw[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+    if ((threadIdx.x & 63) == 0) hpart[wave] = h;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < WPB; k++) img_hash += hpart[k];
+  }
   const int slot = blockIdx.x * WPB + wave;
   if (slot >= d.nworld) return;
   // optional cost-sorted world order: a workgroup's worlds then take similar
-  // time, so its LDS is not held hostage by one slow world
-  const int w = d.world_order ? (int)d.world_order[slot] : slot;
+  // time, so its LDS is not held hostage by one slow world (the position pass,
+  // of nearly uniform cost, keeps the identity order)
+  const int w = (MODE != 1 && d.world_order) ? (int)d.world_order[slot] : slot;
   const int tid = threadIdx.x & 63;
-  float* S = smem + Io.img_words + wave * Lo.total;
+  float* S = smem + Io.img_words + wave * (MODE == 1 ? Lo.ptotal : Lo.total);
   int* SI = reinterpret_cast<int*>(S);
   float* G = d.scratch + (long long)w * d.scratch_words;  // this world's global scratch
   const long long W = w;
   const int nq = Z.nq, nv = Z.nv, nb = Z.nbody, nu = Z.nu, nj = Z.njnt;
   const int ldm = Lo.ldm, ldj = Lo.ldj;
 
-  float* qpos = SP(qpos);
+  constexpr bool HO = MODE == 1;
+  float* qpos = HO ? S : SP(qpos);
   float* qvel = SP(qvel);
   float* qacc = SP(qacc);
   float* qacc_smooth = SP(qacc_smooth);
@@ -983,7 +1057,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   float* sxpos = SP(sxpos);
   float* sxmat = SP(sxmat);
   float* Mm = SP(M);
-  float* Lm = SP(L);
+  float* Lm = HO ? G + Lo.h_L : SP(L);
   float* act_force = SP(act_force);
   float* con_pos = SP(con_pos);
   float* con_frame = SP(con_frame);
@@ -996,24 +1070,26 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   int* con_geom = SPI(con_geom);
   int* con_efcadr = SPI(con_efcadr);
   float* J = SP(J);
-  float* efc_D = SP(efc_D);
-  float* efc_R = SP(efc_R);
-  float* efc_aref = SP(efc_aref);
+  float* efc_D = HO ? G + Lo.h_D : SP(efc_D);
+  float* efc_R = HO ? G + Lo.h_R : SP(efc_R);
+  float* efc_aref = HO ? G + Lo.h_aref : SP(efc_aref);
   float* jaref = SP(efc_jaref);
-  float* jv = SP(efc_jv);
+  float* jv = HO ? G + Lo.h_jv : SP(efc_jv);
   float* efc_force = SP(efc_force);
-  float* efc_fl = SP(efc_fl);
+  float* efc_fl = HO ? G + Lo.h_fl : SP(efc_fl);
   float* efc_pos = SP(efc_pos);
-  int* efc_type = SPI(efc_type);
+  int* efc_type = HO ? reinterpret_cast<int*>(G + Lo.h_type) : SPI(efc_type);
   int* efc_id = SPI(efc_id);
   unsigned long long* efc_mask = reinterpret_cast<unsigned long long*>(SP(efc_mask));
   float* efc_h = SP(efc_h);
   int* arow = SPI(arow);
   float* ash = SP(ash);
   int* sidx = SPI(sidx);
-  float* red = S + Lo.red;
-  int* redi = SI + Lo.red + 2 * (NT / 64) + 2;
-  int* ints = SI + Lo.ints;
+  // the damping coefficient of each row until the velocity stage completes aref
+  float* efc_b = MODE == 0 ? SP(efc_h) : G + Lo.h_b;
+  float* red = S + (MODE == 1 ? Lo.pred : Lo.red);
+  int* redi = SI + (MODE == 1 ? Lo.pred : Lo.red) + 2 * (NT / 64) + 2;
+  int* ints = SI + (MODE == 1 ? Lo.pints : Lo.ints);
 
   // per-world model fields (stride 0 = shared)
   const float* body_pos = WFIELD(body_pos);
@@ -1038,9 +1114,56 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
 
   // ---------------------------------------------------------------- load state
   for (int i = tid; i < nq; i += NT) qpos[i] = DP(qpos)[W * nq + i];
-  for (int i = tid; i < nv; i += NT) qvel[i] = DP(qvel)[W * nv + i];
+  if constexpr (MODE != 1)
+    for (int i = tid; i < nv; i += NT) qvel[i] = DP(qvel)[W * nv + i];
   if (tid < I_COUNT) ints[tid] = (tid == I_MISC) ? 0x7fffffff : 0;
   wsync();
+  // reuse snapshot: [valid, image hash (2 words), per-world model fields hash
+  // (2), launch key (2: the host's hash of the model and data descriptors, so
+  // option scalars and buffer addresses), qpos (nq), mocap pos/quat (7 nmocap)],
+  // raw bits
+  unsigned* const snap = reinterpret_cast<unsigned*>(G + Lo.h_snap);
+  unsigned long long wf_hash = 0ull;
+  if constexpr (MODE == 0) {
+    if (tid == 0) snap[0] = 0u;
+  }
+  if constexpr (MODE == 1) {
+    {  // per-world (expanded) model fields of this world
+      unsigned long long h = 0ull;
+      int fid = 0;
+#define X_DZ(name) const int name = Z.name;
+      MJH_MODEL_SIZES(X_DZ)
+#undef X_DZ
+      (void)nchain; (void)ncolgeom; (void)npair; (void)nsensor; (void)nconmax; (void)njmax; (void)na; (void)nsensordata;
+      (void)nu;
+#define X_WH(type, name, count)                                                                                \
+      if (m.name##_wstride) {                                                                                  \
+        const unsigned* f = reinterpret_cast<const unsigned*>(m.name + W * m.name##_wstride);                  \
+        for (int i = tid; i < (count); i += NT)                                                                \
+          h += mix64(((unsigned long long)fid << 56) ^ ((unsigned long long)i << 32) ^ f[i]);                  \
+      }                                                                                                        \
+      fid++;
+      MJH_MODEL_WARRAYS(X_WH)
+#undef X_WH
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+      wf_hash = h;
+    }
+    if (reuse) {
+      const unsigned* qb = reinterpret_cast<const unsigned*>(qpos);
+      bool same = snap[0] == 1u && snap[1] == (unsigned)img_hash && snap[2] == (unsigned)(img_hash >> 32) &&
+                  snap[3] == (unsigned)wf_hash && snap[4] == (unsigned)(wf_hash >> 32) &&
+                  snap[5] == (unsigned)key && snap[6] == (unsigned)(key >> 32);
+      for (int i = tid; i < nq; i += NT) same = same && snap[7 + i] == qb[i];
+      if (Z.nmocap > 0) {
+        const unsigned* mp = reinterpret_cast<const unsigned*>(DP(mocap_pos) + W * Z.nmocap * 3);
+        const unsigned* mq = reinterpret_cast<const unsigned*>(DP(mocap_quat) + W * Z.nmocap * 4);
+        for (int i = tid; i < 3 * Z.nmocap; i += NT) same = same && snap[7 + nq + i] == mp[i];
+        for (int i = tid; i < 4 * Z.nmocap; i += NT) same = same && snap[7 + nq + 3 * Z.nmocap + i] == mq[i];
+      }
+      if (__all(same)) return;  // the last position pass of this world is current
+    }
+  }
   PROF(0);
 #ifdef MJH_PROFILE
   if (tid == 0 && g_prof) for (int k = 12; k < 20; k++) g_prof[(long long)w * 32 + k] = 0;
@@ -1054,6 +1177,17 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   // exchange them with v_readlane (uniform k) or ds_bpermute, instead of
   // serial chains of dependent global-scratch loads.
   const bool bl = tid < nb;
+  // registers the velocity stage takes from the position stage (reloaded from
+  // scratch by the split velocity kernel)
+  float r_cin[10];
+  float r_cdof[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int ncon = 0, nefc = 0;
+  const unsigned long long* tmk = reinterpret_cast<const unsigned long long*>(IMG_L(body_treemask));
+  const unsigned long long* dmk = reinterpret_cast<const unsigned long long*>(IMG_L(body_dofmask));
+  // lane b holds body b's chain mask; the subtree loops read it by readlane
+  // (no LDS load per body on their dependency chain)
+  const unsigned long long r_tmk = bl ? tmk[tid] : 0ull;
+  if constexpr (MODE != 2) {
   float r_xipos[3] = {0.f, 0.f, 0.f}, r_ximat[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int b = tid; b < nb; b += NT) {
     float p[3] = {0.f, 0.f, 0.f}, q[4] = {1.f, 0.f, 0.f, 0.f};
@@ -1185,14 +1319,6 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
 
   // ---------------------------------------------------------------- com_pos
   PROF(1);
-#if MJH_DEBUG_STOP == 1
-  return;
-#endif
-  const unsigned long long* tmk = reinterpret_cast<const unsigned long long*>(IMG_L(body_treemask));
-  const unsigned long long* dmk = reinterpret_cast<const unsigned long long*>(IMG_L(body_dofmask));
-  // lane b holds body b's chain mask; the subtree loops read it by readlane
-  // (no LDS load per body on their dependency chain)
-  const unsigned long long r_tmk = bl ? tmk[tid] : 0ull;
   // subtree com: lane b sums the bodies k whose chain contains b (ascending k)
   float r_sc[3];
   {
@@ -1215,7 +1341,6 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     if (bl) { subtree_com[3 * tid] = r_sc[0]; subtree_com[3 * tid + 1] = r_sc[1]; subtree_com[3 * tid + 2] = r_sc[2]; }
   }
   // cinert (lane b), about the subtree com of b's root body
-  float r_cin[10];
   {
     const int rt = bl ? IMG_I(body_rootid)[tid] : 0;
     const float c0 = shfl(r_sc[0], rt), c1 = shfl(r_sc[1], rt), c2 = shfl(r_sc[2], rt);
@@ -1288,7 +1413,6 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
   PROF(19);
   // ---------------------------------------------------------------- crb + M
   // lane i's cdof row in registers
-  float r_cdof[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (tid < nv) {
 #pragma unroll
     for (int c = 0; c < 6; c++) r_cdof[c] = cdof[6 * tid + c];
@@ -1349,9 +1473,363 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     ldl_factor_rows<NVP>(a, Lm, nv, ldm);
   }
   PROF(2);
-#if MJH_DEBUG_STOP == 2
-  return;
-#endif
+
+  // ---------------------------------------------------------------- collision
+  {
+    const int npair = Z.npair;
+    for (int base = 0; base < npair; base += NT) {
+      const int p = base + tid;
+      Con cc[4];
+      int n = 0, g1 = 0, g2 = 0;
+      if (p < npair) {
+        g1 = IMG_I(pair_geom1)[p];
+        g2 = IMG_I(pair_geom2)[p];
+        const int s1 = IMG_I(geom_colslot)[g1], s2 = IMG_I(geom_colslot)[g2];
+        const float* p1 = cgpos + 3 * s1;
+        const float* p2 = cgpos + 3 * s2;
+        const float* m1 = cgmat + 9 * s1;
+        const float* m2 = cgmat + 9 * s2;
+        const float margin = fmaxf(IMG_F(geom_margin)[g1], IMG_F(geom_margin)[g2]);
+        const int t1 = IMG_I(geom_type)[g1], t2 = IMG_I(geom_type)[g2];
+        float dif[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+        bool near;
+        if (t1 == 0) {
+          float nrm[3] = {m1[2], m1[5], m1[8]};
+          near = dot3(dif, nrm) <= margin + IMG_F(geom_rbound)[g2];
+        } else {
+          near = sqrtf(dot3(dif, dif)) <= margin + IMG_F(geom_rbound)[g1] + IMG_F(geom_rbound)[g2];
+        }
+        if (near) n = narrowphase(t1, t2, p1, m1, IMG_F(geom_size) + 3 * g1, p2, m2, IMG_F(geom_size) + 3 * g2, margin, cc);
+      }
+      int total;
+      const int off = bscan<NT>(n, &total, redi);
+      const int base_con = ints[I_NCON];
+      if (n > 0) {
+        // contact parameters (mj_contactParam semantics)
+        int condim;
+        float fri[3], solref[2], solimp[5];
+        const int pr1 = IMG_I(geom_priority)[g1], pr2 = IMG_I(geom_priority)[g2];
+        if (pr1 != pr2) {
+          const int g = pr1 > pr2 ? g1 : g2;
+          condim = IMG_I(geom_condim)[g];
+          for (int k = 0; k < 3; k++) fri[k] = geom_friction[3 * g + k];
+          for (int k = 0; k < 2; k++) solref[k] = IMG_F(geom_solref)[2 * g + k];
+          for (int k = 0; k < 5; k++) solimp[k] = IMG_F(geom_solimp)[5 * g + k];
+        } else {
+          condim = max(IMG_I(geom_condim)[g1], IMG_I(geom_condim)[g2]);
+          for (int k = 0; k < 3; k++) fri[k] = fmaxf(geom_friction[3 * g1 + k], geom_friction[3 * g2 + k]);
+          const float sm1 = IMG_F(geom_solmix)[g1], sm2 = IMG_F(geom_solmix)[g2];
+          float mix;
+          if (sm1 >= MJH_MINVAL && sm2 >= MJH_MINVAL) mix = sm1 / (sm1 + sm2);
+          else if (sm1 < MJH_MINVAL && sm2 < MJH_MINVAL) mix = 0.5f;
+          else mix = sm1 < MJH_MINVAL ? 0.f : 1.f;
+          const float* r1 = IMG_F(geom_solref) + 2 * g1;
+          const float* r2 = IMG_F(geom_solref) + 2 * g2;
+          if (r1[0] > 0.f && r2[0] > 0.f)
+            for (int k = 0; k < 2; k++) solref[k] = mix * r1[k] + (1.f - mix) * r2[k];
+          else
+            for (int k = 0; k < 2; k++) solref[k] = fminf(r1[k], r2[k]);
+          for (int k = 0; k < 5; k++) solimp[k] = mix * IMG_F(geom_solimp)[5 * g1 + k] + (1.f - mix) * IMG_F(geom_solimp)[5 * g2 + k];
+        }
+        const float imargin = fmaxf(IMG_F(geom_margin)[g1], IMG_F(geom_margin)[g2]) - fmaxf(IMG_F(geom_gap)[g1], IMG_F(geom_gap)[g2]);
+        for (int e = 0; e < n; e++) {
+          const int ci = base_con + off + e;
+          if (ci >= Lo.ncap) {
+            ints[I_FLAGS] |= MJH_FLAG_CONTACT_OVERFLOW;  // benign race: all writers set the same bit
+            break;
+          }
+          float fr[9] = {cc[e].frame[0], cc[e].frame[1], cc[e].frame[2], cc[e].frame[3], cc[e].frame[4], cc[e].frame[5], 0.f, 0.f, 0.f};
+          make_frame(fr);
+          con_dist[ci] = cc[e].dist;
+          for (int k = 0; k < 3; k++) con_pos[3 * ci + k] = cc[e].pos[k];
+          for (int k = 0; k < 9; k++) con_frame[9 * ci + k] = fr[k];
+          con_fric[5 * ci] = fri[0]; con_fric[5 * ci + 1] = fri[0]; con_fric[5 * ci + 2] = fri[1];
+          con_fric[5 * ci + 3] = fri[2]; con_fric[5 * ci + 4] = fri[2];
+          con_solref[2 * ci] = solref[0]; con_solref[2 * ci + 1] = solref[1];
+          for (int k = 0; k < 5; k++) con_solimp[5 * ci + k] = solimp[k];
+          con_imargin[ci] = imargin;
+          con_dim[ci] = condim;
+          con_geom[2 * ci] = g1;
+          con_geom[2 * ci + 1] = g2;
+          con_efcadr[ci] = -1;
+        }
+      }
+      wsync();
+      if (tid == 0) ints[I_NCON] = min(base_con + total, Lo.ncap);
+      wsync();
+    }
+  }
+  ncon = ints[I_NCON];
+  PROF(4);
+
+  // ---------------------------------------------------------------- make_constraint
+  {
+    int nefc = 0;
+    const int rcap = Lo.rcap;
+    // dof friction loss rows
+    for (int base = 0; base < nv; base += NT) {
+      const int i = base + tid;
+      const int f = (i < nv && dof_frictionloss[i] > 0.f) ? 1 : 0;
+      int total;
+      const int off = bscan<NT>(f, &total, redi);
+      if (f) {
+        const int r = nefc + off;
+        if (r < rcap) {
+          efc_type[r] = MJH_CNSTR_FRICTION_DOF;
+          efc_id[r] = i;
+          efc_fl[r] = dof_frictionloss[i];
+          efc_mask[r] = 1ull << i;
+          efc_pos[r] = 0.f;
+          row_params_pos(m.timestep, 0.f, 0.f, IMG_F(dof_invweight0)[i], IMG_F(dof_solref) + 2 * i,
+                         IMG_F(dof_solimp) + 5 * i, efc_D + r, efc_R + r, efc_aref + r, efc_b + r);
+        }
+      }
+      nefc += total;
+    }
+    // joint limits
+    for (int base = 0; base < nj; base += NT) {
+      const int j = base + tid;
+      int f = 0;
+      float pos = 0.f, sgn = 0.f;
+      if (j < nj && IMG_I(jnt_limited)[j] && (IMG_I(jnt_type)[j] == 2 || IMG_I(jnt_type)[j] == 3)) {
+        const float q = qpos[IMG_I(jnt_qposadr)[j]];
+        const float dlo = q - jnt_range[2 * j], dhi = jnt_range[2 * j + 1] - q;
+        pos = fminf(dlo, dhi) - IMG_F(jnt_margin)[j];
+        sgn = dlo < dhi ? 1.f : -1.f;
+        f = pos < 0.f ? 1 : 0;
+      }
+      int total;
+      const int off = bscan<NT>(f, &total, redi);
+      if (f) {
+        const int r = nefc + off;
+        if (r < rcap) {
+          const int dof = IMG_I(jnt_dofadr)[j];
+          efc_type[r] = MJH_CNSTR_LIMIT_JOINT;
+          efc_id[r] = j;
+          efc_fl[r] = 0.f;
+          efc_mask[r] = 1ull << dof;
+          efc_pos[r] = pos + IMG_F(jnt_margin)[j];
+          jv[r] = sgn;  // temporarily hold the Jacobian sign
+          row_params_pos(m.timestep, pos, pos, IMG_F(dof_invweight0)[dof], IMG_F(jnt_solref) + 2 * j,
+                         IMG_F(jnt_solimp) + 5 * j, efc_D + r, efc_R + r, efc_aref + r, efc_b + r);
+        }
+      }
+      nefc += total;
+    }
+    const int nsimple = min(nefc, rcap);
+    // contact rows
+    for (int base = 0; base < ncon; base += NT) {
+      const int ci = base + tid;
+      int nr = 0;
+      if (ci < ncon && con_dist[ci] - con_imargin[ci] < 0.f) nr = con_dim[ci] == 1 ? 1 : 2 * (con_dim[ci] - 1);
+      int total;
+      const int off = bscan<NT>(nr, &total, redi);
+      if (nr) {
+        const int r0 = nefc + off;
+        if (r0 + nr <= rcap) {
+          con_efcadr[ci] = r0;
+        } else {
+          con_efcadr[ci] = -1;
+          atomicMin(&ints[I_MISC], r0);  // rows of this and later contacts are dropped
+        }
+      }
+      nefc += total;
+    }
+    wsync();
+    if (nefc > rcap) {
+      if (tid == 0) ints[I_FLAGS] |= MJH_FLAG_EFC_OVERFLOW;
+      nefc = max(nsimple, min(rcap, ints[I_MISC]));
+    }
+    wsync();
+    // J rows with lane = column: every entry of every row is stored (zeros
+    // included, so no zero fill) as coalesced row stores, and all of a round's
+    // inputs are loaded before its first store (a load behind a store waits for
+    // it). Single-dof rows first, their (type, column, value) one per lane.
+    for (int base = 0; base < nsimple; base += NT) {
+      int col = -1;
+      float val = 0.f;
+      if (base + tid < nsimple) {
+        const int r = base + tid, t = efc_type[r];
+        col = t == MJH_CNSTR_FRICTION_DOF ? efc_id[r] : IMG_I(jnt_dofadr)[efc_id[r]];
+        val = t == MJH_CNSTR_FRICTION_DOF ? 1.f : jv[r];
+      }
+      const int cnt = min(NT, nsimple - base);
+      for (int k = 0; k < cnt; k++) {
+        const int ck = __builtin_amdgcn_readlane(col, k);
+        const float vk = rl(val, k);
+        if (tid < ldj) J[(base + k) * ldj + tid] = tid == ck ? vk : 0.f;
+      }
+    }
+    // contact rows: lane = contact loads the contact's data, then per contact
+    // (uniform) lane = dof builds the rows' column entries
+    {
+      float cd[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (tid < nv) {
+#pragma unroll
+        for (int c = 0; c < 6; c++) cd[c] = cdof[6 * tid + c];
+      }
+      for (int base = 0; base < ncon; base += NT) {
+        const int cl = base + tid;
+        int r0 = -1, b1 = 0, b2 = 0, dim = 1;
+        float cp[3] = {0.f, 0.f, 0.f}, fr[9], fk[5], c1[3] = {0.f, 0.f, 0.f}, c2[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 9; k++) fr[k] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 5; k++) fk[k] = 0.f;
+        if (cl < ncon) {
+          r0 = con_efcadr[cl];
+          b1 = IMG_I(geom_bodyid)[con_geom[2 * cl]];
+          b2 = IMG_I(geom_bodyid)[con_geom[2 * cl + 1]];
+          dim = con_dim[cl];
+#pragma unroll
+          for (int k = 0; k < 3; k++) cp[k] = con_pos[3 * cl + k];
+#pragma unroll
+          for (int k = 0; k < 9; k++) fr[k] = con_frame[9 * cl + k];
+#pragma unroll
+          for (int k = 0; k < 5; k++) fk[k] = con_fric[5 * cl + k];
+          const float* s1 = subtree_com + 3 * IMG_I(body_rootid)[b1];
+          const float* s2 = subtree_com + 3 * IMG_I(body_rootid)[b2];
+#pragma unroll
+          for (int k = 0; k < 3; k++) { c1[k] = s1[k]; c2[k] = s2[k]; }
+        }
+        const int cnt = min(NT, ncon - base);
+        for (int k = 0; k < cnt; k++) {
+          const int r0k = __builtin_amdgcn_readlane(r0, k);
+          if (r0k < 0) continue;
+          const int b1k = __builtin_amdgcn_readlane(b1, k), b2k = __builtin_amdgcn_readlane(b2, k);
+          const int dimk = __builtin_amdgcn_readlane(dim, k);
+          const int nr = dimk == 1 ? 1 : 2 * (dimk - 1);
+          const bool in1 = tid < nv && (((unsigned long long)IMG_L(body_dofmask)[b1k] >> tid) & 1ull);
+          const bool in2 = tid < nv && (((unsigned long long)IMG_L(body_dofmask)[b2k] >> tid) & 1ull);
+          // not in either chain, or in both (relative motion cancels): zero column
+          const bool use = in1 != in2;
+          const float sg = in2 ? 1.f : -1.f;
+          float off[3], t[3];
+#pragma unroll
+          for (int q = 0; q < 3; q++) off[q] = rl(cp[q], k) - (in2 ? rl(c2[q], k) : rl(c1[q], k));
+          cross3(t, cd, off);
+          const float jp[3] = {sg * (cd[3] + t[0]), sg * (cd[4] + t[1]), sg * (cd[5] + t[2])};
+          const float jr[3] = {sg * cd[0], sg * cd[1], sg * cd[2]};
+          float f[9];
+#pragma unroll
+          for (int q = 0; q < 9; q++) f[q] = rl(fr[q], k);
+          float jf[6];
+          jf[0] = dot3(f, jp); jf[1] = dot3(f + 3, jp); jf[2] = dot3(f + 6, jp);
+          jf[3] = dot3(f, jr); jf[4] = dot3(f + 3, jr); jf[5] = dot3(f + 6, jr);
+          if (tid < ldj) {
+            if (dimk == 1) {
+              J[r0k * ldj + tid] = use ? jf[0] : 0.f;
+            } else {
+              float fkv[5];
+#pragma unroll
+              for (int q = 0; q < 5; q++) fkv[q] = rl(fk[q], k);
+              // pyramid edges e = 2(kk-1), 2(kk-1)+1 of friction direction kk
+              // (static register indices: no private-memory arrays)
+#pragma unroll
+              for (int kk = 1; kk < 6; kk++) {
+                if (2 * (kk - 1) >= nr) break;
+                const int e = 2 * (kk - 1);
+                J[(r0k + e) * ldj + tid] = use ? jf[0] + fkv[kk - 1] * jf[kk] : 0.f;
+                J[(r0k + e + 1) * ldj + tid] = use ? jf[0] + (-fkv[kk - 1]) * jf[kk] : 0.f;
+              }
+            }
+          }
+        }
+      }
+    }
+    // contact row parameters
+    for (int ci = tid; ci < ncon; ci += NT) {
+      const int r0 = con_efcadr[ci];
+      if (r0 < 0) continue;
+      const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
+      const int dim = con_dim[ci];
+      const int nr = dim == 1 ? 1 : 2 * (dim - 1);
+      const unsigned long long msk =
+          (unsigned long long)IMG_L(body_dofmask)[b1] ^ (unsigned long long)IMG_L(body_dofmask)[b2];
+      for (int e = 0; e < nr; e++) {
+        const int r = r0 + e;
+        efc_type[r] = dim == 1 ? MJH_CNSTR_CONTACT_FRICTIONLESS : MJH_CNSTR_CONTACT_PYRAMIDAL;
+        efc_id[r] = ci;
+        efc_fl[r] = 0.f;
+        efc_mask[r] = msk;
+        efc_pos[r] = con_dist[ci];
+      }
+    }
+    wsync();
+    for (int r = tid; r < nefc; r += NT) {
+      if (efc_type[r] != MJH_CNSTR_CONTACT_FRICTIONLESS && efc_type[r] != MJH_CNSTR_CONTACT_PYRAMIDAL) continue;
+      const int ci = efc_id[r];
+      const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
+      float invw = IMG_F(body_invweight0)[2 * b1] + IMG_F(body_invweight0)[2 * b2];
+      if (con_dim[ci] > 1) {
+        const float f0 = con_fric[5 * ci];
+        invw = invw + f0 * f0 * invw;
+        invw = invw * 2.f * f0 * f0 / m.impratio;
+      }
+      const float pos = con_dist[ci] - con_imargin[ci];
+      row_params_pos(m.timestep, pos, pos, invw, con_solref + 2 * ci, con_solimp + 5 * ci, efc_D + r, efc_R + r,
+                     efc_aref + r, efc_b + r);
+    }
+    if (tid == 0) ints[I_NEFC] = nefc;
+    wsync();
+  }
+  nefc = ints[I_NEFC];
+  PROF(5);
+  }  // position stage
+  if constexpr (MODE == 1) {
+    // handoff: counters / overflow flags, then the snapshot that lets the next
+    // pass skip this world while nothing it depends on changed
+    wsync();
+    if (tid < I_COUNT) reinterpret_cast<int*>(G + Lo.h_ints)[tid] = ints[tid];
+    const unsigned* qb = reinterpret_cast<const unsigned*>(qpos);
+    for (int i = tid; i < nq; i += NT) snap[7 + i] = qb[i];
+    if (Z.nmocap > 0) {
+      const unsigned* mp = reinterpret_cast<const unsigned*>(DP(mocap_pos) + W * Z.nmocap * 3);
+      const unsigned* mq = reinterpret_cast<const unsigned*>(DP(mocap_quat) + W * Z.nmocap * 4);
+      for (int i = tid; i < 3 * Z.nmocap; i += NT) snap[7 + nq + i] = mp[i];
+      for (int i = tid; i < 4 * Z.nmocap; i += NT) snap[7 + nq + 3 * Z.nmocap + i] = mq[i];
+    }
+    if (tid == 0) {
+      snap[1] = (unsigned)img_hash; snap[2] = (unsigned)(img_hash >> 32);
+      snap[3] = (unsigned)wf_hash; snap[4] = (unsigned)(wf_hash >> 32);
+      snap[5] = (unsigned)key; snap[6] = (unsigned)(key >> 32);
+    }
+    wsync();
+    if (tid == 0) snap[0] = 1u;
+    return;
+  } else {
+  if constexpr (MODE == 2) {
+    // the position stage's results: counters, the rows' position parameters
+    // (LDS for the solver), registers of the tree passes
+    const int* ih = reinterpret_cast<const int*>(G + Lo.h_ints);
+    if (tid < I_COUNT) ints[tid] = ih[tid];
+    if (bl) {
+#pragma unroll
+      for (int c = 0; c < 10; c++) r_cin[c] = cinert[10 * tid + c];
+    }
+    if (tid < nv) {
+#pragma unroll
+      for (int c = 0; c < 6; c++) r_cdof[c] = cdof[6 * tid + c];
+    }
+    wsync();
+    ncon = ints[I_NCON];
+    nefc = ints[I_NEFC];
+    const int* ht = reinterpret_cast<const int*>(G + Lo.h_type);
+    for (int r = tid; r < nefc; r += NT) {
+      efc_type[r] = ht[r];
+      efc_fl[r] = G[Lo.h_fl + r];
+      efc_D[r] = G[Lo.h_D + r];
+      efc_R[r] = G[Lo.h_R + r];
+      efc_aref[r] = G[Lo.h_aref + r];
+    }
+  }
+  wsync();
+  // aref = aref_pos - b J qvel (row_params: the velocity term)
+  for (int r = tid; r < nefc; r += NT) {
+    const float jq = rowdot_u<NVP>(J + r * ldj, qvel, nv);
+    efc_aref[r] = efc_aref[r] - efc_b[r] * jq;
+  }
+  wsync();
 
   // ---------------------------------------------------------------- com_vel / rne (bias)
   const float r_qv = tid < nv ? qvel[tid] : 0.f;
@@ -1507,323 +1985,8 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
     }
   }
   PROF(25);
-  ldl_solve_reg<NVP>(Lm, nv, ldm, qacc_smooth);
+  ldl_solve_reg<NVP>(MODE == 2 ? G + Lo.h_L : Lm, nv, ldm, qacc_smooth);
   PROF(3);
-#if MJH_DEBUG_STOP == 3
-  return;
-#endif
-
-  // ---------------------------------------------------------------- collision
-  {
-    const int npair = Z.npair;
-    for (int base = 0; base < npair; base += NT) {
-      const int p = base + tid;
-      Con cc[4];
-      int n = 0, g1 = 0, g2 = 0;
-      if (p < npair) {
-        g1 = IMG_I(pair_geom1)[p];
-        g2 = IMG_I(pair_geom2)[p];
-        const int s1 = IMG_I(geom_colslot)[g1], s2 = IMG_I(geom_colslot)[g2];
-        const float* p1 = cgpos + 3 * s1;
-        const float* p2 = cgpos + 3 * s2;
-        const float* m1 = cgmat + 9 * s1;
-        const float* m2 = cgmat + 9 * s2;
-        const float margin = fmaxf(IMG_F(geom_margin)[g1], IMG_F(geom_margin)[g2]);
-        const int t1 = IMG_I(geom_type)[g1], t2 = IMG_I(geom_type)[g2];
-        float dif[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
-        bool near;
-        if (t1 == 0) {
-          float nrm[3] = {m1[2], m1[5], m1[8]};
-          near = dot3(dif, nrm) <= margin + IMG_F(geom_rbound)[g2];
-        } else {
-          near = sqrtf(dot3(dif, dif)) <= margin + IMG_F(geom_rbound)[g1] + IMG_F(geom_rbound)[g2];
-        }
-        if (near) n = narrowphase(t1, t2, p1, m1, IMG_F(geom_size) + 3 * g1, p2, m2, IMG_F(geom_size) + 3 * g2, margin, cc);
-      }
-      int total;
-      const int off = bscan<NT>(n, &total, redi);
-      const int base_con = ints[I_NCON];
-      if (n > 0) {
-        // contact parameters (mj_contactParam semantics)
-        int condim;
-        float fri[3], solref[2], solimp[5];
-        const int pr1 = IMG_I(geom_priority)[g1], pr2 = IMG_I(geom_priority)[g2];
-        if (pr1 != pr2) {
-          const int g = pr1 > pr2 ? g1 : g2;
-          condim = IMG_I(geom_condim)[g];
-          for (int k = 0; k < 3; k++) fri[k] = geom_friction[3 * g + k];
-          for (int k = 0; k < 2; k++) solref[k] = IMG_F(geom_solref)[2 * g + k];
-          for (int k = 0; k < 5; k++) solimp[k] = IMG_F(geom_solimp)[5 * g + k];
-        } else {
-          condim = max(IMG_I(geom_condim)[g1], IMG_I(geom_condim)[g2]);
-          for (int k = 0; k < 3; k++) fri[k] = fmaxf(geom_friction[3 * g1 + k], geom_friction[3 * g2 + k]);
-          const float sm1 = IMG_F(geom_solmix)[g1], sm2 = IMG_F(geom_solmix)[g2];
-          float mix;
-          if (sm1 >= MJH_MINVAL && sm2 >= MJH_MINVAL) mix = sm1 / (sm1 + sm2);
-          else if (sm1 < MJH_MINVAL && sm2 < MJH_MINVAL) mix = 0.5f;
-          else mix = sm1 < MJH_MINVAL ? 0.f : 1.f;
-          const float* r1 = IMG_F(geom_solref) + 2 * g1;
-          const float* r2 = IMG_F(geom_solref) + 2 * g2;
-          if (r1[0] > 0.f && r2[0] > 0.f)
-            for (int k = 0; k < 2; k++) solref[k] = mix * r1[k] + (1.f - mix) * r2[k];
-          else
-            for (int k = 0; k < 2; k++) solref[k] = fminf(r1[k], r2[k]);
-          for (int k = 0; k < 5; k++) solimp[k] = mix * IMG_F(geom_solimp)[5 * g1 + k] + (1.f - mix) * IMG_F(geom_solimp)[5 * g2 + k];
-        }
-        const float imargin = fmaxf(IMG_F(geom_margin)[g1], IMG_F(geom_margin)[g2]) - fmaxf(IMG_F(geom_gap)[g1], IMG_F(geom_gap)[g2]);
-        for (int e = 0; e < n; e++) {
-          const int ci = base_con + off + e;
-          if (ci >= Lo.ncap) {
-            ints[I_FLAGS] |= MJH_FLAG_CONTACT_OVERFLOW;  // benign race: all writers set the same bit
-            break;
-          }
-          float fr[9] = {cc[e].frame[0], cc[e].frame[1], cc[e].frame[2], cc[e].frame[3], cc[e].frame[4], cc[e].frame[5], 0.f, 0.f, 0.f};
-          make_frame(fr);
-          con_dist[ci] = cc[e].dist;
-          for (int k = 0; k < 3; k++) con_pos[3 * ci + k] = cc[e].pos[k];
-          for (int k = 0; k < 9; k++) con_frame[9 * ci + k] = fr[k];
-          con_fric[5 * ci] = fri[0]; con_fric[5 * ci + 1] = fri[0]; con_fric[5 * ci + 2] = fri[1];
-          con_fric[5 * ci + 3] = fri[2]; con_fric[5 * ci + 4] = fri[2];
-          con_solref[2 * ci] = solref[0]; con_solref[2 * ci + 1] = solref[1];
-          for (int k = 0; k < 5; k++) con_solimp[5 * ci + k] = solimp[k];
-          con_imargin[ci] = imargin;
-          con_dim[ci] = condim;
-          con_geom[2 * ci] = g1;
-          con_geom[2 * ci + 1] = g2;
-          con_efcadr[ci] = -1;
-        }
-      }
-      wsync();
-      if (tid == 0) ints[I_NCON] = min(base_con + total, Lo.ncap);
-      wsync();
-    }
-  }
-  const int ncon = ints[I_NCON];
-  PROF(4);
-#if MJH_DEBUG_STOP == 4
-  if (tid == 0) DP(ncon)[W] = ncon;
-  return;
-#endif
-
-  // ---------------------------------------------------------------- make_constraint
-  {
-    int nefc = 0;
-    const int rcap = Lo.rcap;
-    // dof friction loss rows
-    for (int base = 0; base < nv; base += NT) {
-      const int i = base + tid;
-      const int f = (i < nv && dof_frictionloss[i] > 0.f) ? 1 : 0;
-      int total;
-      const int off = bscan<NT>(f, &total, redi);
-      if (f) {
-        const int r = nefc + off;
-        if (r < rcap) {
-          efc_type[r] = MJH_CNSTR_FRICTION_DOF;
-          efc_id[r] = i;
-          efc_fl[r] = dof_frictionloss[i];
-          efc_mask[r] = 1ull << i;
-          efc_pos[r] = 0.f;
-          row_params(m.timestep, 0.f, 0.f, IMG_F(dof_invweight0)[i], IMG_F(dof_solref) + 2 * i, IMG_F(dof_solimp) + 5 * i, qvel[i],
-                     efc_D + r, efc_R + r, efc_aref + r);
-        }
-      }
-      nefc += total;
-    }
-    // joint limits
-    for (int base = 0; base < nj; base += NT) {
-      const int j = base + tid;
-      int f = 0;
-      float pos = 0.f, sgn = 0.f;
-      if (j < nj && IMG_I(jnt_limited)[j] && (IMG_I(jnt_type)[j] == 2 || IMG_I(jnt_type)[j] == 3)) {
-        const float q = qpos[IMG_I(jnt_qposadr)[j]];
-        const float dlo = q - jnt_range[2 * j], dhi = jnt_range[2 * j + 1] - q;
-        pos = fminf(dlo, dhi) - IMG_F(jnt_margin)[j];
-        sgn = dlo < dhi ? 1.f : -1.f;
-        f = pos < 0.f ? 1 : 0;
-      }
-      int total;
-      const int off = bscan<NT>(f, &total, redi);
-      if (f) {
-        const int r = nefc + off;
-        if (r < rcap) {
-          const int dof = IMG_I(jnt_dofadr)[j];
-          efc_type[r] = MJH_CNSTR_LIMIT_JOINT;
-          efc_id[r] = j;
-          efc_fl[r] = 0.f;
-          efc_mask[r] = 1ull << dof;
-          efc_pos[r] = pos + IMG_F(jnt_margin)[j];
-          jv[r] = sgn;  // temporarily hold the Jacobian sign
-          row_params(m.timestep, pos, pos, IMG_F(dof_invweight0)[dof], IMG_F(jnt_solref) + 2 * j, IMG_F(jnt_solimp) + 5 * j,
-                     sgn * qvel[dof], efc_D + r, efc_R + r, efc_aref + r);
-        }
-      }
-      nefc += total;
-    }
-    const int nsimple = min(nefc, rcap);
-    // contact rows
-    for (int base = 0; base < ncon; base += NT) {
-      const int ci = base + tid;
-      int nr = 0;
-      if (ci < ncon && con_dist[ci] - con_imargin[ci] < 0.f) nr = con_dim[ci] == 1 ? 1 : 2 * (con_dim[ci] - 1);
-      int total;
-      const int off = bscan<NT>(nr, &total, redi);
-      if (nr) {
-        const int r0 = nefc + off;
-        if (r0 + nr <= rcap) {
-          con_efcadr[ci] = r0;
-        } else {
-          con_efcadr[ci] = -1;
-          atomicMin(&ints[I_MISC], r0);  // rows of this and later contacts are dropped
-        }
-      }
-      nefc += total;
-    }
-    wsync();
-    if (nefc > rcap) {
-      if (tid == 0) ints[I_FLAGS] |= MJH_FLAG_EFC_OVERFLOW;
-      nefc = max(nsimple, min(rcap, ints[I_MISC]));
-    }
-    wsync();
-    // J rows with lane = column: every entry of every row is stored (zeros
-    // included, so no zero fill) as coalesced row stores, and all of a round's
-    // inputs are loaded before its first store (a load behind a store waits for
-    // it). Single-dof rows first, their (type, column, value) one per lane.
-    for (int base = 0; base < nsimple; base += NT) {
-      int col = -1;
-      float val = 0.f;
-      if (base + tid < nsimple) {
-        const int r = base + tid, t = efc_type[r];
-        col = t == MJH_CNSTR_FRICTION_DOF ? efc_id[r] : IMG_I(jnt_dofadr)[efc_id[r]];
-        val = t == MJH_CNSTR_FRICTION_DOF ? 1.f : jv[r];
-      }
-      const int cnt = min(NT, nsimple - base);
-      for (int k = 0; k < cnt; k++) {
-        const int ck = __builtin_amdgcn_readlane(col, k);
-        const float vk = rl(val, k);
-        if (tid < ldj) J[(base + k) * ldj + tid] = tid == ck ? vk : 0.f;
-      }
-    }
-    // contact rows: lane = contact loads the contact's data, then per contact
-    // (uniform) lane = dof builds the rows' column entries
-    {
-      float cd[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (tid < nv) {
-#pragma unroll
-        for (int c = 0; c < 6; c++) cd[c] = cdof[6 * tid + c];
-      }
-      for (int base = 0; base < ncon; base += NT) {
-        const int cl = base + tid;
-        int r0 = -1, b1 = 0, b2 = 0, dim = 1;
-        float cp[3] = {0.f, 0.f, 0.f}, fr[9], fk[5], c1[3] = {0.f, 0.f, 0.f}, c2[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < 9; k++) fr[k] = 0.f;
-#pragma unroll
-        for (int k = 0; k < 5; k++) fk[k] = 0.f;
-        if (cl < ncon) {
-          r0 = con_efcadr[cl];
-          b1 = IMG_I(geom_bodyid)[con_geom[2 * cl]];
-          b2 = IMG_I(geom_bodyid)[con_geom[2 * cl + 1]];
-          dim = con_dim[cl];
-#pragma unroll
-          for (int k = 0; k < 3; k++) cp[k] = con_pos[3 * cl + k];
-#pragma unroll
-          for (int k = 0; k < 9; k++) fr[k] = con_frame[9 * cl + k];
-#pragma unroll
-          for (int k = 0; k < 5; k++) fk[k] = con_fric[5 * cl + k];
-          const float* s1 = subtree_com + 3 * IMG_I(body_rootid)[b1];
-          const float* s2 = subtree_com + 3 * IMG_I(body_rootid)[b2];
-#pragma unroll
-          for (int k = 0; k < 3; k++) { c1[k] = s1[k]; c2[k] = s2[k]; }
-        }
-        const int cnt = min(NT, ncon - base);
-        for (int k = 0; k < cnt; k++) {
-          const int r0k = __builtin_amdgcn_readlane(r0, k);
-          if (r0k < 0) continue;
-          const int b1k = __builtin_amdgcn_readlane(b1, k), b2k = __builtin_amdgcn_readlane(b2, k);
-          const int dimk = __builtin_amdgcn_readlane(dim, k);
-          const int nr = dimk == 1 ? 1 : 2 * (dimk - 1);
-          const bool in1 = tid < nv && (((unsigned long long)IMG_L(body_dofmask)[b1k] >> tid) & 1ull);
-          const bool in2 = tid < nv && (((unsigned long long)IMG_L(body_dofmask)[b2k] >> tid) & 1ull);
-          // not in either chain, or in both (relative motion cancels): zero column
-          const bool use = in1 != in2;
-          const float sg = in2 ? 1.f : -1.f;
-          float off[3], t[3];
-#pragma unroll
-          for (int q = 0; q < 3; q++) off[q] = rl(cp[q], k) - (in2 ? rl(c2[q], k) : rl(c1[q], k));
-          cross3(t, cd, off);
-          const float jp[3] = {sg * (cd[3] + t[0]), sg * (cd[4] + t[1]), sg * (cd[5] + t[2])};
-          const float jr[3] = {sg * cd[0], sg * cd[1], sg * cd[2]};
-          float f[9];
-#pragma unroll
-          for (int q = 0; q < 9; q++) f[q] = rl(fr[q], k);
-          float jf[6];
-          jf[0] = dot3(f, jp); jf[1] = dot3(f + 3, jp); jf[2] = dot3(f + 6, jp);
-          jf[3] = dot3(f, jr); jf[4] = dot3(f + 3, jr); jf[5] = dot3(f + 6, jr);
-          if (tid < ldj) {
-            if (dimk == 1) {
-              J[r0k * ldj + tid] = use ? jf[0] : 0.f;
-            } else {
-              float fkv[5];
-#pragma unroll
-              for (int q = 0; q < 5; q++) fkv[q] = rl(fk[q], k);
-              // pyramid edges e = 2(kk-1), 2(kk-1)+1 of friction direction kk
-              // (static register indices: no private-memory arrays)
-#pragma unroll
-              for (int kk = 1; kk < 6; kk++) {
-                if (2 * (kk - 1) >= nr) break;
-                const int e = 2 * (kk - 1);
-                J[(r0k + e) * ldj + tid] = use ? jf[0] + fkv[kk - 1] * jf[kk] : 0.f;
-                J[(r0k + e + 1) * ldj + tid] = use ? jf[0] + (-fkv[kk - 1]) * jf[kk] : 0.f;
-              }
-            }
-          }
-        }
-      }
-    }
-    // contact row parameters
-    for (int ci = tid; ci < ncon; ci += NT) {
-      const int r0 = con_efcadr[ci];
-      if (r0 < 0) continue;
-      const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
-      const int dim = con_dim[ci];
-      const int nr = dim == 1 ? 1 : 2 * (dim - 1);
-      const unsigned long long msk =
-          (unsigned long long)IMG_L(body_dofmask)[b1] ^ (unsigned long long)IMG_L(body_dofmask)[b2];
-      for (int e = 0; e < nr; e++) {
-        const int r = r0 + e;
-        efc_type[r] = dim == 1 ? MJH_CNSTR_CONTACT_FRICTIONLESS : MJH_CNSTR_CONTACT_PYRAMIDAL;
-        efc_id[r] = ci;
-        efc_fl[r] = 0.f;
-        efc_mask[r] = msk;
-        efc_pos[r] = con_dist[ci];
-      }
-    }
-    wsync();
-    for (int r = tid; r < nefc; r += NT) {
-      if (efc_type[r] != MJH_CNSTR_CONTACT_FRICTIONLESS && efc_type[r] != MJH_CNSTR_CONTACT_PYRAMIDAL) continue;
-      const int ci = efc_id[r];
-      const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
-      float invw = IMG_F(body_invweight0)[2 * b1] + IMG_F(body_invweight0)[2 * b2];
-      if (con_dim[ci] > 1) {
-        const float f0 = con_fric[5 * ci];
-        invw = invw + f0 * f0 * invw;
-        invw = invw * 2.f * f0 * f0 / m.impratio;
-      }
-      float jq = 0.f;
-      jq = rowdot_u<NVP>(J + r * ldj, qvel, nv);
-      const float pos = con_dist[ci] - con_imargin[ci];
-      row_params(m.timestep, pos, pos, invw, con_solref + 2 * ci, con_solimp + 5 * ci, jq, efc_D + r, efc_R + r,
-                 efc_aref + r);
-    }
-    if (tid == 0) ints[I_NEFC] = nefc;
-    wsync();
-  }
-  const int nefc = ints[I_NEFC];
-  PROF(5);
-#if defined(MJH_DEBUG_STOP_AFTER_CONSTRAINTS) || MJH_DEBUG_STOP == 5
-  if (tid == 0) DP(nefc)[W] = nefc;
-  return;
-#endif
 
   // ---------------------------------------------------------------- Newton solver
   const float scale = 1.f / (m.meaninertia * (float)(nv > 1 ? nv : 1));
@@ -2582,6 +2745,7 @@ __global__ __launch_bounds__(64 * WPB, MJH_MINWAVES) void step_kernel(const mjh_
       DP(flags_acc)[W] |= f;  // sticky until the caller clears it (overflow/NaN statistics)
     }
   }
+  }  // velocity / solver stage
 }
 
 #undef DP
@@ -2647,6 +2811,20 @@ __global__ __launch_bounds__(1024) void pack_kernel(const mjh_model m, const Img
   MJH_MODEL_ARRAYS(X_PACK)
   MJH_MODEL_WARRAYS(X_PACK)
 #undef X_PACK
+}
+
+// Debug copies of the last step/forward's mass matrix and constraint Jacobian
+// out of each world's global scratch (where the step keeps them): qM (nv x nv)
+// and efc_J (njmax x nv, rows < nefc). One workgroup per world.
+__global__ __launch_bounds__(256) void debug_fields_kernel(const float* scratch, long long scratch_words, const int* nefc,
+                                                          int nv, int ldm, int ldj, int offM, int offJ, int njmax,
+                                                          float* qM, float* efc_J) {
+  const long long w = blockIdx.x;
+  const float* G = scratch + w * scratch_words;
+  for (int i = threadIdx.x; i < nv * nv; i += blockDim.x) qM[w * nv * nv + i] = G[offM + (i / nv) * ldm + i % nv];
+  const int ne = min(nefc[w], njmax);
+  for (int i = threadIdx.x; i < ne * nv; i += blockDim.x)
+    efc_J[w * (long long)njmax * nv + i] = G[offJ + (i / nv) * ldj + i % nv];
 }
 
 // ---- host side ---------------------------------------------------------------
@@ -2742,6 +2920,18 @@ Layout make_layout(const mjh_model* m, int budget) {
   TAKE(sidx, 64);
 #undef TAKE
   L.total = al(off);
+  // split-step handoff (global scratch): the factor of M, the rows' position
+  // parameters, counters and the reuse snapshot
+  auto gt = [&](int n) { const int o = goff; goff += al(n); return o; };
+  L.h_L = gt(nv * L.ldm);
+  L.h_type = gt(rcap); L.h_fl = gt(rcap); L.h_D = gt(rcap); L.h_R = gt(rcap);
+  L.h_aref = gt(rcap); L.h_b = gt(rcap); L.h_jv = gt(rcap);
+  L.h_ints = gt(8);
+  L.h_snap = gt(7 + m->nq + 7 * m->nmocap);
+  // the position kernel's LDS per world: qpos, reductions, counters
+  L.pred = al(m->nq);
+  L.pints = L.pred + al(16);
+  L.ptotal = L.pints + al(8);
   L.gtotal = al(goff) + 64;  // +256 B keeps worlds' spans on separate cache lines
   return L;
 }
@@ -2751,11 +2941,13 @@ Layout make_layout(const mjh_model* m, int budget) {
 #endif
 constexpr int kLdsBytes = 160 * 1024;
 constexpr int kWorldsPerBlock = MJH_WPB;
+constexpr int kPosWorldsPerBlock = MJH_PWPB;
 
 struct Plan {
   ImgOff io;
   Layout lo;
   size_t shmem;
+  size_t shmem_pos;  // the split position kernel's
 };
 
 Plan make_plan(const mjh_model* m, int wpb) {
@@ -2764,6 +2956,7 @@ Plan make_plan(const mjh_model* m, int wpb) {
   const int budget = (kLdsBytes / 4 - p.io.img_words) / wpb;
   p.lo = make_layout(m, budget);
   p.shmem = (size_t)(p.io.img_words + wpb * p.lo.total) * 4;
+  p.shmem_pos = (size_t)(p.io.img_words + kPosWorldsPerBlock * p.lo.ptotal) * 4;
   return p;
 }
 
@@ -2803,18 +2996,51 @@ int find_spec(const Plan& p, const mjh_model* m) {
   return -1;
 }
 
+// FNV-1a over the model and data descriptors: any change of an option scalar,
+// size or buffer address invalidates every world's position snapshot
+unsigned long long launch_key(const mjh_model* m, const mjh_data* d) {
+  unsigned long long h = 1469598103934665603ull;
+  auto eat = [&h](const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+  };
+  eat(m, sizeof(*m));
+  eat(d, sizeof(*d));
+  return h;
+}
+
+// one step/forward launch of MODE (0 fused, 1 position, 2 velocity/solver)
+template <int WPB, bool STEP, int NVP, int SPEC, bool SLAB, int MODE>
+void launch_mode(const Plan& p, const mjh_model* m, const mjh_data* d, const unsigned char* gate, hipStream_t s,
+                 int reuse, unsigned long long key) {
+  auto kern = step_kernel<WPB, STEP, NVP, SPEC, SLAB, MODE>;
+  static bool attr = false;
+  if (!attr) {
+    // the position kernel has a little static LDS (the image-hash partials)
+    const int maxdyn = MODE == 1 ? kLdsBytes - 1024 : kLdsBytes;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, maxdyn);
+    attr = true;
+  }
+  const int blocks = (d->nworld + WPB - 1) / WPB;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * WPB), MODE == 1 ? p.shmem_pos : p.shmem, s, *m, *d, p.lo, p.io, gate,
+                     reuse, key);
+}
+
+template <bool STEP, int NVP, int SPEC, bool SLAB>
+void launch_step(const Plan& p, const mjh_model* m, const mjh_data* d, const unsigned char* gate, hipStream_t s) {
+  if constexpr (MJH_SPLIT != 0) {
+    launch_mode<kPosWorldsPerBlock, STEP, NVP, SPEC, SLAB, 1>(p, m, d, gate, s, g_pos_reuse ? 1 : 0, launch_key(m, d));
+    launch_mode<kWorldsPerBlock, STEP, NVP, SPEC, SLAB, 2>(p, m, d, gate, s, 0, 0ull);
+  } else {
+    launch_mode<kWorldsPerBlock, STEP, NVP, SPEC, SLAB, 0>(p, m, d, gate, s, 0, 0ull);
+  }
+}
+
 template <bool STEP, int K>
-void launch_spec(int k, const Plan& p, const mjh_model* m, const mjh_data* d, const unsigned char* gate, hipStream_t s,
-                 int blocks) {
+void launch_spec(int k, const Plan& p, const mjh_model* m, const mjh_data* d, const unsigned char* gate, hipStream_t s) {
   if constexpr (K < MJH_NSPEC) {
-    if (k != K) return launch_spec<STEP, K + 1>(k, p, m, d, gate, s, blocks);
-    auto kern = step_kernel<kWorldsPerBlock, STEP, kSpecNvp[K], K, true>;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-      attr = true;
-    }
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * kWorldsPerBlock), p.shmem, s, *m, *d, p.lo, p.io, gate);
+    if (k != K) return launch_spec<STEP, K + 1>(k, p, m, d, gate, s);
+    launch_step<STEP, kSpecNvp[K], K, true>(p, m, d, gate, s);
   }
 }
 
@@ -2828,28 +3054,21 @@ int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, voi
     return 1;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  static bool attr_set[2] = {false, false};
   const int nvp = nvp_of(m->nv);
-  auto kern = nvp == 20 ? step_kernel<kWorldsPerBlock, STEP, 20>
-            : nvp == 36 ? step_kernel<kWorldsPerBlock, STEP, 36>
-                        : step_kernel<kWorldsPerBlock, STEP, 64>;
-  if (!attr_set[STEP]) {
-    for (auto k : {step_kernel<kWorldsPerBlock, STEP, 20>, step_kernel<kWorldsPerBlock, STEP, 36>,
-                   step_kernel<kWorldsPerBlock, STEP, 64>})
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    attr_set[STEP] = true;
-  }
   const bool order = g_auto_order && d->world_order != nullptr && d->nworld > 1;
   // 1024 threads: the order workgroup's counting sort is the launch's long pole
   hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields + (order ? 1 : 0)), dim3(1024), 0, s, *m, p.io, d->solver_niter, d->nefc,
                      const_cast<long long*>(d->world_order), (long long)d->nworld);
-  const int blocks = (d->nworld + kWorldsPerBlock - 1) / kWorldsPerBlock;
   // specialised instances assume the slab data layout (data_is_slab)
   const int k = (g_disable_spec || !data_is_slab(m, d)) ? -1 : find_spec(p, m);
   if (k >= 0)
-    launch_spec<STEP, 0>(k, p, m, d, gate, s, blocks);
+    launch_spec<STEP, 0>(k, p, m, d, gate, s);
+  else if (nvp == 20)
+    launch_step<STEP, 20, -1, false>(p, m, d, gate, s);
+  else if (nvp == 36)
+    launch_step<STEP, 36, -1, false>(p, m, d, gate, s);
   else
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * kWorldsPerBlock), p.shmem, s, *m, *d, p.lo, p.io, gate);
+    launch_step<STEP, 64, -1, false>(p, m, d, gate, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_err = std::string("step launch failed: ") + hipGetErrorString(e);
@@ -2899,6 +3118,13 @@ int mjh_set_world_ordering(int on) {
   return 0;
 }
 
+int mjh_set_position_reuse(int on) {
+  g_pos_reuse = on != 0;
+  return MJH_SPLIT ? 1 : 0;
+}
+
+int mjh_split_step(void) { return MJH_SPLIT; }
+
 int mjh_spec_index(const mjh_model* m) { return find_spec(make_plan(m, kWorldsPerBlock), m); }
 
 int mjh_data_is_slab(const mjh_model* m, const mjh_data* d) { return data_is_slab(m, d) ? 1 : 0; }
@@ -2931,6 +3157,19 @@ int mjh_forward(const mjh_model* m, const mjh_data* d, void* stream) { return la
 int mjh_forward_gated(const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream) {
   if (!gate) { g_err = "null gate"; return 1; }
   return launch<false>(m, d, gate, stream);
+}
+
+int mjh_debug_fields(const mjh_model* m, const mjh_data* d, float* qM, float* efc_J, void* stream) {
+  if (mjh_model_check(m) != 0) return 1;
+  if (!Rg::M || !Rg::J) { g_err = "this build keeps M or J in LDS (MJH_PRESET): no debug copy"; return 1; }
+  if (!qM || !efc_J || !d->scratch) { g_err = "null output or scratch"; return 1; }
+  if (d->nworld <= 0) return 0;
+  const Plan p = make_plan(m, kWorldsPerBlock);
+  hipLaunchKernelGGL(debug_fields_kernel, dim3(d->nworld), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d->scratch,
+                     d->scratch_words, d->nefc, m->nv, p.lo.ldm, p.lo.ldj, p.lo.M, p.lo.J, m->njmax, qM, efc_J);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { g_err = hipGetErrorString(e); return 2; }
+  return 0;
 }
 
 int mjh_repeat(float* dst, const float* src, long long nelem, int nworld, void* stream) {

@@ -37,6 +37,9 @@ EXPORTS = (
   "mjh_data_is_slab",
   "mjh_set_specialization",
   "mjh_set_world_ordering",
+  "mjh_set_position_reuse",
+  "mjh_split_step",
+  "mjh_debug_fields",
   "mjh_scratch_words",
   "mjh_step",
   "mjh_forward",
@@ -118,6 +121,10 @@ def lib() -> ctypes.CDLL:
   L.mjh_data_is_slab.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
   L.mjh_set_specialization.argtypes = [ctypes.c_int]
   L.mjh_set_world_ordering.argtypes = [ctypes.c_int]
+  L.mjh_set_position_reuse.argtypes = [ctypes.c_int]
+  L.mjh_debug_fields.argtypes = [ctypes.c_void_p] * 5
+  if os.environ.get("MJH_POS_REUSE") == "0":  # A/B timing: the split position pass never skips a world
+    L.mjh_set_position_reuse(0)
   # the step launches order the worlds themselves (in the pack launch) unless
   # MJH_PACK_ORDER=0 (A/B: one mjh_order_worlds launch per step from the host)
   L.mjh_set_world_ordering(0 if os.environ.get("MJH_PACK_ORDER") == "0" else 1)

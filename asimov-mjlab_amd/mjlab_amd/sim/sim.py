@@ -291,7 +291,8 @@ class Simulation:
     ds.nworld = self.num_envs
     if not hasattr(self, "_scratch"):
       words = int(native.lib().mjh_scratch_words(ctypes.addressof(ms))) if self._native_ok() else 16
-      self._scratch = torch.empty(self.num_envs * words, dtype=torch.float32, device=self.device)
+      # zeroed: the split step's per-world position snapshots start invalid
+      self._scratch = torch.zeros(self.num_envs * words, dtype=torch.float32, device=self.device)
       self._scratch_words = words
     ds.scratch = self._scratch.data_ptr()
     ds.scratch_words = self._scratch_words
@@ -489,6 +490,19 @@ class Simulation:
       self._flag_stats[3:] += cur
       fa.zero_()
     return self._flag_stats
+
+  def debug_fields(self) -> dict[str, torch.Tensor]:
+    """Debug copies of the last step/forward's mass matrix ``qM`` (N, nv, nv)
+    and constraint Jacobian ``efc_J`` (N, njmax, nv; rows < nefc), MuJoCo's
+    d.qM / d.efc_J, for parity tests (mjh_debug_fields)."""
+    self._require_gpu()
+    nv, nj = self.sizes["nv"], self.sizes["njmax"]
+    qM = torch.zeros(self.num_envs, nv, nv, dtype=torch.float32, device=self.device)
+    J = torch.zeros(self.num_envs, nj, nv, dtype=torch.float32, device=self.device)
+    native.check(native.lib().mjh_debug_fields(ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct),
+                                               ctypes.c_void_p(qM.data_ptr()), ctypes.c_void_p(J.data_ptr()),
+                                               self._stream()), "mjh_debug_fields")
+    return {"qM": qM, "efc_J": J}
 
   def efc_capacity(self) -> int:
     return int(native.lib().mjh_efc_capacity(ctypes.addressof(self._mstruct)))

@@ -144,6 +144,25 @@ int mjh_set_specialization(int enable);
  * supplies world_order. */
 int mjh_set_world_ordering(int on);
 
+/* Builds with the split step (mjh_split_step() == 1: a position launch, then a
+ * velocity/solver launch): 1 (default) lets the position launch skip a world
+ * whose qpos, mocap poses and model (image and per-world fields) are
+ * bit-identical to its previous position pass, whose results are still in the
+ * world's scratch (e.g. the first physics step after a forward — the env step's
+ * reset-forward, manager_based_rl_env.py:133-137). Results are bit-identical
+ * either way. Returns mjh_split_step(). */
+int mjh_set_position_reuse(int on);
+
+/* 1 if this build launches the step as two kernels (position, then velocity /
+ * solver / integration), 0 for the single fused launch. */
+int mjh_split_step(void);
+
+/* Debug copies of the mass matrix and the constraint Jacobian of the last
+ * mjh_step / mjh_forward on d (kept in d->scratch): qM as (nworld, nv, nv),
+ * efc_J as (nworld, njmax, nv), rows < nefc written. For parity tests
+ * (MuJoCo's d.qM / d.efc_J); not part of the step. */
+int mjh_debug_fields(const mjh_model* m, const mjh_data* d, float* qM, float* efc_J, void* stream);
+
 /* Diagnostic builds only (-DMJH_PROFILE): per-world phase timestamps. */
 int mjh_set_profile_buffer(void* ptr);
 

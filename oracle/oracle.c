@@ -1259,6 +1259,11 @@ static void sensors(const or_model* m, ws_t* w, real* sd) {
 }
 
 /* ---------------------------------------------------------------- driver */
+/* optional per-world debug copies (oracle_set_debug): the mass matrix qM
+   (nv x nv, dense) and the constraint Jacobian efc_J (njmax x nv, rows < nefc) */
+static real* g_dbg_qM = NULL;
+static real* g_dbg_J = NULL;
+
 static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_t* w) {
   int nq = m->nq, nv = m->nv, nu = m->nu, nb = m->nbody;
   const real* qpos_in = d->qpos + (size_t)wi * nq;
@@ -1335,6 +1340,8 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
     d->efc_force[o] = w->efc_force[r];
   }
   d->solver_niter[wi] = w->niter;
+  if (g_dbg_qM) memcpy(g_dbg_qM + (size_t)wi * nv * nv, w->M, sizeof(real) * nv * nv);
+  if (g_dbg_J) memcpy(g_dbg_J + (size_t)wi * m->njmax * nv, w->J, sizeof(real) * (size_t)w->nefc * nv);
 
   if (integrate) {
     real dt = m->timestep;
@@ -1415,6 +1422,11 @@ int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int
   }
   (void)nthreads;
   return 0;
+}
+
+void oracle_set_debug(real* qM, real* efc_J) {
+  g_dbg_qM = qM;
+  g_dbg_J = efc_J;
 }
 
 size_t oracle_sizeof_model(void) { return sizeof(or_model); }

@@ -59,6 +59,9 @@ extern "C" {
 /* Run mj_step (integrate=1) or mj_forward (integrate=0) on worlds [w0, w1),
  * with nthreads OpenMP threads (<=0: library default). Returns 0 on success. */
 int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int nthreads);
+/* Debug copies written by the next oracle_run calls (NULL: off): qM as
+ * (nworld, nv, nv) and efc_J as (nworld, njmax, nv) (rows < nefc written). */
+void oracle_set_debug(real* qM, real* efc_J);
 size_t oracle_sizeof_model(void);
 size_t oracle_sizeof_data(void);
 int oracle_real_bytes(void);

@@ -38,6 +38,7 @@ class Oracle:
     self.dtype = np.float64 if precision == "f64" else np.float32
     self.lib = ctypes.CDLL(str(ORACLE_DIR / f"liboracle_{precision}.so"))
     self.lib.oracle_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    self.lib.oracle_set_debug.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     self.lib.oracle_sizeof_model.restype = ctypes.c_size_t
     self.lib.oracle_sizeof_data.restype = ctypes.c_size_t
     MS = abi.model_struct(self.real, device=False)
@@ -68,7 +69,10 @@ class Oracle:
         setattr(ms, f.name + "_wstride", stride)
     self.ms = ms
 
-  def run(self, nworld: int, state: dict, integrate: bool = True, nthreads: int = 1) -> dict:
+  def run(self, nworld: int, state: dict, integrate: bool = True, nthreads: int = 1, debug: bool = False) -> dict:
+    """One step (or forward) of `nworld` worlds from `state`. debug=True also
+    returns the mass matrix ``qM`` (nworld, nv*nv) and the constraint Jacobian
+    ``efc_J`` (nworld, njmax*nv; rows < nefc) of the forward pass."""
     DS = abi.data_struct(self.real, device=False)
     ds = DS()
     ds.nworld = nworld
@@ -86,7 +90,16 @@ class Oracle:
         a = np.zeros((nworld, n), dt)
       out[f.name] = a
       setattr(ds, f.name, a.ctypes.data)
-    rc = self.lib.oracle_run(ctypes.addressof(self.ms), ctypes.addressof(ds), 0, nworld, int(integrate), nthreads)
+    nv, nj = self.sizes["nv"], self.sizes["njmax"]
+    if debug:
+      out["qM"] = np.zeros((nworld, nv * nv), self.dtype)
+      out["efc_J"] = np.zeros((nworld, nj * nv), self.dtype)
+      self.lib.oracle_set_debug(out["qM"].ctypes.data, out["efc_J"].ctypes.data)
+    try:
+      rc = self.lib.oracle_run(ctypes.addressof(self.ms), ctypes.addressof(ds), 0, nworld, int(integrate), nthreads)
+    finally:
+      if debug:
+        self.lib.oracle_set_debug(None, None)
     if rc != 0:
       raise RuntimeError(f"oracle_run failed: {rc}")
     return out

@@ -257,8 +257,9 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
   rows (`int_mismatch_reason`). Kinematics and smooth dynamics are checked on
   EVERY world (they do not depend on contacts); contact geometry (dist, pos,
   frame) on every contact present on both sides (aligned by geom pair); the
-  constraint rows (efc_pos/D/aref/force) and the solver, integration and
-  sensor outputs on every world whose integer outputs agree.
+  constraint rows (efc_pos/D/aref/force, and efc_J when both sides carry the
+  debug copies) and the solver, integration and sensor outputs on every world
+  whose integer outputs agree; qM (debug copy) on every world.
   Returns {"maxerr", "failures", "int_mismatch_worlds", "int_mismatch_reasons",
   "int_match_rate"}."""
   n = got["qpos"].shape[0]
@@ -339,6 +340,19 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
       maxerr[k] = e
       if not np.isfinite(a).all() or e > tol:
         failures.append(f"{k}: max|d|={e:.3e} > {tol:.3e}")
+  # debug copies (Simulation.debug_fields / Oracle.run(debug=True)), when both sides have them
+  if "qM" in got and "qM" in ref:
+    check_rel("qM", 1e-4, sel)
+  if "efc_J" in got and "efc_J" in ref and len(good):
+    nw, nj = ref["efc_J"].shape[0], ref["efc_pos"].shape[1]
+    gj, rj = got["efc_J"].reshape(nw, nj, -1)[good], ref["efc_J"].reshape(nw, nj, -1)[good]
+    ne = ref["nefc"][good, 0].astype(int)
+    rowm = np.arange(nj)[None, :] < ne[:, None]
+    a, b = gj[rowm], rj[rowm]
+    e = float(np.abs(a - b).max(initial=0.0))
+    maxerr["efc_J"] = e
+    if not np.isfinite(a).all() or e > _bound(b, 1e-4):
+      failures.append(f"efc_J: max|d|={e:.3e} > {_bound(b, 1e-4):.3e}")
   sv = dict(frac=solve_frac, rel_max=solve_max)
   for k in SOLVE:
     check_rel(k, solve_rel, **sv)

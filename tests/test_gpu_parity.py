@@ -55,8 +55,10 @@ def test_single_step_parity(name, integrate):
   put(sim, st)
   sim.step() if integrate else sim.forward()
   got = get(sim, n)
-  ref = Oracle(m).run(n, st, integrate=integrate)
-  assert_parity(got, ref, n, tag=f" {name} integrate={integrate}")
+  got.update({k: v.cpu().numpy().reshape(n, -1) for k, v in sim.debug_fields().items()})
+  ref = Oracle(m).run(n, st, integrate=integrate, debug=True)
+  rep = assert_parity(got, ref, n, tag=f" {name} integrate={integrate}")
+  assert "qM" in rep["maxerr"] and "efc_J" in rep["maxerr"]  # the debug copies were compared
   assert (got["ncon"] > 0).mean() > 0.5  # the states exercise contacts
 
 

@@ -1,0 +1,109 @@
+"""The split step (a position launch, then a velocity/solver launch) and its
+position reuse: a world whose qpos, mocap poses and model are bit-identical to
+its previous position pass skips that pass (mjh_set_position_reuse). Results
+must be bit-identical with reuse on and off, and a change of any input the
+position stage reads must force the pass."""
+
+import numpy as np
+import pytest
+import torch
+
+from mjlab_amd.sim import native
+from tests.scenes import g1_mocap_scene, g1_scene_model, mocap_states, random_states
+from tests.test_gpu_parity import DEV, get, make_sim, put
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _split_only():
+  if int(native.lib().mjh_split_step()) == 0:
+    pytest.skip("library built without the split step (MJH_SPLIT=0)")
+  yield
+  native.lib().mjh_set_position_reuse(1)
+
+
+def _run(sim, reuse, fn):
+  native.lib().mjh_set_position_reuse(1 if reuse else 0)
+  fn()
+  torch.cuda.synchronize()
+
+
+def _same(a, b, tag):
+  for k in a:
+    assert a[k].tobytes() == b[k].tobytes(), f"{tag}: {k}"
+
+
+def _twins(m, n, st, expand=()):
+  sims = [make_sim(m, n, expand), make_sim(m, n, expand)]
+  for s in sims:
+    put(s, st)
+  return sims
+
+
+def test_reuse_is_bitwise_identical_g1():
+  n = 64
+  m = g1_scene_model(n)
+  rng = np.random.default_rng(11)
+  st = random_states(m, n, rng)
+  on, off = _twins(m, n, st, expand=("geom_friction",))
+  for reuse, sim in ((True, on), (False, off)):
+    _run(sim, reuse, sim.forward)  # the env's reset-forward, then physics steps
+    for _ in range(3):
+      _run(sim, reuse, sim.step)
+  _same(get(on, n), get(off, n), "forward + 3 steps")
+  # reset some worlds' poses, then forward + step (those worlds must recompute)
+  st2 = random_states(m, n, np.random.default_rng(12))
+  idx = torch.arange(0, n, 5, device=DEV)
+  for reuse, sim in ((True, on), (False, off)):
+    sim.data.qpos[idx] = torch.as_tensor(st2["qpos"], dtype=torch.float32, device=DEV).view(n, -1)[idx]
+    _run(sim, reuse, sim.forward)
+    _run(sim, reuse, sim.step)
+  _same(get(on, n), get(off, n), "partial reset")
+  # domain randomisation between forward and step: the per-world field hash
+  for reuse, sim in ((True, on), (False, off)):
+    _run(sim, reuse, sim.forward)
+    sim.model.geom_friction[3, :, 0] = 0.1
+    _run(sim, reuse, sim.step)
+  _same(get(on, n), get(off, n), "friction change")
+
+
+def test_reuse_is_bitwise_identical_mocap():
+  n = 32
+  m = g1_mocap_scene(n)
+  st = mocap_states(m, n, np.random.default_rng(13))
+  on, off = _twins(m, n, st)
+  for reuse, sim in ((True, on), (False, off)):
+    _run(sim, reuse, sim.forward)
+    sim.data.mocap_pos[::2] += 0.01  # moved mocap bodies: the pass must rerun
+    _run(sim, reuse, sim.step)
+    _run(sim, reuse, sim.forward)
+    _run(sim, reuse, sim.step)
+  _same(get(on, n), get(off, n), "mocap")
+
+
+def test_reuse_skips_unchanged_worlds():
+  """White-box: geom_xpos is written by the position pass only, so a sentinel
+  written after a forward survives the next step exactly in the skipped worlds."""
+  n = 16
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(14))
+  sim = make_sim(m, n)
+  put(sim, st)
+  _run(sim, True, sim.forward)
+  ref = sim.data.geom_xpos.clone()
+  sim.data.geom_xpos.fill_(123.0)
+  sim.data.qpos[1, 2] += 0.001  # world 1 changed
+  _run(sim, True, sim.step)
+  g = sim.data.geom_xpos
+  skipped = torch.ones(n, dtype=torch.bool, device=DEV)
+  skipped[1] = False
+  assert bool((g[skipped] == 123.0).all())
+  assert not bool((g[1] == 123.0).any())
+  # the same with reuse off: every world recomputes
+  sim2 = make_sim(m, n)
+  put(sim2, st)
+  _run(sim2, False, sim2.forward)
+  sim2.data.geom_xpos.fill_(123.0)
+  _run(sim2, False, sim2.step)
+  assert torch.equal(sim2.data.geom_xpos, ref)

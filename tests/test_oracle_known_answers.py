@@ -52,14 +52,37 @@ def _model(xml, **opt):
 
 def test_free_fall_first_step():
   m = _model(FREE_BALL)
-  out = Oracle(m).run(1, {"qpos": m.qpos0[None]}, integrate=True)
+  out = Oracle(m).run(1, {"qpos": m.qpos0[None]}, integrate=True, debug=True)
   g, dt = 9.81, m.timestep
   assert out["ncon"][0, 0] == 0
+  # qM of a free solid sphere (mass 2, radius 0.1): diag(m, m, m, 2/5 m r^2 x 3)
+  np.testing.assert_allclose(out["qM"][0].reshape(6, 6), np.diag([2.0] * 3 + [0.4 * 2.0 * 0.01] * 3), atol=1e-12)
   np.testing.assert_allclose(out["qacc_smooth"][0], [0, 0, -g, 0, 0, 0], atol=1e-12)
   np.testing.assert_allclose(out["qacc"][0], [0, 0, -g, 0, 0, 0], atol=1e-12)
   assert out["qvel"][0, 2] == pytest.approx(-g * dt, abs=1e-12)
   assert out["qpos"][0, 2] == pytest.approx(1.0 - g * dt * dt, abs=1e-12)  # semi-implicit Euler
   assert out["time"][0, 0] == pytest.approx(dt)
+
+
+def test_resting_ball_contact_jacobian():
+  """Ball touching the floor: one frictional contact (condim 3 -> 4 pyramid
+  rows). Each row of efc_J is frame-row combinations of the contact point
+  Jacobian of the ball's free joint: translation columns = the pyramid edge
+  directions n +/- mu t (frame rows), rotation columns = (c - p) x edge with c
+  the contact point and p the ball centre."""
+  m = _model(FREE_BALL)
+  st = {"qpos": m.qpos0[None].copy()}
+  st["qpos"][0, 2] = 0.0999
+  out = Oracle(m).run(1, st, integrate=False, debug=True)
+  assert out["ncon"][0, 0] == 1 and out["nefc"][0, 0] == 4
+  J = out["efc_J"][0].reshape(m.njmax, 6)[:4]
+  fr = out["contact_frame"][0, :9].reshape(3, 3)
+  mu = out["contact_friction"][0, 0]
+  c, p = out["contact_pos"][0, :3], st["qpos"][0, :3]
+  for r in range(4):
+    edge = fr[0] + (1 if r % 2 == 0 else -1) * mu * fr[1 + r // 2]
+    np.testing.assert_allclose(J[r, :3], edge, atol=1e-12)
+    np.testing.assert_allclose(J[r, 3:], np.cross(c - p, edge), atol=1e-12)
 
 
 def test_ball_comes_to_rest_on_floor():
@@ -199,8 +222,10 @@ def test_compare_step_oracle_f32_vs_f64():
   n = 64
   m = g1_sensor_scene(n).compile(50, 300)
   st = random_states(m, n, np.random.default_rng(12))
-  rep = compare_step(Oracle(m, "f32").run(n, st, integrate=True), Oracle(m).run(n, st, integrate=True))
+  rep = compare_step(Oracle(m, "f32").run(n, st, integrate=True, debug=True),
+                     Oracle(m).run(n, st, integrate=True, debug=True))
   assert not rep["failures"], rep["failures"]
+  assert "qM" in rep["maxerr"] and "efc_J" in rep["maxerr"]
   assert rep["int_match_rate"] >= 0.98
 
 

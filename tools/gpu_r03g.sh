@@ -1,0 +1,9 @@
+#!/bin/bash
+# round-3 split-step check: parity suites on the split build, A/B kernel timing
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+O=gpurun_out/r03g
+mkdir -p $O
+
+MJH_LIB=asimov-mjlab_amd/mjlab_amd/variants/libmjh_split.so timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_split.py tests/test_gpu_parity.py tests/test_gpu_env.py > $O/tests_split.log 2>&1 && \
+bash tools/gpu_variants.sh r03g split

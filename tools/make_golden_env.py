@@ -3,10 +3,11 @@
 The reference's managers, MDP terms, EntityData, ContactSensor/BuiltinSensor and
 UniformVelocityCommand are executed unmodified on a stand-in env whose
 simulation data are plain torch tensors (the physics modules are inert stubs,
-tools/make_golden.py recipe). The sim-data frames fed to them are recorded
-from mjlab_amd's G1 velocity env stepped on the CPU with the float64 oracle
-(tests/oracle_sim.py): they are INPUTS only; every output in the fixture comes
-from reference code:
+tools/make_golden.py recipe). The sim-data frames fed to them are INPUTS only:
+seeded numpy initial states and actions, stepped by the float64 oracle
+(tests/oracle_sim.py) through mjlab_amd's action manager (capture(); no use of
+mjlab_amd's RNG, so a rerun writes byte-identical fixtures). Every output in
+the fixture comes from reference code:
 
   - EntityData.initialize-derived defaults (default_joint_pos from the G1
     keyframe regexes, soft joint limits)                  entity/entity.py:326-400
@@ -64,6 +65,20 @@ TASKS = {
 MOTION_FRAMES = 40
 
 
+def save_npz(path: Path, arrs: dict) -> None:
+  """np.savez_compressed with fixed member timestamps and order: byte-reproducible."""
+  import io
+  import zipfile
+
+  with open(path, "wb") as f, zipfile.ZipFile(f, "w", zipfile.ZIP_DEFLATED) as z:
+    for k in sorted(arrs):
+      b = io.BytesIO()
+      np.save(b, arrs[k], allow_pickle=False)
+      zi = zipfile.ZipInfo(k + ".npy", date_time=(2026, 1, 1, 0, 0, 0))
+      zi.compress_type = zipfile.ZIP_DEFLATED
+      z.writestr(zi, b.getvalue())
+
+
 def synthetic_motion_file(path: Path) -> dict:
   """INPUT motion clip (mjlab_amd's synthetic clip, csv_to_npz.py format)."""
   from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
@@ -81,9 +96,15 @@ def synthetic_motion_file(path: Path) -> dict:
 
 
 def capture(task: str, n: int, frames: int, warm: int, seed: int, motion_file: str | None = None):
-  """INPUT frames: mjlab_amd's env on CPU (oracle physics), random actions."""
+  """INPUT frames, independent of mjlab_amd's own randomness: the
+  initial states, actions and manager states are drawn from a seeded numpy
+  Generator, and the physics is the float64 oracle (tests/oracle_sim.py)
+  stepped through mjlab_amd's action manager (process/apply, decimation) —
+  no env.reset/env.step, so no event, command-resampling or reset draws. The
+  same seed gives byte-identical fixtures on every run."""
   from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
   from mjlab_amd.tasks import load_env_cfg
+  from mjlab_amd.utils.math import quat_mul
   from tests import oracle_sim
 
   cfg = load_env_cfg(task)
@@ -93,41 +114,65 @@ def capture(task: str, n: int, frames: int, warm: int, seed: int, motion_file: s
     cfg.commands["motion"].motion_file = motion_file
   env = ManagerBasedRlEnv(cfg, device="cpu")
   oracle_sim.attach(env.sim, env.event_manager.domain_randomization_fields)
-  env.reset()
-  g = torch.Generator().manual_seed(seed)
-  adim = env.action_manager.total_action_dim
-  for _ in range(warm):
-    env.step(2 * torch.rand(n, adim, generator=g) - 1)
+  rng = np.random.default_rng(seed)
+  f32 = lambda x: torch.as_tensor(np.asarray(x, dtype=np.float32))  # noqa: E731
   robot = env.scene["robot"]
+  ed = robot.data
+  adim = env.action_manager.total_action_dim
+  # initial state: default pose at the env origin, random planar offset / yaw /
+  # joint offsets (within the soft limits), small random velocities
+  root = ed.default_root_state.clone()
+  root[:, :3] += env.scene.env_origins
+  root[:, :2] += f32(rng.uniform(-0.3, 0.3, (n, 2)))
+  yaw = rng.uniform(-np.pi, np.pi, n)
+  qz = f32(np.stack([np.cos(yaw / 2), np.zeros(n), np.zeros(n), np.sin(yaw / 2)], 1))
+  root[:, 3:7] = quat_mul(qz, root[:, 3:7])
+  root[:, 7:13] = f32(rng.uniform(-0.2, 0.2, (n, 6)))
+  lim = ed.soft_joint_pos_limits
+  jp = torch.clamp(ed.default_joint_pos + f32(rng.uniform(-0.2, 0.2, ed.default_joint_pos.shape)), lim[..., 0], lim[..., 1])
+  jv = f32(rng.uniform(-0.5, 0.5, jp.shape))
+  robot.write_root_state_to_sim(root)
+  robot.write_joint_state_to_sim(jp, jv)
+  env.sim.forward()
+
+  def physics_step(a: torch.Tensor) -> None:
+    env.action_manager.process_action(a)
+    for _ in range(env.cfg.decimation):
+      env.action_manager.apply_action()
+      env.sim.step()
+
+  for _ in range(warm):
+    physics_step(f32(rng.uniform(-1, 1, (n, adim))))
   init = {
     "action": env.action_manager.action.clone(), "prev_action": env.action_manager.prev_action.clone(),
-    "episode_length": env.episode_length_buf.clone(), "env_origins": env.scene.env_origins.clone(),
+    "episode_length": torch.as_tensor(rng.integers(0, env.max_episode_length - 10, n)),
+    "env_origins": env.scene.env_origins.clone(),
   }
   if "feet_ground_contact" in env.scene.sensors:
-    st = env.scene["feet_ground_contact"]._air_time_state
-    init.update({"air_cur": st.current_air_time.clone(), "air_last": st.last_air_time.clone(),
-                 "con_cur": st.current_contact_time.clone(), "con_last": st.last_contact_time.clone(),
-                 "air_last_time": st.last_time.clone()})
+    k = env.scene["feet_ground_contact"]._air_time_state.current_air_time.shape[1]
+    cur = rng.uniform(0.0, 0.6, (n, k))
+    in_air = rng.random((n, k)) < 0.5
+    init.update({"air_cur": f32(np.where(in_air, cur, 0.0)), "air_last": f32(rng.uniform(0.0, 0.6, (n, k))),
+                 "con_cur": f32(np.where(in_air, 0.0, cur)), "con_last": f32(rng.uniform(0.0, 0.6, (n, k))),
+                 "air_last_time": f32(np.full(n, float(env.sim.data.time[0])))})
   if "twist" in env.command_manager.active_terms:
-    cmd = env.command_manager.get_term("twist")
-    init.update({"cmd_vel": cmd.vel_command_b.clone(), "cmd_heading_target": cmd.heading_target.clone(),
-                 "cmd_is_heading": cmd.is_heading_env.clone(), "cmd_is_standing": cmd.is_standing_env.clone()})
+    init.update({"cmd_vel": f32(rng.uniform(-1.0, 1.0, (n, 3))),
+                 "cmd_heading_target": f32(rng.uniform(-np.pi, np.pi, n)),
+                 "cmd_is_heading": torch.as_tensor(rng.random(n) < 0.5),
+                 "cmd_is_standing": torch.as_tensor(rng.random(n) < 0.2)})
   if "motion" in env.command_manager.active_terms:
     # motion phase per env, kept clear of the clip end inside the window
-    ts = env.command_manager.get_term("motion").time_steps.clone()
-    init["time_steps"] = torch.remainder(ts, MOTION_FRAMES - frames - 2)
+    init["time_steps"] = torch.as_tensor(rng.integers(0, MOTION_FRAMES - frames - 2, n))
   # a few envs start one step short of the time limit, so time_out fires
   init["episode_length"][:3] = env.max_episode_length - 1
   seq = []
   for t in range(frames):
-    a = 2 * torch.rand(n, adim, generator=g) - 1
-    env.step(a)
+    a = f32(rng.uniform(-1, 1, (n, adim)))
+    physics_step(a)
     fr = {f: getattr(env.sim.data, f).detach().clone() for f in SIM_FIELDS}
     if t == 0:  # tilt a few roots past the fell_over limit (input perturbation)
       tilt = torch.tensor([np.cos(0.7), np.sin(0.7), 0.0, 0.0], dtype=torch.float32)
       rb = robot.indexing.root_body_id
-      from mjlab_amd.utils.math import quat_mul
-
       fr["xquat"][4:7, rb] = quat_mul(fr["xquat"][4:7, rb], tilt.expand(3, 4))
       if motion_file is not None:  # and lift a few robots off the motion (anchor/ee height terms)
         fr["xpos"][8:11, :, 2] += 0.5
@@ -328,7 +373,7 @@ def gen(task: str, n: int = 24, frames: int = 4) -> None:
   out["n_frames"] = torch.tensor(len(seq))
   OUT.mkdir(parents=True, exist_ok=True)
   arrs = {k: (v.numpy() if isinstance(v, torch.Tensor) else np.asarray(v)) for k, v in out.items()}
-  np.savez_compressed(OUT / fixture, **arrs)
+  save_npz(OUT / fixture, arrs)
   print("wrote", fixture, len(arrs), "arrays;", "terminated", [int(out[f"f{t}_terminated"].sum()) for t in range(frames)],
         "time_outs", [int(out[f"f{t}_time_outs"].sum()) for t in range(frames)])
 
