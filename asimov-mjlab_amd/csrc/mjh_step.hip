@@ -2163,9 +2163,38 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
         d1 = g1 + alpha * g2 + a;
         d2 = g2 + b;
       };
+      float alpha = 0.f;
+      if (m.ls_parallel) {
+        // MuJoCo Warp's parallel line search (solver.py, linesearch_parallel):
+        // the cost at nlsp = ls_iterations step sizes log-spaced over
+        // [ls_parallel_min_step, 1]; the cheapest wins (the smallest on ties).
+        // Two step sizes per pass over the rows, one paired wave reduction.
+        const int nlsp = m.ls_iterations;
+        const float lmin = logf(m.ls_parallel_min_step);
+        const float lstep = (0.f - lmin) / fmaxf(1.f, (float)(nlsp - 1));
+        float best = INFINITY;
+        int bi = 0;
+        for (int k = 0; k < nlsp; k += 2) {
+          const float aa = expf(lmin + (float)k * lstep), ab = expf(lmin + (float)(k + 1) * lstep);
+          float ca = 0.f, cb = 0.f;
+          for (int r = tid; r < nefc; r += NT) {
+            float f, cr;
+            const float ja = jaref[r], j1 = jv[r];
+            row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], ja + aa * j1, &f, &cr);
+            ca += cr;
+            row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], ja + ab * j1, &f, &cr);
+            cb += cr;
+          }
+          bsum2<NT>(ca, cb, red);
+          ca += aa * (g1 + 0.5f * aa * g2);
+          cb += ab * (g1 + 0.5f * ab * g2);
+          if (ca < best) { best = ca; bi = k; }
+          if (k + 1 < nlsp && cb < best) { best = cb; bi = k + 1; }
+        }
+        alpha = expf(lmin + (float)bi * lstep);
+      } else {
       float d10, d20;
       derivs(0.f, d10, d20);
-      float alpha = 0.f;
       if (d10 < 0.f) {
         const float gtol = m.ls_tolerance * fabsf(d10);
         float lo = 0.f, hi = -1.f;
@@ -2179,6 +2208,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
           if (an <= lo || (hi >= 0.f && an >= hi)) an = hi >= 0.f ? 0.5f * (lo + hi) : 2.f * alpha;
           alpha = an;
         }
+      }
       }
       PROF_ACC(12, t_ls);
       if (alpha == 0.f) break;

@@ -203,6 +203,7 @@ class Simulation:
     if cfg.njmax is not None:
       model.njmax = int(cfg.njmax)
     model.contact_sensor_maxmatch = cfg.contact_sensor_maxmatch
+    model.ls_parallel = int(bool(cfg.ls_parallel))  # wp_model.opt.ls_parallel (sim.py:117)
     self.sizes = abi.model_sizes(model)
 
     # ---- model buffers (torch-owned) ----

@@ -300,6 +300,10 @@ def compile_spec(spec: Spec, nconmax: int = 0, njmax: int = 0) -> Model:
   m.jacobian = {"dense": 0, "sparse": 1, "auto": 2}[opt.jacobian]
   m.disableflags = 0
   m.contact_sensor_maxmatch = 64
+  # MuJoCo Warp's parallel line search (Option.ls_parallel / ls_parallel_min_step):
+  # off in a bare model as in mjwarp.put_model; SimulationCfg.ls_parallel sets it
+  m.ls_parallel = 0
+  m.ls_parallel_min_step = 1e-6
 
   # --- bodies ---
   m.body_parentid = parent

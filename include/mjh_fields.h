@@ -34,7 +34,8 @@
   MO(float, gravity_z) MO(float, impratio) MO(float, tolerance)              \
   MO(float, ls_tolerance) MO(int, iterations) MO(int, ls_iterations)         \
   MO(int, integrator) MO(int, cone) MO(int, solver) MO(float, meaninertia)   \
-  MO(int, contact_sensor_maxmatch) MO(int, disableflags)
+  MO(int, contact_sensor_maxmatch) MO(int, disableflags)                     \
+  MO(int, ls_parallel) MO(float, ls_parallel_min_step)
 
 /* ---- static (shared) model arrays ---- */
 #define MJH_MODEL_ARRAYS(MA) \

@@ -962,6 +962,29 @@ static real linesearch(const or_model* m, ws_t* w) {
     g1 += w->search[d] * (w->Ma[d] - w->qfrc_smooth[d]);
     g2 += w->search[d] * w->Mv[d];
   }
+  if (m->ls_parallel) {
+    /* MuJoCo Warp's parallel line search (solver.py linesearch_parallel,
+       restated): the cost at nlsp = ls_iterations step sizes log-spaced over
+       [ls_parallel_min_step, 1]; the cheapest wins (the smallest on ties) */
+    int nlsp = m->ls_iterations;
+    real lmin = log((real)m->ls_parallel_min_step);
+    real lstep = (0 - lmin) / (nlsp - 1 > 1 ? (real)(nlsp - 1) : (real)1);
+    real best = INFINITY;
+    int bi = 0;
+    for (int k = 0; k < nlsp; k++) {
+      real a = exp(lmin + k * lstep), c = a * (g1 + 0.5 * a * g2);
+      for (int r = 0; r < w->nefc; r++) {
+        real f, cr;
+        row_eval(w, r, w->jaref[r] + a * w->jv[r], &f, &cr);
+        c += cr;
+      }
+      if (c < best) {
+        best = c;
+        bi = k;
+      }
+    }
+    return exp(lmin + bi * lstep);
+  }
   /* derivative of cost(alpha) */
 #define DERIVS(alpha, d1, d2)                                         \
   do {                                                                \

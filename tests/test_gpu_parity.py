@@ -15,8 +15,8 @@ CFG = dict(nconmax=50, njmax=300, mujoco=MujocoCfg(timestep=0.005, iterations=10
 MODELS = {"g1": g1_scene_model, "go1": go1_scene_model}
 
 
-def make_sim(m, n, expand=()):
-  sim = Simulation(n, SimulationCfg(**CFG), m, DEV)
+def make_sim(m, n, expand=(), ls_parallel=True):
+  sim = Simulation(n, SimulationCfg(**CFG, ls_parallel=ls_parallel), m, DEV)
   if expand:
     sim.expand_model_fields(tuple(expand))
   return sim
@@ -47,11 +47,16 @@ def assert_parity(got, ref, n, min_int_rate=0.98, tag=""):
 
 @pytest.mark.parametrize("name", ["g1", "go1"])
 @pytest.mark.parametrize("integrate", [True, False])
-def test_single_step_parity(name, integrate):
+@pytest.mark.parametrize("ls_parallel", [True, False])
+def test_single_step_parity(name, integrate, ls_parallel):
+  """Both line searches (SimulationCfg.ls_parallel: MuJoCo Warp's parallel
+  search, the reference default, and the exact 1-D Newton search) against the
+  oracle running the same one, at the capped iteration count."""
   n = 256
   m = MODELS[name](n)
   st = random_states(m, n, np.random.default_rng(1))
-  sim = make_sim(m, n)
+  sim = make_sim(m, n, ls_parallel=ls_parallel)
+  assert m.ls_parallel == int(ls_parallel)  # the oracle reads the same model option
   put(sim, st)
   sim.step() if integrate else sim.forward()
   got = get(sim, n)

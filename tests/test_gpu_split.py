@@ -70,7 +70,7 @@ def test_reuse_is_bitwise_identical_g1():
 
 def test_reuse_is_bitwise_identical_mocap():
   n = 32
-  m = g1_mocap_scene(n)
+  m = g1_mocap_scene(n).compile(50, 300)
   st = mocap_states(m, n, np.random.default_rng(13))
   on, off = _twins(m, n, st)
   for reuse, sim in ((True, on), (False, off)):
