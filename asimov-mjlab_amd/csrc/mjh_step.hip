@@ -1166,7 +1166,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   }
   PROF(0);
 #ifdef MJH_PROFILE
-  if (tid == 0 && g_prof) for (int k = 12; k < 20; k++) g_prof[(long long)w * 32 + k] = 0;
+  if (tid == 0 && g_prof) {
+    for (int k = 12; k < 20; k++) g_prof[(long long)w * 32 + k] = 0;
+    g_prof[(long long)w * 32 + 30] = 0;
+  }
 #endif
 
   // ---------------------------------------------------------------- kinematics
@@ -2192,6 +2195,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
           if (k + 1 < nlsp && cb < best) { best = cb; bi = k + 1; }
         }
         alpha = expf(lmin + (float)bi * lstep);
+#ifdef MJH_PROFILE
+        // diagnostics: the chosen step-size index per iteration, 5 bits each
+        if (tid == 0 && g_prof && it < 12) g_prof[(long long)w * 32 + 30] |= (unsigned long long)(bi & 31) << (5 * it);
+#endif
       } else {
       float d10, d20;
       derivs(0.f, d10, d20);

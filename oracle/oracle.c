@@ -150,6 +150,9 @@ typedef struct {
   real *J, *efc_pos, *efc_margin, *efc_D, *efc_R, *efc_aref, *efc_fl, *jaref, *jv, *efc_force;
   int *efc_type, *efc_id;
   int nefc, ncon, flags, niter;
+  real lsgap; /* parallel line search: smallest relative cost gap best vs runner-up */
+  unsigned long long lstrace; /* chosen step-size index per iteration, 5 bits each */
+  int capped;                 /* the solver stopped at the iteration cap, unconverged */
   contact_t* con;
 } ws_t;
 
@@ -969,7 +972,7 @@ static real linesearch(const or_model* m, ws_t* w) {
     int nlsp = m->ls_iterations;
     real lmin = log((real)m->ls_parallel_min_step);
     real lstep = (0 - lmin) / (nlsp - 1 > 1 ? (real)(nlsp - 1) : (real)1);
-    real best = INFINITY;
+    real best = INFINITY, second = INFINITY;
     int bi = 0;
     for (int k = 0; k < nlsp; k++) {
       real a = exp(lmin + k * lstep), c = a * (g1 + 0.5 * a * g2);
@@ -979,10 +982,20 @@ static real linesearch(const or_model* m, ws_t* w) {
         c += cr;
       }
       if (c < best) {
+        second = best;
         best = c;
         bi = k;
+      } else if (c < second) {
+        second = c;
       }
     }
+    /* a near-tie can be decided differently in float32 (test diagnostics) */
+    real sc = fabs(best) > fabs(second) ? fabs(best) : fabs(second);
+    if (nlsp > 1 && sc > 0) {
+      real gap = (second - best) / sc;
+      if (gap < w->lsgap) w->lsgap = gap;
+    }
+    if (w->niter < 12) w->lstrace |= (unsigned long long)(bi & 31) << (5 * w->niter);
     return exp(lmin + bi * lstep);
   }
   /* derivative of cost(alpha) */
@@ -1068,6 +1081,7 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     for (int d = 0; d < nv; d++) gn += w->grad[d] * w->grad[d];
     real improvement = scale * (old - cost), gradient = scale * sqrt(gn);
     if (improvement < m->tolerance || gradient < m->tolerance) break;
+    if (it == m->iterations - 1) w->capped = 1; /* stopped by the iteration cap */
   }
 }
 
@@ -1286,6 +1300,8 @@ static void sensors(const or_model* m, ws_t* w, real* sd) {
    (nv x nv, dense) and the constraint Jacobian efc_J (njmax x nv, rows < nefc) */
 static real* g_dbg_qM = NULL;
 static real* g_dbg_J = NULL;
+static real* g_dbg_lsgap = NULL;
+static long long* g_dbg_lstrace = NULL;
 
 static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_t* w) {
   int nq = m->nq, nv = m->nv, nu = m->nu, nb = m->nbody;
@@ -1296,6 +1312,9 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   const real* qfrc_applied = d->qfrc_applied + (size_t)wi * nv;
   const real* xfrc = d->xfrc_applied + (size_t)wi * nb * 6;
   w->flags = 0;
+  w->lsgap = INFINITY;
+  w->lstrace = 0;
+  w->capped = 0;
 
   kinematics(m, d, wi, w);
   com_pos(m, wi, w);
@@ -1364,6 +1383,8 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   }
   d->solver_niter[wi] = w->niter;
   if (g_dbg_qM) memcpy(g_dbg_qM + (size_t)wi * nv * nv, w->M, sizeof(real) * nv * nv);
+  if (g_dbg_lsgap) g_dbg_lsgap[wi] = w->lsgap;
+  if (g_dbg_lstrace) g_dbg_lstrace[wi] = (long long)w->lstrace | ((long long)w->capped << 62);
   if (g_dbg_J) memcpy(g_dbg_J + (size_t)wi * m->njmax * nv, w->J, sizeof(real) * (size_t)w->nefc * nv);
 
   if (integrate) {
@@ -1447,9 +1468,11 @@ int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int
   return 0;
 }
 
-void oracle_set_debug(real* qM, real* efc_J) {
+void oracle_set_debug(real* qM, real* efc_J, real* lsgap, long long* lstrace) {
   g_dbg_qM = qM;
   g_dbg_J = efc_J;
+  g_dbg_lsgap = lsgap;
+  g_dbg_lstrace = lstrace;
 }
 
 size_t oracle_sizeof_model(void) { return sizeof(or_model); }

@@ -60,8 +60,14 @@ extern "C" {
  * with nthreads OpenMP threads (<=0: library default). Returns 0 on success. */
 int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int nthreads);
 /* Debug copies written by the next oracle_run calls (NULL: off): qM as
- * (nworld, nv, nv) and efc_J as (nworld, njmax, nv) (rows < nefc written). */
-void oracle_set_debug(real* qM, real* efc_J);
+ * (nworld, nv, nv), efc_J as (nworld, njmax, nv) (rows < nefc written), and
+ * lsgap (nworld): the smallest relative cost gap between the best and the
+ * runner-up step size over the world's parallel line searches (INFINITY if
+ * none ran) — a near-tie a float32 step may decide the other way; lstrace
+ * (nworld): the chosen step-size index of each parallel line search, 5 bits
+ * per solver iteration (diagnostics), and bit 62 set if the solver stopped at
+ * the iteration cap without meeting its tolerance. */
+void oracle_set_debug(real* qM, real* efc_J, real* lsgap, long long* lstrace);
 size_t oracle_sizeof_model(void);
 size_t oracle_sizeof_data(void);
 int oracle_real_bytes(void);

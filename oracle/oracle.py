@@ -38,7 +38,7 @@ class Oracle:
     self.dtype = np.float64 if precision == "f64" else np.float32
     self.lib = ctypes.CDLL(str(ORACLE_DIR / f"liboracle_{precision}.so"))
     self.lib.oracle_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
-    self.lib.oracle_set_debug.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    self.lib.oracle_set_debug.argtypes = [ctypes.c_void_p] * 4
     self.lib.oracle_sizeof_model.restype = ctypes.c_size_t
     self.lib.oracle_sizeof_data.restype = ctypes.c_size_t
     MS = abi.model_struct(self.real, device=False)
@@ -72,7 +72,13 @@ class Oracle:
   def run(self, nworld: int, state: dict, integrate: bool = True, nthreads: int = 1, debug: bool = False) -> dict:
     """One step (or forward) of `nworld` worlds from `state`. debug=True also
     returns the mass matrix ``qM`` (nworld, nv*nv) and the constraint Jacobian
-    ``efc_J`` (nworld, njmax*nv; rows < nefc) of the forward pass."""
+    ``efc_J`` (nworld, njmax*nv; rows < nefc) of the forward pass. Always
+    returned (solver diagnostics, (nworld, 1) each): ``ls_gap``, the smallest
+    relative cost gap between the best and the runner-up step size over the
+    parallel line searches (inf: none ran); ``ls_trace``, the chosen step-size
+    indices (5 bits per iteration); ``solver_capped``, 1 if the solver stopped
+    at the iteration cap unconverged. The debug globals are per process: not
+    for concurrent run() calls."""
     DS = abi.data_struct(self.real, device=False)
     ds = DS()
     ds.nworld = nworld
@@ -91,15 +97,19 @@ class Oracle:
       out[f.name] = a
       setattr(ds, f.name, a.ctypes.data)
     nv, nj = self.sizes["nv"], self.sizes["njmax"]
+    out["ls_gap"] = np.zeros((nworld, 1), self.dtype)
+    out["ls_trace"] = np.zeros((nworld, 1), np.int64)
     if debug:
       out["qM"] = np.zeros((nworld, nv * nv), self.dtype)
       out["efc_J"] = np.zeros((nworld, nj * nv), self.dtype)
-      self.lib.oracle_set_debug(out["qM"].ctypes.data, out["efc_J"].ctypes.data)
+    self.lib.oracle_set_debug(out["qM"].ctypes.data if debug else None, out["efc_J"].ctypes.data if debug else None,
+                              out["ls_gap"].ctypes.data, out["ls_trace"].ctypes.data)
     try:
       rc = self.lib.oracle_run(ctypes.addressof(self.ms), ctypes.addressof(ds), 0, nworld, int(integrate), nthreads)
     finally:
-      if debug:
-        self.lib.oracle_set_debug(None, None)
+      self.lib.oracle_set_debug(None, None, None, None)
     if rc != 0:
       raise RuntimeError(f"oracle_run failed: {rc}")
+    out["solver_capped"] = ((out["ls_trace"] >> 62) & 1).astype(np.int32)
+    out["ls_trace"] &= (1 << 62) - 1
     return out

@@ -20,6 +20,13 @@ here once and cited by the tests:
 * integrated state: qvel |d| <= SOLVE_REL * 2 dt (1 + max|ref qacc|) + 1e-5,
   qpos |d| <= SOLVE_REL * 2 dt^2 (1 + max|ref qacc|) + 1e-5 (same world fractions);
 * sensordata: SOLVE_REL / SOLVE_MAX as the solve (contact forces come out of it).
+* parallel line search (ls_parallel): it takes the cheapest of a fixed set of
+  step sizes, so once a float32 iterate path has made a different choice (a
+  row at its activation kink changes the Newton direction) the paths differ
+  until the solver converges. Worlds the oracle leaves unconverged at the
+  iteration cap (its ``solver_capped``) under the parallel search are held to
+  the SOLVE_REL / SOLVE_FRAC test only, not to SOLVE_MAX; at most
+  LS_CAPPED_FRAC (5 %) of the worlds may be such worlds.
 """
 
 from __future__ import annotations
@@ -248,6 +255,9 @@ def int_mismatch_reason(got: dict, ref: dict, w: int) -> tuple[str, bool] | None
   return "; ".join(reasons), border
 
 
+LS_CAPPED_FRAC = 0.05
+
+
 def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: float = 0.005, solve_rel: float = SOLVE_REL,
                  solve_frac: float = SOLVE_FRAC, solve_max: float = SOLVE_MAX) -> dict:
   """Compare one step's outputs (arrays shaped (nworld, -1)).
@@ -275,6 +285,13 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
       if not r[1]:
         failures.append(f"integer outputs differ in world {int(w)} (not borderline): {r[0]}")
   good = np.array([w for w in sel if int(w) not in reasons], dtype=int)
+  # unconverged worlds under the parallel line search: no hard bound (path-dependent)
+  capped: list[int] = []
+  if "solver_capped" in ref and "ls_gap" in ref:
+    capped = [int(w) for w in good if ref["solver_capped"][w, 0] and np.isfinite(ref["ls_gap"][w, 0])]
+    if len(capped) > max(1, int(LS_CAPPED_FRAC * len(sel))):
+      failures.append(f"{len(capped)}/{len(sel)} worlds unconverged at the iteration cap (> {LS_CAPPED_FRAC:.0%})")
+  solved = good
 
   def check(name: str, tol: float, rows=None) -> None:
     rows = good if rows is None else rows
@@ -306,6 +323,7 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
       failures.append(f"{name}: {n_over}/{len(rows)} worlds over the bound; world {int(rows[w])} max|d|={d[w]:.3e}")
     if rel_max is not None:
       rmax = d / (rel_max * unit + floor)
+      rmax[np.isin(rows, capped)] = 0.0  # unconverged under the parallel search: soft test only
       if (rmax > 1).any():
         w = int(np.argmax(rmax))
         failures.append(f"{name}: world {int(rows[w])} max|d|={d[w]:.3e} > hard bound {rel_max * unit[w] + floor:.3e}")
@@ -333,8 +351,11 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
     # efc_D = imp / ((1 - imp) * invweight): near dmax the impedance amplifies the
     # (5e-5) position difference by ~1 / (1 - imp)^2; measured 1.2e-3 x (1 + max)
     # on the tracking N=4096 world sample (round 2), hence 3e-3
+    hard = np.array([w for w in good if w not in set(capped)], dtype=int)
+    fmask = np.arange(ref["efc_pos"].shape[1])[None, :] < ref["nefc"][hard, 0].astype(int)[:, None]
     for k, rel in (("efc_pos", 5e-5), ("efc_D", 3e-3), ("efc_aref", 1e-3), ("efc_force", solve_rel)):
-      a, b = got[k][good][mask], ref[k][good][mask]
+      rows, mk = (hard, fmask) if k == "efc_force" else (good, mask)
+      a, b = got[k][rows][mk], ref[k][rows][mk]
       tol = 5e-5 if k == "efc_pos" else _bound(b, rel if k != "efc_force" else solve_max)
       e = float(np.abs(a - b).max(initial=0.0))
       maxerr[k] = e
@@ -353,7 +374,7 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
     maxerr["efc_J"] = e
     if not np.isfinite(a).all() or e > _bound(b, 1e-4):
       failures.append(f"efc_J: max|d|={e:.3e} > {_bound(b, 1e-4):.3e}")
-  sv = dict(frac=solve_frac, rel_max=solve_max)
+  sv = dict(frac=solve_frac, rel_max=solve_max, rows=solved)
   for k in SOLVE:
     check_rel(k, solve_rel, **sv)
   # qvel' = qvel + dt * qacc_int, where implicitfast solves (M + dt*D) qacc_int
@@ -362,6 +383,7 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
   check_rel("qpos", solve_rel, scale_name="qacc", scale=2 * dt * dt, floor=1e-5, **sv)
   check_rel("sensordata", solve_rel, **sv)
   return {
+    "capped_worlds": capped,
     "maxerr": maxerr,
     "failures": failures,
     "int_mismatch_worlds": bad_int,
