@@ -127,7 +127,11 @@ bool g_pos_reuse = true;      // mjh_set_position_reuse: split position pass ski
 #endif
 
 #ifdef MJH_PROFILE
+#ifndef MJH_LSDBG_IT
+#define MJH_LSDBG_IT 0
+#endif
 __device__ unsigned long long* g_prof;
+__device__ float* g_lsdbg;  // (nworld, 32) candidate costs of the parallel line search (diagnostics)
 #define PROF(k)                                                           \
   do {                                                                    \
     wsync();                                                              \
@@ -1994,6 +1998,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   // ---------------------------------------------------------------- Newton solver
   const float scale = 1.f / (m.meaninertia * (float)(nv > 1 ? nv : 1));
   int niter = 0, nfactor_total = 0;
+  unsigned lstr0 = 0u, lstr1 = 0u;
   if (nefc == 0) {
     for (int i = tid; i < nv; i += NT) {
       qacc[i] = qacc_smooth[i];
@@ -2191,10 +2196,20 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
           bsum2<NT>(ca, cb, red);
           ca += aa * (g1 + 0.5f * aa * g2);
           cb += ab * (g1 + 0.5f * ab * g2);
+#ifdef MJH_PROFILE
+          // diagnostics: candidate costs at iteration MJH_LSDBG_IT into free profile slots
+          if (tid == 0 && g_lsdbg && it == MJH_LSDBG_IT && k + 1 < 32) {
+            g_lsdbg[(long long)w * 32 + k] = ca;
+            if (k + 1 < nlsp) g_lsdbg[(long long)w * 32 + k + 1] = cb;
+          }
+#endif
           if (ca < best) { best = ca; bi = k; }
           if (k + 1 < nlsp && cb < best) { best = cb; bi = k + 1; }
         }
         alpha = expf(lmin + (float)bi * lstep);
+        // the chosen step-size index per iteration (solver_lstrace, 5 bits each)
+        if (it < 6) lstr0 |= (unsigned)bi << (5 * it);
+        else if (it < 12) lstr1 |= (unsigned)bi << (5 * (it - 6));
 #ifdef MJH_PROFILE
         // diagnostics: the chosen step-size index per iteration, 5 bits each
         if (tid == 0 && g_prof && it < 12) g_prof[(long long)w * 32 + 30] |= (unsigned long long)(bi & 31) << (5 * it);
@@ -2702,6 +2717,8 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
     DP(ncon)[W] = ncon;
     DP(nefc)[W] = nefc;
     DP(solver_niter)[W] = niter;
+    DP(solver_lstrace)[2 * W] = (int)lstr0;
+    DP(solver_lstrace)[2 * W + 1] = (int)lstr1;
   }
 
   // ---------------------------------------------------------------- integration
@@ -3176,6 +3193,15 @@ int mjh_plan_ints(const mjh_model* m, int* out, int cap) {
 }
 
 long long mjh_scratch_words(const mjh_model* m) { return make_plan(m, kWorldsPerBlock).lo.gtotal; }
+
+#ifdef MJH_PROFILE
+// diagnostics (profile builds only; not part of the ABI): the parallel line
+// search's candidate costs at iteration MJH_LSDBG_IT, (nworld, 32) floats
+extern "C" int mjh_set_lsdbg_buffer(void* ptr) {
+  float* p = reinterpret_cast<float*>(ptr);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_lsdbg), &p, sizeof(p)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int mjh_set_profile_buffer(void* ptr) {
 #ifdef MJH_PROFILE

@@ -140,6 +140,9 @@ typedef struct {
   int dim, geom[2], efc_address;
 } contact_t;
 
+static real* g_dbg_lscost;
+static int g_dbg_lscost_it;
+
 typedef struct {
   real *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis, *subtree_com;
   real *cinert, *crb, *cdof, *cdof_dot, *cvel, *cacc, *cfrc;
@@ -153,6 +156,10 @@ typedef struct {
   real lsgap; /* parallel line search: smallest relative cost gap best vs runner-up */
   unsigned long long lstrace; /* chosen step-size index per iteration, 5 bits each */
   int capped;                 /* the solver stopped at the iteration cap, unconverged */
+  int follow, fniter;         /* follow mode: replay fniter iterations with the given choices */
+  int wi;
+  unsigned ftrace[2];
+  real lsexcess;              /* follow mode: worst relative cost excess of a given choice */
   contact_t* con;
 } ws_t;
 
@@ -974,13 +981,25 @@ static real linesearch(const or_model* m, ws_t* w) {
     real lstep = (0 - lmin) / (nlsp - 1 > 1 ? (real)(nlsp - 1) : (real)1);
     real best = INFINITY, second = INFINITY;
     int bi = 0;
+    /* follow mode: the step size the device chose at this iteration (its
+       solver_lstrace), if recorded; its cost excess over the best is reported */
+    int fi = -1;
+    if (w->follow && w->niter < 12) fi = (int)((w->ftrace[w->niter / 6] >> (5 * (w->niter % 6))) & 31u);
+    real cf = 0, c0 = 0, sf = 0, sb = 0;
     for (int k = 0; k < nlsp; k++) {
       real a = exp(lmin + k * lstep), c = a * (g1 + 0.5 * a * g2);
+      /* magnitude of the summed terms: the float32 evaluation's error scale */
+      real s = fabs(a * g1) + fabs(0.5 * a * a * g2);
       for (int r = 0; r < w->nefc; r++) {
         real f, cr;
         row_eval(w, r, w->jaref[r] + a * w->jv[r], &f, &cr);
         c += cr;
+        s += fabs(cr);
       }
+      if (k == fi) { cf = c; sf = s; }
+      if (c < best) sb = s;
+      if (k == 0) c0 = c;
+      if (g_dbg_lscost && w->niter == g_dbg_lscost_it && k < 32) g_dbg_lscost[(size_t)w->wi * 32 + k] = c;
       if (c < best) {
         second = best;
         best = c;
@@ -989,11 +1008,20 @@ static real linesearch(const or_model* m, ws_t* w) {
         second = c;
       }
     }
-    /* a near-tie can be decided differently in float32 (test diagnostics) */
-    real sc = fabs(best) > fabs(second) ? fabs(best) : fabs(second);
-    if (nlsp > 1 && sc > 0) {
-      real gap = (second - best) / sc;
+    /* gaps relative to the search's decrease from its smallest step (~ the
+       current cost): a near-tie can be decided differently in float32 */
+    real dec = c0 - best;
+    if (nlsp > 1 && dec > 0) {
+      real gap = (second - best) / dec;
       if (gap < w->lsgap) w->lsgap = gap;
+    }
+    if (fi >= 0 && fi < nlsp) {
+      /* floor: float32 resolution of the cost (an iteration at convergence
+         decreases it by ~nothing, where any choice is a tie) */
+      real den = (dec > 0 ? dec : 0) + 1e-5 * (sf > sb ? sf : sb);
+      real ex = den > 0 ? (cf - best) / den : 0;
+      if (ex > w->lsexcess) w->lsexcess = ex;
+      bi = fi;
     }
     if (w->niter < 12) w->lstrace |= (unsigned long long)(bi & 31) << (5 * w->niter);
     return exp(lmin + bi * lstep);
@@ -1066,6 +1094,7 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
   }
   newton_direction(m, w);
   for (int it = 0; it < m->iterations; it++) {
+    if (w->follow && it >= w->fniter) break;
     real alpha = linesearch(m, w);
     if (alpha == 0) break;
     for (int d = 0; d < nv; d++) {
@@ -1080,7 +1109,7 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     real gn = 0;
     for (int d = 0; d < nv; d++) gn += w->grad[d] * w->grad[d];
     real improvement = scale * (old - cost), gradient = scale * sqrt(gn);
-    if (improvement < m->tolerance || gradient < m->tolerance) break;
+    if (!w->follow && (improvement < m->tolerance || gradient < m->tolerance)) break;
     if (it == m->iterations - 1) w->capped = 1; /* stopped by the iteration cap */
   }
 }
@@ -1298,10 +1327,13 @@ static void sensors(const or_model* m, ws_t* w, real* sd) {
 /* ---------------------------------------------------------------- driver */
 /* optional per-world debug copies (oracle_set_debug): the mass matrix qM
    (nv x nv, dense) and the constraint Jacobian efc_J (njmax x nv, rows < nefc) */
+static real* g_dbg_lscost = NULL; /* (nworld, 32): candidate costs at one iteration */
+static int g_dbg_lscost_it = 0;
 static real* g_dbg_qM = NULL;
 static real* g_dbg_J = NULL;
 static real* g_dbg_lsgap = NULL;
 static long long* g_dbg_lstrace = NULL;
+static int g_follow = 0;
 
 static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_t* w) {
   int nq = m->nq, nv = m->nv, nu = m->nu, nb = m->nbody;
@@ -1314,7 +1346,15 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   w->flags = 0;
   w->lsgap = INFINITY;
   w->lstrace = 0;
+  w->wi = wi;
   w->capped = 0;
+  w->lsexcess = 0;
+  w->follow = g_follow && m->ls_parallel;
+  if (w->follow) {
+    w->fniter = d->solver_niter[wi];
+    w->ftrace[0] = (unsigned)d->solver_lstrace[2 * wi];
+    w->ftrace[1] = (unsigned)d->solver_lstrace[2 * wi + 1];
+  }
 
   kinematics(m, d, wi, w);
   com_pos(m, wi, w);
@@ -1383,7 +1423,9 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   }
   d->solver_niter[wi] = w->niter;
   if (g_dbg_qM) memcpy(g_dbg_qM + (size_t)wi * nv * nv, w->M, sizeof(real) * nv * nv);
-  if (g_dbg_lsgap) g_dbg_lsgap[wi] = w->lsgap;
+  if (g_dbg_lsgap) g_dbg_lsgap[wi] = w->follow ? w->lsexcess : w->lsgap;
+  d->solver_lstrace[2 * wi] = (int)(w->lstrace & 0x3fffffffull);
+  d->solver_lstrace[2 * wi + 1] = (int)((w->lstrace >> 30) & 0x3fffffffull);
   if (g_dbg_lstrace) g_dbg_lstrace[wi] = (long long)w->lstrace | ((long long)w->capped << 62);
   if (g_dbg_J) memcpy(g_dbg_J + (size_t)wi * m->njmax * nv, w->J, sizeof(real) * (size_t)w->nefc * nv);
 
@@ -1466,6 +1508,13 @@ int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int
   }
   (void)nthreads;
   return 0;
+}
+
+void oracle_set_follow(int on) { g_follow = on; }
+
+void oracle_set_lscost(real* cost, int iteration) {
+  g_dbg_lscost = cost;
+  g_dbg_lscost_it = iteration;
 }
 
 void oracle_set_debug(real* qM, real* efc_J, real* lsgap, long long* lstrace) {

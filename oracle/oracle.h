@@ -68,6 +68,15 @@ int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int
  * per solver iteration (diagnostics), and bit 62 set if the solver stopped at
  * the iteration cap without meeting its tolerance. */
 void oracle_set_debug(real* qM, real* efc_J, real* lsgap, long long* lstrace);
+/* Follow mode (parallel line search only): each world replays the device's
+ * discrete choices — solver_niter iterations, the step-size index of each from
+ * solver_lstrace (inputs then) — instead of its own argmin and stopping test;
+ * lsgap then reports the worst relative cost excess of a replayed choice over
+ * the float64 argmin (a correct device choice is a near-tie: excess ~ 0). */
+void oracle_set_follow(int on);
+/* Diagnostics: the parallel line search's candidate costs at one solver
+ * iteration, (nworld, 32) (NULL: off). */
+void oracle_set_lscost(real* cost, int iteration);
 size_t oracle_sizeof_model(void);
 size_t oracle_sizeof_data(void);
 int oracle_real_bytes(void);

@@ -39,6 +39,7 @@ class Oracle:
     self.lib = ctypes.CDLL(str(ORACLE_DIR / f"liboracle_{precision}.so"))
     self.lib.oracle_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     self.lib.oracle_set_debug.argtypes = [ctypes.c_void_p] * 4
+    self.lib.oracle_set_follow.argtypes = [ctypes.c_int]
     self.lib.oracle_sizeof_model.restype = ctypes.c_size_t
     self.lib.oracle_sizeof_data.restype = ctypes.c_size_t
     MS = abi.model_struct(self.real, device=False)
@@ -69,7 +70,8 @@ class Oracle:
         setattr(ms, f.name + "_wstride", stride)
     self.ms = ms
 
-  def run(self, nworld: int, state: dict, integrate: bool = True, nthreads: int = 1, debug: bool = False) -> dict:
+  def run(self, nworld: int, state: dict, integrate: bool = True, nthreads: int = 1, debug: bool = False,
+          follow: dict | None = None) -> dict:
     """One step (or forward) of `nworld` worlds from `state`. debug=True also
     returns the mass matrix ``qM`` (nworld, nv*nv) and the constraint Jacobian
     ``efc_J`` (nworld, njmax*nv; rows < nefc) of the forward pass. Always
@@ -78,7 +80,16 @@ class Oracle:
     parallel line searches (inf: none ran); ``ls_trace``, the chosen step-size
     indices (5 bits per iteration); ``solver_capped``, 1 if the solver stopped
     at the iteration cap unconverged. The debug globals are per process: not
-    for concurrent run() calls."""
+    for concurrent run() calls.
+
+    follow: the device's outputs of the same step (``solver_niter``,
+    ``solver_lstrace``). Under the parallel line search each world then replays
+    the device's discrete choices (iteration count, step-size index per
+    iteration) and ``ls_excess`` (nworld, 1) replaces ``ls_gap``: the worst
+    relative float64 cost excess of a replayed choice over the argmin."""
+    if follow is not None:
+      state = dict(state, solver_niter=np.asarray(follow["solver_niter"]).reshape(nworld, -1),
+                   solver_lstrace=np.asarray(follow["solver_lstrace"]).reshape(nworld, -1))
     DS = abi.data_struct(self.real, device=False)
     ds = DS()
     ds.nworld = nworld
@@ -104,12 +115,16 @@ class Oracle:
       out["efc_J"] = np.zeros((nworld, nj * nv), self.dtype)
     self.lib.oracle_set_debug(out["qM"].ctypes.data if debug else None, out["efc_J"].ctypes.data if debug else None,
                               out["ls_gap"].ctypes.data, out["ls_trace"].ctypes.data)
+    self.lib.oracle_set_follow(1 if follow is not None else 0)
     try:
       rc = self.lib.oracle_run(ctypes.addressof(self.ms), ctypes.addressof(ds), 0, nworld, int(integrate), nthreads)
     finally:
       self.lib.oracle_set_debug(None, None, None, None)
+      self.lib.oracle_set_follow(0)
     if rc != 0:
       raise RuntimeError(f"oracle_run failed: {rc}")
     out["solver_capped"] = ((out["ls_trace"] >> 62) & 1).astype(np.int32)
     out["ls_trace"] &= (1 << 62) - 1
+    if follow is not None and self.ms.ls_parallel:
+      out["ls_excess"] = out.pop("ls_gap")
     return out

@@ -21,12 +21,17 @@ here once and cited by the tests:
   qpos |d| <= SOLVE_REL * 2 dt^2 (1 + max|ref qacc|) + 1e-5 (same world fractions);
 * sensordata: SOLVE_REL / SOLVE_MAX as the solve (contact forces come out of it).
 * parallel line search (ls_parallel): it takes the cheapest of a fixed set of
-  step sizes, so once a float32 iterate path has made a different choice (a
-  row at its activation kink changes the Newton direction) the paths differ
-  until the solver converges. Worlds the oracle leaves unconverged at the
-  iteration cap (its ``solver_capped``) under the parallel search are held to
-  the SOLVE_REL / SOLVE_FRAC test only, not to SOLVE_MAX; at most
-  LS_CAPPED_FRAC (5 %) of the worlds may be such worlds.
+  step sizes — a discrete choice that a float32 run may make differently at a
+  near-tie, after which the iterate paths differ. Compared in follow mode
+  (``Oracle.run(follow=got)``: the oracle replays the device's iteration count
+  and step-size index per iteration, from ``solver_niter`` / ``solver_lstrace``),
+  every replayed choice must cost at most LS_TIE (5 %) of (the search's
+  decrease + 1e-5 of the summed term magnitudes, the float32 resolution of
+  the cost sum) more than the float64 argmin (``ls_excess``); the outputs
+  are held to the bounds above.
+  Without follow mode, worlds the oracle leaves unconverged at the iteration
+  cap (``solver_capped``) are held to the SOLVE_REL / SOLVE_FRAC test only
+  (at most LS_CAPPED_FRAC = 5 % of the worlds).
 """
 
 from __future__ import annotations
@@ -148,7 +153,7 @@ def go1_scene_model(num_envs: int, nconmax: int = 50, njmax: int = 300):
 
 def random_states(m, n: int, rng: np.random.Generator, drop: float = 0.06) -> dict:
   """Keyframe stance perturbed: base height (feet in/above the ground), yaw,
-  joint offsets, random velocities and PD targets."""
+  joint offsets, random velocities and PD targets; zero solver warm start."""
   qpos = np.tile(m.key_qpos, (n, 1)).astype(np.float64)
   qpos[:, 2] += rng.uniform(-drop, 0.02, n)
   yaw = rng.uniform(-np.pi, np.pi, n)
@@ -158,7 +163,10 @@ def random_states(m, n: int, rng: np.random.Generator, drop: float = 0.06) -> di
   qpos[:, 7:] += rng.uniform(-0.15, 0.15, (n, m.nq - 7))
   qvel = rng.normal(0, 0.3, (n, m.nv))
   ctrl = np.tile(m.key_ctrl, (n, 1)) + rng.uniform(-0.3, 0.3, (n, m.nu))
-  return {"qpos": qpos, "qvel": qvel, "ctrl": ctrl}
+  # the solver's warm start is an input too: set it, so that the device (whose
+  # qacc_warmstart otherwise holds the construction-time forward's qacc) and the
+  # oracle start their solves from the same point
+  return {"qpos": qpos, "qvel": qvel, "ctrl": ctrl, "qacc_warmstart": np.zeros((n, m.nv))}
 
 
 def _bound(ref: np.ndarray, rel: float) -> float:
@@ -255,6 +263,7 @@ def int_mismatch_reason(got: dict, ref: dict, w: int) -> tuple[str, bool] | None
   return "; ".join(reasons), border
 
 
+LS_TIE = 0.05
 LS_CAPPED_FRAC = 0.05
 
 
@@ -287,7 +296,13 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
   good = np.array([w for w in sel if int(w) not in reasons], dtype=int)
   # unconverged worlds under the parallel line search: no hard bound (path-dependent)
   capped: list[int] = []
-  if "solver_capped" in ref and "ls_gap" in ref:
+  if "ls_excess" in ref and len(good):
+    ex = ref["ls_excess"][good, 0]
+    maxerr["ls_excess"] = float(ex.max(initial=0.0))
+    if (ex > LS_TIE).any():
+      w = int(good[int(np.argmax(ex))])
+      failures.append(f"ls_excess: world {w} replayed a step size {ex.max():.2e} (relative) above the float64 argmin")
+  elif "solver_capped" in ref and "ls_gap" in ref:
     capped = [int(w) for w in good if ref["solver_capped"][w, 0] and np.isfinite(ref["ls_gap"][w, 0])]
     if len(capped) > max(1, int(LS_CAPPED_FRAC * len(sel))):
       failures.append(f"{len(capped)}/{len(sel)} worlds unconverged at the iteration cap (> {LS_CAPPED_FRAC:.0%})")

