@@ -32,6 +32,10 @@ Rank 0 prints ONE JSON line with, in addition to the contract fields:
                   (5,384 B per world per physics step) / average
                   launch duration, against the 8 TB/s HBM peak. `traffic` is the
                   PMC-measured HBM bytes per launch from profiles/ (or null).
+  roofline_valu — the same launch against the VALU issue peak: SQ_INSTS_VALU
+                  per launch from the committed counter summary
+                  (profiles/step_kernel_sq.json) / live launch time, 2 cycles
+                  per wave64 instruction on 1024 SIMD-32 at 2.4 GHz.
   cpu_baseline  — the CPU restatement (oracle/, float64 and float32, OpenMP
                   over worlds) of the same physics step on this host's cores,
                   bounded sample of the live state.
@@ -59,6 +63,10 @@ DEFAULT_ENVS = {TASK: 4096, "Mjlab-Velocity-Flat-Unitree-Go1": 8192, "Mjlab-Trac
 B_PHYS = {"Unitree-Go1": 3040}
 B_PHYS_G1 = 5384
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+# VALU issue peak: 256 CUs x 4 SIMD-32, a wave64 VALU instruction issues over 2
+# cycles, 2.4 GHz max clock (MI355X_MICROARCH.md:34, :53-54)
+N_SIMD, CLK_HZ, VALU_CYC = 1024, 2.4e9, 2
+VALU_PEAK_GIPS = N_SIMD * CLK_HZ / VALU_CYC / 1e9
 
 
 def parse() -> argparse.Namespace:
@@ -340,6 +348,23 @@ def main() -> None:
         traffic = tj.get("bytes_per_launch")
     except (ValueError, OSError):
       traffic = None
+  # VALU roofline: SQ_INSTS_VALU of the step kernel(s) of one physics step, from
+  # the committed counter summary of the same workload (tools/gpu_pmc_sq.sh ->
+  # profiles/step_kernel_sq.json), over the live launch time: issue cycles
+  # (2 per wave64 instruction) / SIMD-cycles available
+  valu = None
+  sqf = REPO / "profiles" / "step_kernel_sq.json"
+  if sqf.exists():
+    try:
+      sj = json.loads(sqf.read_text())
+      if int(sj.get("num_envs", -1)) == num_envs and sj.get("task", TASK) == args.task:
+        ins = float(sj["valu_insts_per_launch"])
+        gips = ins / t_launch / 1e9
+        valu = {"bound": "valu", "achieved": gips, "peak": VALU_PEAK_GIPS, "unit": "G wave64-VALU-instr/s",
+                "frac": gips / VALU_PEAK_GIPS, "insts_per_launch": ins, "source": sj.get("source", sqf.name),
+                "model": "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x launch time)"}
+    except (ValueError, OSError, KeyError):
+      valu = None
   nv = sim.mj_model.nv
   b_solve = niter * 4 * (nefc * nv + nv * nv + 6 * nefc + 4 * nv) + 4 * (nefc + 2 * nv)
 
@@ -417,6 +442,7 @@ def main() -> None:
         "bytes_per_launch": bytes_per_launch,
         "solver_streamed_model_gbs": b_solve * num_envs / t_launch / 1e9,
       },
+      "roofline_valu": valu,
       "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

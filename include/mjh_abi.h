@@ -150,7 +150,8 @@ int mjh_set_world_ordering(int on);
  * bit-identical to its previous position pass, whose results are still in the
  * world's scratch (e.g. the first physics step after a forward — the env step's
  * reset-forward, manager_based_rl_env.py:133-137). Results are bit-identical
- * either way. Returns mjh_split_step(). */
+ * either way. Applies to launches issued after the call (a captured graph keeps
+ * the setting it was captured with). Returns mjh_split_step(). */
 int mjh_set_position_reuse(int on);
 
 /* 1 if this build launches the step as two kernels (position, then velocity /

@@ -1109,8 +1109,9 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     real gn = 0;
     for (int d = 0; d < nv; d++) gn += w->grad[d] * w->grad[d];
     real improvement = scale * (old - cost), gradient = scale * sqrt(gn);
-    if (!w->follow && (improvement < m->tolerance || gradient < m->tolerance)) break;
-    if (it == m->iterations - 1) w->capped = 1; /* stopped by the iteration cap */
+    int conv = improvement < m->tolerance || gradient < m->tolerance;
+    if (!w->follow && conv) break;
+    if (it == m->iterations - 1 && !conv) w->capped = 1; /* stopped by the iteration cap, unconverged */
   }
 }
 

@@ -24,9 +24,18 @@ def _split_only():
 
 
 def _run(sim, reuse, fn):
-  native.lib().mjh_set_position_reuse(1 if reuse else 0)
-  fn()
+  fn()  # a graph replay: the reuse setting was captured with the graph (_make)
   torch.cuda.synchronize()
+
+
+def _make(m, n, reuse, expand=()):
+  """A Simulation whose captured step/forward graphs launch with position reuse
+  on or off (the setting applies to launches issued after it, graph captures
+  included)."""
+  native.lib().mjh_set_position_reuse(1 if reuse else 0)
+  sim = make_sim(m, n, expand)
+  native.lib().mjh_set_position_reuse(1)
+  return sim
 
 
 def _same(a, b, tag):
@@ -35,7 +44,7 @@ def _same(a, b, tag):
 
 
 def _twins(m, n, st, expand=()):
-  sims = [make_sim(m, n, expand), make_sim(m, n, expand)]
+  sims = [_make(m, n, True, expand), _make(m, n, False, expand)]
   for s in sims:
     put(s, st)
   return sims
@@ -88,7 +97,7 @@ def test_reuse_skips_unchanged_worlds():
   n = 16
   m = g1_scene_model(n)
   st = random_states(m, n, np.random.default_rng(14))
-  sim = make_sim(m, n)
+  sim = _make(m, n, True)
   put(sim, st)
   _run(sim, True, sim.forward)
   ref = sim.data.geom_xpos.clone()
@@ -101,7 +110,7 @@ def test_reuse_skips_unchanged_worlds():
   assert bool((g[skipped] == 123.0).all())
   assert not bool((g[1] == 123.0).any())
   # the same with reuse off: every world recomputes
-  sim2 = make_sim(m, n)
+  sim2 = _make(m, n, False)
   put(sim2, st)
   _run(sim2, False, sim2.forward)
   sim2.data.geom_xpos.fill_(123.0)

@@ -14,6 +14,7 @@ import sys
 def main() -> None:
   pat, skip, files = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
   acc: dict[str, dict[int, float]] = {}
+  per_kernel: dict[str, dict[str, dict[int, float]]] = {}
   for f in files:
     for r in csv.DictReader(open(f)):
       if pat not in r["Kernel_Name"]:
@@ -21,6 +22,8 @@ def main() -> None:
       d = int(r["Dispatch_Id"])
       acc.setdefault(r["Counter_Name"], {})
       acc[r["Counter_Name"]][d] = acc[r["Counter_Name"]].get(d, 0.0) + float(r["Counter_Value"])
+      pk = per_kernel.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], {})
+      pk[d] = pk.get(d, 0.0) + float(r["Counter_Value"])
   out = {}
   for name, per in sorted(acc.items()):
     ks = sorted(per)[skip:] or sorted(per)
@@ -35,6 +38,12 @@ def main() -> None:
       if name in out:
         der[name + "_per_wave"] = out[name] / w
     out["derived"] = der
+  # per kernel instance (a split step launches two step kernels per physics step)
+  def mean_after_skip(per: dict[int, float]) -> float:
+    ks = sorted(per)[skip:] or sorted(per)
+    return sum(per[k] for k in ks) / len(ks)
+
+  out["per_kernel"] = {k: {c: mean_after_skip(v) for c, v in cs.items()} for k, cs in per_kernel.items()}
   print(json.dumps(out, indent=1))
 
 
