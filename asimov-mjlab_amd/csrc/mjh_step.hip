@@ -2176,12 +2176,59 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
         // MuJoCo Warp's parallel line search (solver.py, linesearch_parallel):
         // the cost at nlsp = ls_iterations step sizes log-spaced over
         // [ls_parallel_min_step, 1]; the cheapest wins (the smallest on ties).
-        // Two step sizes per pass over the rows, one paired wave reduction.
         const int nlsp = m.ls_iterations;
         const float lmin = logf(m.ls_parallel_min_step);
         const float lstep = (0.f - lmin) / fmaxf(1.f, (float)(nlsp - 1));
         float best = INFINITY;
         int bi = 0;
+        if (nefc <= 2 * NT) {
+          // a lane's (at most two) rows in registers, loaded once; four step
+          // sizes per block, their four wave reductions independent (the
+          // reduction latency overlaps instead of serialising per step size)
+          int ty[2];
+          float rD[2], rR[2], rf[2], rj[2], rv[2];
+#pragma unroll
+          for (int q = 0; q < 2; q++) {
+            const int r = tid + q * NT;
+            const bool in = r < nefc;
+            ty[q] = in ? efc_type[r] : -1;
+            rD[q] = in ? efc_D[r] : 0.f;
+            rR[q] = in ? efc_R[r] : 0.f;
+            rf[q] = in ? efc_fl[r] : 0.f;
+            rj[q] = in ? jaref[r] : 0.f;
+            rv[q] = in ? jv[r] : 0.f;
+          }
+          // row cost at step a (row_state's cost, branch-free selects)
+          auto rcost = [&](int q, float a) -> float {
+            const float x = rj[q] + a * rv[q];
+            const float quad = 0.5f * rD[q] * x * x;
+            if (ty[q] == MJH_CNSTR_FRICTION_DOF) {
+              const float lim = rR[q] * rf[q], k = 0.5f * rR[q] * rf[q] * rf[q];
+              return x >= lim ? rf[q] * x - k : (x <= -lim ? -rf[q] * x - k : quad);
+            }
+            return (ty[q] >= 0 && x < 0.f) ? quad : 0.f;
+          };
+          // The cost is convex in the step size (a convex quadratic plus
+          // convex piecewise-quadratic rows), so its first minimiser on the
+          // increasing grid is found scanning down from the largest step and
+          // stopping at the first increase — the same index as evaluating
+          // all nlsp (ties go to the smaller step), usually after one pair,
+          // since the full Newton step (1) mostly wins.
+          bi = nlsp - 1;
+          for (int k = nlsp - 1; k >= 0; k -= 2) {
+            const float a0 = expf(lmin + (float)k * lstep), a1 = expf(lmin + (float)(k - 1) * lstep);
+            float c0 = rcost(0, a0) + rcost(1, a0), c1 = rcost(0, a1) + rcost(1, a1);
+            bsum2<NT>(c0, c1, red);
+            c0 += a0 * (g1 + 0.5f * a0 * g2);
+            c1 += a1 * (g1 + 0.5f * a1 * g2);
+            if (!(c0 <= best)) break;
+            best = c0;
+            bi = k;
+            if (k - 1 < 0 || !(c1 <= best)) break;
+            best = c1;
+            bi = k - 1;
+          }
+        } else
         for (int k = 0; k < nlsp; k += 2) {
           const float aa = expf(lmin + (float)k * lstep), ab = expf(lmin + (float)(k + 1) * lstep);
           float ca = 0.f, cb = 0.f;

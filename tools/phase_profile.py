@@ -21,13 +21,15 @@ sys.path.insert(0, str(ROOT))
 from tests.scenes import g1_scene, random_states
 from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg, native
 
-NAMES = ["kinematics", "com/crb/M/factor", "rne/smooth/qacc_smooth", "collision", "constraints", "solver",
+NAMES = ["kinematics", "com/crb/M/factor", "collision", "constraints", "rne/smooth/qacc_smooth", "solver",
          "cacc+sensors", "outputs", "integration"]
+PHASES = [(0, 1), (1, 2), (2, 4), (4, 5), (5, 3), (3, 6), (6, 7), (7, 8), (8, 9)]
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 sc = g1_scene(N)
 m = sc.compile(50, 300)
-cfg = SimulationCfg(nconmax=50, njmax=300, mujoco=MujocoCfg(timestep=0.005, iterations=10, ls_iterations=20))
+cfg = SimulationCfg(nconmax=50, njmax=300, mujoco=MujocoCfg(timestep=0.005, iterations=10, ls_iterations=20),
+                    ls_parallel=os.environ.get("MJH_LS_PARALLEL", "1") == "1")
 buf = torch.zeros(N * 32, dtype=torch.int64, device="cuda:0")
 L = native.lib()
 L.mjh_set_profile_buffer.argtypes = [ctypes.c_void_p]
@@ -42,11 +44,13 @@ for _ in range(int(os.environ.get("SETTLE", "20"))):
   sim.step()
 torch.cuda.synchronize()
 p = buf.view(N, 32).cpu().numpy().astype(np.int64)
-d = np.diff(p[:, :10], axis=1)
 tot = p[:, 9] - p[:, 0]
-print(f"N={N} mean total cycles/world-step: {tot.mean():.0f} (max {tot.max()})")
-for i, n in enumerate(NAMES):
-  print(f"  {n:26s} {d[:, i].mean():10.0f}  ({100*d[:, i].mean()/tot.mean():5.1f}%)")
+print(f"N={N} ls_parallel={int(cfg.ls_parallel)} mean total cycles/world-step: {tot.mean():.0f} (max {tot.max()})")
+# phase stamps in execution order: the position stage (kinematics .. constraint
+# rows) runs before the velocity stage (rne / smooth forces / qacc_smooth)
+for n, (a, b) in zip(NAMES, PHASES):
+  v = (p[:, b] - p[:, a]).mean()
+  print(f"  {n:26s} {v:10.0f}  ({100*v/tot.mean():5.1f}%)")
 print(f"  solver: linesearch {p[:,12].mean():.0f}  update {p[:,13].mean():.0f}  newton_dir {p[:,14].mean():.0f}")
 print(f"    newton_dir parts: hessian {p[:,15].mean():.0f}  factor {p[:,16].mean():.0f}  solve {p[:,17].mean():.0f}")
 print(f"  M factor alone: {(p[:,2]-p[:,10]).mean():.0f}  (com/crb/M before it: {(p[:,10]-p[:,1]).mean():.0f})")
@@ -54,12 +58,12 @@ def seg(a, b):
   return (p[:, b] - p[:, a]).mean()
 print(f"  kinematics: bodies {seg(0,27):.0f} geoms {seg(27,28):.0f} sites {seg(28,1):.0f}")
 print(f"  com: subtree+cinert {seg(1,18):.0f} cdof {seg(18,19):.0f} crb {seg(19,20):.0f} M-fill {seg(20,10):.0f} factor {seg(10,2):.0f}")
-print(f"  rne: cvel {seg(2,21):.0f} cdof_dot {seg(21,22):.0f} rne {seg(22,23):.0f} cfrc-sum+bias {seg(23,24):.0f} "
+print(f"  rne: cvel {seg(5,21):.0f} cdof_dot {seg(21,22):.0f} rne {seg(22,23):.0f} cfrc-sum+bias {seg(23,24):.0f} "
       f"passive/act/smooth {seg(24,25):.0f} qacc_smooth solve {seg(25,3):.0f}")
 niter = sim.data.solver_niter.cpu().numpy()
 nefc = sim.data.nefc.cpu().numpy()
 wg = tot[: (N // 8) * 8].reshape(-1, 8)
-print(f"  hessian+factor recomputations per world-step: {p[:, 29].mean():.2f}  rank-1 factor updates: {p[:, 30].mean():.0f} cycles")
+print(f"  hessian+factor recomputations per world-step: {p[:, 29].mean():.2f}")
 print(f"  workgroup (8 worlds) max/mean: {wg.max(1).mean():.0f} / {tot.mean():.0f}; "
       f"p50 {np.percentile(tot, 50):.0f} p90 {np.percentile(tot, 90):.0f} p99 {np.percentile(tot, 99):.0f}")
 for nm, x in (("nefc", nefc), ("niter", niter)):
