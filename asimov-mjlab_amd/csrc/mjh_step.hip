@@ -2133,6 +2133,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
       cs += cr;
     }
     const float cost_smooth = bsum<NT>(cs, red);
+    // the warm-start choice is recorded with the step-size choices (bit 30 of
+    // solver_lstrace[1]): the parity tests replay it too
+    if (cost > cost_smooth) lstr1 |= 1u << 30;
     if (cost > cost_smooth) {
       for (int i = tid; i < nv; i += NT) {
         qacc[i] = qacc_smooth[i];

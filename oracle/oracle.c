@@ -157,6 +157,7 @@ typedef struct {
   unsigned long long lstrace; /* chosen step-size index per iteration, 5 bits each */
   int capped;                 /* the solver stopped at the iteration cap, unconverged */
   int follow, fniter;         /* follow mode: replay fniter iterations with the given choices */
+  int warm_smooth;            /* the solve started from qacc_smooth (not qacc_warmstart) */
   int wi;
   unsigned ftrace[2];
   real lsexcess;              /* follow mode: worst relative cost excess of a given choice */
@@ -1081,7 +1082,9 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     row_eval(w, r, s - w->efc_aref[r], &f, &c);
     cost_smooth += c;
   }
-  if (cost > cost_smooth) {
+  int from_smooth = w->follow ? (int)((w->ftrace[1] >> 30) & 1u) : cost > cost_smooth;
+  w->warm_smooth = from_smooth;
+  if (from_smooth) {
     memcpy(w->qacc, w->qacc_smooth, sizeof(real) * nv);
     memcpy(w->Ma, w->qfrc_smooth, sizeof(real) * nv);
     mat_vec_n(w->M, w->qacc, w->Ma, nv);
@@ -1347,6 +1350,7 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   w->flags = 0;
   w->lsgap = INFINITY;
   w->lstrace = 0;
+  w->warm_smooth = 0;
   w->wi = wi;
   w->capped = 0;
   w->lsexcess = 0;
@@ -1426,7 +1430,7 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   if (g_dbg_qM) memcpy(g_dbg_qM + (size_t)wi * nv * nv, w->M, sizeof(real) * nv * nv);
   if (g_dbg_lsgap) g_dbg_lsgap[wi] = w->follow ? w->lsexcess : w->lsgap;
   d->solver_lstrace[2 * wi] = (int)(w->lstrace & 0x3fffffffull);
-  d->solver_lstrace[2 * wi + 1] = (int)((w->lstrace >> 30) & 0x3fffffffull);
+  d->solver_lstrace[2 * wi + 1] = (int)((w->lstrace >> 30) & 0x3fffffffull) | (w->warm_smooth << 30);
   if (g_dbg_lstrace) g_dbg_lstrace[wi] = (long long)w->lstrace | ((long long)w->capped << 62);
   if (g_dbg_J) memcpy(g_dbg_J + (size_t)wi * m->njmax * nv, w->J, sizeof(real) * (size_t)w->nefc * nv);
 

@@ -72,7 +72,9 @@ void oracle_set_debug(real* qM, real* efc_J, real* lsgap, long long* lstrace);
  * discrete choices — solver_niter iterations, the step-size index of each from
  * solver_lstrace (inputs then) — instead of its own argmin and stopping test;
  * lsgap then reports the worst relative cost excess of a replayed choice over
- * the float64 argmin (a correct device choice is a near-tie: excess ~ 0). */
+ * the float64 argmin (a correct device choice is a near-tie: excess ~ 0). The
+ * warm-start choice (bit 30 of solver_lstrace[1]: start from qacc_smooth) is
+ * replayed as well. */
 void oracle_set_follow(int on);
 /* Diagnostics: the parallel line search's candidate costs at one solver
  * iteration, (nworld, 32) (NULL: off). */

@@ -34,6 +34,8 @@ class Oracle:
   def __init__(self, model, precision: str = "f64", overrides: dict | None = None) -> None:
     build()
     self.model = model
+    self._overrides = overrides
+    self._f32 = None
     self.real = ctypes.c_double if precision == "f64" else ctypes.c_float
     self.dtype = np.float64 if precision == "f64" else np.float32
     self.lib = ctypes.CDLL(str(ORACLE_DIR / f"liboracle_{precision}.so"))
@@ -86,7 +88,10 @@ class Oracle:
     ``solver_lstrace``). Under the parallel line search each world then replays
     the device's discrete choices (iteration count, step-size index per
     iteration) and ``ls_excess`` (nworld, 1) replaces ``ls_gap``: the worst
-    relative float64 cost excess of a replayed choice over the argmin."""
+    relative float64 cost excess of a replayed choice over the argmin. A float64
+    follow run also replays the step in the float32 build and returns its
+    outputs under ``f32`` — the same algorithm and choices at float32: each
+    world's own rounding sensitivity, which the parity checker uses as a floor."""
     if follow is not None:
       state = dict(state, solver_niter=np.asarray(follow["solver_niter"]).reshape(nworld, -1),
                    solver_lstrace=np.asarray(follow["solver_lstrace"]).reshape(nworld, -1))
@@ -127,4 +132,8 @@ class Oracle:
     out["ls_trace"] &= (1 << 62) - 1
     if follow is not None and self.ms.ls_parallel:
       out["ls_excess"] = out.pop("ls_gap")
+    if follow is not None and self.dtype == np.float64:
+      if self._f32 is None:
+        self._f32 = Oracle(self.model, "f32", overrides=self._overrides)
+      out["f32"] = self._f32.run(nworld, state, integrate=integrate, nthreads=nthreads, follow=follow)
     return out

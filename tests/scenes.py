@@ -20,6 +20,13 @@ here once and cited by the tests:
 * integrated state: qvel |d| <= SOLVE_REL * 2 dt (1 + max|ref qacc|) + 1e-5,
   qpos |d| <= SOLVE_REL * 2 dt^2 (1 + max|ref qacc|) + 1e-5 (same world fractions);
 * sensordata: SOLVE_REL / SOLVE_MAX as the solve (contact forces come out of it).
+* float32 sensitivity floor: when the oracle replays the device's solver choices
+  (follow mode) it also runs its float32 build on the same inputs; every
+  per-world solve/integration/sensor bound above is floored at F32_SENSITIVITY
+  (4) x that float32 run's deviation from float64 — a world whose stiff
+  contacts make even the same algorithm in float32 deviate (measured: the
+  device is within 0.6-2.6x of it, G1 env sample) is not held tighter than
+  float32 allows.
 * parallel line search (ls_parallel): it takes the cheapest of a fixed set of
   step sizes — a discrete choice that a float32 run may make differently at a
   near-tie, after which the iterate paths differ. Compared in follow mode
@@ -269,6 +276,7 @@ def int_mismatch_reason(got: dict, ref: dict, w: int) -> tuple[str, bool] | None
   return "; ".join(reasons), border
 
 
+F32_SENSITIVITY = 4.0
 LS_TIE = 0.05
 LS_TIE_FRAC = 0.01
 LS_CAPPED_FRAC = 0.15
@@ -339,6 +347,11 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
     s_ref = ref[scale_name or name][rows]
     d = np.abs(a - b).max(axis=1)
     unit = scale * (1.0 + np.abs(s_ref).max(axis=1))
+    # floor: F32_SENSITIVITY x the float32 oracle's own deviation (same algorithm
+    # and choices, follow mode), i.e. the world's float32 rounding sensitivity
+    f32 = ref.get("f32")
+    sens = F32_SENSITIVITY * np.abs(f32[name][rows] - b).max(axis=1) if f32 is not None and name in f32 else 0.0
+    floor = np.maximum(floor, sens)
     ratio = d / (rel * unit + floor)
     maxerr[name] = float(d.max(initial=0.0))
     maxerr[name + "/bound"] = float(ratio.max(initial=0.0))
