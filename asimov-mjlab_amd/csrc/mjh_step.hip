@@ -972,10 +972,10 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 // integration), starting from the handoff region. Split, the position stage
 // needs far fewer registers and LDS, so it runs at higher occupancy, and the
 // first physics step after a gated forward skips it.
-template <int WPB, bool STEP, int NVP, int SPEC = -1, bool SLAB = false, int MODE = 0>
+template <int WPB, int NVP, int SPEC = -1, bool SLAB = false, int MODE = 0>
 __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo_,
                                                          const ImgOff Io_, const unsigned char* gate, int reuse,
-                                                         unsigned long long key) {
+                                                         unsigned long long key, int step_flag) {
   constexpr int NT = 64;  // one wave per world
   const Layout Lo = spec_layout<SPEC>(Lo_);
   const ImgOff Io = spec_imgoff<SPEC>(Io_);
@@ -994,20 +994,26 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   }
   __syncthreads();
   const int wave = threadIdx.x >> 6;
-  // position pass: a hash of the model image this workgroup staged (every
-  // workgroup computes the same value), part of the reuse snapshot
+  // a checksum of the staged model image (each wave over the whole image: no
+  // cross-wave exchange), part of the position-reuse snapshot, so an in-place
+  // edit of a shared model field between a forward and a step is seen
   unsigned long long img_hash = 0ull;
-  if constexpr (MODE == 1) {
-    __shared__ unsigned long long hpart[WPB];
-    const unsigned* iw = reinterpret_cast<const unsigned*>(smem);
-    unsigned long long h = 0ull;
-    for (int i = threadIdx.x; i < Io.img_words; i += 64 * WPB) h += mix64(((unsigned long long)i << 32) | iw[i]);
+  if (MODE == 1 || (MODE == 0 && reuse)) {
+    const uint4* iw = reinterpret_cast<const uint4*>(smem);
+    unsigned h1 = 0u, h2 = 0u;
+    const int lane = threadIdx.x & 63;
+    for (int i = lane; i < (Io.img_words >> 2); i += 64) {
+      const uint4 v = iw[i];
+      const unsigned k = 8u * (unsigned)i + 1u;
+      h1 += v.x * k + v.y * (k + 2u) + v.z * (k + 4u) + v.w * (k + 6u);
+      h2 += (v.x ^ 0x9E3779B9u) * 0x85EBCA6Bu + (v.y ^ k) * 0xC2B2AE35u + (v.z + k) * 0x27D4EB2Fu + (v.w ^ (k << 7)) * 0x165667B1u;
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
-    if ((threadIdx.x & 63) == 0) hpart[wave] = h;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < WPB; k++) img_hash += hpart[k];
+    for (int o = 32; o > 0; o >>= 1) {
+      h1 += __shfl_xor(h1, o, 64);
+      h2 += __shfl_xor(h2, o, 64);
+    }
+    img_hash = ((unsigned long long)h2 << 32) | h1;
   }
   const int slot = blockIdx.x * WPB + wave;
   if (slot >= d.nworld) return;
@@ -1016,6 +1022,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   // of nearly uniform cost, keeps the identity order)
   const int w = (MODE != 1 && d.world_order) ? (int)d.world_order[slot] : slot;
   const int tid = threadIdx.x & 63;
+  // mj_step (integration) or mj_forward: a runtime flag, not a template
+  // parameter, so both run the very same code up to the integration (a step
+  // reusing a forward's position stage is then bit-identical to recomputing it)
+  const bool STEP = step_flag != 0;
   float* S = smem + Io.img_words + wave * (MODE == 1 ? Lo.ptotal : Lo.total);
   int* SI = reinterpret_cast<int*>(S);
   float* G = d.scratch + (long long)w * d.scratch_words;  // this world's global scratch
@@ -1128,10 +1138,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   // raw bits
   unsigned* const snap = reinterpret_cast<unsigned*>(G + Lo.h_snap);
   unsigned long long wf_hash = 0ull;
-  if constexpr (MODE == 0) {
-    if (tid == 0) snap[0] = 0u;
-  }
-  if constexpr (MODE == 1) {
+  // fused kernel: a step launch whose world is unchanged since the last
+  // forward's position stage (which saved its LDS results, below) reuses them
+  bool reused = false;
+  if constexpr (MODE == 1 || MODE == 0) {
     {  // per-world (expanded) model fields of this world
       unsigned long long h = 0ull;
       int fid = 0;
@@ -1165,8 +1175,17 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
         for (int i = tid; i < 3 * Z.nmocap; i += NT) same = same && snap[7 + nq + i] == mp[i];
         for (int i = tid; i < 4 * Z.nmocap; i += NT) same = same && snap[7 + nq + 3 * Z.nmocap + i] == mq[i];
       }
-      if (__all(same)) return;  // the last position pass of this world is current
+      if constexpr (MODE == 1) {
+        if (__all(same)) return;  // the last position pass of this world is current
+      } else {
+        reused = STEP && __all(same);
+      }
     }
+  }
+  // a fused launch that recomputes the position stage overwrites the arrays a
+  // saved snapshot describes (a forward saves a new one at the end of its stage)
+  if constexpr (MODE == 0) {
+    if (!reused && tid == 0) snap[0] = 0u;
   }
   PROF(0);
 #ifdef MJH_PROFILE
@@ -1194,7 +1213,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   // lane b holds body b's chain mask; the subtree loops read it by readlane
   // (no LDS load per body on their dependency chain)
   const unsigned long long r_tmk = bl ? tmk[tid] : 0ull;
-  if constexpr (MODE != 2) {
+  if (MODE == 1 || (MODE == 0 && !reused)) {
   float r_xipos[3] = {0.f, 0.f, 0.f}, r_ximat[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int b = tid; b < nb; b += NT) {
     float p[3] = {0.f, 0.f, 0.f}, q[4] = {1.f, 0.f, 0.f, 0.f};
@@ -1782,6 +1801,39 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   }
   nefc = ints[I_NEFC];
   PROF(5);
+  if (MODE == 0 && !STEP && reuse) {
+    // a forward saves its position stage's LDS results (the factor of M, the
+    // rows' position parameters, counters) and the snapshot: the next step
+    // launch on an unchanged world (qpos is only integrated by steps, so the
+    // first step after a forward) skips the position stage
+    wsync();
+    if (tid < I_COUNT) reinterpret_cast<int*>(G + Lo.h_ints)[tid] = ints[tid];
+    for (int i = tid; i < nv * ldm; i += NT) G[Lo.h_L + i] = Lm[i];
+    int* ht = reinterpret_cast<int*>(G + Lo.h_type);
+    for (int r = tid; r < nefc; r += NT) {
+      ht[r] = efc_type[r];
+      G[Lo.h_fl + r] = efc_fl[r];
+      G[Lo.h_D + r] = efc_D[r];
+      G[Lo.h_R + r] = efc_R[r];
+      G[Lo.h_aref + r] = efc_aref[r];
+      G[Lo.h_b + r] = efc_b[r];
+    }
+    const unsigned* qb = reinterpret_cast<const unsigned*>(qpos);
+    for (int i = tid; i < nq; i += NT) snap[7 + i] = qb[i];
+    if (Z.nmocap > 0) {
+      const unsigned* mp = reinterpret_cast<const unsigned*>(DP(mocap_pos) + W * Z.nmocap * 3);
+      const unsigned* mq = reinterpret_cast<const unsigned*>(DP(mocap_quat) + W * Z.nmocap * 4);
+      for (int i = tid; i < 3 * Z.nmocap; i += NT) snap[7 + nq + i] = mp[i];
+      for (int i = tid; i < 4 * Z.nmocap; i += NT) snap[7 + nq + 3 * Z.nmocap + i] = mq[i];
+    }
+    if (tid == 0) {
+      snap[1] = (unsigned)img_hash; snap[2] = (unsigned)(img_hash >> 32);
+      snap[3] = (unsigned)wf_hash; snap[4] = (unsigned)(wf_hash >> 32);
+      snap[5] = (unsigned)key; snap[6] = (unsigned)(key >> 32);
+    }
+    wsync();
+    if (tid == 0) snap[0] = 1u;
+  }
   }  // position stage
   if constexpr (MODE == 1) {
     // handoff: counters / overflow flags, then the snapshot that lets the next
@@ -1805,7 +1857,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
     if (tid == 0) snap[0] = 1u;
     return;
   } else {
-  if constexpr (MODE == 2) {
+  if (MODE == 2 || reused) {
     // the position stage's results: counters, the rows' position parameters
     // (LDS for the solver), registers of the tree passes
     const int* ih = reinterpret_cast<const int*>(G + Lo.h_ints);
@@ -1828,7 +1880,11 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
       efc_D[r] = G[Lo.h_D + r];
       efc_R[r] = G[Lo.h_R + r];
       efc_aref[r] = G[Lo.h_aref + r];
+      if constexpr (MODE == 0) efc_b[r] = G[Lo.h_b + r];
     }
+    // the fused kernel keeps the factor of M in LDS
+    if constexpr (MODE == 0)
+      for (int i = tid; i < nv * ldm; i += NT) Lm[i] = G[Lo.h_L + i];
   }
   wsync();
   // aref = aref_pos - b J qvel (row_params: the velocity term)
@@ -2773,7 +2829,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
 
   // ---------------------------------------------------------------- integration
   PROF(8);
-  if constexpr (STEP) {
+  if (STEP) {
     const float dt = m.timestep;
     float* qa_int = tmp;
     if (m.integrator == MJH_INT_IMPLICITFAST) {
@@ -3117,17 +3173,15 @@ unsigned long long launch_key(const mjh_model* m, const mjh_data* d) {
 template <int WPB, bool STEP, int NVP, int SPEC, bool SLAB, int MODE>
 void launch_mode(const Plan& p, const mjh_model* m, const mjh_data* d, const unsigned char* gate, hipStream_t s,
                  int reuse, unsigned long long key) {
-  auto kern = step_kernel<WPB, STEP, NVP, SPEC, SLAB, MODE>;
+  auto kern = step_kernel<WPB, NVP, SPEC, SLAB, MODE>;
   static bool attr = false;
   if (!attr) {
-    // the position kernel has a little static LDS (the image-hash partials)
-    const int maxdyn = MODE == 1 ? kLdsBytes - 1024 : kLdsBytes;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, maxdyn);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     attr = true;
   }
   const int blocks = (d->nworld + WPB - 1) / WPB;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * WPB), MODE == 1 ? p.shmem_pos : p.shmem, s, *m, *d, p.lo, p.io, gate,
-                     reuse, key);
+                     reuse, key, STEP ? 1 : 0);
 }
 
 template <bool STEP, int NVP, int SPEC, bool SLAB>
@@ -3136,7 +3190,7 @@ void launch_step(const Plan& p, const mjh_model* m, const mjh_data* d, const uns
     launch_mode<kPosWorldsPerBlock, STEP, NVP, SPEC, SLAB, 1>(p, m, d, gate, s, g_pos_reuse ? 1 : 0, launch_key(m, d));
     launch_mode<kWorldsPerBlock, STEP, NVP, SPEC, SLAB, 2>(p, m, d, gate, s, 0, 0ull);
   } else {
-    launch_mode<kWorldsPerBlock, STEP, NVP, SPEC, SLAB, 0>(p, m, d, gate, s, 0, 0ull);
+    launch_mode<kWorldsPerBlock, STEP, NVP, SPEC, SLAB, 0>(p, m, d, gate, s, g_pos_reuse ? 1 : 0, launch_key(m, d));
   }
 }
 

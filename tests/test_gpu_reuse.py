@@ -1,8 +1,10 @@
-"""The split step (a position launch, then a velocity/solver launch) and its
-position reuse: a world whose qpos, mocap poses and model are bit-identical to
-its previous position pass skips that pass (mjh_set_position_reuse). Results
-must be bit-identical with reuse on and off, and a change of any input the
-position stage reads must force the pass."""
+"""Position reuse (mjh_set_position_reuse): a step launch on a world whose
+qpos, mocap poses and model are bit-identical to the last forward's position
+pass reuses that pass's results instead of recomputing kinematics, collision
+and the constraint rows (the fused kernel: the forward saves them; the split
+build, MJH_SPLIT=1: its position launch skips the world). Results must be
+bit-identical with reuse on and off, and a change of any input the position
+stage reads must force the pass."""
 
 import numpy as np
 import pytest
@@ -16,9 +18,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _split_only():
-  if int(native.lib().mjh_split_step()) == 0:
-    pytest.skip("library built without the split step (MJH_SPLIT=0)")
+def _restore_reuse():
   yield
   native.lib().mjh_set_position_reuse(1)
 
@@ -116,3 +116,37 @@ def test_reuse_skips_unchanged_worlds():
   sim2.data.geom_xpos.fill_(123.0)
   _run(sim2, False, sim2.step)
   assert torch.equal(sim2.data.geom_xpos, ref)
+
+
+def test_env_steps_bitwise_with_and_without_reuse():
+  """The G1 velocity env (resets, DR, pushes, the gated forward every step):
+  observations, rewards and dones identical with position reuse on and off."""
+  from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
+  from mjlab_amd.tasks import load_env_cfg
+
+  n = 64
+
+  def make(reuse):
+    native.lib().mjh_set_position_reuse(1 if reuse else 0)
+    cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+    cfg.scene.num_envs = n
+    cfg.seed = 7
+    env = ManagerBasedRlEnv(cfg, device=DEV)
+    env.reset()
+    env.episode_length_buf.copy_(torch.arange(n, device=DEV) * 15 % int(env.max_episode_length))
+    g = torch.Generator(device=DEV).manual_seed(3)
+    for _ in range(3):  # the env-step graph is captured here, with this reuse setting
+      env.step(2 * torch.rand(n, env.action_manager.total_action_dim, device=DEV, generator=g) - 1)
+    native.lib().mjh_set_position_reuse(1)
+    return env, g
+
+  (a, ga), (b, _) = make(True), make(False)
+  for k in range(20):
+    act = 2 * torch.rand(n, a.action_manager.total_action_dim, device=DEV, generator=ga) - 1
+    oa, ra, ta, tra, _ = a.step(act)
+    ob, rb, tb, trb, _ = b.step(act.clone())
+    torch.cuda.synchronize()
+    for grp in oa:
+      assert torch.equal(oa[grp], ob[grp]), (k, grp)
+    assert torch.equal(ra, rb) and torch.equal(ta, tb) and torch.equal(tra, trb), k
+  assert torch.equal(a.sim.data.qpos, b.sim.data.qpos)
