@@ -76,7 +76,7 @@ def test_trajectory_parity_along_gpu_rollout():
   st = random_states(m, n, np.random.default_rng(2), drop=0.03)
   put(sim, st)
   orc = Oracle(m)
-  worst = 0.0
+  worst = worst32 = 0.0
   for k in range(40):
     cur = get(sim, n)
     state = {f: cur[f] for f in INPUTS if f in cur}
@@ -85,7 +85,10 @@ def test_trajectory_parity_along_gpu_rollout():
     ref = orc.run(n, state, integrate=True, follow=nxt)
     rep = assert_parity(nxt, ref, n, min_int_rate=0.95, tag=f" step {k}")
     worst = max(worst, rep["maxerr"]["qvel"])
-  assert worst < 0.05
+    worst32 = max(worst32, float(np.abs(ref["f32"]["qvel"] - ref["qvel"]).max()))
+  # 0.05 m/s, or the float32 oracle's own deviation along the same choices (x4,
+  # tests/scenes.py F32_SENSITIVITY) where stiff contacts make that larger
+  assert worst < max(0.05, 4.0 * worst32), (worst, worst32)
 
 
 def test_per_world_randomized_friction():
