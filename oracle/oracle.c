@@ -1000,7 +1000,12 @@ static real linesearch(const or_model* m, ws_t* w) {
       if (k == fi) { cf = c; sf = s; }
       if (c < best) sb = s;
       if (k == 0) c0 = c;
-      if (g_dbg_lscost && w->niter == g_dbg_lscost_it && k < 32) g_dbg_lscost[(size_t)w->wi * 32 + k] = c;
+      if (g_dbg_lscost && k < 32) {
+        if (g_dbg_lscost_it < 0 && w->niter < 12)
+          g_dbg_lscost[((size_t)w->wi * 12 + w->niter) * 32 + k] = c;
+        else if (w->niter == g_dbg_lscost_it)
+          g_dbg_lscost[(size_t)w->wi * 32 + k] = c;
+      }
       if (c < best) {
         second = best;
         best = c;

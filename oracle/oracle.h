@@ -76,8 +76,9 @@ void oracle_set_debug(real* qM, real* efc_J, real* lsgap, long long* lstrace);
  * warm-start choice (bit 30 of solver_lstrace[1]: start from qacc_smooth) is
  * replayed as well. */
 void oracle_set_follow(int on);
-/* Diagnostics: the parallel line search's candidate costs at one solver
- * iteration, (nworld, 32) (NULL: off). */
+/* The parallel line search's candidate costs at one solver iteration,
+ * (nworld, 32), or with iteration = -1 at every iteration < 12, (nworld, 12, 32)
+ * (NULL: off). */
 void oracle_set_lscost(real* cost, int iteration);
 size_t oracle_sizeof_model(void);
 size_t oracle_sizeof_data(void);

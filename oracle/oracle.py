@@ -42,6 +42,7 @@ class Oracle:
     self.lib.oracle_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     self.lib.oracle_set_debug.argtypes = [ctypes.c_void_p] * 4
     self.lib.oracle_set_follow.argtypes = [ctypes.c_int]
+    self.lib.oracle_set_lscost.argtypes = [ctypes.c_void_p, ctypes.c_int]
     self.lib.oracle_sizeof_model.restype = ctypes.c_size_t
     self.lib.oracle_sizeof_data.restype = ctypes.c_size_t
     MS = abi.model_struct(self.real, device=False)
@@ -121,11 +122,15 @@ class Oracle:
     self.lib.oracle_set_debug(out["qM"].ctypes.data if debug else None, out["efc_J"].ctypes.data if debug else None,
                               out["ls_gap"].ctypes.data, out["ls_trace"].ctypes.data)
     self.lib.oracle_set_follow(1 if follow is not None else 0)
+    if follow is not None:  # every candidate cost of every replayed search (the choice check)
+      out["ls_costs"] = np.full((nworld, 12, 32), np.nan, self.dtype)
+      self.lib.oracle_set_lscost(out["ls_costs"].ctypes.data, -1)
     try:
       rc = self.lib.oracle_run(ctypes.addressof(self.ms), ctypes.addressof(ds), 0, nworld, int(integrate), nthreads)
     finally:
       self.lib.oracle_set_debug(None, None, None, None)
       self.lib.oracle_set_follow(0)
+      self.lib.oracle_set_lscost(None, 0)
     if rc != 0:
       raise RuntimeError(f"oracle_run failed: {rc}")
     out["solver_capped"] = ((out["ls_trace"] >> 62) & 1).astype(np.int32)

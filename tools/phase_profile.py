@@ -90,3 +90,9 @@ def wg_max(order):
 print(f"  next step: corr(cycles_t, cycles_t+1) = {np.corrcoef(tot1, tot2)[0, 1]:.2f}; "
       f"workgroup max mean: identity {wg_max(np.arange(N)):.0f}, by prev cycles {wg_max(np.argsort(-tot1)):.0f}, "
       f"by prev (niter+2)*nefc {wg_max(np.argsort(-key1, kind='stable')):.0f}, by true cost {wg_max(np.argsort(-tot2)):.0f}")
+
+# per-world data of the two steps for offline predictor studies
+if os.environ.get("DUMP"):
+  np.savez_compressed(os.environ["DUMP"], tot1=tot1, tot2=tot2, niter=niter.reshape(-1), nefc=nefc.reshape(-1),
+                      ncon=sim.data.ncon.cpu().numpy().reshape(-1), niter2=sim.data.solver_niter.cpu().numpy().reshape(-1),
+                      nefc2=sim.data.nefc.cpu().numpy().reshape(-1))
