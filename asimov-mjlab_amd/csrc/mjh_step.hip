@@ -2054,7 +2054,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   // ---------------------------------------------------------------- Newton solver
   const float scale = 1.f / (m.meaninertia * (float)(nv > 1 ? nv : 1));
   int niter = 0, nfactor_total = 0;
-  unsigned lstr0 = 0u, lstr1 = 0u;
+  // solver_lstrace: the parallel line search's step-size index (6 bits) of
+  // iterations 5w..5w+4 in word w (15 iterations), bit 30 of word 0: the solve
+  // started from qacc_smooth (the parity tests replay both choices)
+  unsigned lstr0 = 0u, lstr1 = 0u, lstr2 = 0u;
   if (nefc == 0) {
     for (int i = tid; i < nv; i += NT) {
       qacc[i] = qacc_smooth[i];
@@ -2189,9 +2192,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
       cs += cr;
     }
     const float cost_smooth = bsum<NT>(cs, red);
-    // the warm-start choice is recorded with the step-size choices (bit 30 of
-    // solver_lstrace[1]): the parity tests replay it too
-    if (cost > cost_smooth) lstr1 |= 1u << 30;
+    if (cost > cost_smooth) lstr0 |= 1u << 30;
     if (cost > cost_smooth) {
       for (int i = tid; i < nv; i += NT) {
         qacc[i] = qacc_smooth[i];
@@ -2313,13 +2314,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
           if (k + 1 < nlsp && cb < best) { best = cb; bi = k + 1; }
         }
         alpha = expf(lmin + (float)bi * lstep);
-        // the chosen step-size index per iteration (solver_lstrace, 5 bits each)
-        if (it < 6) lstr0 |= (unsigned)bi << (5 * it);
-        else if (it < 12) lstr1 |= (unsigned)bi << (5 * (it - 6));
-#ifdef MJH_PROFILE
-        // diagnostics: the chosen step-size index per iteration, 5 bits each
-        if (tid == 0 && g_prof && it < 12) g_prof[(long long)w * 32 + 30] |= (unsigned long long)(bi & 31) << (5 * it);
-#endif
+        if (it < 5) lstr0 |= (unsigned)(bi & 63) << (6 * it);
+        else if (it < 10) lstr1 |= (unsigned)(bi & 63) << (6 * (it - 5));
+        else if (it < 15) lstr2 |= (unsigned)(bi & 63) << (6 * (it - 10));
       } else {
       float d10, d20;
       derivs(0.f, d10, d20);
@@ -2823,8 +2820,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
     DP(ncon)[W] = ncon;
     DP(nefc)[W] = nefc;
     DP(solver_niter)[W] = niter;
-    DP(solver_lstrace)[2 * W] = (int)lstr0;
-    DP(solver_lstrace)[2 * W + 1] = (int)lstr1;
+    DP(solver_lstrace)[3 * W] = (int)lstr0;
+    DP(solver_lstrace)[3 * W + 1] = (int)lstr1;
+    DP(solver_lstrace)[3 * W + 2] = (int)lstr2;
   }
 
   // ---------------------------------------------------------------- integration

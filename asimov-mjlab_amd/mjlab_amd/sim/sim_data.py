@@ -70,7 +70,7 @@ DATA_SHAPES: dict[str, tuple] = {
   "solver_niter": (),
   "flags": (),
   "flags_acc": (),
-  "solver_lstrace": (2,),
+  "solver_lstrace": (3,),
 }
 
 MODEL_SHAPES: dict[str, tuple] = {

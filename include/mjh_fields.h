@@ -117,4 +117,4 @@
   DA(int, nefc, 1) DA(int, efc_type, njmax) DA(int, efc_id, njmax)           \
   DA(float, efc_pos, njmax) DA(float, efc_D, njmax) DA(float, efc_aref, njmax) \
   DA(float, efc_force, njmax) DA(int, solver_niter, 1) DA(int, flags, 1)    \
-  DA(int, flags_acc, 1) DA(int, solver_lstrace, 2)
+  DA(int, flags_acc, 1) DA(int, solver_lstrace, 3)

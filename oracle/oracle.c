@@ -142,6 +142,8 @@ typedef struct {
 
 static real* g_dbg_lscost;
 static int g_dbg_lscost_it;
+static int g_ls_scan = 0;
+static _Thread_local real g_dbg_scan_cost[64];
 
 typedef struct {
   real *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis, *subtree_com;
@@ -154,12 +156,12 @@ typedef struct {
   int *efc_type, *efc_id;
   int nefc, ncon, flags, niter;
   real lsgap; /* parallel line search: smallest relative cost gap best vs runner-up */
-  unsigned long long lstrace; /* chosen step-size index per iteration, 5 bits each */
+  unsigned lstrace[3];        /* solver_lstrace: step-size index (6 bits) of iterations 5w..5w+4 in word w */
   int capped;                 /* the solver stopped at the iteration cap, unconverged */
   int follow, fniter;         /* follow mode: replay fniter iterations with the given choices */
   int warm_smooth;            /* the solve started from qacc_smooth (not qacc_warmstart) */
   int wi;
-  unsigned ftrace[2];
+  unsigned ftrace[3];
   real lsexcess;              /* follow mode: worst relative cost excess of a given choice */
   contact_t* con;
 } ws_t;
@@ -985,7 +987,7 @@ static real linesearch(const or_model* m, ws_t* w) {
     /* follow mode: the step size the device chose at this iteration (its
        solver_lstrace), if recorded; its cost excess over the best is reported */
     int fi = -1;
-    if (w->follow && w->niter < 12) fi = (int)((w->ftrace[w->niter / 6] >> (5 * (w->niter % 6))) & 31u);
+    if (w->follow && w->niter < 15) fi = (int)((w->ftrace[w->niter / 5] >> (6 * (w->niter % 5))) & 63u);
     real cf = 0, c0 = 0, sf = 0, sb = 0;
     for (int k = 0; k < nlsp; k++) {
       real a = exp(lmin + k * lstep), c = a * (g1 + 0.5 * a * g2);
@@ -998,13 +1000,14 @@ static real linesearch(const or_model* m, ws_t* w) {
         s += fabs(cr);
       }
       if (k == fi) { cf = c; sf = s; }
+      if (k < 64) g_dbg_scan_cost[k] = c;
       if (c < best) sb = s;
       if (k == 0) c0 = c;
-      if (g_dbg_lscost && k < 32) {
-        if (g_dbg_lscost_it < 0 && w->niter < 12)
-          g_dbg_lscost[((size_t)w->wi * 12 + w->niter) * 32 + k] = c;
+      if (g_dbg_lscost && k < 64) {
+        if (g_dbg_lscost_it < 0 && w->niter < 15)
+          g_dbg_lscost[((size_t)w->wi * 15 + w->niter) * 64 + k] = c;
         else if (w->niter == g_dbg_lscost_it)
-          g_dbg_lscost[(size_t)w->wi * 32 + k] = c;
+          g_dbg_lscost[(size_t)w->wi * 64 + k] = c;
       }
       if (c < best) {
         second = best;
@@ -1021,6 +1024,13 @@ static real linesearch(const or_model* m, ws_t* w) {
       real gap = (second - best) / dec;
       if (gap < w->lsgap) w->lsgap = gap;
     }
+    if (g_ls_scan && fi < 0) {
+      /* diagnostics: the device's rule (scan down from the full step, stop at
+         the first increase) on the same candidate costs */
+      int k = nlsp - 1;
+      while (k > 0 && g_dbg_scan_cost[k - 1] <= g_dbg_scan_cost[k]) k--;
+      bi = k;
+    }
     if (fi >= 0 && fi < nlsp) {
       /* floor: float32 resolution of the cost (an iteration at convergence
          decreases it by ~nothing, where any choice is a tie) */
@@ -1029,7 +1039,7 @@ static real linesearch(const or_model* m, ws_t* w) {
       if (ex > w->lsexcess) w->lsexcess = ex;
       bi = fi;
     }
-    if (w->niter < 12) w->lstrace |= (unsigned long long)(bi & 31) << (5 * w->niter);
+    if (w->niter < 15) w->lstrace[w->niter / 5] |= (unsigned)(bi & 63) << (6 * (w->niter % 5));
     return exp(lmin + bi * lstep);
   }
   /* derivative of cost(alpha) */
@@ -1087,7 +1097,7 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     row_eval(w, r, s - w->efc_aref[r], &f, &c);
     cost_smooth += c;
   }
-  int from_smooth = w->follow ? (int)((w->ftrace[1] >> 30) & 1u) : cost > cost_smooth;
+  int from_smooth = w->follow ? (int)((w->ftrace[0] >> 30) & 1u) : cost > cost_smooth;
   w->warm_smooth = from_smooth;
   if (from_smooth) {
     memcpy(w->qacc, w->qacc_smooth, sizeof(real) * nv);
@@ -1354,7 +1364,7 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   const real* xfrc = d->xfrc_applied + (size_t)wi * nb * 6;
   w->flags = 0;
   w->lsgap = INFINITY;
-  w->lstrace = 0;
+  w->lstrace[0] = w->lstrace[1] = w->lstrace[2] = 0u;
   w->warm_smooth = 0;
   w->wi = wi;
   w->capped = 0;
@@ -1362,8 +1372,7 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   w->follow = g_follow && m->ls_parallel;
   if (w->follow) {
     w->fniter = d->solver_niter[wi];
-    w->ftrace[0] = (unsigned)d->solver_lstrace[2 * wi];
-    w->ftrace[1] = (unsigned)d->solver_lstrace[2 * wi + 1];
+    for (int k = 0; k < 3; k++) w->ftrace[k] = (unsigned)d->solver_lstrace[3 * wi + k];
   }
 
   kinematics(m, d, wi, w);
@@ -1434,9 +1443,10 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   d->solver_niter[wi] = w->niter;
   if (g_dbg_qM) memcpy(g_dbg_qM + (size_t)wi * nv * nv, w->M, sizeof(real) * nv * nv);
   if (g_dbg_lsgap) g_dbg_lsgap[wi] = w->follow ? w->lsexcess : w->lsgap;
-  d->solver_lstrace[2 * wi] = (int)(w->lstrace & 0x3fffffffull);
-  d->solver_lstrace[2 * wi + 1] = (int)((w->lstrace >> 30) & 0x3fffffffull) | (w->warm_smooth << 30);
-  if (g_dbg_lstrace) g_dbg_lstrace[wi] = (long long)w->lstrace | ((long long)w->capped << 62);
+  d->solver_lstrace[3 * wi] = (int)(w->lstrace[0] | ((unsigned)w->warm_smooth << 30));
+  d->solver_lstrace[3 * wi + 1] = (int)w->lstrace[1];
+  d->solver_lstrace[3 * wi + 2] = (int)w->lstrace[2];
+  if (g_dbg_lstrace) g_dbg_lstrace[wi] = (long long)w->capped;
   if (g_dbg_J) memcpy(g_dbg_J + (size_t)wi * m->njmax * nv, w->J, sizeof(real) * (size_t)w->nefc * nv);
 
   if (integrate) {
@@ -1521,6 +1531,8 @@ int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int
 }
 
 void oracle_set_follow(int on) { g_follow = on; }
+
+void oracle_set_ls_scan(int on) { g_ls_scan = on; }
 
 void oracle_set_lscost(real* cost, int iteration) {
   g_dbg_lscost = cost;

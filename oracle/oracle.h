@@ -64,9 +64,8 @@ int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int
  * lsgap (nworld): the smallest relative cost gap between the best and the
  * runner-up step size over the world's parallel line searches (INFINITY if
  * none ran) — a near-tie a float32 step may decide the other way; lstrace
- * (nworld): the chosen step-size index of each parallel line search, 5 bits
- * per solver iteration (diagnostics), and bit 62 set if the solver stopped at
- * the iteration cap without meeting its tolerance. */
+ * (nworld): 1 if the solver stopped at the iteration cap without meeting its
+ * tolerance (the step-size choices are in data.solver_lstrace). */
 void oracle_set_debug(real* qM, real* efc_J, real* lsgap, long long* lstrace);
 /* Follow mode (parallel line search only): each world replays the device's
  * discrete choices — solver_niter iterations, the step-size index of each from
@@ -77,8 +76,9 @@ void oracle_set_debug(real* qM, real* efc_J, real* lsgap, long long* lstrace);
  * replayed as well. */
 void oracle_set_follow(int on);
 /* The parallel line search's candidate costs at one solver iteration,
- * (nworld, 32), or with iteration = -1 at every iteration < 12, (nworld, 12, 32)
+ * (nworld, 64), or with iteration = -1 at every iteration < 15, (nworld, 15, 64)
  * (NULL: off). */
+void oracle_set_ls_scan(int on);
 void oracle_set_lscost(real* cost, int iteration);
 size_t oracle_sizeof_model(void);
 size_t oracle_sizeof_data(void);

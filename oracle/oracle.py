@@ -80,9 +80,9 @@ class Oracle:
     ``efc_J`` (nworld, njmax*nv; rows < nefc) of the forward pass. Always
     returned (solver diagnostics, (nworld, 1) each): ``ls_gap``, the smallest
     relative cost gap between the best and the runner-up step size over the
-    parallel line searches (inf: none ran); ``ls_trace``, the chosen step-size
-    indices (5 bits per iteration); ``solver_capped``, 1 if the solver stopped
-    at the iteration cap unconverged. The debug globals are per process: not
+    parallel line searches (inf: none ran); ``solver_capped``, 1 if the solver
+    stopped at the iteration cap unconverged (the step-size choices are in
+    ``solver_lstrace``). The debug globals are per process: not
     for concurrent run() calls.
 
     follow: the device's outputs of the same step (``solver_niter``,
@@ -123,7 +123,7 @@ class Oracle:
                               out["ls_gap"].ctypes.data, out["ls_trace"].ctypes.data)
     self.lib.oracle_set_follow(1 if follow is not None else 0)
     if follow is not None:  # every candidate cost of every replayed search (the choice check)
-      out["ls_costs"] = np.full((nworld, 12, 32), np.nan, self.dtype)
+      out["ls_costs"] = np.full((nworld, 15, 64), np.nan, self.dtype)
       self.lib.oracle_set_lscost(out["ls_costs"].ctypes.data, -1)
     try:
       rc = self.lib.oracle_run(ctypes.addressof(self.ms), ctypes.addressof(ds), 0, nworld, int(integrate), nthreads)
@@ -133,8 +133,7 @@ class Oracle:
       self.lib.oracle_set_lscost(None, 0)
     if rc != 0:
       raise RuntimeError(f"oracle_run failed: {rc}")
-    out["solver_capped"] = ((out["ls_trace"] >> 62) & 1).astype(np.int32)
-    out["ls_trace"] &= (1 << 62) - 1
+    out["solver_capped"] = out.pop("ls_trace").astype(np.int32)
     if follow is not None and self.ms.ls_parallel:
       out["ls_excess"] = out.pop("ls_gap")
     if follow is not None and self.dtype == np.float64:

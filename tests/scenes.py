@@ -324,9 +324,8 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
     # difference of the same search (the float32 oracle replaying the same choices)
     if "ls_costs" in ref and "f32" in ref and "ls_costs" in ref["f32"]:
       c64, c32 = ref["ls_costs"][good], ref["f32"]["ls_costs"][good]
-      tr = got["solver_lstrace"][good].astype(np.int64)
-      code = (tr[:, 0] & 0x3FFFFFFF) | ((tr[:, 1] & 0x3FFFFFFF) << 30)
-      nit = np.minimum(ref["solver_niter"][good, 0], 12)
+      tr = got["solver_lstrace"][good].astype(np.int64) & 0x3FFFFFFF
+      nit = np.minimum(ref["solver_niter"][good, 0], 15)
       bad = []
       worst = 0.0
       for i in range(len(good)):
@@ -334,7 +333,7 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
           row = c64[i, t]
           if not np.isfinite(row).any():
             continue
-          k = int((code[i] >> (5 * t)) & 31)
+          k = int((tr[i, t // 5] >> (6 * (t % 5))) & 63)
           best = np.nanmin(row)
           noise = np.nanmax(np.abs(c32[i, t] - row)) + 1e-12 * abs(best)
           r = (row[k] - best) / noise

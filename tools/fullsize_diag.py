@@ -52,7 +52,7 @@ dq = rel(got["qacc"], fol["qacc"])
 dv = np.abs(got["qvel"] - fol["qvel"]).max(1)
 for w in np.argsort(-dv)[:8]:
   print(f"w{w}: qvel d {dv[w]:.2e} qacc rel {dq[w]:.2e} excess {fol['ls_excess'][w, 0]:.2e} niter gpu {got['solver_niter'][w, 0]} "
-        f"free {free['solver_niter'][w, 0]} warm gpu {(got['solver_lstrace'][w, 1] >> 30) & 1} free {(free['solver_lstrace'][w, 1] >> 30) & 1} "
+        f"free {free['solver_niter'][w, 0]} warm gpu {(got['solver_lstrace'][w, 0] >> 30) & 1} free {(free['solver_lstrace'][w, 0] >> 30) & 1} "
         f"nefc {got['nefc'][w, 0]} capped {fol['solver_capped'][w, 0]} free-vs-gpu qacc rel {rel(got['qacc'], free['qacc'])[w]:.2e}")
 ex = fol["ls_excess"][:, 0]
 print("excess quantiles", np.quantile(ex, [0.5, 0.9, 0.99, 1.0]))

@@ -30,13 +30,13 @@ sim.step()
 got = get(sim, n)
 gc = buf.view(n, 32).cpu().numpy()[:, :20]
 orc = Oracle(m)
-oc = np.zeros((n, 32))
+oc = np.zeros((n, 64))
 orc.lib.oracle_set_lscost.argtypes = [ctypes.c_void_p, ctypes.c_int]
 orc.lib.oracle_set_lscost(oc.ctypes.data, 0)
 ref = orc.run(n, st, integrate=True, follow=got)
 orc.lib.oracle_set_lscost(None, 0)
 oc = oc[:, :20]
-g0 = got["solver_lstrace"][:, 0] & 31
+g0 = got["solver_lstrace"][:, 0] & 63
 r0 = np.argmin(oc, axis=1)
 diff = np.nonzero((g0 != r0) & (got["nefc"][:, 0] > 0))[0]
 print("worlds whose first step-size choice differs:", len(diff), "of", int((got["nefc"][:, 0] > 0).sum()))

@@ -14,8 +14,7 @@ from tests.test_gpu_parity import get, make_sim, put  # noqa: E402
 
 
 def dec(t, k=10):
-  v = int(t[0]) | (int(t[1]) << 30)
-  return [(v >> (5 * i)) & 31 for i in range(k)]
+  return [(int(t[i // 5]) >> (6 * (i % 5))) & 63 for i in range(k)]
 
 
 n = 256
