@@ -391,7 +391,8 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
       rmax[np.isin(rows, capped)] = 0.0  # unconverged under the parallel search: soft test only
       if (rmax > 1).any():
         w = int(np.argmax(rmax))
-        failures.append(f"{name}: world {int(rows[w])} max|d|={d[w]:.3e} > hard bound {rel_max * unit[w] + floor:.3e}")
+        fw = float(np.broadcast_to(floor, d.shape)[w])
+        failures.append(f"{name}: world {int(rows[w])} max|d|={d[w]:.3e} > hard bound {rel_max * unit[w] + fw:.3e}")
 
   for k in KIN:
     check(k, 5e-5, sel)

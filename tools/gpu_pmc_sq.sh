@@ -7,6 +7,7 @@ TAG=${1:-sq}
 N=${2:-4096}
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
+export MJH_BALANCE=1  # world ordering on, as in the bench
 O=gpurun_out/$TAG
 mkdir -p $O
 timeout -s KILL 60 rocprofv3 -L > $O/counters_list.txt 2>&1 || true
@@ -20,4 +21,6 @@ for G in "$A" "$B"; do
 done
 python tools/pmc_summary.py "step_kernel" 20 $(find $O/p1 $O/p2 -name '*counter_collection.csv') > $O/sq_summary.json
 cat $O/sq_summary.json
+# the bench line's roofline_valu input (commit it under profiles/)
+python tools/sq_to_roofline.py $O/sq_summary.json Mjlab-Velocity-Flat-Unitree-G1 $N "$TAG SQ_INSTS_VALU, kernel_bench G1 N=$N" $O/step_kernel_sq.json
 find $O/p1 $O/p2 -name '*.csv' -delete
