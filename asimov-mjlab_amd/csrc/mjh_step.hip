@@ -173,10 +173,21 @@ struct ImgOff {
   int nfields;
 };
 
-#define IMG_I(name) (reinterpret_cast<const int*>(smem + Io.name))
-#define IMG_F(name) (reinterpret_cast<const float*>(smem + Io.name))
-#define IMG_L(name) (reinterpret_cast<const long long*>(smem + Io.name))
-#define WFIELD(name) (m.name##_wstride ? (const float*)(m.name + W * m.name##_wstride) : (const float*)(smem + Io.name))
+// MJH_IMG_GLOBAL=1: the model image is read in place from global memory (L1 /
+// scalar cache) instead of a per-workgroup LDS copy; the LDS it frees goes to
+// constraint rows
+#ifndef MJH_IMG_GLOBAL
+#define MJH_IMG_GLOBAL 0
+#endif
+#if MJH_IMG_GLOBAL
+#define IMGB gimg
+#else
+#define IMGB smem
+#endif
+#define IMG_I(name) (reinterpret_cast<const int*>(IMGB + Io.name))
+#define IMG_F(name) (reinterpret_cast<const float*>(IMGB + Io.name))
+#define IMG_L(name) (reinterpret_cast<const long long*>(IMGB + Io.name))
+#define WFIELD(name) (m.name##_wstride ? (const float*)(m.name + W * m.name##_wstride) : (const float*)(IMGB + Io.name))
 
 // ---- cross-lane exchange ------------------------------------------------------
 // lane k's value to every lane (k wave-uniform): v_readlane_b32
@@ -986,6 +997,11 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
 #define DP(name) (SLAB ? reinterpret_cast<decltype(d.name)>(slab + DO.name * nw4) : d.name)
   extern __shared__ float smem[];
   if (gate != nullptr && *gate == 0) return;  // gated forward: nothing to recompute
+#if MJH_IMG_GLOBAL
+  const float* __restrict__ gimg = reinterpret_cast<const float*>(m.image);
+  constexpr int kImgLds = 0;
+#else
+  const int kImgLds = Io.img_words;
   // shared model image -> LDS (whole workgroup, 16-byte coalesced)
   {
     const float4* src = reinterpret_cast<const float4*>(m.image);
@@ -993,13 +1009,14 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
     for (int i = threadIdx.x; i < (Io.img_words >> 2); i += 64 * WPB) dst[i] = src[i];
   }
   __syncthreads();
+#endif
   const int wave = threadIdx.x >> 6;
   // a checksum of the staged model image (each wave over the whole image: no
   // cross-wave exchange), part of the position-reuse snapshot, so an in-place
   // edit of a shared model field between a forward and a step is seen
   unsigned long long img_hash = 0ull;
   if (MODE == 1 || (MODE == 0 && reuse)) {
-    const uint4* iw = reinterpret_cast<const uint4*>(smem);
+    const uint4* iw = reinterpret_cast<const uint4*>(IMGB);
     unsigned h1 = 0u, h2 = 0u;
     const int lane = threadIdx.x & 63;
     for (int i = lane; i < (Io.img_words >> 2); i += 64) {
@@ -1026,7 +1043,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   // parameter, so both run the very same code up to the integration (a step
   // reusing a forward's position stage is then bit-identical to recomputing it)
   const bool STEP = step_flag != 0;
-  float* S = smem + Io.img_words + wave * (MODE == 1 ? Lo.ptotal : Lo.total);
+  float* S = smem + kImgLds + wave * (MODE == 1 ? Lo.ptotal : Lo.total);
   int* SI = reinterpret_cast<int*>(S);
   float* G = d.scratch + (long long)w * d.scratch_words;  // this world's global scratch
   const long long W = w;
@@ -2111,8 +2128,13 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
     unsigned long long act_prev[kMaskWords] = {0ull, 0ull, 0ull, 0ull, 0ull};
     bool have_prev = false;
     int nfactor = 0;
-    auto newton_direction = [&]() {
+    // gradient at the current point (the convergence test reads only this)
+    auto gradient = [&]() {
       for (int i = tid; i < nv; i += NT) grad[i] = Ma[i] - qfrc_smooth[i] - qfrc_con[i];
+    };
+    // Newton direction from grad: Hessian (kept while the active set is
+    // unchanged), factor, solve
+    auto newton_direction = [&]() {
       // compact the rows in the quadratic zone: H = M + sum h_r J_r J_r^T
       int nact = 0;
       unsigned long long act[kMaskWords] = {0ull, 0ull, 0ull, 0ull, 0ull};
@@ -2203,6 +2225,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
       cost = update_constraint();
     }
     wsync();
+    gradient();
     newton_direction();
 
     for (int it = 0; it < m.iterations; it++) {
@@ -2348,15 +2371,19 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
       cost = update_constraint();
       wsync();
       PROF_ACC(13, t_up);
-      unsigned long long t_nd = PROF_NOW();
-      newton_direction();
-      PROF_ACC(14, t_nd);
+      gradient();
       niter++;
       float gn = 0.f;
       for (int i = tid; i < nv; i += NT) gn += grad[i] * grad[i];
       gn = bsum<NT>(gn, red);
-      const float improvement = scale * (old - cost), gradient = scale * sqrtf(gn);
-      if (improvement < m.tolerance || gradient < m.tolerance) break;
+      const float improvement = scale * (old - cost), gnorm = scale * sqrtf(gn);
+      if (improvement < m.tolerance || gnorm < m.tolerance) break;
+      // the direction is read only by a further iteration: none after the last
+      // (MuJoCo / MuJoCo Warp compute it before the test; nothing reads it after)
+      if (it + 1 >= m.iterations) break;
+      unsigned long long t_nd = PROF_NOW();
+      newton_direction();
+      PROF_ACC(14, t_nd);
     }
   }
   wsync();
@@ -3097,6 +3124,9 @@ Layout make_layout(const mjh_model* m, int budget) {
 #ifndef MJH_WPB
 #define MJH_WPB 8
 #endif
+#ifndef MJH_WG_PER_CU
+#define MJH_WG_PER_CU 1
+#endif
 constexpr int kLdsBytes = 160 * 1024;
 constexpr int kWorldsPerBlock = MJH_WPB;
 constexpr int kPosWorldsPerBlock = MJH_PWPB;
@@ -3111,10 +3141,12 @@ struct Plan {
 Plan make_plan(const mjh_model* m, int wpb) {
   Plan p;
   p.io = make_imgoff(m);
-  const int budget = (kLdsBytes / 4 - p.io.img_words) / wpb;
+  const int img_lds = MJH_IMG_GLOBAL ? 0 : p.io.img_words;
+  // MJH_WG_PER_CU workgroups share a CU's LDS (WPB 4 with the image global: 2)
+  const int budget = (kLdsBytes / 4 / MJH_WG_PER_CU - img_lds) / wpb;
   p.lo = make_layout(m, budget);
-  p.shmem = (size_t)(p.io.img_words + wpb * p.lo.total) * 4;
-  p.shmem_pos = (size_t)(p.io.img_words + kPosWorldsPerBlock * p.lo.ptotal) * 4;
+  p.shmem = (size_t)(img_lds + wpb * p.lo.total) * 4;
+  p.shmem_pos = (size_t)(img_lds + kPosWorldsPerBlock * p.lo.ptotal) * 4;
   return p;
 }
 
