@@ -16,6 +16,7 @@ for P in 1 2; do
   done
 done
 grep "ms/launch" $O/kb.log
+[ "${AB_ONLY:-0}" = 1 ] && exit 0
 t tests
 timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gputests.log 2>&1 || { tail -30 $O/gputests.log; exit 1; }
 tail -2 $O/gputests.log
