@@ -173,17 +173,27 @@ struct ImgOff {
   int nfields;
 };
 
-// MJH_IMG_GLOBAL=1: the model image is read in place from global memory (L1 /
-// scalar cache) instead of a per-workgroup LDS copy; the LDS it frees goes to
-// constraint rows
-#ifndef MJH_IMG_GLOBAL
-#define MJH_IMG_GLOBAL 0
-#endif
-#if MJH_IMG_GLOBAL
-#define IMGB gimg
+// Worlds per workgroup by padded dof count: one-world workgroups for the 35-dof
+// humanoid (each wave retires on its own, so a CU starts the next world as soon
+// as any one is done instead of waiting for the slowest of 8; the model image is
+// then read in place from global memory, and the LDS it frees raises the row
+// capacity to njmax), 8-world workgroups sharing an LDS copy of the image
+// otherwise (Go1: the image reads dominate, profiles/r03t_variants_kb.log).
+// MJH_WPB overrides it for A/B builds.
+__host__ __device__ constexpr int wpb_of_nvp(int nvp) {
+#ifdef MJH_WPB
+  return (void)nvp, MJH_WPB;
 #else
-#define IMGB smem
+  return nvp == 36 ? 1 : 8;
 #endif
+}
+// the image lives in global memory for workgroups of fewer than 8 worlds
+__host__ __device__ constexpr bool img_global(int wpb) { return wpb < 8; }
+template <bool G>
+__device__ __forceinline__ const float* img_base(const float* g, const float* l) {
+  if constexpr (G) return g; else return l;
+}
+#define IMGB imgb
 #define IMG_I(name) (reinterpret_cast<const int*>(IMGB + Io.name))
 #define IMG_F(name) (reinterpret_cast<const float*>(IMGB + Io.name))
 #define IMG_L(name) (reinterpret_cast<const long long*>(IMGB + Io.name))
@@ -971,8 +981,11 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 #ifndef MJH_PMINWAVES
 #define MJH_PMINWAVES 1
 #endif
+#ifndef MJH_PERSIST
+#define MJH_PERSIST 0
+#endif
 #ifndef MJH_MINWAVES
-#define MJH_MINWAVES 1
+#define MJH_MINWAVES(wpb) ((wpb) < 8 ? 2 : 1)  // one-world workgroups: keep <= 256 VGPRs + AGPRs
 #endif
 // MODE 0: the whole step in one launch. MODE 1: the position stage only
 // (kinematics, com, CRB, M and its factor, collision, constraint rows and their
@@ -984,7 +997,7 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 // needs far fewer registers and LDS, so it runs at higher occupancy, and the
 // first physics step after a gated forward skips it.
 template <int WPB, int NVP, int SPEC = -1, bool SLAB = false, int MODE = 0>
-__global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo_,
+__global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(WPB)) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo_,
                                                          const ImgOff Io_, const unsigned char* gate, int reuse,
                                                          unsigned long long key, int step_flag) {
   constexpr int NT = 64;  // one wave per world
@@ -992,24 +1005,21 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   const ImgOff Io = spec_imgoff<SPEC>(Io_);
   const Sizes Z = spec_sizes<SPEC>(m);
   const DataOff DO = data_offsets(Z);
-  char* const slab = reinterpret_cast<char*>(d.qpos);
+  char* const slab0 = reinterpret_cast<char*>(d.qpos);
   const long long nw4 = 4ll * d.nworld;
 #define DP(name) (SLAB ? reinterpret_cast<decltype(d.name)>(slab + DO.name * nw4) : d.name)
   extern __shared__ float smem[];
   if (gate != nullptr && *gate == 0) return;  // gated forward: nothing to recompute
-#if MJH_IMG_GLOBAL
-  const float* __restrict__ gimg = reinterpret_cast<const float*>(m.image);
-  constexpr int kImgLds = 0;
-#else
-  const int kImgLds = Io.img_words;
+  constexpr bool IMG_GLOBAL = img_global(WPB);
+  const float* const imgb = img_base<IMG_GLOBAL>(reinterpret_cast<const float*>(m.image), smem);
+  const int kImgLds = IMG_GLOBAL ? 0 : Io.img_words;
   // shared model image -> LDS (whole workgroup, 16-byte coalesced)
-  {
+  if constexpr (!IMG_GLOBAL) {
     const float4* src = reinterpret_cast<const float4*>(m.image);
     float4* dst = reinterpret_cast<float4*>(smem);
     for (int i = threadIdx.x; i < (Io.img_words >> 2); i += 64 * WPB) dst[i] = src[i];
+    __syncthreads();
   }
-  __syncthreads();
-#endif
   const int wave = threadIdx.x >> 6;
   // a checksum of the staged model image (each wave over the whole image: no
   // cross-wave exchange), part of the position-reuse snapshot, so an in-place
@@ -1032,8 +1042,24 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
     }
     img_hash = ((unsigned long long)h2 << 32) | h1;
   }
-  const int slot = blockIdx.x * WPB + wave;
-  if (slot >= d.nworld) return;
+  // MJH_PERSIST (fused kernel): one workgroup per resident slot, each wave
+  // claims the next world (in the cost order below) from a counter the pack
+  // launch zeroes, so a wave done with a cheap world starts another instead of
+  // idling until its workgroup's slowest world is done
+  constexpr bool PERSIST = MJH_PERSIST != 0 && MODE == 0;
+  unsigned* const claim = reinterpret_cast<unsigned*>(m.image) + Io.img_words;
+  for (;;) {
+  int slot;
+  if constexpr (PERSIST) {
+    unsigned c = 0u;
+    if ((threadIdx.x & 63) == 0) c = atomicAdd(claim, 1u);
+    slot = __builtin_amdgcn_readfirstlane((int)c);
+    if (slot >= d.nworld) return;
+  } else {
+    (void)claim;
+    slot = blockIdx.x * WPB + wave;
+    if (slot >= d.nworld) return;
+  }
   // optional cost-sorted world order: a workgroup's worlds then take similar
   // time, so its LDS is not held hostage by one slow world (the position pass,
   // of nearly uniform cost, keeps the identity order)
@@ -1043,7 +1069,14 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
   // parameter, so both run the very same code up to the integration (a step
   // reusing a forward's position stage is then bit-identical to recomputing it)
   const bool STEP = step_flag != 0;
-  float* S = smem + kImgLds + wave * (MODE == 1 ? Lo.ptotal : Lo.total);
+  // the world's LDS and data bases, made opaque per claimed world: otherwise
+  // every address derived from them is hoisted out of the world loop and kept
+  // live across it (register spills)
+  int sofs = kImgLds + wave * (MODE == 1 ? Lo.ptotal : Lo.total);
+  long long zofs = 0;
+  if constexpr (PERSIST) asm volatile("" : "+v"(sofs), "+s"(zofs));
+  char* const slab = slab0 + zofs;
+  float* S = smem + sofs;
   int* SI = reinterpret_cast<int*>(S);
   float* G = d.scratch + (long long)w * d.scratch_words;  // this world's global scratch
   const long long W = w;
@@ -2931,6 +2964,8 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES)
     }
   }
   }  // velocity / solver stage
+  if constexpr (!PERSIST) return;
+  }  // world loop
 }
 
 #undef DP
@@ -2984,6 +3019,7 @@ __global__ __launch_bounds__(1024) void pack_kernel(const mjh_model m, const Img
   (void)nchain; (void)ncolgeom; (void)npair; (void)nsensor; (void)nmocap; (void)nconmax; (void)njmax; (void)na;
   (void)nsensordata; (void)nq; (void)nv; (void)nu; (void)nbody; (void)njnt; (void)ngeom; (void)nsite;
   unsigned int* img = reinterpret_cast<unsigned int*>(m.image);
+  if (blockIdx.x == 0 && threadIdx.x == 0) img[io.img_words] = 0u;  // the step launch's world-claim counter
   int f = 0;
 #define X_PACK(type, name, count)                                                          \
   if ((int)blockIdx.x == f) {                                                              \
@@ -3121,14 +3157,7 @@ Layout make_layout(const mjh_model* m, int budget) {
   return L;
 }
 
-#ifndef MJH_WPB
-#define MJH_WPB 8
-#endif
-#ifndef MJH_WG_PER_CU
-#define MJH_WG_PER_CU 1
-#endif
 constexpr int kLdsBytes = 160 * 1024;
-constexpr int kWorldsPerBlock = MJH_WPB;
 constexpr int kPosWorldsPerBlock = MJH_PWPB;
 
 struct Plan {
@@ -3138,15 +3167,17 @@ struct Plan {
   size_t shmem_pos;  // the split position kernel's
 };
 
-Plan make_plan(const mjh_model* m, int wpb) {
+Plan make_plan(const mjh_model* m) {
   Plan p;
+  const int wpb = wpb_of_nvp(nvp_of(m->nv));
   p.io = make_imgoff(m);
-  const int img_lds = MJH_IMG_GLOBAL ? 0 : p.io.img_words;
-  // MJH_WG_PER_CU workgroups share a CU's LDS (WPB 4 with the image global: 2)
-  const int budget = (kLdsBytes / 4 / MJH_WG_PER_CU - img_lds) / wpb;
+  const int img_lds = img_global(wpb) ? 0 : p.io.img_words;
+  // 8 / wpb workgroups share a CU's LDS (one-world workgroups: 8 per CU, the
+  // two waves per SIMD that 2 x 256 VGPRs allow)
+  const int budget = (kLdsBytes / 4 / (8 / wpb) - img_lds) / wpb;
   p.lo = make_layout(m, budget);
   p.shmem = (size_t)(img_lds + wpb * p.lo.total) * 4;
-  p.shmem_pos = (size_t)(img_lds + kPosWorldsPerBlock * p.lo.ptotal) * 4;
+  p.shmem_pos = (size_t)((img_global(kPosWorldsPerBlock) ? 0 : p.io.img_words) + kPosWorldsPerBlock * p.lo.ptotal) * 4;
   return p;
 }
 
@@ -3209,7 +3240,19 @@ void launch_mode(const Plan& p, const mjh_model* m, const mjh_data* d, const uns
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     attr = true;
   }
-  const int blocks = (d->nworld + WPB - 1) / WPB;
+  int blocks = (d->nworld + WPB - 1) / WPB;
+  if (MJH_PERSIST && MODE == 0) {
+    // persistent: as many workgroups as are resident at once
+    static int resident = 0;
+    if (resident == 0) {
+      int per_cu = 0, dev = 0, ncu = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 64 * WPB, p.shmem);
+      resident = (per_cu > 0 ? per_cu : 1) * (ncu > 0 ? ncu : 1);
+    }
+    if (blocks > resident) blocks = resident;
+  }
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * WPB), MODE == 1 ? p.shmem_pos : p.shmem, s, *m, *d, p.lo, p.io, gate,
                      reuse, key, STEP ? 1 : 0);
 }
@@ -3218,9 +3261,9 @@ template <bool STEP, int NVP, int SPEC, bool SLAB>
 void launch_step(const Plan& p, const mjh_model* m, const mjh_data* d, const unsigned char* gate, hipStream_t s) {
   if constexpr (MJH_SPLIT != 0) {
     launch_mode<kPosWorldsPerBlock, STEP, NVP, SPEC, SLAB, 1>(p, m, d, gate, s, g_pos_reuse ? 1 : 0, launch_key(m, d));
-    launch_mode<kWorldsPerBlock, STEP, NVP, SPEC, SLAB, 2>(p, m, d, gate, s, 0, 0ull);
+    launch_mode<wpb_of_nvp(NVP), STEP, NVP, SPEC, SLAB, 2>(p, m, d, gate, s, 0, 0ull);
   } else {
-    launch_mode<kWorldsPerBlock, STEP, NVP, SPEC, SLAB, 0>(p, m, d, gate, s, g_pos_reuse ? 1 : 0, launch_key(m, d));
+    launch_mode<wpb_of_nvp(NVP), STEP, NVP, SPEC, SLAB, 0>(p, m, d, gate, s, g_pos_reuse ? 1 : 0, launch_key(m, d));
   }
 }
 
@@ -3236,7 +3279,7 @@ template <bool STEP>
 int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream) {
   if (mjh_model_check(m) != 0) return 1;
   if (d->nworld <= 0) return 0;
-  Plan p = make_plan(m, kWorldsPerBlock);
+  Plan p = make_plan(m);
   if (!d->scratch || d->scratch_words < p.lo.gtotal) {
     g_err = "data scratch buffer missing or too small (mjh_scratch_words)";
     return 1;
@@ -3276,23 +3319,24 @@ const char* mjh_last_error(void) { return g_err.c_str(); }
 size_t mjh_sizeof_model(void) { return sizeof(mjh_model); }
 size_t mjh_sizeof_data(void) { return sizeof(mjh_data); }
 
-int mjh_image_words(const mjh_model* m) { return make_imgoff(m).img_words; }
+// + 4 words after the image: the step launch's world-claim counter (+ padding)
+int mjh_image_words(const mjh_model* m) { return make_imgoff(m).img_words + 4; }
 
 int mjh_model_check(const mjh_model* m) {
   if (!m) { g_err = "null model"; return 1; }
   if (m->nv > 63 || m->nbody > 63) { g_err = "device path supports nv <= 63 and nbody <= 63"; return 1; }
   if (m->nconmax <= 0 || m->njmax <= 0) { g_err = "nconmax and njmax must be positive"; return 1; }
-  Plan p = make_plan(m, kWorldsPerBlock);
-  if (!m->image || m->image_words < p.io.img_words) { g_err = "model image buffer missing or too small (mjh_image_words)"; return 1; }
+  Plan p = make_plan(m);
+  if (!m->image || m->image_words < p.io.img_words + 4) { g_err = "model image buffer missing or too small (mjh_image_words)"; return 1; }
   if (p.shmem > (size_t)kLdsBytes) { g_err = "model image + per-world scratch exceed LDS"; return 1; }
   if (p.lo.rcap < 8) { g_err = "too little LDS left for constraint rows"; return 1; }
   g_err.clear();
   return 0;
 }
 
-int mjh_scratch_bytes(const mjh_model* m) { return (int)make_plan(m, kWorldsPerBlock).shmem; }
+int mjh_scratch_bytes(const mjh_model* m) { return (int)make_plan(m).shmem; }
 
-int mjh_efc_capacity(const mjh_model* m) { return make_plan(m, kWorldsPerBlock).lo.rcap; }
+int mjh_efc_capacity(const mjh_model* m) { return make_plan(m).lo.rcap; }
 
 extern const int mjh_layout_ints = kLayoutInts;  // for tools/gen_spec.py
 
@@ -3313,12 +3357,12 @@ int mjh_set_position_reuse(int on) {
 
 int mjh_split_step(void) { return MJH_SPLIT; }
 
-int mjh_spec_index(const mjh_model* m) { return find_spec(make_plan(m, kWorldsPerBlock), m); }
+int mjh_spec_index(const mjh_model* m) { return find_spec(make_plan(m), m); }
 
 int mjh_data_is_slab(const mjh_model* m, const mjh_data* d) { return data_is_slab(m, d) ? 1 : 0; }
 
 int mjh_plan_ints(const mjh_model* m, int* out, int cap) {
-  const Plan p = make_plan(m, kWorldsPerBlock);
+  const Plan p = make_plan(m);
   int v[kPlanInts];
   plan_to_ints(p, m, v);
   if (cap < kPlanInts) return -1;
@@ -3326,7 +3370,7 @@ int mjh_plan_ints(const mjh_model* m, int* out, int cap) {
   return kPlanInts;
 }
 
-long long mjh_scratch_words(const mjh_model* m) { return make_plan(m, kWorldsPerBlock).lo.gtotal; }
+long long mjh_scratch_words(const mjh_model* m) { return make_plan(m).lo.gtotal; }
 
 #ifdef MJH_PROFILE
 // diagnostics (profile builds only; not part of the ABI): the parallel line
@@ -3361,7 +3405,7 @@ int mjh_debug_fields(const mjh_model* m, const mjh_data* d, float* qM, float* ef
   if (!Rg::M || !Rg::J) { g_err = "this build keeps M or J in LDS (MJH_PRESET): no debug copy"; return 1; }
   if (!qM || !efc_J || !d->scratch) { g_err = "null output or scratch"; return 1; }
   if (d->nworld <= 0) return 0;
-  const Plan p = make_plan(m, kWorldsPerBlock);
+  const Plan p = make_plan(m);
   hipLaunchKernelGGL(debug_fields_kernel, dim3(d->nworld), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d->scratch,
                      d->scratch_words, d->nefc, m->nv, p.lo.ldm, p.lo.ldj, p.lo.M, p.lo.J, m->njmax, qM, efc_J);
   hipError_t e = hipGetLastError();

@@ -86,7 +86,8 @@ typedef struct mjh_data {
   long long scratch_words;
   /* optional permutation of [0, nworld) (NULL = identity): the order in which
      worlds are assigned to waves. Results do not depend on it; sorting worlds
-     by expected cost balances the waves of a workgroup. */
+     by expected cost balances the waves of a workgroup (and, with one-world
+     workgroups, starts the most expensive worlds first). */
   const long long* world_order;
 } mjh_data;
 
@@ -105,8 +106,10 @@ size_t mjh_sizeof_data(void);
  * model can be stepped. Replaces put_model's checks (sim.py:116). */
 int mjh_model_check(const mjh_model* m);
 
-/* Words of device scratch the caller must provide in m->image (the packed
- * model image staged into LDS by every launch). */
+/* Words of device scratch the caller must provide in m->image: the packed
+ * model image (rewritten by every launch; staged into LDS by 8-world
+ * workgroups, read in place by one-world workgroups) + 4 words of launch
+ * bookkeeping. */
 int mjh_image_words(const mjh_model* m);
 
 /* LDS bytes per workgroup the step kernel uses for this model. */
