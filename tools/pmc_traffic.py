@@ -10,11 +10,15 @@ import json
 import sys
 
 
+NAMES = set()
+
+
 def per_dispatch(path, counter):
   vals = {}
   for r in csv.DictReader(open(path)):
     if r["Counter_Name"] != counter or "step_kernel" not in r["Kernel_Name"] or "true" not in r["Kernel_Name"]:
       continue
+    NAMES.add(r["Kernel_Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", ""))
     d = int(r["Dispatch_Id"])
     vals[d] = vals.get(d, 0.0) + float(r["Counter_Value"])
   ks = sorted(vals)
@@ -29,7 +33,7 @@ fetch_kb = sum(f) / len(f)
 write_kb = sum(w) / len(w)
 out = {
   "num_envs": n,
-  "kernel": "step_kernel<8,true,36> (G1, settled states, tools/kernel_bench.py)",
+  "kernel": " + ".join(sorted(NAMES)) + " (G1, settled states, tools/kernel_bench.py)",
   "fetch_size_kb_raw": fetch_kb,
   "write_size_kb": write_kb,
   "bytes_per_launch": (2.0 * fetch_kb + write_kb) * 1024.0,
