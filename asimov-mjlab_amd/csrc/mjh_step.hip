@@ -1024,8 +1024,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   // a checksum of the staged model image (each wave over the whole image: no
   // cross-wave exchange), part of the position-reuse snapshot, so an in-place
   // edit of a shared model field between a forward and a step is seen
-  unsigned long long img_hash = 0ull;
-  if (MODE == 1 || (MODE == 0 && reuse)) {
+  // (the fused kernel computes it only where it is compared or saved: a step
+  // whose qpos / fields / key already match a saved snapshot, or a forward
+  // saving one — not on the steps that integrated since the last forward)
+  auto image_hash = [&]() -> unsigned long long {
     const uint4* iw = reinterpret_cast<const uint4*>(IMGB);
     unsigned h1 = 0u, h2 = 0u;
     const int lane = threadIdx.x & 63;
@@ -1040,8 +1042,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       h1 += __shfl_xor(h1, o, 64);
       h2 += __shfl_xor(h2, o, 64);
     }
-    img_hash = ((unsigned long long)h2 << 32) | h1;
-  }
+    return ((unsigned long long)h2 << 32) | h1;
+  };
+  unsigned long long img_hash = MODE == 1 ? image_hash() : 0ull;
   // MJH_PERSIST (fused kernel): one workgroup per resident slot, each wave
   // claims the next world (in the cost order below) from a counter the pack
   // launch zeroes, so a wave done with a cheap world starts another instead of
@@ -1215,7 +1218,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     }
     if (reuse) {
       const unsigned* qb = reinterpret_cast<const unsigned*>(qpos);
-      bool same = snap[0] == 1u && snap[1] == (unsigned)img_hash && snap[2] == (unsigned)(img_hash >> 32) &&
+      bool same = snap[0] == 1u && (MODE != 1 || (snap[1] == (unsigned)img_hash && snap[2] == (unsigned)(img_hash >> 32))) &&
                   snap[3] == (unsigned)wf_hash && snap[4] == (unsigned)(wf_hash >> 32) &&
                   snap[5] == (unsigned)key && snap[6] == (unsigned)(key >> 32);
       for (int i = tid; i < nq; i += NT) same = same && snap[7 + i] == qb[i];
@@ -1227,8 +1230,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       }
       if constexpr (MODE == 1) {
         if (__all(same)) return;  // the last position pass of this world is current
-      } else {
-        reused = STEP && __all(same);
+      } else if (STEP && __all(same)) {
+        img_hash = image_hash();
+        reused = snap[1] == (unsigned)img_hash && snap[2] == (unsigned)(img_hash >> 32);
       }
     }
   }
@@ -1856,6 +1860,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     // rows' position parameters, counters) and the snapshot: the next step
     // launch on an unchanged world (qpos is only integrated by steps, so the
     // first step after a forward) skips the position stage
+    img_hash = image_hash();
     wsync();
     if (tid < I_COUNT) reinterpret_cast<int*>(G + Lo.h_ints)[tid] = ints[tid];
     for (int i = tid; i < nv * ldm; i += NT) G[Lo.h_L + i] = Lm[i];
