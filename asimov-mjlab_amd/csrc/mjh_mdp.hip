@@ -66,6 +66,9 @@ __global__ void diffsq_kernel(const float* a, long long as, const float* b, long
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   float s = 0.f;
+  // unrolled so a batch of the row's strided loads is in flight at once (the
+  // sum keeps its order: bit-identical)
+#pragma unroll 8
   for (int j = 0; j < k; j++) {
     const float d = a[e * as + j] - b[e * bs + j];
     s += d * d;
@@ -79,6 +82,7 @@ __global__ void pos_limits_kernel(const float* q, long long qs, const float* lim
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   float s = 0.f;
+#pragma unroll 8
   for (int j = 0; j < k; j++) {
     const float v = q[e * qs + j], lo = lim[e * ls + 2 * j], hi = lim[e * ls + 2 * j + 1];
     s += -fminf(v - lo, 0.f);
@@ -96,6 +100,7 @@ __global__ void posture_kernel(const float* q, long long qs, const float* q0, lo
   const float tot = cmd_total(cmd + e * cs);
   const float* sd = tot < walk_thr ? std_stand : (tot < run_thr ? std_walk : std_run);
   float s = 0.f;
+#pragma unroll 8
   for (int j = 0; j < k; j++) {
     const float d = q[e * qs + j] - q0[e * q0s + j];
     s += d * d / (sd[j] * sd[j]);

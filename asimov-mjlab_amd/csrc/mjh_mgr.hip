@@ -76,9 +76,16 @@ __global__ void reward_combine_kernel(const RewArgs a, const float* __restrict__
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const int T = a.nterms;
+  // every term's value loaded before the first store (the stores may alias the
+  // term buffers as far as the compiler knows, so a load behind one waits for it)
+  float xs[MJH_MAX_TERMS];
+#pragma unroll
+  for (int i = 0; i < MJH_MAX_TERMS; i++) xs[i] = (i < T && a.v[i]) ? a.v[i][e * a.vs[i]] : 0.f;
   float r = 0.f;
-  for (int i = 0; i < T; i++) {
-    const float x = a.v[i] ? a.v[i][e * a.vs[i]] : 0.f;
+#pragma unroll
+  for (int i = 0; i < MJH_MAX_TERMS; i++) {
+    if (i >= T) break;
+    const float x = xs[i];
     const float wi = w[i];
     const float wd = wi * dt;
     const float weighted = x * wd;

@@ -315,8 +315,10 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
   def _step_body(self) -> None:
     self._begin_rng_phase(outside_step=False)
     self.action_manager.process_action(self._action_in)
-    for _ in range(self.cfg.decimation):
-      self.action_manager.apply_action()
+    once = self.action_manager.apply_is_idempotent
+    for i in range(self.cfg.decimation):
+      if i == 0 or not once:
+        self.action_manager.apply_action()
       self.scene.write_data_to_sim()
       self.sim.step()
       self.scene.update(dt=self.physics_dt)

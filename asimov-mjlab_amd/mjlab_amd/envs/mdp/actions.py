@@ -67,6 +67,11 @@ class JointAction(ActionTerm):
 
 
 class JointPositionAction(JointAction):
+  # apply_actions writes the same processed targets at every physics substep of an
+  # env step and nothing else writes ctrl between substeps, so the env applies it
+  # once per env step (the later writes would store identical values)
+  apply_is_idempotent = True
+
   def __init__(self, cfg, env) -> None:
     super().__init__(cfg, env)
     if cfg.use_default_offset:

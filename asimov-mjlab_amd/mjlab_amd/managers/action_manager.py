@@ -95,6 +95,12 @@ class ActionManager:
       t.process_actions(self._action[:, idx : idx + t.action_dim])
       idx += t.action_dim
 
+  @property
+  def apply_is_idempotent(self) -> bool:
+    """True when every term's apply_actions only rewrites the targets that
+    process_action set (a repeat within one env step stores identical values)."""
+    return all(getattr(t, "apply_is_idempotent", False) for t in self._terms.values())
+
   def apply_action(self) -> None:
     for t in self._terms.values():
       t.apply_actions()
