@@ -18,7 +18,7 @@ def per_dispatch(path, counter):
   for r in csv.DictReader(open(path)):
     if r["Counter_Name"] != counter or "step_kernel" not in r["Kernel_Name"] or "true" not in r["Kernel_Name"]:
       continue
-    NAMES.add(r["Kernel_Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", ""))
+    NAMES.add(r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0])
     d = int(r["Dispatch_Id"])
     vals[d] = vals.get(d, 0.0) + float(r["Counter_Value"])
   ks = sorted(vals)
