@@ -112,16 +112,29 @@ struct Rg {
   MJH_REGIONS(X_RG)
 #undef X_RG
 };
+// Position reuse and the split step read the position stage's results from a
+// later launch. The handoff area restores the factor of M, the rows' position
+// parameters and the counters; every other array the stage writes and the
+// velocity/solver/sensor stages read must sit in global scratch, where the last
+// launch left it (an LDS copy belongs to whatever ran on that CU since).
+constexpr bool kPositionStageGlobal =
+    Rg::xpos && Rg::xquat && Rg::xmat && Rg::xipos && Rg::ximat && Rg::subtree_com && Rg::cinert && Rg::crb &&
+    Rg::cdof && Rg::xanchor && Rg::xaxis && Rg::cgpos && Rg::cgmat && Rg::sxpos && Rg::sxmat && Rg::M && Rg::J &&
+    Rg::con_pos && Rg::con_frame && Rg::con_dist && Rg::con_fric && Rg::con_solref && Rg::con_solimp &&
+    Rg::con_imargin && Rg::con_dim && Rg::con_geom && Rg::con_efcadr && Rg::efc_pos && Rg::efc_id && Rg::efc_mask &&
+    Rg::sidx;
 #define SP(name) ((Rg::name ? G : S) + Lo.name)
 #define SPI(name) reinterpret_cast<int*>((Rg::name ? G : S) + Lo.name)
 
 thread_local std::string g_err;
 bool g_disable_spec = false;  // mjh_set_specialization(0): always the generic instance
 bool g_auto_order = false;    // mjh_set_world_ordering(1): order the worlds in the pack launch
-bool g_pos_reuse = true;      // mjh_set_position_reuse: split position pass skips unchanged worlds
+bool g_pos_reuse = kPositionStageGlobal;  // mjh_set_position_reuse: reuse the position stage of unchanged worlds
 #ifndef MJH_SPLIT
 #define MJH_SPLIT 0
 #endif
+static_assert(MJH_SPLIT == 0 || kPositionStageGlobal,
+              "MJH_SPLIT hands the position stage over in global scratch: this MJH_PRESET keeps part of it in LDS");
 #ifndef MJH_PWPB
 #define MJH_PWPB 8
 #endif
@@ -3356,7 +3369,8 @@ int mjh_set_world_ordering(int on) {
 }
 
 int mjh_set_position_reuse(int on) {
-  g_pos_reuse = on != 0;
+  // a preset that keeps position-stage arrays in LDS cannot reuse them
+  g_pos_reuse = on != 0 && kPositionStageGlobal;
   return MJH_SPLIT ? 1 : 0;
 }
 

@@ -74,6 +74,19 @@ class ManagerBasedRlEnvCfg(ManagerBasedEnvCfg):
   is_finite_horizon: bool = False
 
 
+class _EnvSeed:
+  """``seed`` as the reference's staticmethod on the class (``Env.seed(s)``) and as
+  a method on an instance (``env.seed(s)``, which also reseeds the device stream)."""
+
+  def __init__(self, fn):
+    self._fn = fn
+    self.__doc__ = fn.__doc__
+
+  def __get__(self, obj, objtype=None):
+    fn = self._fn
+    return lambda seed=-1: fn(obj, seed)
+
+
 def seed_rng(seed: int) -> None:
   """``src/mjlab/utils/random.py``: seed python/numpy/torch."""
   import random
@@ -116,14 +129,17 @@ class ManagerBasedEnv:
       self.event_manager.apply(mode="startup")
       self.sim.create_graph()
 
+  @_EnvSeed
   def seed(self, seed: int = -1) -> int:
-    """Seed python/numpy/torch (``manager_based_env.py`` ``seed``) and restart the
-    device random stream from that seed, so ``reset(seed=s)`` reproduces the
-    fused kernels' draws exactly as it reproduces the reference's torch draws."""
+    """Seed python/numpy/torch (``manager_based_env.py:171-177``, a staticmethod
+    there) and, when called on an env, restart the device random stream from that
+    seed, so ``reset(seed=s)`` reproduces the fused kernels' draws exactly as it
+    reproduces the reference's torch draws. ``ManagerBasedRlEnv.seed(42)`` on the
+    class seeds the host generators only, as the reference's static method does."""
     if seed == -1:
       seed = int(np.random.randint(0, 10_000))
     seed_rng(seed)
-    if hasattr(self, "_rng_ctr"):
+    if self is not None and hasattr(self, "_rng_ctr"):
       self._reseed_stream()
     return seed
 

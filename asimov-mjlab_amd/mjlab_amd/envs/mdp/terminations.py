@@ -19,11 +19,14 @@ def time_out(env) -> torch.Tensor:
 def bad_orientation(env, limit_angle: float, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
   """acos(-g_z) > limit (reference terminations.py, ``torch.acos(-g[:, 2]).abs() >
   limit_angle``). acos is decreasing with values in [0, pi], so for a limit in
-  [0, pi] this is g_z > -cos(limit): one launch instead of four (NaN and |g_z| > 1
-  give False either way)."""
+  [0, pi] this is -cos(limit) < g_z <= 1. The reference's acos is NaN (so False)
+  for g_z outside [-1, 1] and for NaN; the comparisons are False there too. The
+  two forms can differ only for g_z within float32 rounding of -cos(limit)
+  (the reference rounds acos's result, this form the threshold)."""
   g = env.scene[asset_cfg.name].data.projected_gravity_b
   if 0.0 <= limit_angle <= math.pi:
-    return g[:, 2] > -math.cos(limit_angle)
+    gz = g[:, 2]
+    return (gz > -math.cos(limit_angle)) & (gz <= 1.0)
   return torch.acos(-g[:, 2]).abs() > limit_angle
 
 

@@ -99,8 +99,23 @@ class ActionManager:
   def apply_is_idempotent(self) -> bool:
     """True when every term's apply_actions only rewrites the targets that
     process_action set (a repeat within one env step stores identical values)."""
-    return all(getattr(t, "apply_is_idempotent", False) for t in self._terms.values())
+    return all(_idempotent(t) for t in self._terms.values())
 
   def apply_action(self) -> None:
     for t in self._terms.values():
       t.apply_actions()
+
+
+def _idempotent(term) -> bool:
+  """A term's ``apply_is_idempotent`` holds only for the class that declares it
+  with its own ``apply_actions``: a subclass that overrides apply_actions (per
+  substep interpolation, rate limits) does not inherit it and must opt in by
+  declaring the attribute itself. The nearest class in the MRO that declares
+  either decides."""
+  for klass in type(term).__mro__:
+    v = vars(klass)
+    if "apply_is_idempotent" in v:
+      return bool(v["apply_is_idempotent"])
+    if "apply_actions" in v:
+      return False
+  return False

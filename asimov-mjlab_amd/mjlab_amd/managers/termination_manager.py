@@ -48,7 +48,9 @@ class TerminationManager:
     m = as_mask(env_ids, self._env.num_envs, self._env.device)
     from mjlab_amd import envops
 
-    if envops.masked_counts(list(self._term_dones.values()), m, self._reset_counts):
+    if not self._term_dones:  # no terms (the reference accepts an empty config)
+      extras = {}
+    elif envops.masked_counts(list(self._term_dones.values()), m, self._reset_counts):
       extras = {"Episode_Termination/" + k: self._reset_counts[i] for i, k in enumerate(self._term_dones)}
     else:
       counts = torch.stack([(v & m).sum() for v in self._term_dones.values()])

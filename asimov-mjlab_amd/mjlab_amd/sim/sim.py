@@ -202,6 +202,14 @@ class Simulation:
       model.nconmax = int(cfg.nconmax)
     if cfg.njmax is not None:
       model.njmax = int(cfg.njmax)
+    # the kernel keeps one wave lane per contact-sensor match (64): a cap above 64
+    # is honoured exactly when no world can hold more than 64 contacts, since a
+    # sensor never matches more contacts than the world has
+    if cfg.contact_sensor_maxmatch > 64 and model.nconmax > 64:
+      raise ValueError(f"contact_sensor_maxmatch={cfg.contact_sensor_maxmatch} > 64 needs nconmax <= 64 per world "
+                       f"(got nconmax={model.nconmax}): the contact sensor keeps at most 64 matches")
+    if cfg.contact_sensor_maxmatch < 1:
+      raise ValueError("contact_sensor_maxmatch must be >= 1")
     model.contact_sensor_maxmatch = cfg.contact_sensor_maxmatch
     model.ls_parallel = int(bool(cfg.ls_parallel))  # wp_model.opt.ls_parallel (sim.py:117)
     self.sizes = abi.model_sizes(model)

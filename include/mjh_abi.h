@@ -154,7 +154,9 @@ int mjh_set_world_ordering(int on);
  * world's scratch (e.g. the first physics step after a forward — the env step's
  * reset-forward, manager_based_rl_env.py:133-137). Results are bit-identical
  * either way. Applies to launches issued after the call (a captured graph keeps
- * the setting it was captured with). Returns mjh_split_step(). */
+ * the setting it was captured with). A build whose MJH_PRESET keeps part of the
+ * position stage in LDS never reuses (the call is accepted and ignored).
+ * Returns mjh_split_step(). */
 int mjh_set_position_reuse(int on);
 
 /* 1 if this build launches the step as two kernels (position, then velocity /

@@ -116,3 +116,73 @@ def test_capture_guard_catches_hazards():
       x[x > 0]
     with pytest.raises(CaptureHazard):
       torch.tensor(0.1)
+
+
+def test_empty_terminations_config():
+  """The reference's TerminationManager accepts an empty config: reset and step
+  run with no terms and log no Episode_Termination entries."""
+  cfg = load_env_cfg(G1)
+  cfg.scene.num_envs = 3
+  cfg.terminations = {}
+  env = ManagerBasedRlEnv(cfg, device="cpu")
+  oracle_sim.attach(env.sim, env.event_manager.domain_randomization_fields)
+  env.reset()
+  _, _, term, trunc, extras = env.step(torch.zeros(3, env.action_manager.total_action_dim))
+  assert not term.any() and not trunc.any()
+  assert not any(k.startswith("Episode_Termination/") for k in extras.get("log", {}))
+
+
+def test_seed_static_and_bound():
+  """manager_based_env.py:171-177 declares seed a staticmethod: a class-level
+  call seeds the host generators and returns the seed; on an instance it also
+  restarts the device stream (same draws after the same seed)."""
+  assert ManagerBasedRlEnv.seed(42) == 42
+  a = torch.rand(3)
+  ManagerBasedRlEnv.seed(42)
+  assert torch.equal(a, torch.rand(3))
+  env = make(G1, n=2)
+  assert env.seed(7) == 7
+  k1 = env._rng_seed
+  env.seed(7)
+  assert env._rng_seed == k1
+
+
+def test_bad_orientation_edges():
+  """terminations.py (reference): acos(-g_z).abs() > limit. NaN for |g_z| > 1 or
+  NaN g_z gives False; the threshold form agrees away from float32 rounding of
+  -cos(limit)."""
+  from types import SimpleNamespace
+
+  from mjlab_amd.envs.mdp.terminations import bad_orientation
+
+  lim = math.radians(70.0)
+  th = -math.cos(lim)
+  gz = torch.tensor([1.0 + 1e-6, 1.0, float("nan"), -1.0, th + 1e-4, th - 1e-4, 0.0, -1.0 - 1e-6], dtype=torch.float32)
+  g = torch.zeros(len(gz), 3)
+  g[:, 2] = gz
+  env = SimpleNamespace(scene={"robot": SimpleNamespace(data=SimpleNamespace(projected_gravity_b=g))})
+  ref = torch.acos(-gz).abs() > lim
+  assert torch.equal(bad_orientation(env, lim), ref)
+  assert not bool(bad_orientation(env, lim)[0])  # g_z just above 1: NaN in the reference
+
+
+def test_idempotent_apply_not_inherited():
+  """A JointPositionAction subclass that overrides apply_actions is applied at
+  every physics substep unless it declares apply_is_idempotent itself."""
+  from mjlab_amd.envs.mdp.actions import JointPositionAction
+  from mjlab_amd.managers.action_manager import _idempotent
+
+  class Interp(JointPositionAction):
+    def apply_actions(self):
+      super().apply_actions()
+
+  class Declared(Interp):
+    apply_is_idempotent = True
+
+  class Plain(JointPositionAction):
+    pass
+
+  mk = lambda k: k.__new__(k)
+  assert _idempotent(mk(JointPositionAction)) and _idempotent(mk(Plain))
+  assert not _idempotent(mk(Interp))
+  assert _idempotent(mk(Declared))
