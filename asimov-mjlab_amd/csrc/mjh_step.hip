@@ -2124,7 +2124,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   int niter = 0, nfactor_total = 0;
   // solver_lstrace: the parallel line search's step-size index (6 bits) of
   // iterations 5w..5w+4 in word w (15 iterations), bit 30 of word 0: the solve
-  // started from qacc_smooth (the parity tests replay both choices)
+  // started from qacc_smooth, bit 30 of word 1: the last iteration passed the
+  // convergence test (the parity tests replay the choices and check both
+  // decisions against the oracle's own)
   unsigned lstr0 = 0u, lstr1 = 0u, lstr2 = 0u;
   if (nefc == 0) {
     for (int i = tid; i < nv; i += NT) {
@@ -2428,7 +2430,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       for (int i = tid; i < nv; i += NT) gn += grad[i] * grad[i];
       gn = bsum<NT>(gn, red);
       const float improvement = scale * (old - cost), gnorm = scale * sqrtf(gn);
-      if (improvement < m.tolerance || gnorm < m.tolerance) break;
+      if (improvement < m.tolerance || gnorm < m.tolerance) {
+        lstr1 |= 1u << 30;  // stopped by the convergence test (the parity tests check this decision)
+        break;
+      }
       // the direction is read only by a further iteration: none after the last
       // (MuJoCo / MuJoCo Warp compute it before the test; nothing reads it after)
       if (it + 1 >= m.iterations) break;

@@ -83,17 +83,22 @@ def parse() -> argparse.Namespace:
   p.add_argument("--cpu-seconds", type=float, default=8.0, help="per precision")
   p.add_argument("--kernel-launches", type=int, default=50)
   p.add_argument("--motion-file", default="", help="tracking tasks: motion npz (default: synthetic 500-frame clip)")
+  # test harness only (tests/bench_cpu_ranks.py): the multi-rank path on CPU
+  # tensors over gloo, with the test's stand-in physics attached by env_hook
+  p.add_argument("--device", default="cuda", choices=("cuda", "cpu"), help=argparse.SUPPRESS)
   return p.parse_args()
 
 
 def spawn_ranks(args) -> None:
   """`python bench.py --gpus N` with no torchrun around it: run N ranks as a
-  child `torch.distributed.run` (before any GPU call) and exit with its code."""
+  child `torch.distributed.run` (before any GPU call) and exit with its code.
+  The child runs the script that was started (bench.py, or a test harness that
+  calls bench.main)."""
   with socket.socket() as s:
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
   cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-         "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *sys.argv[1:]]
+         "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(sys.argv[0]).resolve()), *sys.argv[1:]]
   env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
   sys.exit(subprocess.call(cmd, env=env))
 
@@ -228,7 +233,9 @@ def cpu_config1(args) -> dict:
           "(env layer on CPU tensors + oracle float64 physics; MuJoCo C is not available)"}
 
 
-def main() -> None:
+def main(env_hook=None) -> None:
+  """env_hook(env): called on each rank's env before its first reset (the CPU
+  test harness attaches its stand-in physics there; None on the GPU)."""
   args = parse()
   if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
     spawn_ranks(args)
@@ -240,11 +247,23 @@ def main() -> None:
   local = int(os.environ.get("LOCAL_RANK", "0"))
   if world != args.gpus:
     raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+  on_gpu = args.device == "cuda"
+  if on_gpu:
+    torch.cuda.set_device(local)
+    dev = f"cuda:{local}"
+  else:
+    dev = "cpu"
   if world > 1:
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-  torch.cuda.set_device(local)
-  dev = f"cuda:{local}"
+    if on_gpu:
+      dist.init_process_group("nccl", device_id=torch.device(dev))
+    else:
+      dist.init_process_group("gloo")
+
+  def sync() -> None:
+    if on_gpu:
+      torch.cuda.synchronize()
+
   num_envs = args.num_envs or DEFAULT_ENVS.get(args.task, 4096)
 
   from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
@@ -259,6 +278,8 @@ def main() -> None:
 
   cfg.seed = shard_seed(42, rank)
   env = ManagerBasedRlEnv(cfg, device=dev)
+  if env_hook is not None:
+    env_hook(env)
   env.reset()
   # rsl_rl OnPolicyRunner.learn(init_at_random_ep_len=True) (reference train.py:121)
   g_ep = torch.Generator(device=dev)
@@ -286,19 +307,19 @@ def main() -> None:
   for _ in range(2 + args.settle + args.warmup):
     o, r, te, tr, _ = env.step(agent())
     exchange(o, r, te, tr)
-  torch.cuda.synchronize()
+  sync()
   stats0 = env.step_stats().clone()
   flags0 = env.sim.flag_stats()[3:].clone()  # running totals of worlds that overflowed / went non-finite
   if world > 1:
     dist.barrier()
-  torch.cuda.synchronize()
+  sync()
   t0 = time.perf_counter()
   for _ in range(args.steps):
     o, r, te, tr, _ = env.step(agent())
     exchange(o, r, te, tr)
   if world > 1:
     dist.barrier()
-  torch.cuda.synchronize()
+  sync()
   el = time.perf_counter() - t0
   if world > 1:
     t = torch.tensor([el], device=dev, dtype=torch.float64)
@@ -314,28 +335,34 @@ def main() -> None:
   # the per-step RCCL all-gather alone (same buffers), timed separately
   gather_ms = None
   if use_gather:
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     tg = time.perf_counter()
     for _ in range(args.steps):
       exchange(o, r, te, tr)
-    torch.cuda.synchronize()
+    sync()
     gather_ms = (time.perf_counter() - tg) / args.steps * 1e3
 
   # ---- dominant kernel: the fused physics step, HIP events on its stream ----
   sim = env.sim
-  stream = torch.cuda.current_stream()
   nefc = sim.data.nefc.float().mean().item()
   niter = sim.data.solver_niter.float().mean().item()
-  e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
   L = args.kernel_launches
   sim.step()
-  e0.record(stream)
-  for _ in range(L):
-    sim.step()
-  e1.record(stream)
-  torch.cuda.synchronize()
-  t_launch = e0.elapsed_time(e1) / 1e3 / L  # s per physics step (pack + step kernels)
+  if on_gpu:
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(L):
+      sim.step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    t_launch = e0.elapsed_time(e1) / 1e3 / L  # s per physics step (pack + step kernels)
+  else:  # CPU test harness: host time of its stand-in physics (not a measurement)
+    tl = time.perf_counter()
+    for _ in range(L):
+      sim.step()
+    t_launch = (time.perf_counter() - tl) / L
   b_phys = next((v for k, v in B_PHYS.items() if k in args.task), B_PHYS_G1)
   bytes_per_launch = b_phys * num_envs
   achieved = bytes_per_launch / t_launch / 1e9

@@ -142,6 +142,8 @@ typedef struct {
 
 static real* g_dbg_lscost;
 static int g_dbg_lscost_it;
+static real* g_dbg_conv;
+static real* g_dbg_warm;
 static int g_ls_scan = 0;
 static _Thread_local real g_dbg_scan_cost[64];
 
@@ -158,6 +160,7 @@ typedef struct {
   real lsgap; /* parallel line search: smallest relative cost gap best vs runner-up */
   unsigned lstrace[3];        /* solver_lstrace: step-size index (6 bits) of iterations 5w..5w+4 in word w */
   int capped;                 /* the solver stopped at the iteration cap, unconverged */
+  int conv;                   /* the last iteration passed the convergence test */
   int follow, fniter;         /* follow mode: replay fniter iterations with the given choices */
   int warm_smooth;            /* the solve started from qacc_smooth (not qacc_warmstart) */
   int wi;
@@ -1097,6 +1100,10 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     row_eval(w, r, s - w->efc_aref[r], &f, &c);
     cost_smooth += c;
   }
+  if (g_dbg_warm) {
+    g_dbg_warm[2 * (size_t)w->wi] = cost;
+    g_dbg_warm[2 * (size_t)w->wi + 1] = cost_smooth;
+  }
   int from_smooth = w->follow ? (int)((w->ftrace[0] >> 30) & 1u) : cost > cost_smooth;
   w->warm_smooth = from_smooth;
   if (from_smooth) {
@@ -1128,6 +1135,13 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     for (int d = 0; d < nv; d++) gn += w->grad[d] * w->grad[d];
     real improvement = scale * (old - cost), gradient = scale * sqrt(gn);
     int conv = improvement < m->tolerance || gradient < m->tolerance;
+    if (g_dbg_conv && it < 15) {
+      real* cv = g_dbg_conv + ((size_t)w->wi * 15 + it) * 3;
+      cv[0] = improvement;
+      cv[1] = gradient;
+      cv[2] = scale * (fabs(old) + fabs(cost));
+    }
+    w->conv = conv;
     if (!w->follow && conv) break;
     if (it == m->iterations - 1 && !conv) w->capped = 1; /* stopped by the iteration cap, unconverged */
   }
@@ -1352,6 +1366,13 @@ static real* g_dbg_qM = NULL;
 static real* g_dbg_J = NULL;
 static real* g_dbg_lsgap = NULL;
 static long long* g_dbg_lstrace = NULL;
+/* the solver's own discrete decisions (oracle_set_decisions), evaluated at every
+   iteration also in follow mode: per world 15 x {improvement, gradient, the
+   scaled cost magnitude |old| + |cost|} (the convergence test's inputs, NaN
+   where no iteration ran), and {cost at qacc_warmstart, cost at qacc_smooth}
+   (the warm-start comparison) */
+static real* g_dbg_conv = NULL;
+static real* g_dbg_warm = NULL;
 static int g_follow = 0;
 
 static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_t* w) {
@@ -1368,6 +1389,7 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   w->warm_smooth = 0;
   w->wi = wi;
   w->capped = 0;
+  w->conv = 0;
   w->lsexcess = 0;
   w->follow = g_follow && m->ls_parallel;
   if (w->follow) {
@@ -1444,7 +1466,7 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   if (g_dbg_qM) memcpy(g_dbg_qM + (size_t)wi * nv * nv, w->M, sizeof(real) * nv * nv);
   if (g_dbg_lsgap) g_dbg_lsgap[wi] = w->follow ? w->lsexcess : w->lsgap;
   d->solver_lstrace[3 * wi] = (int)(w->lstrace[0] | ((unsigned)w->warm_smooth << 30));
-  d->solver_lstrace[3 * wi + 1] = (int)w->lstrace[1];
+  d->solver_lstrace[3 * wi + 1] = (int)(w->lstrace[1] | ((unsigned)(w->conv && !w->follow) << 30));
   d->solver_lstrace[3 * wi + 2] = (int)w->lstrace[2];
   if (g_dbg_lstrace) g_dbg_lstrace[wi] = (long long)w->capped;
   if (g_dbg_J) memcpy(g_dbg_J + (size_t)wi * m->njmax * nv, w->J, sizeof(real) * (size_t)w->nefc * nv);
@@ -1537,6 +1559,11 @@ void oracle_set_ls_scan(int on) { g_ls_scan = on; }
 void oracle_set_lscost(real* cost, int iteration) {
   g_dbg_lscost = cost;
   g_dbg_lscost_it = iteration;
+}
+
+void oracle_set_decisions(real* conv, real* warm) {
+  g_dbg_conv = conv;
+  g_dbg_warm = warm;
 }
 
 void oracle_set_debug(real* qM, real* efc_J, real* lsgap, long long* lstrace) {

@@ -43,6 +43,7 @@ class Oracle:
     self.lib.oracle_set_debug.argtypes = [ctypes.c_void_p] * 4
     self.lib.oracle_set_follow.argtypes = [ctypes.c_int]
     self.lib.oracle_set_lscost.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    self.lib.oracle_set_decisions.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     self.lib.oracle_sizeof_model.restype = ctypes.c_size_t
     self.lib.oracle_sizeof_data.restype = ctypes.c_size_t
     MS = abi.model_struct(self.real, device=False)
@@ -92,7 +93,15 @@ class Oracle:
     relative float64 cost excess of a replayed choice over the argmin. A float64
     follow run also replays the step in the float32 build and returns its
     outputs under ``f32`` — the same algorithm and choices at float32: each
-    world's own rounding sensitivity, which the parity checker uses as a floor."""
+    world's own rounding sensitivity, which the parity checker uses as a floor.
+
+    Also returned: the solver's own decision inputs, evaluated at every
+    iteration in follow mode too (the oracle never takes them from the device
+    for the check): ``solver_conv`` (nworld, 15, 3) = improvement, gradient
+    (both scaled by 1 / (meaninertia nv), the test is ``< tolerance``) and the
+    scaled cost magnitude |old| + |cost| per iteration (NaN where none ran), and
+    ``warm_costs`` (nworld, 2) = the cost at qacc_warmstart and at qacc_smooth
+    (the solve starts from qacc_smooth when the first is larger)."""
     if follow is not None:
       state = dict(state, solver_niter=np.asarray(follow["solver_niter"]).reshape(nworld, -1),
                    solver_lstrace=np.asarray(follow["solver_lstrace"]).reshape(nworld, -1))
@@ -121,6 +130,9 @@ class Oracle:
       out["efc_J"] = np.zeros((nworld, nj * nv), self.dtype)
     self.lib.oracle_set_debug(out["qM"].ctypes.data if debug else None, out["efc_J"].ctypes.data if debug else None,
                               out["ls_gap"].ctypes.data, out["ls_trace"].ctypes.data)
+    out["solver_conv"] = np.full((nworld, 15, 3), np.nan, self.dtype)
+    out["warm_costs"] = np.full((nworld, 2), np.nan, self.dtype)
+    self.lib.oracle_set_decisions(out["solver_conv"].ctypes.data, out["warm_costs"].ctypes.data)
     self.lib.oracle_set_follow(1 if follow is not None else 0)
     if follow is not None:  # every candidate cost of every replayed search (the choice check)
       out["ls_costs"] = np.full((nworld, 15, 64), np.nan, self.dtype)
@@ -131,9 +143,11 @@ class Oracle:
       self.lib.oracle_set_debug(None, None, None, None)
       self.lib.oracle_set_follow(0)
       self.lib.oracle_set_lscost(None, 0)
+      self.lib.oracle_set_decisions(None, None)
     if rc != 0:
       raise RuntimeError(f"oracle_run failed: {rc}")
     out["solver_capped"] = out.pop("ls_trace").astype(np.int32)
+    out["solver_opt"] = {"tolerance": float(self.ms.tolerance), "iterations": int(self.ms.iterations)}
     if follow is not None and self.ms.ls_parallel:
       out["ls_excess"] = out.pop("ls_gap")
     if follow is not None and self.dtype == np.float64:

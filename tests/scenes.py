@@ -45,9 +45,37 @@ here once and cited by the tests:
   SOLVE_FRAC test only, not SOLVE_MAX — a float32 and a float64 iterate of an
   ill-conditioned, unconverged solve drift apart even along the same choices
   (at most LS_CAPPED_FRAC = 15 % of the worlds).
+* the solver's own decisions (follow mode): the oracle replays the device's
+  choices but evaluates, at every replayed iteration, its own float64
+  convergence test (improvement or gradient < tolerance, both scaled by
+  1 / (meaninertia nv), ``solver_conv``) and its own warm-start comparison
+  (cost at qacc_warmstart > cost at qacc_smooth, ``warm_costs``). The device
+  records its stop reason (bit 30 of ``solver_lstrace[1]``: stopped by the test)
+  and its warm-start pick (bit 30 of word 0). A decision that differs from the
+  float64 one is explained only when the deciding quantity lies within
+  DECISION_NOISE_K (4) x its float32 noise of the threshold (the float32
+  oracle's deviation along the same choices, floored at DECISION_ULPS (2)
+  float32 eps of the scaled cost magnitude |old| + |cost|); an unexplained one
+  fails the call — a device that stops while the float64 improvement and
+  gradient are both clearly above the tolerance, or goes on after the float64
+  test clearly passed, fails. The warm-start pick must agree outside float32
+  ties in all but DECISION_FRAC (1 %) of a test's world-steps (one near-tie
+  admitted per test; the autouse fixture in tests/conftest.py). The stop
+  decisions are reported, not bounded by a fraction: at the reference's
+  tolerance (1e-8, sim.py:57) the improvement test sits below float32
+  resolution in most worlds — the float32 MuJoCo Warp solver the reference runs
+  makes the same noise-level decision — so the guard against systematic early
+  stopping is statistical instead: the device's mean iteration count is at
+  least ITER_RATIO_MIN of the float32 oracle's own (non-follow) mean on the same
+  states (``check_iteration_counts``).
+* every compare_step call appends its counts (worst bound ratio, capped
+  worlds, line-search outliers, integer mismatches, decision mismatches) to
+  PARITY_LOG; tests/conftest.py prints them per test in the terminal summary.
 """
 
 from __future__ import annotations
+
+import os
 
 import numpy as np
 
@@ -276,6 +304,121 @@ def int_mismatch_reason(got: dict, ref: dict, w: int) -> tuple[str, bool] | None
   return "; ".join(reasons), border
 
 
+# every compare_step call: one record (tests/conftest.py prints them per test)
+PARITY_LOG: list[dict] = []
+ITER_LOG: list[dict] = []  # check_iteration_counts results
+DECISION_NOISE_K = 4.0
+# float32 resolution floor of a decision: a float32 cost (improvement = old -
+# cost) carries at least half an ulp of each operand, ~EPS32/2 x (|old| + |cost|);
+# DECISION_NOISE_K x that = 2 EPS32 (|old| + |cost|)
+DECISION_ULPS = 2.0
+DECISION_FRAC = 0.01
+ITER_RATIO_MIN = 0.9
+EPS32 = float(np.finfo(np.float32).eps)
+
+
+def solver_decisions(got: dict, ref: dict, worlds: np.ndarray) -> dict:
+  """The device's stop iteration and warm-start pick against the oracle's own
+  float64 decisions on the replayed path (follow mode; tests/scenes.py
+  docstring). Returns counts and the worst worlds."""
+  out = {"stop_checked": 0, "stop_worlds": 0, "stop_mismatch": 0, "stop_early": 0, "stop_unexplained": [],
+         "warm_checked": 0, "warm_tie": 0, "warm_mismatch": 0, "warm_unexplained": [], "stop_worst": 0.0,
+         "warm_worst": 0.0, "detail": []}
+  warm_seen: set = set()
+  if "ls_excess" not in ref or "f32" not in ref or "solver_conv" not in ref["f32"]:
+    # not a follow run of the parallel search: each side took its own path; the
+    # iteration counts are reported (not asserted)
+    if "solver_niter" in ref:
+      out["niter_differs"] = int((got["solver_niter"][worlds, 0] != ref["solver_niter"][worlds, 0]).sum())
+    return out
+  tol, iters = ref["solver_opt"]["tolerance"], ref["solver_opt"]["iterations"]
+  c64, c32 = ref["solver_conv"], ref["f32"]["solver_conv"]
+  w64, w32 = ref["warm_costs"], ref["f32"]["warm_costs"]
+  lst = got["solver_lstrace"].astype(np.int64)
+  nd_all = got["solver_niter"][:, 0].astype(int)
+  for w in worlds:
+    w = int(w)
+    if int(ref["nefc"][w, 0]) == 0:
+      continue
+    # warm start: the device started from qacc_smooth iff cost(warm) > cost(smooth)
+    cw, cs = float(w64[w, 0]), float(w64[w, 1])
+    if np.isfinite(cw) and np.isfinite(cs):
+      out["warm_checked"] += 1
+      dev = bool((lst[w, 0] >> 30) & 1)
+      if dev != (cw > cs):
+        # a tie at float32 resolution (e.g. qacc_warmstart == qacc_smooth): either pick is the reference's
+        if abs(cw - cs) <= DECISION_ULPS * EPS32 * (abs(cw) + abs(cs)):
+          out["warm_tie"] += 1
+          continue
+        # worlds with identical float64 costs are one decision (the restated
+        # reference tests step several copies of one state)
+        if (cw, cs) in warm_seen:
+          continue
+        warm_seen.add((cw, cs))
+        out["warm_mismatch"] += 1
+        noise = DECISION_NOISE_K * max(abs(float(w32[w, 0]) - cw), abs(float(w32[w, 1]) - cs)) + DECISION_ULPS * EPS32 * (abs(cw) + abs(cs))
+        r = abs(cw - cs) / noise
+        out["warm_worst"] = max(out["warm_worst"], r)
+        if r > 1.0:
+          out["warm_unexplained"].append(w)
+          out["detail"].append(f"w{w} warm: cost(warmstart) {cw:.9e} cost(smooth) {cs:.9e} (f32 {float(w32[w, 0]):.9e} "
+                               f"{float(w32[w, 1]):.9e}), device from_smooth={dev}")
+    # stop: no test passes before the device's last iteration; the last one
+    # passes iff the device says it stopped by the test
+    # (a world counts once however many of its iterations disagree)
+    nd = int(nd_all[w])
+    dev_conv = bool((lst[w, 1] >> 30) & 1)
+    out["stop_worlds"] += 1
+    if nd < iters and not dev_conv:
+      out["stop_mismatch"] += 1
+      out["stop_worst"] = float("inf")
+      out["stop_unexplained"].append(w)  # stopped early without passing the test
+      continue
+    wr, early = -1.0, False
+    for t in range(min(nd, 15)):
+      imp, gr, mag = (float(x) for x in c64[w, t])
+      if not np.isfinite(imp):
+        break
+      out["stop_checked"] += 1
+      dev = t == nd - 1 and dev_conv
+      if dev == (imp < tol or gr < tol):
+        continue
+      early |= dev  # the device stopped where the float64 test would go on
+      ni = DECISION_NOISE_K * abs(float(c32[w, t, 0]) - imp) + DECISION_ULPS * EPS32 * mag
+      ng = DECISION_NOISE_K * abs(float(c32[w, t, 1]) - gr) + DECISION_ULPS * EPS32 * gr
+      rt = min(abs(imp - tol) / ni, abs(gr - tol) / ng)
+      if rt > 1.0:
+        out["detail"].append(f"w{w} it{t}/{nd} device_stops={dev} improvement {imp:.3e} (f32 {float(c32[w, t, 0]):.3e}) "
+                             f"gradient {gr:.3e} (f32 {float(c32[w, t, 1]):.3e}) tol {tol:.1e} |old|+|cost| {mag:.3e} "
+                             f"-> {rt:.2f}x the noise")
+      wr = max(wr, rt)
+    if wr >= 0.0:
+      out["stop_mismatch"] += 1
+      out["stop_early"] += int(early)
+      out["stop_worst"] = max(out["stop_worst"], wr)
+      if wr > 1.0:
+        out["stop_unexplained"].append(w)
+  return out
+
+
+def check_iteration_counts(got: dict, model, state: dict, integrate: bool, nthreads: int = 8, overrides=None) -> dict:
+  """The statistical guard against early stopping (docstring above): the float32
+  oracle solves the same states with its own choices and its own float32
+  convergence test; the device's mean Newton iteration count must be at least
+  ITER_RATIO_MIN x the oracle's. Returns both means (float64 oracle's too)."""
+  from oracle.oracle import Oracle
+
+  n = got["qpos"].shape[0]
+  m32 = Oracle(model, "f32", overrides=overrides).run(n, state, integrate=integrate, nthreads=nthreads)["solver_niter"]
+  m64 = Oracle(model, "f64", overrides=overrides).run(n, state, integrate=integrate, nthreads=nthreads)["solver_niter"]
+  dev = float(got["solver_niter"][:, 0].mean())
+  r = {"device": dev, "oracle_f32": float(m32[:, 0].mean()), "oracle_f64": float(m64[:, 0].mean())}
+  r["ok"] = dev >= ITER_RATIO_MIN * r["oracle_f32"]
+  r["test"] = os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0]
+  ITER_LOG.append(r)
+  return r
+
+
 F32_SENSITIVITY = 4.0
 LS_NOISE_K = 4.0
 LS_TIE = 0.05
@@ -312,6 +455,7 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
   good = np.array([w for w in sel if int(w) not in reasons], dtype=int)
   # unconverged worlds under the parallel line search: no hard bound (path-dependent)
   capped: list[int] = []
+  n_ls_bad = 0
   if "ls_excess" in ref and len(good):
     ex = ref["ls_excess"][good, 0]
     maxerr["ls_excess"] = float(ex.max(initial=0.0))
@@ -342,6 +486,7 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
             bad.append(int(good[i]))
             break
       maxerr["ls_choice/noise"] = float(worst)
+      n_ls_bad = len(bad)
       if len(bad) > max(1, int(LS_TIE_FRAC * len(good))):
         failures.append(f"ls_choice: {len(bad)} worlds replayed a step size beyond {LS_NOISE_K}x the float32 cost "
                         f"noise (worst {worst:.2f}x, worlds {bad[:8]})")
@@ -448,7 +593,40 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
   check_rel("qvel", solve_rel, scale_name="qacc", scale=2 * dt, floor=1e-5, **sv)
   check_rel("qpos", solve_rel, scale_name="qacc", scale=2 * dt * dt, floor=1e-5, **sv)
   check_rel("sensordata", solve_rel, **sv)
+  dec = solver_decisions(got, ref, good)
+  if "ls_excess" in ref and "f32" in ref:
+    for kind in ("stop", "warm"):
+      if dec[f"{kind}_unexplained"]:
+        failures.append(f"solver {kind} decision differs from the float64 oracle's beyond float32 noise in worlds "
+                        f"{dec[f'{kind}_unexplained'][:8]} (worst {dec[f'{kind}_worst']:.2f}x the noise): "
+                        f"{dec['detail'][:4]}")
+    # the warm-start pick, outside float32 ties: per call at least one near-tie
+    # is admitted; tests/conftest.py bounds the fraction over all calls of a test
+    if dec["warm_mismatch"] > max(1, int(DECISION_FRAC * len(sel))):
+      failures.append(f"solver warm-start pick differs (within float32 noise) in {dec['warm_mismatch']} of "
+                      f"{len(sel)} worlds (> {DECISION_FRAC:.0%})")
+  ratios = [v for k, v in maxerr.items() if k.endswith("/bound")]
+  PARITY_LOG.append({
+    "test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0],
+    "worlds": len(sel),
+    "worst_bound": max(ratios, default=0.0),
+    "capped": len(capped),
+    "ls_outliers": n_ls_bad,
+    "int_mismatch": len(bad_int),
+    "stop_mismatch": dec["stop_mismatch"],
+    "warm_mismatch": dec["warm_mismatch"],
+    "stop_worlds": dec["stop_worlds"],
+    "stop_early": dec["stop_early"],
+    "warm_tie": dec["warm_tie"],
+    "warm_worlds": dec["warm_checked"],
+    "decision_worst": max(dec["stop_worst"], dec["warm_worst"]),
+    "decision_unexplained": len(dec["stop_unexplained"]) + len(dec["warm_unexplained"]),
+    "decisions_checked": dec["stop_checked"] + dec["warm_checked"],
+    "niter_differs": dec.get("niter_differs", 0),
+    "failed": bool(failures),
+  })
   return {
+    "decisions": dec,
     "capped_worlds": capped,
     "maxerr": maxerr,
     "failures": failures,

@@ -167,3 +167,45 @@ def test_step_gather_to_learner_in_a_subgroup():
   assert got.shape == (4, 2 + 3)
   assert got[:2, 0].tolist() == [1.0, 1.0] and got[2:, 0].tolist() == [2.0, 2.0]
   assert got[:2, 2].tolist() == [10.0, 10.0] and got[2:, 2].tolist() == [20.0, 20.0]
+
+
+def _bench_cpu(args: list[str], env_extra: dict | None = None):
+  import subprocess
+  import sys
+  from pathlib import Path
+
+  root = Path(__file__).resolve().parents[1]
+  env = dict(os.environ, OMP_NUM_THREADS="1", **(env_extra or {}))
+  for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+    if not env_extra or k not in env_extra:
+      env.pop(k, None)
+  return subprocess.run([sys.executable, str(root / "tests" / "bench_cpu_ranks.py"), *args], capture_output=True,
+                        text=True, timeout=600, env=env)
+
+
+def test_bench_multirank_path_world2_cpu():
+  """bench.py's N > 1 path end to end: `--gpus 2` without
+  torchrun spawns 2 ranks through torch.distributed.run (bench.spawn_ranks),
+  each asserts WORLD_SIZE == --gpus, runs its own env shard (seed 42+rank,
+  oracle physics on CPU standing in for the HIP step), barriers around the
+  timed window, all-reduces its time with MAX, all-gathers the packed
+  learner outputs every step; rank 0 alone prints one JSON line."""
+  import json
+
+  out = _bench_cpu(["--gpus", "2", "--device", "cpu", "--steps", "2", "--warmup", "1", "--settle", "1", "--num-envs", "4",
+                    "--kernel-launches", "1", "--no-cpu-baseline"])
+  assert out.returncode == 0, out.stderr[-4000:]
+  lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+  assert len(lines) == 1, out.stdout[-2000:]
+  j = json.loads(lines[0])
+  assert j["n_gpus"] == 2 and j["config"]["world_size"] == 2 and j["scaling"] == "weak"
+  assert "all-gather" in j["config"]["parallelism"]
+  assert j["config"]["gather_ms_per_step"] is not None and j["config"]["gather_ms_per_step"] > 0
+  # value = all ranks' env steps / the slowest rank's window
+  assert abs(j["value"] - 2 * 4 * 2 / (j["ms_per_step"] * 2 / 1e3)) < 1e-6 * j["value"]
+  assert j["cpu_baseline"] is None  # rank 0 at N = 1 only
+
+
+def test_bench_rejects_world_size_mismatch():
+  out = _bench_cpu(["--gpus", "1", "--device", "cpu", "--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+  assert out.returncode != 0 and "WORLD_SIZE=2 but --gpus 1" in out.stderr

@@ -13,6 +13,7 @@ from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
 from mjlab_amd.tasks import load_env_cfg
 from oracle.oracle import INPUTS, Oracle
 from tests.test_gpu_env import _gpu_motion
+from tests.scenes import check_iteration_counts
 from tests.test_gpu_parity import assert_parity
 
 pytestmark = pytest.mark.gpu
@@ -50,18 +51,25 @@ def test_benchmark_config_at_full_size(task, n, tmp_path):
   # 64 worlds of the live state, one more physics step on GPU vs the oracle
   sim = env.sim
   idx = torch.randperm(n, generator=torch.Generator().manual_seed(0))[:64].sort().values.numpy()
-  state = {}
+  full = {}
   for f in INPUTS:
     t = getattr(sim.data, f, None)
     if t is not None and t.numel():
-      state[f] = t.detach().cpu().numpy().reshape(n, -1)[idx]
-  ov = {}
+      full[f] = t.detach().cpu().numpy().reshape(n, -1)
+  ovf = {}
   for f in env.event_manager.domain_randomization_fields:
     t = getattr(sim.model, f)
     if t.shape[0] == n:
-      ov[f] = t.detach().cpu().numpy()[idx]
+      ovf[f] = t.detach().cpu().numpy()
+  state = {f: v[idx] for f, v in full.items()}
+  ov = {f: v[idx] for f, v in ovf.items()}
   sim.step()
   torch.cuda.synchronize()
+  gall = {k: getattr(sim.data, k).detach().cpu().numpy().reshape(n, -1) for k in ("qpos", "solver_niter")}
   got = {k: getattr(sim.data, k).detach().cpu().numpy().reshape(n, -1)[idx] for k in sim.data.fields()}
   ref = Oracle(sim.mj_model, overrides=ov).run(len(idx), state, integrate=True, follow=got)
   assert_parity(got, ref, len(idx), min_int_rate=0.95, tag=f" {task} N={n} sample=64")
+  # every world: the device's mean Newton iterations against the float32 oracle's own
+  it = check_iteration_counts(gall, sim.mj_model, full, True, nthreads=16, overrides=ovf)
+  print(f"[iterations {task} N={n}] {it}")
+  assert it["ok"], it

@@ -7,7 +7,7 @@ import torch
 
 from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg
 from oracle.oracle import INPUTS, Oracle
-from tests.scenes import compare_step, g1_mocap_scene, g1_scene_model, g1_sensor_scene, go1_scene_model, mocap_states, random_states
+from tests.scenes import check_iteration_counts, compare_step, g1_mocap_scene, g1_scene_model, g1_sensor_scene, go1_scene_model, mocap_states, random_states
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -65,6 +65,9 @@ def test_single_step_parity(name, integrate, ls_parallel):
   rep = assert_parity(got, ref, n, tag=f" {name} integrate={integrate}")
   assert "qM" in rep["maxerr"] and "efc_J" in rep["maxerr"]  # the debug copies were compared
   assert (got["ncon"] > 0).mean() > 0.5  # the states exercise contacts
+  it = check_iteration_counts(got, m, st, integrate)
+  print(f"[iterations {name}] {it}")
+  assert it["ok"], it  # no systematic early stop against the float32 oracle's own test
 
 
 def test_trajectory_parity_along_gpu_rollout():
@@ -241,6 +244,30 @@ def test_converged_solver_parity():
   # (qfrc_constraint), 2.2e-5 (sensordata) relative; bound 1e-4 for every world
   rep = compare_step(got, ref, solve_rel=1e-4, solve_frac=1.0, solve_max=1e-4)
   print("[converged]", rep["int_match_rate"], {k: f"{v:.2e}" for k, v in rep["maxerr"].items() if "/" in k})
+  assert not rep["failures"], rep["failures"]
+
+
+def test_converged_solver_parity_parallel_search():
+  """The reference default (ls_parallel=True, sim.py:91,117) without follow
+  mode: each side takes its own step-size choices, and with the iteration cap
+  lifted (iterations 100, tolerance 1e-10) both reach the same qacc in every
+  world — the minimiser does not depend on the path."""
+  n = 512
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(13))
+  cfg = dict(CFG, mujoco=MujocoCfg(timestep=0.005, iterations=100, ls_iterations=20, tolerance=1e-10))
+  sim = Simulation(n, SimulationCfg(**cfg, ls_parallel=True), m, DEV)
+  assert m.ls_parallel == 1
+  put(sim, st)
+  sim.forward()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=False)  # no follow: the oracle's own choices
+  # the float32 oracle's own converged solve (its own choices and stop): each
+  # world's float32 resolution, the per-world floor of the bounds (F32_SENSITIVITY)
+  ref["f32"] = Oracle(m, "f32").run(n, st, integrate=False)
+  rep = compare_step(got, ref, solve_rel=1e-4, solve_frac=1.0, solve_max=1e-4)
+  print("[converged parallel]", rep["int_match_rate"], {k: f"{v:.2e}" for k, v in rep["maxerr"].items() if "/" in k},
+        "niter_differs", rep["decisions"].get("niter_differs"))
   assert not rep["failures"], rep["failures"]
 
 
