@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 
 #include "../../include/mjh_abi.h"
 #include "mjh_math.h"
@@ -48,6 +49,10 @@ struct Layout {
   int red, ints;
   int total, gtotal;  // per-world words: LDS, global scratch
   int ncap, rcap;
+  // one-world workgroups: the LDS holds the row arrays for lcap rows; a world
+  // with more (up to rcap = njmax) keeps them at these global-scratch offsets
+  int lcap;
+  int g_efc_D, g_efc_R, g_efc_aref, g_efc_jaref, g_efc_jv, g_efc_force, g_efc_fl, g_efc_type, g_efc_h, g_arow, g_ash;
   // split step (MODE 1 position kernel -> MODE 2 velocity/solver kernel): the
   // position kernel's outputs that the full kernel keeps in LDS go through a
   // per-world global handoff region, plus the reuse snapshot
@@ -104,6 +109,16 @@ struct Rg {
     (#name[0] == 'c' && (#name[1] == 'i' || #name[1] == 'r' || #name[1] == 'v' || #name[1] == 'f' || #name[1] == 'd')) || \
     (#name[0] == 'e' && #name[1] == 'f' && #name[2] == 'c') || (#name[0] == 'a' && (#name[1] == 'r' || #name[1] == 's'))) && \
     !(#name[0] == 'L' && #name[1] == 0);
+#elif MJH_PRESET == 7
+// like 4 (body arrays, J and the factor L in global scratch), and the
+// constraint rows' colder arrays as well (R, frictionloss, aref, the active-set
+// lists): ~6 words of LDS per row, so 300 rows fit 16 worlds per CU
+#define X_RG(name, r) static constexpr bool name = (r) != 0 || (#name[0] == 'J' && #name[1] == 0) || \
+    (#name[0] == 'L' && #name[1] == 0) || \
+    (#name[0] == 'c' && (#name[1] == 'i' || #name[1] == 'r' || #name[1] == 'v' || #name[1] == 'f' || #name[1] == 'd')) || \
+    (#name[0] == 'e' && #name[1] == 'f' && #name[2] == 'c' && #name[3] == '_' && \
+     ((#name[4] == 'R' && #name[5] == 0) || (#name[4] == 'f' && #name[5] == 'l') || (#name[4] == 'a' && #name[5] == 'r'))) || \
+    (#name[0] == 'a' && (#name[1] == 'r' || #name[1] == 's'));
 #elif MJH_PRESET == 3
 #define X_RG(name, r) static constexpr bool name = (r) != 0 || (#name[0] == 'J' && #name[1] == 0);
 #else
@@ -130,6 +145,7 @@ thread_local std::string g_err;
 bool g_disable_spec = false;  // mjh_set_specialization(0): always the generic instance
 bool g_auto_order = false;    // mjh_set_world_ordering(1): order the worlds in the pack launch
 bool g_pos_reuse = kPositionStageGlobal;  // mjh_set_position_reuse: reuse the position stage of unchanged worlds
+int g_lds_row_cap = 0;  // mjh_set_lds_row_cap: test cap on the LDS-resident constraint rows (0: none)
 #ifndef MJH_SPLIT
 #define MJH_SPLIT 0
 #endif
@@ -460,15 +476,29 @@ __device__ void ldl_solve_fast(const float* A, int n, int ld, float* x) {
   }
 }
 
+// The factor L (and the Hessian it is factored from, and the mass matrix's
+// staging rows) lives as packed lower-triangular rows: row i holds entries
+// 0..i padded to a multiple of 4, 16-byte aligned. NVP rows take lrow(NVP)
+// words (G1, NVP 36: 720 instead of 35 x 36 = 1,260), so more constraint rows
+// fit the LDS. Entries right of the diagonal inside a row's padding are scratch.
+// Packed for one-world workgroups (PK), whose LDS budget is tight; 8-world
+// workgroups keep full rows of stride ld.
+__host__ __device__ constexpr int lrow(int i) { return 4 * ((i >> 2) + 1) * (2 * (i >> 2) + (i & 3)); }
+__host__ __device__ constexpr int llen(int i) { return ((i >> 2) + 1) << 2; }
+static_assert(lrow(0) == 0 && lrow(1) == 4 && lrow(4) == 16 && lrow(5) == 24 && lrow(36) == 720, "packed rows");
+template <bool PK> __device__ __forceinline__ int lofs(int i, int ld) { return PK ? lrow(i) : i * ld; }
+template <bool PK> __device__ __forceinline__ int lspan(int i, int ld) { return PK ? llen(i) : ld; }
+__host__ __device__ constexpr bool pack_l(int wpb) { return wpb == 1; }
+
 #ifndef MJH_HESS_PF
 #define MJH_HESS_PF 4  // k-steps of J loads in flight in the Hessian
 #endif
-// H (lower triangle of Hout) = M + sum_k ash[k]^2 J[arow[k]] J[arow[k]]^T over the
+// H (lower triangle of Hout, packed rows) = M + sum_k ash[k]^2 J[arow[k]] J[arow[k]]^T over the
 // nact compacted active rows, on the f32 matrix cores (v_mfma_f32_16x16x4_f32:
 // exact fp32 FMA chains). Tiles of 16x16 on the lower block triangle; at most
 // NB = NVP/16 (rounded up) tile rows. The accumulators start from M's lower
 // triangle (its loads overlap the first J loads instead of trailing the loop).
-template <int NT, int NVP>
+template <int NT, int NVP, bool PK>
 __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const float* J, int ldj, const int* arow, const float* ash,
                              int nact, int n, float* Hout) {
   typedef float v4f __attribute__((ext_vector_type(4)));
@@ -530,7 +560,7 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int i = I * 16 + kq * 4 + q, j = Jb * 16 + ci;
-        if (i < n && j <= i) Hout[i * ldm + j] = acc[t][q];
+        if (i < n && j <= i) Hout[lofs<PK>(i, ldm) + j] = acc[t][q];
       }
     }
 }
@@ -606,10 +636,12 @@ __device__ __forceinline__ float rowdot(const float* r, const float* x, int n) {
 // Right-looking LDL^T fully unrolled over compile-time column indices: the
 // entries of other rows come from v_readlane, so the factorisation never
 // touches LDS between columns. Rows >= n are inert identity rows.
-template <int NVP>
+template <int NVP, bool PK>
 __device__ __forceinline__ void load_row_lower(const float* A, int n, int ld, float (&a)[NVP]) {
   const int lane = threadIdx.x & 63;
-  const float* r = A + (lane < n ? lane : 0) * ld;
+  // a packed row's float4s beyond its length are the next rows' (scratch right
+  // of the diagonal); the region holds lrow(NVP) words, so no read leaves it
+  const float* r = A + lofs<PK>(lane < n ? lane : 0, ld);
 #pragma unroll
   for (int k = 0; k < NVP; k += 4) {
     const float4 v = *reinterpret_cast<const float4*>(r + k);
@@ -623,7 +655,7 @@ __device__ __forceinline__ void load_row_lower(const float* A, int n, int ld, fl
 
 // factor of the rows already in registers (lane i: row i, identity rows for
 // lanes >= n); the factored rows are stored to A
-template <int NVP>
+template <int NVP, bool PK>
 __device__ __forceinline__ void ldl_factor_rows(float (&a)[NVP], float* A, int n, int ld) {
   // Branch-free: lane i updates its whole row each step; entries right of the
   // diagonal are scratch never read back (only rdlane(a[k], j) with k < j, i.e.
@@ -657,31 +689,33 @@ __device__ __forceinline__ void ldl_factor_rows(float (&a)[NVP], float* A, int n
     a[k] = lane > k ? lik : (lane == k ? piv : a[k]);
   }
   if (lane < n) {
-    float* r = A + lane * ld;
+    float* r = A + lofs<PK>(lane, ld);
+    const int len = lspan<PK>(lane, ld);
 #pragma unroll
-    for (int k = 0; k < NVP; k += 4) *reinterpret_cast<float4*>(r + k) = make_float4(a[k], a[k + 1], a[k + 2], a[k + 3]);
+    for (int k = 0; k < NVP; k += 4)
+      if (k < len) *reinterpret_cast<float4*>(r + k) = make_float4(a[k], a[k + 1], a[k + 2], a[k + 3]);
   }
   wsync();
 }
 
-template <int NVP>
+template <int NVP, bool PK>
 __device__ MJH_SOLVER_INLINE void ldl_factor_reg(float* A, int n, int ld) {
   float a[NVP];
   wsync();
-  load_row_lower<NVP>(A, n, ld, a);
-  ldl_factor_rows<NVP>(a, A, n, ld);
+  load_row_lower<NVP, PK>(A, n, ld, a);
+  ldl_factor_rows<NVP, PK>(a, A, n, ld);
 }
 
 // (L D L^T) x = b with the factor from ldl_factor_reg; x in LDS (in place).
-template <int NVP>
+template <int NVP, bool PK>
 __device__ MJH_SOLVER_INLINE void ldl_solve_reg(const float* A, int n, int ld, float* x) {
   const int lane = threadIdx.x & 63;
   float a[NVP], c[NVP];
   wsync();
-  load_row_lower<NVP>(A, n, ld, a);  // L[i][k<i], D[i] at k == i
+  load_row_lower<NVP, PK>(A, n, ld, a);  // L[i][k<i], D[i] at k == i
   const int cl = lane < n ? lane : 0;
 #pragma unroll
-  for (int k = 0; k < NVP; k++) c[k] = A[(k < n ? k : 0) * ld + cl];  // column i: L[k][i] (used for k > i)
+  for (int k = 0; k < NVP; k++) c[k] = A[lofs<PK>(k < n ? k : 0, ld) + cl];  // column i: L[k][i] (used for k > i)
   float xi = lane < n ? x[lane] : 0.f;
   float di = 1.f;
 #pragma unroll
@@ -997,8 +1031,15 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 #ifndef MJH_PERSIST
 #define MJH_PERSIST 0
 #endif
+// resident worlds per CU for workgroups of fewer than 8 worlds (one-world
+// workgroups: MJH_WPCU / 4 waves per SIMD); it sets the launch bound's wave
+// target (the VGPR budget: 8 -> 256, 12 -> 168, 16 -> 128) and the per-world
+// LDS budget alike
+#ifndef MJH_WPCU
+#define MJH_WPCU 8
+#endif
 #ifndef MJH_MINWAVES
-#define MJH_MINWAVES(wpb) ((wpb) < 8 ? 2 : 1)  // one-world workgroups: keep <= 256 VGPRs + AGPRs
+#define MJH_MINWAVES(wpb) ((wpb) < 8 ? MJH_WPCU / 4 : 1)
 #endif
 // MODE 0: the whole step in one launch. MODE 1: the position stage only
 // (kinematics, com, CRB, M and its factor, collision, constraint rows and their
@@ -1079,7 +1120,13 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   // optional cost-sorted world order: a workgroup's worlds then take similar
   // time, so its LDS is not held hostage by one slow world (the position pass,
   // of nearly uniform cost, keeps the identity order)
-  const int w = (MODE != 1 && d.world_order) ? (int)d.world_order[slot] : slot;
+  // wave-uniform: readfirstlane keeps w, the world bases and every pointer
+  // derived from them in SGPRs (a vector load of world_order otherwise puts
+  // ~20 64-bit scratch pointers in VGPR pairs, live across the whole step).
+  // One-world workgroups only: the 8-world instance is not VGPR-bound and the
+  // SGPR pairs spill there (Go1 0.551 -> 0.559 ms)
+  const int w0 = (MODE != 1 && d.world_order) ? (int)d.world_order[slot] : slot;
+  const int w = WPB == 1 ? __builtin_amdgcn_readfirstlane(w0) : w0;
   const int tid = threadIdx.x & 63;
   // mj_step (integration) or mj_forward: a runtime flag, not a template
   // parameter, so both run the very same code up to the integration (a step
@@ -1098,6 +1145,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   const long long W = w;
   const int nq = Z.nq, nv = Z.nv, nb = Z.nbody, nu = Z.nu, nj = Z.njnt;
   const int ldm = Lo.ldm, ldj = Lo.ldj;
+  // the factor's rows: packed lower-triangular for one-world workgroups
+  constexpr bool PKL = pack_l(WPB);
+  const int kLWords = PKL ? lrow(NVP) : nv * ldm;
 
   constexpr bool HO = MODE == 1;
   float* qpos = HO ? S : SP(qpos);
@@ -1150,23 +1200,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   int* con_geom = SPI(con_geom);
   int* con_efcadr = SPI(con_efcadr);
   float* J = SP(J);
-  float* efc_D = HO ? G + Lo.h_D : SP(efc_D);
-  float* efc_R = HO ? G + Lo.h_R : SP(efc_R);
-  float* efc_aref = HO ? G + Lo.h_aref : SP(efc_aref);
-  float* jaref = SP(efc_jaref);
-  float* jv = HO ? G + Lo.h_jv : SP(efc_jv);
-  float* efc_force = SP(efc_force);
-  float* efc_fl = HO ? G + Lo.h_fl : SP(efc_fl);
   float* efc_pos = SP(efc_pos);
-  int* efc_type = HO ? reinterpret_cast<int*>(G + Lo.h_type) : SPI(efc_type);
   int* efc_id = SPI(efc_id);
   unsigned long long* efc_mask = reinterpret_cast<unsigned long long*>(SP(efc_mask));
-  float* efc_h = SP(efc_h);
-  int* arow = SPI(arow);
-  float* ash = SP(ash);
   int* sidx = SPI(sidx);
-  // the damping coefficient of each row until the velocity stage completes aref
-  float* efc_b = MODE == 0 ? SP(efc_h) : G + Lo.h_b;
   float* red = S + (MODE == 1 ? Lo.pred : Lo.red);
   int* redi = SI + (MODE == 1 ? Lo.pred : Lo.red) + 2 * (NT / 64) + 2;
   int* ints = SI + (MODE == 1 ? Lo.pints : Lo.ints);
@@ -1546,15 +1583,17 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       a[j] = ((mask >> j) & 1ull) ? v : 0.f;
     }
     if (tid < nv) {
-      float* r = Lm + tid * ldm;
+      float* r = Lm + lofs<PKL>(tid, ldm);
+      const int len = lspan<PKL>(tid, ldm);
 #pragma unroll
-      for (int k = 0; k < NVP; k += 4) *reinterpret_cast<float4*>(r + k) = make_float4(a[k], a[k + 1], a[k + 2], a[k + 3]);
+      for (int k = 0; k < NVP; k += 4)
+        if (k < len) *reinterpret_cast<float4*>(r + k) = make_float4(a[k], a[k + 1], a[k + 2], a[k + 3]);
     }
     wsync();
     if (tid < nv) {
 #pragma unroll
       for (int j = 1; j < NVP; j++)
-        if (j > tid && j < nv) a[j] = Lm[j * ldm + tid];
+        if (j > tid && j < nv) a[j] = Lm[lofs<PKL>(j, ldm) + tid];
       float* r = Mm + tid * ldm;
 #pragma unroll
       for (int k = 0; k < NVP; k += 4) *reinterpret_cast<float4*>(r + k) = make_float4(a[k], a[k + 1], a[k + 2], a[k + 3]);
@@ -1563,7 +1602,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       for (int j = 0; j < NVP; j++) a[j] = j == tid ? 1.f : 0.f;
     }
     PROF(10);
-    ldl_factor_rows<NVP>(a, Lm, nv, ldm);
+    ldl_factor_rows<NVP, PKL>(a, Lm, nv, ldm);
   }
   PROF(2);
 
@@ -1654,6 +1693,72 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   }
   ncon = ints[I_NCON];
   PROF(4);
+  }  // position stage, part 1 (kinematics .. collision)
+
+  // ---------------------------------------------------------------- row capacity
+  // The constraint rows' arrays live in LDS for up to Lo.lcap rows. A world with
+  // more rows (one-world workgroups, lcap < rcap = njmax) runs the rest of the
+  // step with them in global scratch instead (BIG): the same code on other
+  // addresses, so its results are the same. Its row count is known before any
+  // row is written: the counts of the rows make_constraint emits (frictionloss
+  // dofs, active limits, contacts within their margin) or the handoff's.
+  constexpr bool kTwoTier = WPB == 1 && MODE != 1;
+  bool big = false;
+  if constexpr (kTwoTier) {
+    if (Lo.lcap < Lo.rcap) {
+      int need = 0;
+      if (MODE == 2 || reused) {
+        need = reinterpret_cast<const int*>(G + Lo.h_ints)[I_NEFC];
+      } else {
+        for (int base = 0; base < nv; base += NT) {
+          const int i = base + tid;
+          need += __popcll(__ballot(i < nv && dof_frictionloss[i] > 0.f));
+        }
+        for (int base = 0; base < nj; base += NT) {
+          const int j = base + tid;
+          bool f = false;
+          if (j < nj && IMG_I(jnt_limited)[j] && (IMG_I(jnt_type)[j] == 2 || IMG_I(jnt_type)[j] == 3)) {
+            const float q = qpos[IMG_I(jnt_qposadr)[j]];
+            const float dlo = q - jnt_range[2 * j], dhi = jnt_range[2 * j + 1] - q;
+            f = fminf(dlo, dhi) - IMG_F(jnt_margin)[j] < 0.f;
+          }
+          need += __popcll(__ballot(f));
+        }
+        for (int base = 0; base < ncon; base += NT) {
+          const int ci = base + tid;
+          int nr = 0;
+          if (ci < ncon && con_dist[ci] - con_imargin[ci] < 0.f) nr = con_dim[ci] == 1 ? 1 : 2 * (con_dim[ci] - 1);
+          int total;
+          (void)bscan<NT>(nr, &total, redi);
+          need += total;
+        }
+      }
+      big = need > Lo.lcap;
+    }
+  }
+
+  auto tail = [&](auto big_tag) {
+  constexpr bool BIG = decltype(big_tag)::value;
+  // row arrays: LDS (or the preset's region) for up to lcap rows, global scratch for BIG worlds
+#define SPR(name) (BIG && !Rg::name ? G + Lo.g_##name : SP(name))
+#define SPRI(name) reinterpret_cast<int*>(SPR(name))
+  float* efc_D = HO ? G + Lo.h_D : SPR(efc_D);
+  float* efc_R = HO ? G + Lo.h_R : SPR(efc_R);
+  float* efc_aref = HO ? G + Lo.h_aref : SPR(efc_aref);
+  float* jaref = SPR(efc_jaref);
+  float* jv = HO ? G + Lo.h_jv : SPR(efc_jv);
+  float* efc_force = SPR(efc_force);
+  float* efc_fl = HO ? G + Lo.h_fl : SPR(efc_fl);
+  int* efc_type = HO ? reinterpret_cast<int*>(G + Lo.h_type) : SPRI(efc_type);
+  float* efc_h = SPR(efc_h);
+  int* arow = SPRI(arow);
+  float* ash = SPR(ash);
+  // the damping coefficient of each row until the velocity stage completes aref
+  float* efc_b = MODE == 0 ? SPR(efc_h) : G + Lo.h_b;
+#undef SPRI
+#undef SPR
+  const int acap = (BIG || Rg::arow) ? Lo.rcap : Lo.lcap;  // arow's entries
+  if (MODE == 1 || (MODE == 0 && !reused)) {  // position stage, part 2
 
   // ---------------------------------------------------------------- make_constraint
   {
@@ -1876,7 +1981,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     img_hash = image_hash();
     wsync();
     if (tid < I_COUNT) reinterpret_cast<int*>(G + Lo.h_ints)[tid] = ints[tid];
-    for (int i = tid; i < nv * ldm; i += NT) G[Lo.h_L + i] = Lm[i];
+    for (int i = tid; i < kLWords; i += NT) G[Lo.h_L + i] = Lm[i];
     int* ht = reinterpret_cast<int*>(G + Lo.h_type);
     for (int r = tid; r < nefc; r += NT) {
       ht[r] = efc_type[r];
@@ -1952,7 +2057,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     }
     // the fused kernel keeps the factor of M in LDS
     if constexpr (MODE == 0)
-      for (int i = tid; i < nv * ldm; i += NT) Lm[i] = G[Lo.h_L + i];
+      for (int i = tid; i < kLWords; i += NT) Lm[i] = G[Lo.h_L + i];
   }
   wsync();
   // aref = aref_pos - b J qvel (row_params: the velocity term)
@@ -2116,7 +2221,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     }
   }
   PROF(25);
-  ldl_solve_reg<NVP>(MODE == 2 ? G + Lo.h_L : Lm, nv, ldm, qacc_smooth);
+  ldl_solve_reg<NVP, PKL>(MODE == 2 ? G + Lo.h_L : Lm, nv, ldm, qacc_smooth);
   PROF(3);
 
   // ---------------------------------------------------------------- Newton solver
@@ -2223,14 +2328,14 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           for (int j = 0; j <= i; j++) {
             float hs = Mm[i * ldm + j];
             for (int k = 0; k < nact; k++) hs += ash[k] * ash[k] * J[arow[k] * ldj + i] * J[arow[k] * ldj + j];
-            Lm[i * ldm + j] = hs;
+            Lm[lofs<PKL>(i, ldm) + j] = hs;
           }
 #else
-        hessian_mfma<NT, NVP>(Mm, ldm, J, ldj, arow, ash, nact, nv, Lm);
+        hessian_mfma<NT, NVP, PKL>(Mm, ldm, J, ldj, arow, ash, nact, nv, Lm);
 #endif
         PROF_ACC(15, th);
         unsigned long long tf = PROF_NOW();
-        ldl_factor_reg<NVP>(Lm, nv, ldm);
+        ldl_factor_reg<NVP, PKL>(Lm, nv, ldm);
         PROF_ACC(16, tf);
 #pragma unroll
         for (int q = 0; q < kMaskWords; q++) act_prev[q] = act[q];
@@ -2240,7 +2345,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       }
       for (int i = tid; i < nv; i += NT) search[i] = grad[i];
       unsigned long long ts = PROF_NOW();
-      ldl_solve_reg<NVP>(Lm, nv, ldm, search);
+      ldl_solve_reg<NVP, PKL>(Lm, nv, ldm, search);
       PROF_ACC(17, ts);
       for (int i = tid; i < nv; i += NT) search[i] = -search[i];
       wsync();
@@ -2516,7 +2621,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         // large enough (always for the benchmark models), else in global scratch.
         // The record is zeroed where it is written (below), so no store precedes
         // this sensor's scratch loads.
-        int* const sx = Lo.rcap + 4 >= 64 ? arow : sidx;
+        int* const sx = acap + 4 >= 64 ? arow : sidx;
         auto om = [&](int ty, int oid, int g) -> bool {
           if (oid < 0) return true;
           const int gb = IMG_I(geom_bodyid)[g];
@@ -2914,9 +3019,12 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     const float dt = m.timestep;
     float* qa_int = tmp;
     if (m.integrator == MJH_INT_IMPLICITFAST) {
-      for (int i = tid; i < nv * ldm; i += NT) Lm[i] = Mm[i];
+      for (int i = tid; i < nv * ldm; i += NT) {
+        const int row = i / ldm, col = i - row * ldm;
+        if (col < lspan<PKL>(row, ldm)) Lm[lofs<PKL>(row, ldm) + col] = Mm[i];
+      }
       wsync();
-      for (int i = tid; i < nv; i += NT) Lm[i * ldm + i] += dt * dof_damping[i];
+      for (int i = tid; i < nv; i += NT) Lm[lofs<PKL>(i, ldm) + i] += dt * dof_damping[i];
       wsync();
       for (int i = tid; i < nu; i += NT) {
         if (IMG_I(actuator_forcelimited)[i]) {
@@ -2925,22 +3033,25 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         }
         const int dof = IMG_I(jnt_dofadr)[IMG_I(actuator_trnid)[i]];
         const float g = IMG_F(actuator_gear)[i];
-        atomicAdd(&Lm[dof * ldm + dof], -dt * g * g * IMG_F(actuator_biasprm)[10 * i + 2]);
+        atomicAdd(&Lm[lofs<PKL>(dof, ldm) + dof], -dt * g * g * IMG_F(actuator_biasprm)[10 * i + 2]);
       }
       for (int i = tid; i < nv; i += NT) qa_int[i] = qfrc_smooth[i] + qfrc_con[i];
-      ldl_factor_reg<NVP>(Lm, nv, ldm);
-      ldl_solve_reg<NVP>(Lm, nv, ldm, qa_int);
+      ldl_factor_reg<NVP, PKL>(Lm, nv, ldm);
+      ldl_solve_reg<NVP, PKL>(Lm, nv, ldm, qa_int);
     } else {
       float anyd = 0.f;
       for (int i = tid; i < nv; i += NT) anyd += dof_damping[i] > 0.f ? 1.f : 0.f;
       anyd = bsum<NT>(anyd, red);
       if (anyd > 0.f) {
-        for (int i = tid; i < nv * ldm; i += NT) Lm[i] = Mm[i];
+        for (int i = tid; i < nv * ldm; i += NT) {
+          const int row = i / ldm, col = i - row * ldm;
+          if (col < lspan<PKL>(row, ldm)) Lm[lofs<PKL>(row, ldm) + col] = Mm[i];
+        }
         wsync();
-        for (int i = tid; i < nv; i += NT) Lm[i * ldm + i] += dt * dof_damping[i];
+        for (int i = tid; i < nv; i += NT) Lm[lofs<PKL>(i, ldm) + i] += dt * dof_damping[i];
         symv_u<NT, NVP>(Mm, nv, ldm, qacc, qa_int);
-        ldl_factor_reg<NVP>(Lm, nv, ldm);
-        ldl_solve_reg<NVP>(Lm, nv, ldm, qa_int);
+        ldl_factor_reg<NVP, PKL>(Lm, nv, ldm);
+        ldl_solve_reg<NVP, PKL>(Lm, nv, ldm, qa_int);
       } else {
         for (int i = tid; i < nv; i += NT) qa_int[i] = qacc[i];
         wsync();
@@ -2987,6 +3098,16 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     }
   }
   }  // velocity / solver stage
+  };  // tail
+  if constexpr (kTwoTier) {
+    if (big)
+      tail(std::integral_constant<bool, true>{});
+    else
+      tail(std::integral_constant<bool, false>{});
+  } else {
+    (void)big;
+    tail(std::integral_constant<bool, false>{});
+  }
   if constexpr (!PERSIST) return;
   }  // world loop
 }
@@ -3100,7 +3221,7 @@ ImgOff make_imgoff(const mjh_model* m) {
 // Per-world layout: arrays go to LDS (`off`) or to the global scratch
 // (`goff`) according to the region table Rg. `budget` = LDS words available to
 // one world; the constraint-row capacity is what fits (LDS rows) or njmax.
-Layout make_layout(const mjh_model* m, int budget) {
+Layout make_layout(const mjh_model* m, int budget, int wpb) {
   Layout L;
   std::memset(&L, 0, sizeof(L));
   int off = 0, goff = 0;
@@ -3132,7 +3253,8 @@ Layout make_layout(const mjh_model* m, int budget) {
   TAKE(xanchor, 3 * nj); TAKE(xaxis, 3 * nj); TAKE(cdof, 6 * nv); TAKE(cdof_dot, 6 * nv);
   TAKE(cgpos, 3 * m->ncolgeom); TAKE(cgmat, 9 * m->ncolgeom);
   TAKE(sxpos, 3 * m->nsite); TAKE(sxmat, 9 * m->nsite);
-  TAKE(M, nv * L.ldm); TAKE(L, nv * L.ldm);
+  const int lwords = pack_l(wpb) ? lrow(nvp_of(nv)) : nv * L.ldm;
+  TAKE(M, nv * L.ldm); TAKE(L, lwords);
   TAKE(act_force, m->nu);
   const int C = m->nconmax;
   L.ncap = C;
@@ -3148,26 +3270,42 @@ Layout make_layout(const mjh_model* m, int budget) {
   const int per_row_lds = (Rg::J ? 0 : L.ldj) + !Rg::efc_D + !Rg::efc_R + !Rg::efc_aref + !Rg::efc_jaref +
                           !Rg::efc_jv + !Rg::efc_force + !Rg::efc_fl + !Rg::efc_pos + !Rg::efc_type + !Rg::efc_id +
                           2 * !Rg::efc_mask + !Rg::efc_h + !Rg::arow + !Rg::ash;
-  int rcap = m->njmax;
+  int rcap = m->njmax, lcap = rcap;
   if (per_row_lds > 0) {
     const int r = (budget - off - 64) / per_row_lds;
-    if (r < rcap) rcap = r;
+    if (r < lcap) lcap = r;
   }
-  if (rcap < 1) rcap = 1;
+  if (wpb == 1 && g_lds_row_cap > 0 && g_lds_row_cap < lcap) lcap = g_lds_row_cap;
+  if (lcap < 1) lcap = 1;
+  // 8-world workgroups: rows beyond the LDS are dropped (flagged as overflow);
+  // one-world workgroups: up to njmax, beyond lcap in global scratch (BIG)
+  if (wpb > 1) rcap = lcap;
   L.rcap = rcap;
+  L.lcap = lcap;
+  // LDS-resident row arrays take lcap rows, global ones rcap
+#define TAKER(name, extra) TAKE(name, (Rg::name ? rcap : lcap) + (extra))
   TAKE(J, rcap * L.ldj);
-  TAKE(efc_D, rcap); TAKE(efc_R, rcap); TAKE(efc_aref, rcap); TAKE(efc_jaref, rcap);
-  TAKE(efc_jv, rcap); TAKE(efc_force, rcap); TAKE(efc_fl, rcap); TAKE(efc_pos, rcap);
-  TAKE(efc_type, rcap); TAKE(efc_id, rcap);
+  TAKER(efc_D, 0); TAKER(efc_R, 0); TAKER(efc_aref, 0); TAKER(efc_jaref, 0);
+  TAKER(efc_jv, 0); TAKER(efc_force, 0); TAKER(efc_fl, 0); TAKE(efc_pos, rcap);
+  TAKER(efc_type, 0); TAKE(efc_id, rcap);
   TAKE(efc_mask, 2 * rcap);
-  TAKE(efc_h, rcap); TAKE(arow, rcap + 4); TAKE(ash, rcap + 4);
+  TAKER(efc_h, 0); TAKER(arow, 4); TAKER(ash, 4);
+#undef TAKER
   TAKE(sidx, 64);
 #undef TAKE
   L.total = al(off);
   // split-step handoff (global scratch): the factor of M, the rows' position
   // parameters, counters and the reuse snapshot
   auto gt = [&](int n) { const int o = goff; goff += al(n); return o; };
-  L.h_L = gt(nv * L.ldm);
+  // the BIG worlds' row arrays (one-world workgroups with lcap < rcap)
+  {
+    const bool two = wpb == 1;  // allocated whatever lcap is: the scratch size does not depend on it
+    L.g_efc_D = two ? gt(rcap) : 0; L.g_efc_R = two ? gt(rcap) : 0; L.g_efc_aref = two ? gt(rcap) : 0;
+    L.g_efc_jaref = two ? gt(rcap) : 0; L.g_efc_jv = two ? gt(rcap) : 0; L.g_efc_force = two ? gt(rcap) : 0;
+    L.g_efc_fl = two ? gt(rcap) : 0; L.g_efc_type = two ? gt(rcap) : 0; L.g_efc_h = two ? gt(rcap) : 0;
+    L.g_arow = two ? gt(rcap + 4) : 0; L.g_ash = two ? gt(rcap + 4) : 0;
+  }
+  L.h_L = gt(lwords);
   L.h_type = gt(rcap); L.h_fl = gt(rcap); L.h_D = gt(rcap); L.h_R = gt(rcap);
   L.h_aref = gt(rcap); L.h_b = gt(rcap); L.h_jv = gt(rcap);
   L.h_ints = gt(8);
@@ -3195,10 +3333,11 @@ Plan make_plan(const mjh_model* m) {
   const int wpb = wpb_of_nvp(nvp_of(m->nv));
   p.io = make_imgoff(m);
   const int img_lds = img_global(wpb) ? 0 : p.io.img_words;
-  // 8 / wpb workgroups share a CU's LDS (one-world workgroups: 8 per CU, the
-  // two waves per SIMD that 2 x 256 VGPRs allow)
-  const int budget = (kLdsBytes / 4 / (8 / wpb) - img_lds) / wpb;
-  p.lo = make_layout(m, budget);
+  // MJH_WPCU / wpb workgroups share a CU's LDS (one-world workgroups: MJH_WPCU
+  // per CU, the waves per SIMD the launch bound's VGPR budget allows); 8-world
+  // workgroups: one per CU
+  const int budget = (kLdsBytes / 4 / (wpb < 8 ? MJH_WPCU / wpb : 1) - img_lds) / wpb;
+  p.lo = make_layout(m, budget, wpb);
   p.shmem = (size_t)(img_lds + wpb * p.lo.total) * 4;
   p.shmem_pos = (size_t)((img_global(kPosWorldsPerBlock) ? 0 : p.io.img_words) + kPosWorldsPerBlock * p.lo.ptotal) * 4;
   return p;
@@ -3360,6 +3499,7 @@ int mjh_model_check(const mjh_model* m) {
 int mjh_scratch_bytes(const mjh_model* m) { return (int)make_plan(m).shmem; }
 
 int mjh_efc_capacity(const mjh_model* m) { return make_plan(m).lo.rcap; }
+int mjh_lds_rows(const mjh_model* m) { return make_plan(m).lo.lcap; }
 
 extern const int mjh_layout_ints = kLayoutInts;  // for tools/gen_spec.py
 
@@ -3380,6 +3520,11 @@ int mjh_set_position_reuse(int on) {
 }
 
 int mjh_split_step(void) { return MJH_SPLIT; }
+
+int mjh_set_lds_row_cap(int rows) {
+  g_lds_row_cap = rows > 0 ? rows : 0;
+  return 0;
+}
 
 int mjh_spec_index(const mjh_model* m) { return find_spec(make_plan(m), m); }
 

@@ -32,6 +32,7 @@ EXPORTS = (
   "mjh_image_words",
   "mjh_set_profile_buffer",
   "mjh_efc_capacity",
+  "mjh_lds_rows",
   "mjh_plan_ints",
   "mjh_spec_index",
   "mjh_data_is_slab",
@@ -39,6 +40,7 @@ EXPORTS = (
   "mjh_set_world_ordering",
   "mjh_set_position_reuse",
   "mjh_split_step",
+  "mjh_set_lds_row_cap",
   "mjh_debug_fields",
   "mjh_scratch_words",
   "mjh_step",
@@ -116,12 +118,14 @@ def lib() -> ctypes.CDLL:
   L.mjh_model_check.argtypes = [ctypes.c_void_p]
   L.mjh_scratch_bytes.argtypes = [ctypes.c_void_p]
   L.mjh_efc_capacity.argtypes = [ctypes.c_void_p]
+  L.mjh_lds_rows.argtypes = [ctypes.c_void_p]
   L.mjh_plan_ints.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
   L.mjh_spec_index.argtypes = [ctypes.c_void_p]
   L.mjh_data_is_slab.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
   L.mjh_set_specialization.argtypes = [ctypes.c_int]
   L.mjh_set_world_ordering.argtypes = [ctypes.c_int]
   L.mjh_set_position_reuse.argtypes = [ctypes.c_int]
+  L.mjh_set_lds_row_cap.argtypes = [ctypes.c_int]
   L.mjh_debug_fields.argtypes = [ctypes.c_void_p] * 5
   if os.environ.get("MJH_POS_REUSE") == "0":  # A/B timing: the split position pass never skips a world
     L.mjh_set_position_reuse(0)

@@ -516,6 +516,11 @@ class Simulation:
   def efc_capacity(self) -> int:
     return int(native.lib().mjh_efc_capacity(ctypes.addressof(self._mstruct)))
 
+  def lds_row_capacity(self) -> int:
+    """Constraint rows a world keeps in LDS; a world with more runs the rest of
+    its step with them in global scratch (same results)."""
+    return int(native.lib().mjh_lds_rows(ctypes.addressof(self._mstruct)))
+
   def scratch_bytes(self) -> int:
     return int(native.lib().mjh_scratch_bytes(ctypes.addressof(self._mstruct)))
 

@@ -118,9 +118,13 @@ int mjh_scratch_bytes(const mjh_model* m);
 /* Words of per-world global scratch the caller must provide in d->scratch. */
 long long mjh_scratch_words(const mjh_model* m);
 
-/* Constraint rows per world that fit on chip (<= njmax); rows beyond it are
- * dropped and reported through flags bit 1. */
+/* Constraint rows per world (one-world workgroups: njmax; 8-world workgroups:
+ * those that fit their LDS, <= njmax); rows beyond it are dropped and reported
+ * through flags bit 1. */
 int mjh_efc_capacity(const mjh_model* m);
+/* Constraint rows a world keeps in LDS (<= mjh_efc_capacity; a world with more
+ * keeps them in global scratch for the rest of its step). */
+int mjh_lds_rows(const mjh_model* m);
 
 /* Build-time introspection (tools/gen_spec.py): the launch plan of model m as
  * ints — [nvp, model sizes (MJH_MODEL_SIZES order), per-world layout, model
@@ -158,6 +162,13 @@ int mjh_set_world_ordering(int on);
  * position stage in LDS never reuses (the call is accepted and ignored).
  * Returns mjh_split_step(). */
 int mjh_set_position_reuse(int on);
+
+/* Test / diagnostic: cap the constraint rows a one-world workgroup keeps in LDS
+ * (0, the default: as many as its LDS budget holds). A world with more rows runs
+ * the rest of its step with the row arrays in global scratch; the results are
+ * the same either way. A cap changes the launch plan, so the generic kernel
+ * instance runs. Applies to launches issued after the call. */
+int mjh_set_lds_row_cap(int rows);
 
 /* 1 if this build launches the step as two kernels (position, then velocity /
  * solver / integration), 0 for the single fused launch. */

@@ -1136,10 +1136,16 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     real improvement = scale * (old - cost), gradient = scale * sqrt(gn);
     int conv = improvement < m->tolerance || gradient < m->tolerance;
     if (g_dbg_conv && it < 15) {
-      real* cv = g_dbg_conv + ((size_t)w->wi * 15 + it) * 3;
+      real* cv = g_dbg_conv + ((size_t)w->wi * 15 + it) * 4;
+      real gm = 0;
+      for (int d = 0; d < nv; d++) {
+        const real t = fabs(w->Ma[d]) + fabs(w->qfrc_smooth[d]) + fabs(w->qfrc_constraint[d]);
+        gm += t * t;
+      }
       cv[0] = improvement;
       cv[1] = gradient;
       cv[2] = scale * (fabs(old) + fabs(cost));
+      cv[3] = scale * sqrt(gm);
     }
     w->conv = conv;
     if (!w->follow && conv) break;
@@ -1368,8 +1374,9 @@ static real* g_dbg_lsgap = NULL;
 static long long* g_dbg_lstrace = NULL;
 /* the solver's own discrete decisions (oracle_set_decisions), evaluated at every
    iteration also in follow mode: per world 15 x {improvement, gradient, the
-   scaled cost magnitude |old| + |cost|} (the convergence test's inputs, NaN
-   where no iteration ran), and {cost at qacc_warmstart, cost at qacc_smooth}
+   scaled cost magnitude |old| + |cost|, the scaled magnitude of the gradient's
+   terms |Ma| + |qfrc_smooth| + |qfrc_constraint|} (the convergence test's
+   inputs and their float32 resolution scales, NaN where no iteration ran), and {cost at qacc_warmstart, cost at qacc_smooth}
    (the warm-start comparison) */
 static real* g_dbg_conv = NULL;
 static real* g_dbg_warm = NULL;

@@ -97,9 +97,11 @@ class Oracle:
 
     Also returned: the solver's own decision inputs, evaluated at every
     iteration in follow mode too (the oracle never takes them from the device
-    for the check): ``solver_conv`` (nworld, 15, 3) = improvement, gradient
-    (both scaled by 1 / (meaninertia nv), the test is ``< tolerance``) and the
-    scaled cost magnitude |old| + |cost| per iteration (NaN where none ran), and
+    for the check): ``solver_conv`` (nworld, 15, 4) = improvement, gradient
+    (both scaled by 1 / (meaninertia nv), the test is ``< tolerance``), the
+    scaled cost magnitude |old| + |cost| and the scaled norm of the gradient's
+    terms' magnitudes |Ma| + |qfrc_smooth| + |qfrc_constraint| per iteration
+    (NaN where none ran), and
     ``warm_costs`` (nworld, 2) = the cost at qacc_warmstart and at qacc_smooth
     (the solve starts from qacc_smooth when the first is larger)."""
     if follow is not None:
@@ -130,7 +132,7 @@ class Oracle:
       out["efc_J"] = np.zeros((nworld, nj * nv), self.dtype)
     self.lib.oracle_set_debug(out["qM"].ctypes.data if debug else None, out["efc_J"].ctypes.data if debug else None,
                               out["ls_gap"].ctypes.data, out["ls_trace"].ctypes.data)
-    out["solver_conv"] = np.full((nworld, 15, 3), np.nan, self.dtype)
+    out["solver_conv"] = np.full((nworld, 15, 4), np.nan, self.dtype)
     out["warm_costs"] = np.full((nworld, 2), np.nan, self.dtype)
     self.lib.oracle_set_decisions(out["solver_conv"].ctypes.data, out["warm_costs"].ctypes.data)
     self.lib.oracle_set_follow(1 if follow is not None else 0)
