@@ -46,6 +46,7 @@ struct Layout {
   int J, ldj, efc_D, efc_R, efc_aref, efc_jaref, efc_jv, efc_force, efc_fl, efc_pos, efc_type, efc_id, efc_mask;
   int efc_h, arow, ash;
   int sidx;  // contact sensor: kept matches (contact index, ~index if flipped)
+  int cg_g, cg_mg;  // CG solver: the previous iteration's gradient and M^-1 gradient
   int red, ints;
   int total, gtotal;  // per-world words: LDS, global scratch
   int ncap, rcap;
@@ -61,6 +62,7 @@ struct Layout {
 };
 
 enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
+constexpr int kSolverCG = 1;  // mjtSolver: mjSOL_PGS 0, mjSOL_CG 1, mjSOL_NEWTON 2
 
 // Where each per-world array lives: LDS (fast, but it bounds how many worlds
 // share a CU) or the per-world global scratch (L1/L2-resident; coalesced since
@@ -88,7 +90,7 @@ enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
   X(con_imargin, 1) X(con_dim, 1) X(con_geom, 1) X(con_efcadr, 1)                                     \
   X(J, 0) X(efc_D, 0) X(efc_R, 0) X(efc_aref, 0) X(efc_jaref, 0) X(efc_jv, 0) X(efc_force, 0)        \
   X(efc_fl, 0) X(efc_pos, 1) X(efc_type, 0) X(efc_id, 1) X(efc_mask, 1) X(efc_h, 0) X(arow, 0)       \
-  X(ash, 0) X(sidx, 1)
+  X(ash, 0) X(sidx, 1) X(cg_g, 1) X(cg_mg, 1)
 struct Rg {
 #if MJH_PRESET == 0
 #define X_RG(name, r) static constexpr bool name = false;
@@ -565,6 +567,17 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
     }
 }
 
+// Loads in flight per unrolled row dot: at most MJH_DOT_CHUNK entries of each
+// operand are scheduled ahead (a scheduling barrier between chunks; 0: all of a
+// row at once). Four waves per SIMD hide the latency the chunks expose, and the
+// registers the whole-row form needs (two NVP-wide operands) do not fit 128.
+#ifndef MJH_DOT_CHUNK
+#define MJH_DOT_CHUNK 0
+#endif
+__device__ __forceinline__ void dot_chunk_barrier(int j) {
+  if (MJH_DOT_CHUNK > 0 && j > 0 && (j % (MJH_DOT_CHUNK > 0 ? MJH_DOT_CHUNK : 1)) == 0) __builtin_amdgcn_sched_barrier(0);
+}
+
 // dot of an aligned row with an aligned vector, fully unrolled to the padded
 // size NVP so all loads of a row are in flight at once (rows may live in L2);
 // vector entries >= n are masked (padding may hold garbage)
@@ -573,6 +586,7 @@ __device__ __forceinline__ float rowdot_u(const float* r, const float* x, int n)
   float s0 = 0.f, s1 = 0.f;
 #pragma unroll
   for (int j = 0; j < NVP; j += 4) {
+    dot_chunk_barrier(j);
     const float4 a = *reinterpret_cast<const float4*>(r + j);
     float4 b = *reinterpret_cast<const float4*>(x + j);
     if (j + 4 > n) {
@@ -593,6 +607,7 @@ __device__ __forceinline__ void rowdot2_u(const float* r, const float* x, const 
   float s0 = 0.f, s1 = 0.f, t0 = 0.f, t1 = 0.f;
 #pragma unroll
   for (int j = 0; j < NVP; j += 4) {
+    dot_chunk_barrier(j);
     const float4 a = *reinterpret_cast<const float4*>(r + j);
     float4 b = *reinterpret_cast<const float4*>(x + j);
     float4 c = *reinterpret_cast<const float4*>(y + j);
@@ -713,9 +728,7 @@ __device__ MJH_SOLVER_INLINE void ldl_solve_reg(const float* A, int n, int ld, f
   float a[NVP], c[NVP];
   wsync();
   load_row_lower<NVP, PK>(A, n, ld, a);  // L[i][k<i], D[i] at k == i
-  const int cl = lane < n ? lane : 0;
-#pragma unroll
-  for (int k = 0; k < NVP; k++) c[k] = A[lofs<PK>(k < n ? k : 0, ld) + cl];  // column i: L[k][i] (used for k > i)
+  int cl = lane < n ? lane : 0;
   float xi = lane < n ? x[lane] : 0.f;
   float di = 1.f;
 #pragma unroll
@@ -724,6 +737,12 @@ __device__ MJH_SOLVER_INLINE void ldl_solve_reg(const float* A, int n, int ld, f
     xi -= (lane > k ? a[k] : 0.f) * xk;
     di = lane == k ? a[k] : di;
   }
+  // the column loads wait until the row is dead (an opaque column index keeps
+  // the compiler from hoisting them above the forward sweep): NVP live values
+  // instead of 2 NVP
+  asm volatile("" : "+v"(cl));
+#pragma unroll
+  for (int k = 0; k < NVP; k++) c[k] = A[lofs<PK>(k < n ? k : 0, ld) + cl];  // column i: L[k][i] (used for k > i)
   xi = lane < n ? xi / di : 0.f;
 #pragma unroll
   for (int k = NVP - 1; k > 0; k--) {
@@ -2351,6 +2370,43 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       wsync();
     };
 
+    // CG (opt.solver == mjSOL_CG): MuJoCo's primal solver with the search
+    // direction from M instead of the Hessian (engine_solver.c mj_solPrimal,
+    // MuJoCo Warp solver.py): Mgrad = M^-1 grad through M's factor (still in
+    // Lm: CG never builds a Hessian), the first search -Mgrad, later ones
+    // Polak-Ribiere: search = -Mgrad + max(0, beta) search with beta =
+    // grad.(Mgrad - Mgrad_old) / max(mjMINVAL, grad_old.Mgrad_old)
+    const bool use_cg = m.solver == kSolverCG;
+    float* const Mgrad = tmp;
+    float* const cg_g = SP(cg_g);
+    float* const cg_mg = SP(cg_mg);
+    auto cg_direction = [&](bool first) {
+      for (int i = tid; i < nv; i += NT) Mgrad[i] = grad[i];
+      ldl_solve_reg<NVP, PKL>(MODE == 2 ? G + Lo.h_L : Lm, nv, ldm, Mgrad);  // M's factor
+      float num = 0.f, den = 0.f;
+      if (!first) {
+        for (int i = tid; i < nv; i += NT) {
+          num += grad[i] * (Mgrad[i] - cg_mg[i]);
+          den += cg_g[i] * cg_mg[i];
+        }
+        bsum2<NT>(num, den, red);
+      }
+      const float beta = first ? 0.f : fmaxf(0.f, num / fmaxf(MJH_MINVAL, den));
+      for (int i = tid; i < nv; i += NT) {
+        const float mg = Mgrad[i];
+        search[i] = first ? -mg : -mg + beta * search[i];
+        cg_g[i] = grad[i];
+        cg_mg[i] = mg;
+      }
+      wsync();
+    };
+    auto direction = [&](bool first) {
+      if (use_cg)
+        cg_direction(first);
+      else
+        newton_direction();
+    };
+
     // warm start: the cheaper of qacc_warmstart and qacc_smooth, both
     // evaluated in one pass over M's and J's rows (each row loaded once; the
     // qacc_smooth values wait in Mv / jv in case they win)
@@ -2384,7 +2440,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     }
     wsync();
     gradient();
-    newton_direction();
+    direction(true);
 
     for (int it = 0; it < m.iterations; it++) {
       unsigned long long t_ls = PROF_NOW();
@@ -2543,7 +2599,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       // (MuJoCo / MuJoCo Warp compute it before the test; nothing reads it after)
       if (it + 1 >= m.iterations) break;
       unsigned long long t_nd = PROF_NOW();
-      newton_direction();
+      direction(false);
       PROF_ACC(14, t_nd);
     }
   }
@@ -3292,6 +3348,7 @@ Layout make_layout(const mjh_model* m, int budget, int wpb) {
   TAKER(efc_h, 0); TAKER(arow, 4); TAKER(ash, 4);
 #undef TAKER
   TAKE(sidx, 64);
+  TAKE(cg_g, nvv); TAKE(cg_mg, nvv);
 #undef TAKE
   L.total = al(off);
   // split-step handoff (global scratch): the factor of M, the rows' position

@@ -55,8 +55,8 @@ class MujocoCfg:
   def apply(self, model: Model) -> None:
     if self.cone != "pyramidal":
       raise NotImplementedError("only pyramidal friction cones are implemented")
-    if self.solver != "newton":
-      raise NotImplementedError("only the Newton solver is implemented")
+    if self.solver == "pgs":
+      raise NotImplementedError("the PGS solver is not implemented (Newton and CG are)")
     model.cone = _CONES[self.cone]
     model.solver = _SOLVERS[self.solver]
     model.jacobian = {"dense": 0, "sparse": 1, "auto": 2}[self.jacobian]

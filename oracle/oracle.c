@@ -153,7 +153,7 @@ typedef struct {
   real *gxpos, *gxmat, *sxpos, *sxmat;
   real *M, *LD, *H, *qvel, *qpos, *qacc, *qacc_smooth, *qfrc_smooth, *qfrc_bias, *qfrc_passive,
       *qfrc_actuator, *qfrc_constraint, *act_force, *act_length, *act_vel, *tmpv, *tmpv2, *grad, *search,
-      *Ma, *Mv, *Mgrad, *qacc_int;
+      *Ma, *Mv, *Mgrad, *qacc_int, *cg_g, *cg_mg;
   real *J, *efc_pos, *efc_margin, *efc_D, *efc_R, *efc_aref, *efc_fl, *jaref, *jv, *efc_force;
   int *efc_type, *efc_id;
   int nefc, ncon, flags, niter;
@@ -183,7 +183,7 @@ static void ws_alloc(ws_t* w, const or_model* m) {
   AR(qacc_smooth, nv); AR(qfrc_smooth, nv); AR(qfrc_bias, nv); AR(qfrc_passive, nv); AR(qfrc_actuator, nv);
   AR(qfrc_constraint, nv); AR(act_force, m->nu); AR(act_length, m->nu); AR(act_vel, m->nu);
   AR(tmpv, nv); AR(tmpv2, nv); AR(grad, nv); AR(search, nv); AR(Ma, nv); AR(Mv, nv); AR(Mgrad, nv);
-  AR(qacc_int, nv);
+  AR(qacc_int, nv); AR(cg_g, nv); AR(cg_mg, nv);
   AR(J, (size_t)m->njmax * nv); AR(efc_pos, m->njmax); AR(efc_margin, m->njmax); AR(efc_D, m->njmax);
   AR(efc_R, m->njmax); AR(efc_aref, m->njmax); AR(efc_fl, m->njmax); AR(jaref, m->njmax); AR(jv, m->njmax);
   AR(efc_force, m->njmax);
@@ -199,7 +199,7 @@ static void ws_free(ws_t* w) {
                    &w->sxpos, &w->sxmat, &w->M, &w->LD, &w->H, &w->qvel, &w->qpos, &w->qacc, &w->qacc_smooth,
                    &w->qfrc_smooth, &w->qfrc_bias, &w->qfrc_passive, &w->qfrc_actuator, &w->qfrc_constraint,
                    &w->act_force, &w->act_length, &w->act_vel, &w->tmpv, &w->tmpv2, &w->grad, &w->search, &w->Ma,
-                   &w->Mv, &w->Mgrad, &w->qacc_int, &w->J, &w->efc_pos, &w->efc_margin, &w->efc_D, &w->efc_R,
+                   &w->Mv, &w->Mgrad, &w->qacc_int, &w->cg_g, &w->cg_mg, &w->J, &w->efc_pos, &w->efc_margin, &w->efc_D, &w->efc_R,
                    &w->efc_aref, &w->efc_fl, &w->jaref, &w->jv, &w->efc_force};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); i++) free(*ptrs[i]);
   free(w->efc_type);
@@ -964,6 +964,40 @@ static void newton_direction(const or_model* m, ws_t* w) {
   for (int d = 0; d < nv; d++) w->search[d] = -w->Mgrad[d];
 }
 
+/* CG (opt.solver == mjSOL_CG): MuJoCo's primal solver with the search
+   direction from M instead of the Hessian (engine_solver.c mj_solPrimal,
+   restated; MuJoCo Warp solver.py): Mgrad = M^-1 grad from M's factor, the
+   first search -Mgrad, later ones Polak-Ribiere: search = -Mgrad + max(0, beta)
+   search, beta = grad.(Mgrad - Mgrad_old) / max(mjMINVAL, grad_old.Mgrad_old) */
+static void cg_direction(const or_model* m, ws_t* w, int first) {
+  int nv = m->nv;
+  for (int d = 0; d < nv; d++) w->grad[d] = w->Ma[d] - w->qfrc_smooth[d] - w->qfrc_constraint[d];
+  memcpy(w->Mgrad, w->grad, sizeof(real) * nv);
+  solve_tree(m, w->LD, w->Mgrad);
+  real beta = 0;
+  if (!first) {
+    real num = 0, den = 0;
+    for (int d = 0; d < nv; d++) {
+      num += w->grad[d] * (w->Mgrad[d] - w->cg_mg[d]);
+      den += w->cg_g[d] * w->cg_mg[d];
+    }
+    beta = num / (den > 1e-15 ? den : (real)1e-15);
+    if (beta < 0) beta = 0;
+  }
+  for (int d = 0; d < nv; d++) {
+    w->search[d] = first ? -w->Mgrad[d] : -w->Mgrad[d] + beta * w->search[d];
+    w->cg_g[d] = w->grad[d];
+    w->cg_mg[d] = w->Mgrad[d];
+  }
+}
+
+static void direction(const or_model* m, ws_t* w, int first) {
+  if (m->solver == 1)
+    cg_direction(m, w, first);
+  else
+    newton_direction(m, w);
+}
+
 /* exact line search on the convex piecewise-quadratic cost along search */
 static real linesearch(const or_model* m, ws_t* w) {
   int nv = m->nv;
@@ -1117,7 +1151,7 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     }
     cost = update_constraint(m, w, w->qacc_smooth);
   }
-  newton_direction(m, w);
+  direction(m, w, 1);
   for (int it = 0; it < m->iterations; it++) {
     if (w->follow && it >= w->fniter) break;
     real alpha = linesearch(m, w);
@@ -1129,7 +1163,7 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     for (int r = 0; r < w->nefc; r++) w->jaref[r] += alpha * w->jv[r];
     real old = cost;
     cost = update_constraint(m, w, w->qacc_smooth);
-    newton_direction(m, w);
+    direction(m, w, 0);
     w->niter++;
     real gn = 0;
     for (int d = 0; d < nv; d++) gn += w->grad[d] * w->grad[d];

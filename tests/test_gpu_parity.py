@@ -376,8 +376,58 @@ def test_rows_in_global_scratch_are_bit_identical():
     native.lib().mjh_set_lds_row_cap(0)
   a, b = outs
   assert (a["nefc"] > 8).mean() > 0.5  # most worlds took the global-scratch path
+  diffs = {}
   for k in ("qpos", "qvel", "qacc", "qfrc_constraint", "efc_force", "efc_D", "efc_aref", "sensordata", "nefc", "solver_niter",
             "solver_lstrace"):
-    assert np.array_equal(a[k], b[k]), k
+    d = np.abs(a[k].astype(np.float64) - b[k].astype(np.float64)).max(axis=1)
+    if (d > 0).any():
+      diffs[k] = (int((d > 0).sum()), float(d.max()), [int(w) for w in np.nonzero(d)[0][:6]])
+  print("[rows in global scratch] differing fields (worlds, max |d|, first worlds):", diffs)
+  assert not diffs, diffs
   ref = Oracle(m).run(n, st, integrate=True, follow=a)
   assert_parity(a, ref, n)
+
+
+@pytest.mark.parametrize("ls_parallel", [True, False])
+def test_cg_solver_parity(ls_parallel):
+  """opt.solver = CG (the reference's own test pipes solver="cg",
+  test_sim.py:43-82; MuJoCo Warp implements it): Polak-Ribiere directions from
+  M's factor, the same line searches and stop test as Newton, against the
+  oracle running CG (follow mode for the parallel search). 50 iterations: CG's
+  first-order directions converge more slowly than Newton's."""
+  n = 256
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(41))
+  cfg = dict(CFG, mujoco=MujocoCfg(timestep=0.005, iterations=50, ls_iterations=20, solver="cg"))
+  sim = Simulation(n, SimulationCfg(**cfg, ls_parallel=ls_parallel), m, DEV)
+  assert m.solver == 1 and m.ls_parallel == int(ls_parallel)
+  put(sim, st)
+  sim.step()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=True, follow=got if ls_parallel else None)
+  rep = assert_parity(got, ref, n, tag=f" cg ls_parallel={ls_parallel}")
+  print("[cg] mean iterations", float(got["solver_niter"].mean()), rep["decisions"].get("niter_differs"))
+  if ls_parallel:
+    it = check_iteration_counts(got, m, st, True)
+    print(f"[iterations cg] {it}")
+    assert it["ok"], it
+
+
+def test_converged_cg_solver_parity():
+  """CG with the iteration cap lifted reaches the qacc of the float64 oracle's
+  converged Newton solve (the minimiser does not depend on the method)."""
+  n = 256
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(43))
+  cfg = dict(CFG, mujoco=MujocoCfg(timestep=0.005, iterations=300, ls_iterations=50, tolerance=1e-10, solver="cg"))
+  sim = Simulation(n, SimulationCfg(**cfg, ls_parallel=False), m, DEV)
+  put(sim, st)
+  sim.forward()
+  got = get(sim, n)
+  m.solver = 2  # the oracle's Newton solve: the same minimiser
+  ref = Oracle(m).run(n, st, integrate=False)
+  ref["f32"] = Oracle(m, "f32").run(n, st, integrate=False)
+  rep = compare_step(got, ref, solve_rel=3e-4, solve_frac=1.0, solve_max=3e-4)
+  print("[converged cg]", {k: f"{v:.2e}" for k, v in rep["maxerr"].items() if "/" in k},
+        "mean iterations", float(got["solver_niter"].mean()))
+  assert not rep["failures"], rep["failures"]

@@ -311,3 +311,24 @@ def test_block_on_incline_stick_slip_threshold(tan_theta, slides):
     assert a == pytest.approx(g * (np.sin(th) - mu * np.cos(th)), rel=0.05)
   else:
     assert abs(vx[-1]) < 5e-3 and abs(st["qpos"][0, 0]) < 5e-3
+
+
+def test_cg_and_newton_reach_the_same_minimiser():
+  """CG (opt.solver = mjSOL_CG, Polak-Ribiere on the M-preconditioned
+  gradient) and Newton minimise the same convex cost, so with the iteration cap
+  lifted (float64 oracle, exact line search) both reach the same qacc; CG takes
+  more iterations (first-order directions)."""
+  from tests.scenes import random_states
+
+  n = 16
+  m = g1_scene_model(n)
+  m.iterations, m.tolerance, m.ls_iterations, m.ls_parallel = 300, 1e-14, 50, 0
+  st = random_states(m, n, np.random.default_rng(31))
+  m.solver = 2
+  newton = Oracle(m).run(n, st, integrate=False)
+  m.solver = 1
+  cg = Oracle(m).run(n, st, integrate=False)
+  assert (newton["nefc"] > 0).mean() > 0.8
+  scale = 1 + np.abs(newton["qacc"]).max(axis=1, keepdims=True)
+  assert (np.abs(cg["qacc"] - newton["qacc"]) / scale).max() < 1e-6
+  assert cg["solver_niter"].mean() > newton["solver_niter"].mean()

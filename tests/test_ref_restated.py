@@ -750,27 +750,26 @@ SIM_ROBOT_XML = """
   </body>
 </worldbody></mujoco>"""
 
-MJ_INT_EULER, MJ_SOL_NEWTON = 0, 2
+MJ_INT_EULER, MJ_SOL_CG = 0, 1
 
 
 def test_simulation_config_is_piped(backend):
-  """test_sim.py:43-82. The reference pipes ``solver="cg"``; this build
-  implements the Newton solver only, so the same test runs with Newton and a
-  second block checks that CG is refused rather than silently replaced."""
+  """test_sim.py:43-82, as the reference writes it (solver="cg"); the PGS
+  solver is refused rather than silently replaced."""
   model = compile_spec(read_mjcf_string(SIM_ROBOT_XML))
   cfg = SimulationCfg(contact_sensor_maxmatch=128, ls_parallel=False,
-                      mujoco=MujocoCfg(timestep=0.02, integrator="euler", solver="newton", iterations=7,
+                      mujoco=MujocoCfg(timestep=0.02, integrator="euler", solver="cg", iterations=7,
                                        ls_iterations=14, gravity=(0, 0, 7.5)))
   sim = make_sim(1, cfg, model, backend)
   assert sim.mj_model.opt.timestep == cfg.mujoco.timestep
   assert sim.mj_model.opt.integrator == MJ_INT_EULER
-  assert sim.mj_model.opt.solver == MJ_SOL_NEWTON
+  assert sim.mj_model.opt.solver == MJ_SOL_CG
   assert sim.mj_model.opt.iterations == cfg.mujoco.iterations
   assert tuple(sim.mj_model.opt.gravity) == cfg.mujoco.gravity
   np.testing.assert_almost_equal(sim.model.opt.timestep[0].cpu().numpy(), cfg.mujoco.timestep)
   np.testing.assert_almost_equal(sim.model.opt.gravity[0].cpu().numpy(), cfg.mujoco.gravity)
   assert sim.model.opt.integrator == MJ_INT_EULER
-  assert sim.model.opt.solver == MJ_SOL_NEWTON
+  assert sim.model.opt.solver == MJ_SOL_CG
   assert sim.model.opt.iterations == cfg.mujoco.iterations
   assert sim.wp_model.opt.contact_sensor_maxmatch == cfg.contact_sensor_maxmatch
   assert sim.wp_model.opt.ls_parallel == cfg.ls_parallel
@@ -778,7 +777,7 @@ def test_simulation_config_is_piped(backend):
   sim.step()
   assert abs(float(sim.data.qvel[0, 2]) - 7.5 * 0.02) < 1e-5
   with pytest.raises(NotImplementedError):
-    make_sim(1, SimulationCfg(mujoco=MujocoCfg(solver="cg")), compile_spec(read_mjcf_string(SIM_ROBOT_XML)), backend)
+    make_sim(1, SimulationCfg(mujoco=MujocoCfg(solver="pgs")), compile_spec(read_mjcf_string(SIM_ROBOT_XML)), backend)
 
 
 # ---------------------------------------------------------------------------
