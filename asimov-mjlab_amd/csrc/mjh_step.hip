@@ -814,9 +814,292 @@ __device__ __forceinline__ int plane_sphere(Con* c, float margin, const float* p
   return 1;
 }
 
-// Narrowphase for one pair (types ascending). Up to 4 contacts.
+// ---- box pairs (sphere-box, capsule-box, box-box): the oracle's algorithms
+// (oracle/oracle.c raw_sphere_box / raw_capsule_box / raw_box_box) in float32.
+// Boxes: centre bp, rotation bm (row-major, column k = axis k), half sizes bs.
+__device__ __forceinline__ void to_box(const float* bp, const float* bm, const float* p, float* o) {
+  const float d[3] = {p[0] - bp[0], p[1] - bp[1], p[2] - bp[2]};
+#pragma unroll
+  for (int k = 0; k < 3; k++) o[k] = bm[k] * d[0] + bm[3 + k] * d[1] + bm[6 + k] * d[2];
+}
+__device__ __forceinline__ void from_box(const float* bm, const float* v, float* o) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) o[k] = bm[3 * k] * v[0] + bm[3 * k + 1] * v[1] + bm[3 * k + 2] * v[2];
+}
+
+// sphere (geom1) - box (geom2): the box point nearest the centre; a centre
+// inside leaves through the nearest face (MuJoCo Warp sphere_box)
+__device__ __noinline__ int sphere_box(Con* c, float margin, const float* sp, float r, const float* bp, const float* bm,
+                                       const float* bs) {
+  float lc[3], cl[3], dif[3];
+  to_box(bp, bm, sp, lc);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    cl[k] = clampf(lc[k], -bs[k], bs[k]);
+    dif[k] = cl[k] - lc[k];
+  }
+  const float dist = sqrtf(dot3(dif, dif));
+  if (dist - r > margin) return 0;
+  float nl[3] = {0.f, 0.f, 0.f}, pl[3];
+  if (dist <= MJH_MINVAL) {
+    float closest = 2.f * (bs[0] + bs[1] + bs[2]);
+    int kf = 0;
+    for (int i = 0; i < 6; i++) {
+      const float fd = fabsf((i & 1 ? 1.f : -1.f) * bs[i >> 1] - lc[i >> 1]);
+      if (closest > fd) { closest = fd; kf = i; }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) nl[k] = k == (kf >> 1) ? (kf & 1 ? -1.f : 1.f) : 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) pl[k] = lc[k] + nl[k] * (r - closest) * 0.5f;
+    c->dist = -closest - r;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; k++) nl[k] = dif[k] / dist;
+#pragma unroll
+    for (int k = 0; k < 3; k++) pl[k] = 0.5f * (cl[k] + lc[k] + nl[k] * r);
+    c->dist = dist - r;
+  }
+  float pw[3], nw[3];
+  from_box(bm, pl, pw);
+  from_box(bm, nl, nw);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    c->pos[k] = bp[k] + pw[k];
+    c->frame[k] = nw[k];
+    c->frame[3 + k] = 0.f;
+  }
+  return 1;
+}
+
+__device__ __forceinline__ float box_sdf(const float* bs, const float* q) {
+  float out = 0.f, in = -1e30f;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float o = fabsf(q[k]) - bs[k], e = fmaxf(o, 0.f);
+    out += e * e;
+    in = fmaxf(in, o);
+  }
+  return out > 0.f ? sqrtf(out) : in;
+}
+
+// capsule (geom1) - box (geom2): both segment ends as spheres when both touch,
+// otherwise one sphere at the segment point nearest the box (golden section on
+// the convex signed distance, 40 steps)
+__device__ __noinline__ int capsule_box(Con* out, float margin, const float* cp, const float* ax, float h, float r,
+                                        const float* bp, const float* bm, const float* bs) {
+  float a[3], b[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { a[k] = cp[k] + ax[k] * h; b[k] = cp[k] - ax[k] * h; }
+  Con ca, cb;
+  const int na = sphere_box(&ca, margin, a, r, bp, bm, bs), nb = sphere_box(&cb, margin, b, r, bp, bm, bs);
+  if (na && nb) {
+    out[0] = ca;
+    out[1] = cb;
+#pragma unroll
+    for (int k = 0; k < 3; k++) { out[0].frame[3 + k] = ax[k]; out[1].frame[3 + k] = ax[k]; }
+    return 2;
+  }
+  float la[3], lb[3], q[3];
+  to_box(bp, bm, a, la);
+  to_box(bp, bm, b, lb);
+  const float g = 0.6180339887498949f;
+  float lo = 0.f, hi = 1.f, x1 = hi - g * (hi - lo), x2 = lo + g * (hi - lo);
+#pragma unroll
+  for (int k = 0; k < 3; k++) q[k] = la[k] + (lb[k] - la[k]) * x1;
+  float f1 = box_sdf(bs, q);
+#pragma unroll
+  for (int k = 0; k < 3; k++) q[k] = la[k] + (lb[k] - la[k]) * x2;
+  float f2 = box_sdf(bs, q);
+  for (int it = 0; it < 40; it++) {
+    if (f1 <= f2) {
+      hi = x2; x2 = x1; f2 = f1; x1 = hi - g * (hi - lo);
+#pragma unroll
+      for (int k = 0; k < 3; k++) q[k] = la[k] + (lb[k] - la[k]) * x1;
+      f1 = box_sdf(bs, q);
+    } else {
+      lo = x1; x1 = x2; f1 = f2; x2 = lo + g * (hi - lo);
+#pragma unroll
+      for (int k = 0; k < 3; k++) q[k] = la[k] + (lb[k] - la[k]) * x2;
+      f2 = box_sdf(bs, q);
+    }
+  }
+  const float t = 0.5f * (lo + hi);
+  float p[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) p[k] = a[k] + (b[k] - a[k]) * t;
+  const int n = sphere_box(out, margin, p, r, bp, bm, bs);
+  if (n) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) out[0].frame[3 + k] = ax[k];
+  }
+  return n;
+}
+
+// box (geom1) - box (geom2): separating axes (face axes preferred within 5 %),
+// face: incident face clipped against the reference face's side planes (the
+// deepest point, then up to 3 more, each farthest from those kept); edge-edge:
+// closest points of the two support edges
+__device__ __noinline__ int box_box(Con* out, float margin, const float* pa, const float* ma, const float* sa, const float* pb,
+                                    const float* mb, const float* sb) {
+  float A[3][3], B[3][3];
+  const float d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) { A[i][k] = ma[3 * k + i]; B[i][k] = mb[3 * k + i]; }
+  float best = 1e30f, bn[3] = {0.f, 0.f, 0.f};
+  int bk = -1;
+  for (int k = 0; k < 15; k++) {
+    float L[3];
+    if (k < 3) { L[0] = A[k][0]; L[1] = A[k][1]; L[2] = A[k][2]; }
+    else if (k < 6) { L[0] = B[k - 3][0]; L[1] = B[k - 3][1]; L[2] = B[k - 3][2]; }
+    else cross3(L, A[(k - 6) / 3], B[(k - 6) % 3]);
+    const float ln = sqrtf(dot3(L, L));
+    if (ln < 1e-6f) continue;
+    for (int q = 0; q < 3; q++) L[q] /= ln;
+    float ra = 0.f, rb = 0.f;
+    for (int i = 0; i < 3; i++) { ra += sa[i] * fabsf(dot3(A[i], L)); rb += sb[i] * fabsf(dot3(B[i], L)); }
+    const float dl = dot3(d, L), ov = ra + rb - fabsf(dl);
+    if (ov < -margin) return 0;
+    const float score = k < 6 ? ov : ov * 1.05f + 1e-9f;
+    if (score < best) {
+      best = score;
+      bk = k;
+      for (int q = 0; q < 3; q++) bn[q] = dl < 0.f ? -L[q] : L[q];
+    }
+  }
+  if (bk < 0) return 0;
+  if (bk < 6) {
+    const bool refA = bk < 3;
+    const float *rp = refA ? pa : pb, *ip = refA ? pb : pa, *rs = refA ? sa : sb, *is = refA ? sb : sa;
+    float R[3][3], I[3][3];
+    for (int i = 0; i < 3; i++)
+      for (int k = 0; k < 3; k++) { R[i][k] = refA ? A[i][k] : B[i][k]; I[i][k] = refA ? B[i][k] : A[i][k]; }
+    float nr[3];
+    for (int q = 0; q < 3; q++) nr[q] = refA ? bn[q] : -bn[q];
+    const int ra = refA ? bk : bk - 3;
+    int ia = 0;
+    float mx = -1.f;
+    for (int i = 0; i < 3; i++) {
+      const float v = fabsf(dot3(I[i], nr));
+      if (v > mx) { mx = v; ia = i; }
+    }
+    const float isg = dot3(I[ia], nr) > 0.f ? -1.f : 1.f;
+    float fc[3];
+    for (int q = 0; q < 3; q++) fc[q] = ip[q] + I[ia][q] * is[ia] * isg;
+    const int u = (ia + 1) % 3, v = (ia + 2) % 3;
+    float poly[16][3], tmpp[16][3];
+    int np = 4;
+    for (int c = 0; c < 4; c++) {
+      const float su = (c == 0 || c == 3) ? 1.f : -1.f, sv = (c < 2) ? 1.f : -1.f;
+      for (int q = 0; q < 3; q++) poly[c][q] = fc[q] + I[u][q] * is[u] * su + I[v][q] * is[v] * sv;
+    }
+    for (int e = 0; e < 4 && np > 0; e++) {
+      const int axis = e < 2 ? (ra + 1) % 3 : (ra + 2) % 3;
+      const float sg = (e & 1) ? -1.f : 1.f;
+      const float off = dot3(R[axis], rp) * sg + rs[axis];
+      int nn = 0;
+      for (int i = 0; i < np; i++) {
+        const float* P = poly[i];
+        const float* Q = poly[(i + 1) % np];
+        const float dp = sg * dot3(R[axis], P) - off, dq = sg * dot3(R[axis], Q) - off;
+        if (dp <= 0.f) { for (int q = 0; q < 3; q++) tmpp[nn][q] = P[q]; nn++; }
+        if ((dp <= 0.f) != (dq <= 0.f)) {
+          const float t = dp / (dp - dq);
+          for (int q = 0; q < 3; q++) tmpp[nn][q] = P[q] + (Q[q] - P[q]) * t;
+          nn++;
+        }
+      }
+      np = nn;
+      for (int i = 0; i < nn; i++)
+        for (int q = 0; q < 3; q++) poly[i][q] = tmpp[i][q];
+    }
+    const float rfc = dot3(nr, rp) + rs[ra] * fabsf(dot3(R[ra], nr));
+    float dep[16];
+    int keep[16], nk = 0;
+    for (int i = 0; i < np; i++) {
+      dep[i] = dot3(nr, poly[i]) - rfc;
+      if (dep[i] <= margin) keep[nk++] = i;
+    }
+    if (nk == 0) return 0;
+    int sel[4], ns = 0, di = keep[0];
+    for (int j = 1; j < nk; j++) if (dep[keep[j]] < dep[di]) di = keep[j];
+    sel[ns++] = di;
+    while (ns < 4 && ns < nk) {
+      int bj = -1;
+      float bd = -1.f;
+      for (int j = 0; j < nk; j++) {
+        const int i = keep[j];
+        bool used = false;
+        float md = 1e30f;
+        for (int s2 = 0; s2 < ns; s2++) {
+          if (sel[s2] == i) used = true;
+          const float dd[3] = {poly[i][0] - poly[sel[s2]][0], poly[i][1] - poly[sel[s2]][1], poly[i][2] - poly[sel[s2]][2]};
+          md = fminf(md, sqrtf(dot3(dd, dd)));
+        }
+        if (!used && md > bd) { bd = md; bj = i; }
+      }
+      if (bj < 0) break;
+      sel[ns++] = bj;
+    }
+    for (int i = 0; i < ns; i++) {
+      Con* c = out + i;
+      c->dist = dep[sel[i]];
+      for (int q = 0; q < 3; q++) {
+        c->pos[q] = poly[sel[i]][q] - nr[q] * 0.5f * c->dist;
+        c->frame[q] = bn[q];
+        c->frame[3 + q] = 0.f;
+      }
+    }
+    return ns;
+  }
+  const int ai = (bk - 6) / 3, bj = (bk - 6) % 3;
+  float ca[3] = {pa[0], pa[1], pa[2]}, cb[3] = {pb[0], pb[1], pb[2]};
+  for (int i = 0; i < 3; i++) {
+    if (i != ai) {
+      const float sg = dot3(A[i], bn) > 0.f ? 1.f : -1.f;
+      for (int q = 0; q < 3; q++) ca[q] += A[i][q] * sa[i] * sg;
+    }
+    if (i != bj) {
+      const float sg = dot3(B[i], bn) > 0.f ? -1.f : 1.f;
+      for (int q = 0; q < 3; q++) cb[q] += B[i][q] * sb[i] * sg;
+    }
+  }
+  const float w0[3] = {ca[0] - cb[0], ca[1] - cb[1], ca[2] - cb[2]};
+  const float aa = dot3(A[ai], A[ai]), ab = dot3(A[ai], B[bj]), bb = dot3(B[bj], B[bj]);
+  const float da = dot3(A[ai], w0), db = dot3(B[bj], w0), den = aa * bb - ab * ab;
+  float s = den > 1e-12f ? (ab * db - bb * da) / den : 0.f;
+  s = clampf(s, -sa[ai], sa[ai]);
+  float t = clampf((ab * s + db) / bb, -sb[bj], sb[bj]);
+  s = clampf((ab * t - da) / aa, -sa[ai], sa[ai]);
+  float p1[3], p2[3];
+  for (int q = 0; q < 3; q++) { p1[q] = ca[q] + A[ai][q] * s; p2[q] = cb[q] + B[bj][q] * t; }
+  const float dd[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  const float dist = dot3(dd, bn);
+  if (dist > margin) return 0;
+  out[0].dist = dist;
+  for (int q = 0; q < 3; q++) {
+    out[0].pos[q] = 0.5f * (p1[q] + p2[q]);
+    out[0].frame[q] = bn[q];
+    out[0].frame[3 + q] = 0.f;
+  }
+  return 1;
+}
+
+// Narrowphase for one pair (types ascending). Up to 4 contacts. `boxes`: the
+// model has pairs that need the box functions (Sizes::nboxpair; a compile-time
+// 0 in the model-specialised instances of models without such pairs, whose
+// code then carries none of them).
 __device__ MJH_COLL_INLINE int narrowphase(int t1, int t2, const float* p1, const float* m1, const float* s1, const float* p2,
-                           const float* m2, const float* s2, float margin, Con* out) {
+                           const float* m2, const float* s2, float margin, Con* out, bool boxes) {
+  if (boxes && t2 == 6 && t1 >= 2) {
+    if (t1 == 2) return sphere_box(out, margin, p1, s1[0], p2, m2, s2);
+    if (t1 == 3) {
+      const float ax[3] = {m1[2], m1[5], m1[8]};
+      return capsule_box(out, margin, p1, ax, s1[1], s1[0], p2, m2, s2);
+    }
+    if (t1 == 6) return box_box(out, margin, p1, m1, s1, p2, m2, s2);
+    return 0;
+  }
   if (t1 == 0 && t2 == 2) return plane_sphere(out, margin, p1, m1, p2, s2[0]);
   if (t1 == 0 && t2 == 3) {
     float ax[3] = {m2[2], m2[5], m2[8]};
@@ -1650,7 +1933,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         } else {
           near = sqrtf(dot3(dif, dif)) <= margin + IMG_F(geom_rbound)[g1] + IMG_F(geom_rbound)[g2];
         }
-        if (near) n = narrowphase(t1, t2, p1, m1, IMG_F(geom_size) + 3 * g1, p2, m2, IMG_F(geom_size) + 3 * g2, margin, cc);
+        if (near)
+          n = narrowphase(t1, t2, p1, m1, IMG_F(geom_size) + 3 * g1, p2, m2, IMG_F(geom_size) + 3 * g2, margin, cc,
+                          Z.nboxpair > 0);
       }
       int total;
       const int off = bscan<NT>(n, &total, redi);

@@ -32,7 +32,9 @@ from mjlab_amd.spec.spec import GEOM_TYPES, JOINT_TYPES, Spec
 from mjlab_amd.utils import rot
 
 MINVAL = 1e-15
-SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3)}
+SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3), (2, 6), (3, 6), (6, 6)}
+# pairs that need the box narrowphase functions (Model.nboxpair counts them)
+BOX_PAIRS = {(2, 6), (3, 6), (6, 6)}
 
 # Sensor type codes used by the kernels (order is ours; names follow mjtSensor).
 SENSOR_TYPES = {
@@ -746,7 +748,8 @@ def _compile_pairs(m: Model, spec: Spec) -> None:
       colgeoms.add(g1)
       colgeoms.add(g2)
   # geom-type pairs with a narrowphase in the HIP step (and the oracle):
-  # plane-{sphere,capsule,box}, sphere-{sphere,capsule}, capsule-capsule.
+  # plane-{sphere,capsule,box}, sphere-{sphere,capsule,box}, capsule-{capsule,box},
+  # box-box.
   # Other pairs stay in the table (the kernels return no contact for them)
   # and are reported here instead of being silently ignored.
   unsupported = sorted({(int(m.geom_type[a]), int(m.geom_type[b])) for a, b in pairs
@@ -757,6 +760,7 @@ def _compile_pairs(m: Model, spec: Spec) -> None:
     warnings.warn("collision pairs without a narrowphase on the HIP path (no contacts are generated): "
                   + ", ".join(f"{inv[a]}-{inv[b]}" for a, b in unsupported), UserWarning, stacklevel=3)
   m.npair = len(pairs)
+  m.nboxpair = sum(1 for a, b in pairs if (int(m.geom_type[a]), int(m.geom_type[b])) in BOX_PAIRS)
   m.pair_geom1 = np.array([p[0] for p in pairs] or [0], np.int32)
   m.pair_geom2 = np.array([p[1] for p in pairs] or [0], np.int32)
   cg = sorted(colgeoms)

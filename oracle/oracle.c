@@ -594,6 +594,271 @@ static int raw_plane_sphere(contact_t* c, real margin, const real pp[3], const r
   return 1;
 }
 
+/* ---- box pairs (sphere-box, capsule-box, box-box). Boxes: centre bp,
+   rotation bm (row-major, column k = axis k), half sizes bs. Normals point from
+   geom1 to geom2 (pairs are ordered by type, so the box is geom2 except in
+   box-box). The kernel (csrc/mjh_step.hip, box_* functions) runs the same
+   algorithms in float32. */
+static void to_box(const real bp[3], const real bm[9], const real p[3], real out[3]) {
+  real d[3] = {p[0] - bp[0], p[1] - bp[1], p[2] - bp[2]};
+  for (int k = 0; k < 3; k++) out[k] = bm[k] * d[0] + bm[3 + k] * d[1] + bm[6 + k] * d[2];
+}
+static void from_box(const real bm[9], const real v[3], real out[3]) {
+  for (int k = 0; k < 3; k++) out[k] = bm[3 * k] * v[0] + bm[3 * k + 1] * v[1] + bm[3 * k + 2] * v[2];
+}
+
+/* sphere (centre sp, radius r; geom1) - box (geom2): the box point closest to
+   the centre; a centre inside the box leaves through its nearest face
+   (MuJoCo Warp collision_primitive.sphere_box, restated) */
+static int raw_sphere_box(contact_t* c, real margin, const real sp[3], real r, const real bp[3], const real bm[9],
+                          const real bs[3]) {
+  real lc[3], cl[3], dif[3];
+  to_box(bp, bm, sp, lc);
+  for (int k = 0; k < 3; k++) {
+    cl[k] = lc[k] < -bs[k] ? -bs[k] : (lc[k] > bs[k] ? bs[k] : lc[k]);
+    dif[k] = cl[k] - lc[k];
+  }
+  real dist = norm3(dif);
+  if (dist - r > margin) return 0;
+  real nl[3] = {0, 0, 0}, pl[3];
+  if (dist <= MINVAL) {
+    /* inside: the nearest face (ties to the lower axis, the negative face first) */
+    real closest = 2 * (bs[0] + bs[1] + bs[2]);
+    int kf = 0;
+    for (int i = 0; i < 6; i++) {
+      real fd = fabs((i & 1 ? 1 : -1) * bs[i >> 1] - lc[i >> 1]);
+      if (closest > fd) { closest = fd; kf = i; }
+    }
+    nl[kf >> 1] = kf & 1 ? -1 : 1; /* from the sphere into the box */
+    for (int k = 0; k < 3; k++) pl[k] = lc[k] + nl[k] * (r - closest) * 0.5;
+    c->dist = -closest - r;
+  } else {
+    for (int k = 0; k < 3; k++) nl[k] = dif[k] / dist;
+    for (int k = 0; k < 3; k++) pl[k] = 0.5 * (cl[k] + lc[k] + nl[k] * r);
+    c->dist = dist - r;
+  }
+  real pw[3];
+  from_box(bm, pl, pw);
+  from_box(bm, nl, c->frame);
+  for (int k = 0; k < 3; k++) {
+    c->pos[k] = bp[k] + pw[k];
+    c->frame[3 + k] = 0;
+  }
+  return 1;
+}
+
+/* signed distance of a box-frame point to the box (convex) */
+static real box_sdf(const real bs[3], const real q[3]) {
+  real o[3], out = 0, in = -1e30;
+  for (int k = 0; k < 3; k++) {
+    o[k] = fabs(q[k]) - bs[k];
+    real e = o[k] > 0 ? o[k] : 0;
+    out += e * e;
+    if (o[k] > in) in = o[k];
+  }
+  return out > 0 ? sqrt(out) : in;
+}
+
+/* capsule (centre cp, axis ax, half length h, radius r; geom1) - box (geom2):
+   both segment ends as spheres when both touch (a capsule lying on a face),
+   otherwise one sphere at the segment point nearest the box (the signed
+   distance is convex along the segment: golden-section search, 40 steps) */
+static int raw_capsule_box(contact_t* out, real margin, const real cp[3], const real ax[3], real h, real r,
+                           const real bp[3], const real bm[9], const real bs[3]) {
+  real a[3], b[3];
+  for (int k = 0; k < 3; k++) { a[k] = cp[k] + ax[k] * h; b[k] = cp[k] - ax[k] * h; }
+  contact_t ca, cb;
+  int na = raw_sphere_box(&ca, margin, a, r, bp, bm, bs), nb = raw_sphere_box(&cb, margin, b, r, bp, bm, bs);
+  if (na && nb) {
+    out[0] = ca;
+    out[1] = cb;
+    for (int i = 0; i < 2; i++) memcpy(out[i].frame + 3, ax, 3 * sizeof(real));
+    return 2;
+  }
+  real la[3], lb[3];
+  to_box(bp, bm, a, la);
+  to_box(bp, bm, b, lb);
+  const real g = 0.6180339887498949;
+  real lo = 0, hi = 1, x1 = hi - g * (hi - lo), x2 = lo + g * (hi - lo), q[3];
+  for (int k = 0; k < 3; k++) q[k] = la[k] + (lb[k] - la[k]) * x1;
+  real f1 = box_sdf(bs, q);
+  for (int k = 0; k < 3; k++) q[k] = la[k] + (lb[k] - la[k]) * x2;
+  real f2 = box_sdf(bs, q);
+  for (int it = 0; it < 40; it++) {
+    if (f1 <= f2) {
+      hi = x2; x2 = x1; f2 = f1; x1 = hi - g * (hi - lo);
+      for (int k = 0; k < 3; k++) q[k] = la[k] + (lb[k] - la[k]) * x1;
+      f1 = box_sdf(bs, q);
+    } else {
+      lo = x1; x1 = x2; f1 = f2; x2 = lo + g * (hi - lo);
+      for (int k = 0; k < 3; k++) q[k] = la[k] + (lb[k] - la[k]) * x2;
+      f2 = box_sdf(bs, q);
+    }
+  }
+  real t = 0.5 * (lo + hi), p[3];
+  for (int k = 0; k < 3; k++) p[k] = a[k] + (b[k] - a[k]) * t;
+  int n = raw_sphere_box(out, margin, p, r, bp, bm, bs);
+  if (n) memcpy(out[0].frame + 3, ax, 3 * sizeof(real));
+  return n;
+}
+
+/* box (geom1) - box (geom2): separating-axis test over the 15 axes (3 + 3
+   face normals, 9 edge-edge cross products; face axes preferred within 5 %);
+   a face axis clips the incident face of the other box against the reference
+   face's side planes (up to 8 points, the deepest kept and then up to 3 more,
+   each farthest from those kept), an edge-edge axis gives the closest points
+   of the two support edges */
+static int raw_box_box(contact_t* out, real margin, const real pa[3], const real ma[9], const real sa[3],
+                       const real pb[3], const real mb[9], const real sb[3]) {
+  real A[3][3], B[3][3], d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) { A[i][k] = ma[3 * k + i]; B[i][k] = mb[3 * k + i]; }
+  real best = 1e30, bn[3] = {0, 0, 0};
+  int bk = -1;
+  for (int k = 0; k < 15; k++) {
+    real L[3];
+    if (k < 3) memcpy(L, A[k], sizeof(L));
+    else if (k < 6) memcpy(L, B[k - 3], sizeof(L));
+    else cross3(L, A[(k - 6) / 3], B[(k - 6) % 3]);
+    real ln = norm3(L);
+    if (ln < 1e-6) continue;
+    for (int q = 0; q < 3; q++) L[q] /= ln;
+    real ra = 0, rb = 0;
+    for (int i = 0; i < 3; i++) { ra += sa[i] * fabs(dot3(A[i], L)); rb += sb[i] * fabs(dot3(B[i], L)); }
+    real dl = dot3(d, L), ov = ra + rb - fabs(dl);
+    if (ov < -margin) return 0;
+    real score = k < 6 ? ov : ov * 1.05 + 1e-9; /* prefer face axes */
+    if (score < best) {
+      best = score;
+      bk = k;
+      for (int q = 0; q < 3; q++) bn[q] = dl < 0 ? -L[q] : L[q]; /* from A to B */
+    }
+  }
+  if (bk < 0) return 0;
+  if (bk < 6) {
+    /* reference face: of A (normal bn) or of B (normal -bn); incident box the other */
+    int refA = bk < 3;
+    const real *rp = refA ? pa : pb, *ip = refA ? pb : pa, *rs = refA ? sa : sb, *is = refA ? sb : sa;
+    real (*R)[3] = refA ? A : B, (*I)[3] = refA ? B : A;
+    real nr[3];
+    for (int q = 0; q < 3; q++) nr[q] = refA ? bn[q] : -bn[q]; /* out of the reference face */
+    int ra = refA ? bk : bk - 3;
+    /* incident face: the face of the other box most opposed to nr */
+    int ia = 0;
+    real mx = -1;
+    for (int i = 0; i < 3; i++) {
+      real v = fabs(dot3(I[i], nr));
+      if (v > mx) { mx = v; ia = i; }
+    }
+    real isg = dot3(I[ia], nr) > 0 ? -1 : 1;
+    real fc[3];
+    for (int q = 0; q < 3; q++) fc[q] = ip[q] + I[ia][q] * is[ia] * isg;
+    int u = (ia + 1) % 3, v = (ia + 2) % 3;
+    real poly[16][3], tmpp[16][3];
+    int np = 4;
+    for (int c = 0; c < 4; c++) {
+      real su = (c == 0 || c == 3) ? 1 : -1, sv = (c < 2) ? 1 : -1;
+      for (int q = 0; q < 3; q++) poly[c][q] = fc[q] + I[u][q] * is[u] * su + I[v][q] * is[v] * sv;
+    }
+    /* clip against the 4 side planes of the reference face */
+    for (int e = 0; e < 4 && np > 0; e++) {
+      int axis = e < 2 ? (ra + 1) % 3 : (ra + 2) % 3;
+      real sg = (e & 1) ? -1 : 1;
+      real off = dot3(R[axis], rp) * sg + rs[axis];
+      int nn = 0;
+      for (int i = 0; i < np; i++) {
+        const real *P = poly[i], *Q = poly[(i + 1) % np];
+        real dp = sg * dot3(R[axis], P) - off, dq = sg * dot3(R[axis], Q) - off;
+        if (dp <= 0) { memcpy(tmpp[nn++], P, 3 * sizeof(real)); }
+        if ((dp <= 0) != (dq <= 0)) {
+          real t = dp / (dp - dq);
+          for (int q = 0; q < 3; q++) tmpp[nn][q] = P[q] + (Q[q] - P[q]) * t;
+          nn++;
+        }
+      }
+      np = nn;
+      memcpy(poly, tmpp, sizeof(real) * 3 * nn);
+    }
+    /* depth below the reference face */
+    real rfc = dot3(nr, rp) + rs[ra] * fabs(dot3(R[ra], nr));
+    real dep[16];
+    int keep[16], nk = 0;
+    for (int i = 0; i < np; i++) {
+      dep[i] = dot3(nr, poly[i]) - rfc;
+      if (dep[i] <= margin) keep[nk++] = i;
+    }
+    if (nk == 0) return 0;
+    int sel[4], ns = 0;
+    int di = keep[0];
+    for (int j = 1; j < nk; j++) if (dep[keep[j]] < dep[di]) di = keep[j];
+    sel[ns++] = di;
+    while (ns < 4 && ns < nk) {
+      int bj = -1;
+      real bd = -1;
+      for (int j = 0; j < nk; j++) {
+        int i = keep[j], used = 0;
+        real md = 1e30;
+        for (int s2 = 0; s2 < ns; s2++) {
+          if (sel[s2] == i) used = 1;
+          real dd[3] = {poly[i][0] - poly[sel[s2]][0], poly[i][1] - poly[sel[s2]][1], poly[i][2] - poly[sel[s2]][2]};
+          real dn = norm3(dd);
+          if (dn < md) md = dn;
+        }
+        if (!used && md > bd) { bd = md; bj = i; }
+      }
+      if (bj < 0) break;
+      sel[ns++] = bj;
+    }
+    for (int i = 0; i < ns; i++) {
+      contact_t* c = out + i;
+      c->dist = dep[sel[i]];
+      for (int q = 0; q < 3; q++) {
+        c->pos[q] = poly[sel[i]][q] - nr[q] * 0.5 * c->dist;
+        c->frame[q] = bn[q];
+        c->frame[3 + q] = 0;
+      }
+    }
+    return ns;
+  }
+  /* edge-edge: the support edges (along A_i and B_j) */
+  int ai = (bk - 6) / 3, bj = (bk - 6) % 3;
+  real ca[3], cb[3];
+  memcpy(ca, pa, sizeof(ca));
+  memcpy(cb, pb, sizeof(cb));
+  for (int i = 0; i < 3; i++) {
+    if (i != ai) {
+      real sg = dot3(A[i], bn) > 0 ? 1 : -1;
+      for (int q = 0; q < 3; q++) ca[q] += A[i][q] * sa[i] * sg;
+    }
+    if (i != bj) {
+      real sg = dot3(B[i], bn) > 0 ? -1 : 1;
+      for (int q = 0; q < 3; q++) cb[q] += B[i][q] * sb[i] * sg;
+    }
+  }
+  /* closest points of the segments ca + s A_ai (|s| <= sa[ai]), cb + t B_bj */
+  real w0[3] = {ca[0] - cb[0], ca[1] - cb[1], ca[2] - cb[2]};
+  real aa = dot3(A[ai], A[ai]), ab = dot3(A[ai], B[bj]), bb = dot3(B[bj], B[bj]);
+  real da = dot3(A[ai], w0), db = dot3(B[bj], w0), den = aa * bb - ab * ab;
+  real s = den > 1e-12 ? (ab * db - bb * da) / den : 0;
+  s = s < -sa[ai] ? -sa[ai] : (s > sa[ai] ? sa[ai] : s);
+  real t = (ab * s + db) / bb;
+  t = t < -sb[bj] ? -sb[bj] : (t > sb[bj] ? sb[bj] : t);
+  s = (ab * t - da) / aa;
+  s = s < -sa[ai] ? -sa[ai] : (s > sa[ai] ? sa[ai] : s);
+  real p1[3], p2[3];
+  for (int q = 0; q < 3; q++) { p1[q] = ca[q] + A[ai][q] * s; p2[q] = cb[q] + B[bj][q] * t; }
+  real dd[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  real dist = dot3(dd, bn);
+  if (dist > margin) return 0;
+  out[0].dist = dist;
+  for (int q = 0; q < 3; q++) {
+    out[0].pos[q] = 0.5 * (p1[q] + p2[q]);
+    out[0].frame[q] = bn[q];
+    out[0].frame[3 + q] = 0;
+  }
+  return 1;
+}
+
 static int collide(const or_model* m, ws_t* w, int g1, int g2, real margin, contact_t* out) {
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   const real *p1 = w->gxpos + 3 * g1, *m1 = w->gxmat + 9 * g1, *s1 = m->geom_size + 3 * g1;
@@ -674,6 +939,12 @@ static int collide(const or_model* m, ws_t* w, int g1, int g2, real margin, cont
     }
     return n;
   }
+  if (t1 == 2 && t2 == 6) return raw_sphere_box(out, margin, p1, s1[0], p2, m2, s2);
+  if (t1 == 3 && t2 == 6) {
+    real ax[3] = {m1[2], m1[5], m1[8]};
+    return raw_capsule_box(out, margin, p1, ax, s1[1], s1[0], p2, m2, s2);
+  }
+  if (t1 == 6 && t2 == 6) return raw_box_box(out, margin, p1, m1, s1, p2, m2, s2);
   return 0; /* unsupported pairs are rejected by the compiler */
 }
 

@@ -251,12 +251,12 @@ def test_external_force_clearing(backend):
 
 
 def test_external_force_on_specific_body(backend):
-  """test_entity.py:298-326. The two sibling link boxes overlap completely;
-  box-box is not a collision pair the HIP step implements, so (unlike MuJoCo)
-  they do not push each other apart: the compiler reports the dropped pair."""
+  """test_entity.py:298-326, as the reference writes it: the overlapping link
+  boxes collide (box-box narrowphase), the wrench moves link1."""
   dev = device_of(backend)
   e = _entity(FLOATING_BASE_ARTICULATED_XML, articulation=_ACT)
-  with pytest.warns(UserWarning, match="box-box"):
+  with warnings.catch_warnings():
+    warnings.simplefilter("error")  # every collision pair of the model has a narrowphase
     e.compile()
   entity, sim = _init_entity_with_sim(e, backend)
   body_ids = entity.find_bodies("link1")[0]
