@@ -515,7 +515,7 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
     """per world: max|d_w| <= scale * rel * (1 + max|ref_w[scale_name]|) + floor
     for at least `frac` of the worlds, and with rel_max (if given) for all."""
     rows = good if rows is None else rows
-    if len(rows) == 0:
+    if len(rows) == 0 or got[name].shape[1] == 0:
       return
     a, b = got[name][rows], ref[name][rows]
     s_ref = ref[scale_name or name][rows]
