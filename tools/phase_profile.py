@@ -46,6 +46,12 @@ torch.cuda.synchronize()
 p = buf.view(N, 32).cpu().numpy().astype(np.int64)
 tot = p[:, 9] - p[:, 0]
 print(f"N={N} ls_parallel={int(cfg.ls_parallel)} mean total cycles/world-step: {tot.mean():.0f} (max {tot.max()})")
+# the launch as a whole: span from the first world's start to the last world's
+# end (shader clock), and when worlds start (late starts = a second round)
+st0 = p[:, 0] - p[:, 0].min()
+print(f"  launch span {(p[:, 9].max() - p[:, 0].min()):.0f} cycles; world start p50 {np.percentile(st0, 50):.0f} "
+      f"p90 {np.percentile(st0, 90):.0f} max {st0.max():.0f}; world cycles p50 {np.percentile(tot, 50):.0f} "
+      f"p90 {np.percentile(tot, 90):.0f} p99 {np.percentile(tot, 99):.0f} max {tot.max():.0f}")
 # phase stamps in execution order: the position stage (kinematics .. constraint
 # rows) runs before the velocity stage (rne / smooth forces / qacc_smooth)
 for n, (a, b) in zip(NAMES, PHASES):
