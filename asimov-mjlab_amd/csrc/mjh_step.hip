@@ -204,18 +204,18 @@ struct ImgOff {
   int nfields;
 };
 
-// Worlds per workgroup by padded dof count: one-world workgroups for the 35-dof
-// humanoid (each wave retires on its own, so a CU starts the next world as soon
-// as any one is done instead of waiting for the slowest of 8; the model image is
-// then read in place from global memory, and the LDS it frees raises the row
-// capacity to njmax), 8-world workgroups sharing an LDS copy of the image
-// otherwise (Go1: the image reads dominate, profiles/r03t_variants_kb.log).
-// MJH_WPB overrides it for A/B builds.
+// Worlds per workgroup by padded dof count: one-world workgroups up to 36 dofs
+// (G1, Go1): each wave retires on its own, the model image is read in place from
+// global memory, and MJH_WPCU (16) of them share a CU — 4 waves per SIMD, so all
+// 4,096 G1 worlds are resident at once (one round instead of two; G1 step
+// launch 0.605 -> 0.505 ms, Go1 8192 0.559 -> 0.522 ms, env bench 1.37M ->
+// 1.57M env-steps/s, profiles/r04m_*). 8-world workgroups sharing an LDS copy of
+// the image for larger models. MJH_WPB overrides it for A/B builds.
 __host__ __device__ constexpr int wpb_of_nvp(int nvp) {
 #ifdef MJH_WPB
   return (void)nvp, MJH_WPB;
 #else
-  return nvp == 36 ? 1 : 8;
+  return nvp <= 36 ? 1 : 8;
 #endif
 }
 // the image lives in global memory for workgroups of fewer than 8 worlds
@@ -1338,7 +1338,7 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 // target (the VGPR budget: 8 -> 256, 12 -> 168, 16 -> 128) and the per-world
 // LDS budget alike
 #ifndef MJH_WPCU
-#define MJH_WPCU 8
+#define MJH_WPCU 16
 #endif
 #ifndef MJH_MINWAVES
 #define MJH_MINWAVES(wpb) ((wpb) < 8 ? MJH_WPCU / 4 : 1)

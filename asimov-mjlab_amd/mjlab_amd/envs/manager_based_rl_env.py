@@ -320,10 +320,12 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     return (self.reward_manager.active_pattern, self.sim.struct_version)
 
   def _capture(self, key) -> None:
+    from mjlab_amd.utils.capture import no_gc
+
     self._graph = None
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with no_gc(), torch.cuda.graph(g):
       self._step_body()
       out = (self.obs_buf, dict(self.extras["log"]))
     self._graph, self._graph_key, self._graph_out = g, key, out

@@ -399,13 +399,16 @@ class Simulation:
     # no warm-up launch here: it would run a real forward (and overwrite
     # qacc_warmstart); the constructor's first forward() already set the
     # kernels' LDS attributes outside any capture
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-      self._launch_step()
+    from mjlab_amd.utils.capture import no_gc
+
+    with no_gc():
+      g = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g):
+        self._launch_step()
+      g2 = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g2):
+        self._launch_forward()
     self.step_graph = g
-    g2 = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g2):
-      self._launch_forward()
     self.forward_graph = g2
 
   def _stream(self) -> ctypes.c_void_p:

@@ -356,20 +356,23 @@ def test_rows_in_global_scratch_are_bit_identical():
   """Worlds whose constraint rows exceed the LDS-resident capacity run the rest
   of their step with the row arrays in global scratch (mjh_step.hip, BIG): the
   same arithmetic on other addresses. With the LDS capacity capped at 8 rows
-  (most worlds take that path) every output is bitwise equal to a run capped at
-  njmax - 1 (no world does; both caps change the launch plan, so both runs use
-  the generic kernel instance), and both match the oracle."""
+  (most worlds take that path) every output is bitwise equal to a run capped one
+  row below the LDS budget's capacity (few worlds do; both caps change the
+  launch plan, so both runs use the generic kernel instance), and both match
+  the oracle."""
   from mjlab_amd.sim import native
 
   n = 256
   m = g1_scene_model(n)
   st = random_states(m, n, np.random.default_rng(21), drop=0.03)
   outs = []
+  lcap = make_sim(m, 8).lds_row_capacity()  # the LDS budget's rows (uncapped)
   try:
-    for cap in (8, 299):
+    # both caps change the launch plan (generic instance in both runs)
+    for cap in (8, lcap - 1):
       native.lib().mjh_set_lds_row_cap(cap)
       sim = make_sim(m, n)
-      assert sim.lds_row_capacity() == min(cap, sim.efc_capacity())
+      assert sim.lds_row_capacity() == cap
       put(sim, st)
       sim.step()
       outs.append(get(sim, n))
