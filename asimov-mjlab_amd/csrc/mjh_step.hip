@@ -814,6 +814,10 @@ __device__ __forceinline__ int plane_sphere(Con* c, float margin, const float* p
   return 1;
 }
 
+// near-ties in the box functions' discrete choices go to the earlier candidate
+// unless the later wins by kBoxTie x the size scale (the oracle's BOX_TIE), so
+// float32 and float64 choose alike
+constexpr float kBoxTie = 1e-5f;
 // ---- box pairs (sphere-box, capsule-box, box-box): the oracle's algorithms
 // (oracle/oracle.c raw_sphere_box / raw_capsule_box / raw_box_box) in float32.
 // Boxes: centre bp, rotation bm (row-major, column k = axis k), half sizes bs.
@@ -843,10 +847,11 @@ __device__ __noinline__ int sphere_box(Con* c, float margin, const float* sp, fl
   float nl[3] = {0.f, 0.f, 0.f}, pl[3];
   if (dist <= MJH_MINVAL) {
     float closest = 2.f * (bs[0] + bs[1] + bs[2]);
+    const float tie = kBoxTie * (bs[0] + bs[1] + bs[2]);
     int kf = 0;
     for (int i = 0; i < 6; i++) {
       const float fd = fabsf((i & 1 ? 1.f : -1.f) * bs[i >> 1] - lc[i >> 1]);
-      if (closest > fd) { closest = fd; kf = i; }
+      if (closest > fd + tie) { closest = fd; kf = i; }
     }
 #pragma unroll
     for (int k = 0; k < 3; k++) nl[k] = k == (kf >> 1) ? (kf & 1 ? -1.f : 1.f) : 0.f;
@@ -947,6 +952,7 @@ __device__ __noinline__ int box_box(Con* out, float margin, const float* pa, con
   for (int i = 0; i < 3; i++)
     for (int k = 0; k < 3; k++) { A[i][k] = ma[3 * k + i]; B[i][k] = mb[3 * k + i]; }
   float best = 1e30f, bn[3] = {0.f, 0.f, 0.f};
+  const float tie = kBoxTie * (sa[0] + sa[1] + sa[2] + sb[0] + sb[1] + sb[2]);
   int bk = -1;
   for (int k = 0; k < 15; k++) {
     float L[3];
@@ -961,7 +967,7 @@ __device__ __noinline__ int box_box(Con* out, float margin, const float* pa, con
     const float dl = dot3(d, L), ov = ra + rb - fabsf(dl);
     if (ov < -margin) return 0;
     const float score = k < 6 ? ov : ov * 1.05f + 1e-9f;
-    if (score < best) {
+    if (score < best - tie) {
       best = score;
       bk = k;
       for (int q = 0; q < 3; q++) bn[q] = dl < 0.f ? -L[q] : L[q];
@@ -981,7 +987,7 @@ __device__ __noinline__ int box_box(Con* out, float margin, const float* pa, con
     float mx = -1.f;
     for (int i = 0; i < 3; i++) {
       const float v = fabsf(dot3(I[i], nr));
-      if (v > mx) { mx = v; ia = i; }
+      if (v > mx + kBoxTie) { mx = v; ia = i; }
     }
     const float isg = dot3(I[ia], nr) > 0.f ? -1.f : 1.f;
     float fc[3];
@@ -1022,7 +1028,7 @@ __device__ __noinline__ int box_box(Con* out, float margin, const float* pa, con
     }
     if (nk == 0) return 0;
     int sel[4], ns = 0, di = keep[0];
-    for (int j = 1; j < nk; j++) if (dep[keep[j]] < dep[di]) di = keep[j];
+    for (int j = 1; j < nk; j++) if (dep[keep[j]] < dep[di] - tie) di = keep[j];
     sel[ns++] = di;
     while (ns < 4 && ns < nk) {
       int bj = -1;
@@ -1036,7 +1042,7 @@ __device__ __noinline__ int box_box(Con* out, float margin, const float* pa, con
           const float dd[3] = {poly[i][0] - poly[sel[s2]][0], poly[i][1] - poly[sel[s2]][1], poly[i][2] - poly[sel[s2]][2]};
           md = fminf(md, sqrtf(dot3(dd, dd)));
         }
-        if (!used && md > bd) { bd = md; bj = i; }
+        if (!used && md > bd + tie) { bd = md; bj = i; }
       }
       if (bj < 0) break;
       sel[ns++] = bj;

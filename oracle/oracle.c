@@ -594,6 +594,11 @@ static int raw_plane_sphere(contact_t* c, real margin, const real pp[3], const r
   return 1;
 }
 
+/* Near-ties in the box functions' discrete choices (nearest face, separating
+   axis, incident face, kept clip points) go to the earlier candidate unless the
+   later one wins by BOX_TIE x the boxes' size scale, so a float32 and a float64
+   evaluation choose alike (the kernel uses the same rule). */
+#define BOX_TIE 1e-5
 /* ---- box pairs (sphere-box, capsule-box, box-box). Boxes: centre bp,
    rotation bm (row-major, column k = axis k), half sizes bs. Normals point from
    geom1 to geom2 (pairs are ordered by type, so the box is geom2 except in
@@ -623,11 +628,11 @@ static int raw_sphere_box(contact_t* c, real margin, const real sp[3], real r, c
   real nl[3] = {0, 0, 0}, pl[3];
   if (dist <= MINVAL) {
     /* inside: the nearest face (ties to the lower axis, the negative face first) */
-    real closest = 2 * (bs[0] + bs[1] + bs[2]);
+    real closest = 2 * (bs[0] + bs[1] + bs[2]), tie = BOX_TIE * (bs[0] + bs[1] + bs[2]);
     int kf = 0;
     for (int i = 0; i < 6; i++) {
       real fd = fabs((i & 1 ? 1 : -1) * bs[i >> 1] - lc[i >> 1]);
-      if (closest > fd) { closest = fd; kf = i; }
+      if (closest > fd + tie) { closest = fd; kf = i; }
     }
     nl[kf >> 1] = kf & 1 ? -1 : 1; /* from the sphere into the box */
     for (int k = 0; k < 3; k++) pl[k] = lc[k] + nl[k] * (r - closest) * 0.5;
@@ -713,7 +718,7 @@ static int raw_box_box(contact_t* out, real margin, const real pa[3], const real
   real A[3][3], B[3][3], d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
   for (int i = 0; i < 3; i++)
     for (int k = 0; k < 3; k++) { A[i][k] = ma[3 * k + i]; B[i][k] = mb[3 * k + i]; }
-  real best = 1e30, bn[3] = {0, 0, 0};
+  real best = 1e30, bn[3] = {0, 0, 0}, tie = BOX_TIE * (sa[0] + sa[1] + sa[2] + sb[0] + sb[1] + sb[2]);
   int bk = -1;
   for (int k = 0; k < 15; k++) {
     real L[3];
@@ -728,7 +733,7 @@ static int raw_box_box(contact_t* out, real margin, const real pa[3], const real
     real dl = dot3(d, L), ov = ra + rb - fabs(dl);
     if (ov < -margin) return 0;
     real score = k < 6 ? ov : ov * 1.05 + 1e-9; /* prefer face axes */
-    if (score < best) {
+    if (score < best - tie) {
       best = score;
       bk = k;
       for (int q = 0; q < 3; q++) bn[q] = dl < 0 ? -L[q] : L[q]; /* from A to B */
@@ -748,7 +753,7 @@ static int raw_box_box(contact_t* out, real margin, const real pa[3], const real
     real mx = -1;
     for (int i = 0; i < 3; i++) {
       real v = fabs(dot3(I[i], nr));
-      if (v > mx) { mx = v; ia = i; }
+      if (v > mx + BOX_TIE) { mx = v; ia = i; }
     }
     real isg = dot3(I[ia], nr) > 0 ? -1 : 1;
     real fc[3];
@@ -790,7 +795,7 @@ static int raw_box_box(contact_t* out, real margin, const real pa[3], const real
     if (nk == 0) return 0;
     int sel[4], ns = 0;
     int di = keep[0];
-    for (int j = 1; j < nk; j++) if (dep[keep[j]] < dep[di]) di = keep[j];
+    for (int j = 1; j < nk; j++) if (dep[keep[j]] < dep[di] - tie) di = keep[j];
     sel[ns++] = di;
     while (ns < 4 && ns < nk) {
       int bj = -1;
@@ -804,7 +809,7 @@ static int raw_box_box(contact_t* out, real margin, const real pa[3], const real
           real dn = norm3(dd);
           if (dn < md) md = dn;
         }
-        if (!used && md > bd) { bd = md; bj = i; }
+        if (!used && md > bd + tie) { bd = md; bj = i; }
       }
       if (bj < 0) break;
       sel[ns++] = bj;

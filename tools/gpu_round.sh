@@ -9,6 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
 t() { echo "[$(date +%T)] $*"; }
+if [ -n "$DIAG" ]; then timeout -k 10 120 python $DIAG > $O/diag.log 2>&1; tail -30 $O/diag.log; fi
 t tests
 timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gputests.log 2>&1 || { tail -30 $O/gputests.log; exit 1; }
 tail -2 $O/gputests.log
