@@ -1274,6 +1274,71 @@ __device__ __forceinline__ float row_state(int type, float D, float R, float fl,
   *force = 0.f; *cost = 0.f; return 0.f;
 }
 
+// ---- elliptic cones (opt.cone == mjCONE_ELLIPTIC; generic instances only) ----
+// A contact's dim rows (normal, then the frame's tangents / torsion / rolling)
+// are evaluated together (MuJoCo Warp solver.py _update_constraint_efc,
+// CONTACT_ELLIPTIC; oracle/oracle.c cone_eval): U0 = mu jar0, Uj = s_j jarj with
+// the row scales s in efc_fl (mu = friction0 / sqrt(impratio), then
+// friction_{j-1}), N = U0, T = |U1..|. Top zone (N >= mu T): free; bottom zone
+// (mu N + T <= 0): every row quadratic; else the cone, cost 0.5 Dm (N - mu T)^2,
+// Dm = D0 / (mu^2 (1 + mu^2)).
+constexpr int kConeTop = 0, kConeBottom = 1, kConeMid = 2;
+struct ConeRows {
+  float jar[6], D[6], s[6];
+};
+// cost; forces f; zone; along a direction jv: *q2 = jv^T Hc jv (the cost's
+// curvature, for the exact line search) when q2 != nullptr
+__device__ __forceinline__ float cone_eval(int dim, const ConeRows& c, float (&f)[6], int* zone,
+                                           const float* jv = nullptr, float* q2 = nullptr) {
+  const float mu = c.s[0];
+  float U[6], TT = 0.f;
+  U[0] = c.jar[0] * mu;
+#pragma unroll
+  for (int j = 1; j < 6; j++) {
+    U[j] = j < dim ? c.jar[j] * c.s[j] : 0.f;
+    TT += U[j] * U[j];
+  }
+  const float N = U[0], T = TT > 0.f ? sqrtf(TT) : 0.f;
+  if (N >= mu * T || (T <= 0.f && N >= 0.f)) {
+#pragma unroll
+    for (int j = 0; j < 6; j++) f[j] = 0.f;
+    *zone = kConeTop;
+    if (q2) *q2 = 0.f;
+    return 0.f;
+  }
+  if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {
+    float cost = 0.f, q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      f[j] = j < dim ? -c.D[j] * c.jar[j] : 0.f;
+      cost += j < dim ? 0.5f * c.D[j] * c.jar[j] * c.jar[j] : 0.f;
+      if (q2) q += j < dim ? c.D[j] * jv[j] * jv[j] : 0.f;
+    }
+    *zone = kConeBottom;
+    if (q2) *q2 = q;
+    return cost;
+  }
+  const float Dm = c.D[0] / fmaxf(mu * mu * (1.f + mu * mu), MJH_MINVAL), NmT = N - mu * T;
+  f[0] = -Dm * NmT * mu;
+#pragma unroll
+  for (int j = 1; j < 6; j++) f[j] = j < dim ? -f[0] / T * U[j] * c.s[j] : 0.f;
+  *zone = kConeMid;
+  if (q2) {
+    // w = S jv: jv^T Hc jv = Dm ((w0 - mu u.wt)^2 - (N - mu T) mu / T (|wt|^2 - (u.wt)^2)), u = Ut / T
+    const float w0 = mu * jv[0];
+    float uw = 0.f, ww = 0.f;
+#pragma unroll
+    for (int j = 1; j < 6; j++) {
+      const float wj = j < dim ? c.s[j] * jv[j] : 0.f;
+      uw += U[j] / T * wj;
+      ww += wj * wj;
+    }
+    const float g = w0 - mu * uw;
+    *q2 = Dm * (g * g - NmT * mu / T * (ww - uw * uw));
+  }
+  return 0.5f * Dm * NmT * NmT;
+}
+
 // ---- model specialisation -----------------------------------------------------
 // A kernel instance with SPEC >= 0 takes the model sizes, the per-world layout
 // and the model-image offsets as compile-time constants (mjh_spec_table.h,
@@ -1456,6 +1521,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   // the factor's rows: packed lower-triangular for one-world workgroups
   constexpr bool PKL = pack_l(WPB);
   const int kLWords = PKL ? lrow(NVP) : nv * ldm;
+  // elliptic friction cones: the generic instances only (the model-specialised
+  // ones are picked for pyramidal cones), J in global scratch (virtual rows of
+  // the cone Hessian after row rcap)
+  const bool ELL = SPEC < 0 && Rg::J && m.cone == 1;
 
   constexpr bool HO = MODE == 1;
   float* qpos = HO ? S : SP(qpos);
@@ -2037,7 +2106,8 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         for (int base = 0; base < ncon; base += NT) {
           const int ci = base + tid;
           int nr = 0;
-          if (ci < ncon && con_dist[ci] - con_imargin[ci] < 0.f) nr = con_dim[ci] == 1 ? 1 : 2 * (con_dim[ci] - 1);
+          if (ci < ncon && con_dist[ci] - con_imargin[ci] < 0.f)
+            nr = con_dim[ci] == 1 ? 1 : (ELL ? con_dim[ci] : 2 * (con_dim[ci] - 1));
           int total;
           (void)bscan<NT>(nr, &total, redi);
           need += total;
@@ -2129,7 +2199,8 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     for (int base = 0; base < ncon; base += NT) {
       const int ci = base + tid;
       int nr = 0;
-      if (ci < ncon && con_dist[ci] - con_imargin[ci] < 0.f) nr = con_dim[ci] == 1 ? 1 : 2 * (con_dim[ci] - 1);
+      if (ci < ncon && con_dist[ci] - con_imargin[ci] < 0.f)
+        nr = con_dim[ci] == 1 ? 1 : (ELL ? con_dim[ci] : 2 * (con_dim[ci] - 1));
       int total;
       const int off = bscan<NT>(nr, &total, redi);
       if (nr) {
@@ -2206,7 +2277,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           if (r0k < 0) continue;
           const int b1k = __builtin_amdgcn_readlane(b1, k), b2k = __builtin_amdgcn_readlane(b2, k);
           const int dimk = __builtin_amdgcn_readlane(dim, k);
-          const int nr = dimk == 1 ? 1 : 2 * (dimk - 1);
+          const int nr = dimk == 1 ? 1 : 2 * (dimk - 1);  // pyramidal (elliptic: dimk rows)
           const bool in1 = tid < nv && (((unsigned long long)IMG_L(body_dofmask)[b1k] >> tid) & 1ull);
           const bool in2 = tid < nv && (((unsigned long long)IMG_L(body_dofmask)[b2k] >> tid) & 1ull);
           // not in either chain, or in both (relative motion cancels): zero column
@@ -2227,6 +2298,12 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           if (tid < ldj) {
             if (dimk == 1) {
               J[r0k * ldj + tid] = use ? jf[0] : 0.f;
+            } else if (ELL) {
+              // elliptic: row e is the frame component e (translational for
+              // e < 3, rotational after)
+#pragma unroll
+              for (int e = 0; e < 6; e++)
+                if (e < dimk) J[(r0k + e) * ldj + tid] = use ? jf[e] : 0.f;
             } else {
               float fkv[5];
 #pragma unroll
@@ -2251,31 +2328,48 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       if (r0 < 0) continue;
       const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
       const int dim = con_dim[ci];
-      const int nr = dim == 1 ? 1 : 2 * (dim - 1);
+      const bool ell = ELL && dim > 1;
+      const int nr = dim == 1 ? 1 : (ell ? dim : 2 * (dim - 1));
       const unsigned long long msk =
           (unsigned long long)IMG_L(body_dofmask)[b1] ^ (unsigned long long)IMG_L(body_dofmask)[b2];
       for (int e = 0; e < nr; e++) {
         const int r = r0 + e;
-        efc_type[r] = dim == 1 ? MJH_CNSTR_CONTACT_FRICTIONLESS : MJH_CNSTR_CONTACT_PYRAMIDAL;
+        efc_type[r] = dim == 1 ? MJH_CNSTR_CONTACT_FRICTIONLESS
+                               : (ell ? MJH_CNSTR_CONTACT_ELLIPTIC : MJH_CNSTR_CONTACT_PYRAMIDAL);
         efc_id[r] = ci;
-        efc_fl[r] = 0.f;
+        // elliptic: the cone's row scales (mu = friction0 / sqrt(impratio), then friction_{e-1})
+        efc_fl[r] = !ell ? 0.f : (e == 0 ? con_fric[5 * ci] / sqrtf(m.impratio) : con_fric[5 * ci + e - 1]);
         efc_mask[r] = msk;
-        efc_pos[r] = con_dist[ci];
+        // elliptic friction rows: no position term (efc_pos = margin, as MuJoCo Warp)
+        efc_pos[r] = ell && e > 0 ? con_imargin[ci] : con_dist[ci];
       }
     }
     wsync();
     for (int r = tid; r < nefc; r += NT) {
-      if (efc_type[r] != MJH_CNSTR_CONTACT_FRICTIONLESS && efc_type[r] != MJH_CNSTR_CONTACT_PYRAMIDAL) continue;
+      const int ty = efc_type[r];
+      if (ty != MJH_CNSTR_CONTACT_FRICTIONLESS && ty != MJH_CNSTR_CONTACT_PYRAMIDAL && ty != MJH_CNSTR_CONTACT_ELLIPTIC)
+        continue;
       const int ci = efc_id[r];
       const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
       float invw = IMG_F(body_invweight0)[2 * b1] + IMG_F(body_invweight0)[2 * b2];
-      if (con_dim[ci] > 1) {
+      const float pos = con_dist[ci] - con_imargin[ci];
+      float pos_aref = pos;
+      if (ELL && ty == MJH_CNSTR_CONTACT_ELLIPTIC) {
+        // MuJoCo Warp constraint.py _efc_contact_elliptic: friction rows without
+        // a position term, invweight / impratio (times f0^2 / f_{e-1}^2 beyond the first)
+        const int e = r - con_efcadr[ci];
+        if (e > 0) {
+          const float f0 = con_fric[5 * ci], fe = con_fric[5 * ci + e - 1];
+          pos_aref = 0.f;
+          invw = invw / m.impratio;
+          if (e > 1) invw *= f0 * f0 / (fe * fe);
+        }
+      } else if (con_dim[ci] > 1) {
         const float f0 = con_fric[5 * ci];
         invw = invw + f0 * f0 * invw;
         invw = invw * 2.f * f0 * f0 / m.impratio;
       }
-      const float pos = con_dist[ci] - con_imargin[ci];
-      row_params_pos(m.timestep, pos, pos, invw, con_solref + 2 * ci, con_solimp + 5 * ci, efc_D + r, efc_R + r,
+      row_params_pos(m.timestep, pos_aref, pos, invw, con_solref + 2 * ci, con_solimp + 5 * ci, efc_D + r, efc_R + r,
                      efc_aref + r, efc_b + r);
     }
     if (tid == 0) ints[I_NEFC] = nefc;
@@ -2551,10 +2645,45 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     wsync();
   } else {
     // forces, qfrc_constraint and cost at the point whose jaref / Ma are set
+    // elliptic cones: the contact's rows, gathered by the lane of its first
+    // row (rows of other contacts' lanes are skipped there); at step a along jv
+    auto cone_first = [&](int r, int& dim) -> bool {
+      const int ci = efc_id[r];
+      dim = con_dim[ci];
+      return con_efcadr[ci] == r;
+    };
+    auto cone_load = [&](int r0, int dim, const float* x, float a, ConeRows& c, float* jvv) {
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        const int rj = j < dim ? r0 + j : r0;
+        c.jar[j] = x[rj] + a * jv[rj];
+        c.D[j] = efc_D[rj];
+        c.s[j] = efc_fl[rj];
+        if (jvv) jvv[j] = jv[rj];
+      }
+    };
     auto update_constraint = [&]() -> float {
       float c = 0.f;
       for (int r = tid; r < nefc; r += NT) {
         float f, cr;
+        if (ELL && efc_type[r] == MJH_CNSTR_CONTACT_ELLIPTIC) {
+          int dim;
+          if (!cone_first(r, dim)) continue;
+          ConeRows cr6;
+          cone_load(r, dim, jaref, 0.f, cr6, nullptr);
+          float fc[6];
+          int zone;
+          c += cone_eval(dim, cr6, fc, &zone);
+          // Hessian weights: bottom zone per row; the cone's block is added by
+          // newton_direction as virtual rows (marked by -1 on the first row)
+#pragma unroll
+          for (int j = 0; j < 6; j++)
+            if (j < dim) {
+              efc_force[r + j] = fc[j];
+              efc_h[r + j] = zone == kConeBottom ? cr6.D[j] : (zone == kConeMid && j == 0 ? -1.f : 0.f);
+            }
+          continue;
+        }
         efc_h[r] = row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], jaref[r], &f, &cr);
         efc_force[r] = f;
         c += cr;
@@ -2594,7 +2723,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     // global copy of the row list put a store ahead of the next J loads)
     constexpr int kMaskWords = 5;  // rows beyond 320: always rebuild
     unsigned long long act_prev[kMaskWords] = {0ull, 0ull, 0ull, 0ull, 0ull};
-    bool have_prev = false;
+    bool have_prev = false, cone_prev = false;
     int nfactor = 0;
     // gradient at the current point (the convergence test reads only this)
     auto gradient = [&]() {
@@ -2622,8 +2751,73 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         nact += total;
       }
       wsync();
+      // elliptic contacts in the cone zone (efc_h -1 on the first row): their
+      // Hessian block Hc = a a^T + sum_q b_q b_q^T (a = sqrt(Dm) S grad(N - mu T),
+      // b_q = sqrt(Dm mu (mu T - N) / T) S e_q, e_q an orthonormal basis of the
+      // tangent plane's complement of U / T from a Householder reflection) as
+      // virtual rows sum_j coef_j J_{r0+j}, stored after row rcap
+      int ncone = 0;
+      if (ELL) {
+        for (int base = 0; base < nefc; base += NT) {
+          const int rr = base + tid;
+          unsigned long long bal = __ballot(rr < nefc && efc_h[rr] < 0.f);
+          while (bal) {
+            const int r0 = base + __builtin_ctzll(bal);
+            bal &= bal - 1ull;
+            int dim;
+            (void)cone_first(r0, dim);
+            ConeRows c;
+            cone_load(r0, dim, jaref, 0.f, c, nullptr);
+            const float mu = c.s[0];
+            float U[6], TT = 0.f;
+#pragma unroll
+            for (int j = 1; j < 6; j++) {
+              U[j] = j < dim ? c.jar[j] * c.s[j] : 0.f;
+              TT += U[j] * U[j];
+            }
+            const float N = c.jar[0] * mu, T = sqrtf(TT);
+            const float Dm = c.D[0] / fmaxf(mu * mu * (1.f + mu * mu), MJH_MINVAL);
+            const float sa = sqrtf(Dm), sb = sqrtf(fmaxf(Dm * mu * (mu * T - N) / T, 0.f));
+            // Householder v = u + sign(u1) e1 over the tangent dims 1..dim-1
+            float v[6], vv = 0.f;
+#pragma unroll
+            for (int j = 1; j < 6; j++) v[j] = j < dim ? U[j] / T : 0.f;
+            v[1] += v[1] >= 0.f ? 1.f : -1.f;
+#pragma unroll
+            for (int j = 1; j < 6; j++) vv += v[j] * v[j];
+#pragma unroll
+            for (int q = 0; q < 5; q++) {
+              if (q >= dim - 1) break;
+              float cf[6];
+              cf[0] = q == 0 ? sa * mu : 0.f;
+#pragma unroll
+              for (int j = 1; j < 6; j++) {
+                // q = 0: -sqrt(Dm) mu u_j s_j; q >= 1: sb e_q[j] s_j, e_q column q+1 of I - 2 v v^T / |v|^2
+                const float eq = (j == q + 1 ? 1.f : 0.f) - 2.f * v[j] * v[q + 1 < 6 ? q + 1 : 5] / vv;
+                cf[j] = j >= dim ? 0.f : (q == 0 ? -sa * mu * (U[j] / T) * c.s[j] : sb * eq * c.s[j]);
+              }
+              const int vr = Lo.rcap + ncone;
+              if (tid < ldj) {
+                float val = 0.f;
+#pragma unroll
+                for (int j = 0; j < 6; j++)
+                  if (j < dim) val += cf[j] * J[(r0 + j) * ldj + tid];
+                J[vr * ldj + tid] = val;
+              }
+              if (tid == 0) {
+                arow[nact] = vr;
+                ash[nact] = 1.f;
+              }
+              nact++;
+              ncone++;
+            }
+          }
+        }
+        wsync();
+      }
       // same active set as the factor in Lm -> H is identical, keep the factor
-      bool same = have_prev && nefc <= kMaskWords * NT;
+      // (never with cone-zone contacts: their blocks move with jar)
+      bool same = have_prev && nefc <= kMaskWords * NT && ncone == 0 && !cone_prev;
 #pragma unroll
       for (int q = 0; q < kMaskWords; q++) same = same && act[q] == act_prev[q];
       float diff = same ? 0.f : 1.f;
@@ -2650,6 +2844,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
 #pragma unroll
         for (int q = 0; q < kMaskWords; q++) act_prev[q] = act[q];
         have_prev = true;
+        cone_prev = ncone > 0;
         nfactor++;
         nfactor_total++;
       }
@@ -2715,6 +2910,16 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     float cs = 0.f;
     for (int r = tid; r < nefc; r += NT) {
       float f, cr;
+      if (ELL && efc_type[r] == MJH_CNSTR_CONTACT_ELLIPTIC) {
+        int dim;
+        if (!cone_first(r, dim)) continue;
+        ConeRows c;
+        cone_load(r, dim, jv, 0.f, c, nullptr);
+        float fc[6];
+        int zone;
+        cs += cone_eval(dim, c, fc, &zone);
+        continue;
+      }
       row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], jv[r], &f, &cr);
       cs += cr;
     }
@@ -2751,6 +2956,19 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         float a = 0.f, b = 0.f;
         for (int r = tid; r < nefc; r += NT) {
           float f, cr;
+          if (ELL && efc_type[r] == MJH_CNSTR_CONTACT_ELLIPTIC) {
+            int dim;
+            if (!cone_first(r, dim)) continue;
+            ConeRows c;
+            float jvv[6], fc[6], q2;
+            int zone;
+            cone_load(r, dim, jaref, alpha, c, jvv);
+            cone_eval(dim, c, fc, &zone, jvv, &q2);
+#pragma unroll
+            for (int j = 0; j < 6; j++) a -= j < dim ? fc[j] * jvv[j] : 0.f;
+            b += q2;
+            continue;
+          }
           const float h = row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], jaref[r] + alpha * jv[r], &f, &cr);
           a -= f * jv[r];
           b += h * jv[r] * jv[r];
@@ -2769,7 +2987,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         const float lstep = (0.f - lmin) / fmaxf(1.f, (float)(nlsp - 1));
         float best = INFINITY;
         int bi = 0;
-        if (nefc <= 2 * NT) {
+        if (nefc <= 2 * NT && !ELL) {
           // a lane's (at most two) rows in registers, loaded once; four step
           // sizes per block, their four wave reductions independent (the
           // reduction latency overlaps instead of serialising per step size)
@@ -2822,6 +3040,18 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           float ca = 0.f, cb = 0.f;
           for (int r = tid; r < nefc; r += NT) {
             float f, cr;
+            if (ELL && efc_type[r] == MJH_CNSTR_CONTACT_ELLIPTIC) {
+              int dim;
+              if (!cone_first(r, dim)) continue;
+              ConeRows c;
+              float fc[6];
+              int zone;
+              cone_load(r, dim, jaref, aa, c, nullptr);
+              ca += cone_eval(dim, c, fc, &zone);
+              cone_load(r, dim, jaref, ab, c, nullptr);
+              cb += cone_eval(dim, c, fc, &zone);
+              continue;
+            }
             const float ja = jaref[r], j1 = jv[r];
             row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], ja + aa * j1, &f, &cr);
             ca += cr;
@@ -2948,6 +3178,8 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         const int cdm = con_dim[ci];
         if (cdm == 1) {
           F[0] = efc_force[r0];
+        } else if (ELL) {  // elliptic: the rows are the frame components
+          for (int k = 0; k < cdm && k < 6; k++) F[k] = efc_force[r0 + k];
         } else {
           for (int e = 0; e < 2 * (cdm - 1); e++) F[0] += efc_force[r0 + e];
           for (int k = 1; k < cdm && k < 6; k++) F[k] = con_fric[5 * ci + k - 1] * (efc_force[r0 + 2 * k - 2] - efc_force[r0 + 2 * k - 1]);
@@ -3631,7 +3863,8 @@ Layout make_layout(const mjh_model* m, int budget, int wpb) {
   L.lcap = lcap;
   // LDS-resident row arrays take lcap rows, global ones rcap
 #define TAKER(name, extra) TAKE(name, (Rg::name ? rcap : lcap) + (extra))
-  TAKE(J, rcap * L.ldj);
+  // elliptic cones: the cone Hessian's virtual rows after row rcap (at most one per row)
+  TAKE(J, (m->cone == 1 ? 2 * rcap : rcap) * L.ldj);
   TAKER(efc_D, 0); TAKER(efc_R, 0); TAKER(efc_aref, 0); TAKER(efc_jaref, 0);
   TAKER(efc_jv, 0); TAKER(efc_force, 0); TAKER(efc_fl, 0); TAKE(efc_pos, rcap);
   TAKER(efc_type, 0); TAKE(efc_id, rcap);
@@ -3720,6 +3953,7 @@ bool data_is_slab(const mjh_model* m, const mjh_data* d) {
 // the specialised instance whose plan equals this model's, or -1
 int find_spec(const Plan& p, const mjh_model* m) {
   if (MJH_NSPEC == 0) return -1;
+  if (m->cone == 1) return -1;  // elliptic cones: generic instances only
   int v[kPlanInts];
   plan_to_ints(p, m, v);
   for (int k = 0; k < MJH_NSPEC; k++)

@@ -53,8 +53,8 @@ class MujocoCfg:
   gravity: tuple[float, float, float] = (0, 0, -9.81)
 
   def apply(self, model: Model) -> None:
-    if self.cone != "pyramidal":
-      raise NotImplementedError("only pyramidal friction cones are implemented")
+    if self.cone not in _CONES:
+      raise ValueError(f"unknown friction cone {self.cone!r}")
     if self.solver == "pgs":
       raise NotImplementedError("the PGS solver is not implemented (Newton and CG are)")
     model.cone = _CONES[self.cone]

@@ -41,6 +41,7 @@ extern "C" {
 #define MJH_CNSTR_LIMIT_JOINT 3
 #define MJH_CNSTR_CONTACT_FRICTIONLESS 5
 #define MJH_CNSTR_CONTACT_PYRAMIDAL 6
+#define MJH_CNSTR_CONTACT_ELLIPTIC 7
 
 /* flags bits */
 #define MJH_FLAG_CONTACT_OVERFLOW 1

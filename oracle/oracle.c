@@ -154,7 +154,7 @@ typedef struct {
   real *M, *LD, *H, *qvel, *qpos, *qacc, *qacc_smooth, *qfrc_smooth, *qfrc_bias, *qfrc_passive,
       *qfrc_actuator, *qfrc_constraint, *act_force, *act_length, *act_vel, *tmpv, *tmpv2, *grad, *search,
       *Ma, *Mv, *Mgrad, *qacc_int, *cg_g, *cg_mg;
-  real *J, *efc_pos, *efc_margin, *efc_D, *efc_R, *efc_aref, *efc_fl, *jaref, *jv, *efc_force;
+  real *J, *efc_pos, *efc_margin, *efc_D, *efc_R, *efc_aref, *efc_fl, *jaref, *jv, *efc_force, *jtmp;
   int *efc_type, *efc_id;
   int nefc, ncon, flags, niter;
   real lsgap; /* parallel line search: smallest relative cost gap best vs runner-up */
@@ -186,7 +186,7 @@ static void ws_alloc(ws_t* w, const or_model* m) {
   AR(qacc_int, nv); AR(cg_g, nv); AR(cg_mg, nv);
   AR(J, (size_t)m->njmax * nv); AR(efc_pos, m->njmax); AR(efc_margin, m->njmax); AR(efc_D, m->njmax);
   AR(efc_R, m->njmax); AR(efc_aref, m->njmax); AR(efc_fl, m->njmax); AR(jaref, m->njmax); AR(jv, m->njmax);
-  AR(efc_force, m->njmax);
+  AR(efc_force, m->njmax); AR(jtmp, m->njmax);
 #undef AR
   w->efc_type = (int*)xcalloc(m->njmax, sizeof(int));
   w->efc_id = (int*)xcalloc(m->njmax, sizeof(int));
@@ -200,7 +200,7 @@ static void ws_free(ws_t* w) {
                    &w->qfrc_smooth, &w->qfrc_bias, &w->qfrc_passive, &w->qfrc_actuator, &w->qfrc_constraint,
                    &w->act_force, &w->act_length, &w->act_vel, &w->tmpv, &w->tmpv2, &w->grad, &w->search, &w->Ma,
                    &w->Mv, &w->Mgrad, &w->qacc_int, &w->cg_g, &w->cg_mg, &w->J, &w->efc_pos, &w->efc_margin, &w->efc_D, &w->efc_R,
-                   &w->efc_aref, &w->efc_fl, &w->jaref, &w->jv, &w->efc_force};
+                   &w->efc_aref, &w->efc_fl, &w->jaref, &w->jv, &w->efc_force, &w->jtmp};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); i++) free(*ptrs[i]);
   free(w->efc_type);
   free(w->efc_id);
@@ -1106,9 +1106,16 @@ static void make_constraint(const or_model* m, int wi, ws_t* w) {
     real pos = c->dist - c->includemargin;
     if (pos >= 0) continue;
     int b1 = m->geom_bodyid[c->geom[0]], b2 = m->geom_bodyid[c->geom[1]];
-    int nrow = c->dim == 1 ? 1 : 2 * (c->dim - 1);
+    /* elliptic cones (opt.cone == mjCONE_ELLIPTIC): one row per contact
+       dimension (MuJoCo Warp constraint.py _efc_contact_elliptic, restated):
+       row 0 the normal, row j the frame direction j (tangents, then torsion and
+       rolling from the rotational Jacobian); the friction rows have no position
+       term (aref from the velocity only), impedance from the normal's distance,
+       invweight / impratio (times friction0^2 / friction_{j-1}^2 for j > 1) */
+    int ell = m->cone == 1 && c->dim > 1;
+    int nrow = c->dim == 1 ? 1 : (ell ? c->dim : 2 * (c->dim - 1));
     real invw = m->body_invweight0[2 * b1] + m->body_invweight0[2 * b2];
-    if (c->dim > 1) {
+    if (c->dim > 1 && !ell) {
       real f0 = c->friction[0];
       invw = invw + f0 * f0 * invw;
       invw = invw * 2 * f0 * f0 / m->impratio;
@@ -1134,9 +1141,22 @@ static void make_constraint(const or_model* m, int wi, ws_t* w) {
         return;
       }
       real* Jr = w->J + (size_t)r * nv;
+      real pos_aref = pos, invw_r = invw;
       if (c->dim == 1) {
         for (int d = 0; d < nv; d++) Jr[d] = jf[d];
         w->efc_type[r] = 5;
+      } else if (ell) {
+        for (int d = 0; d < nv; d++) Jr[d] = jf[e * nv + d];
+        w->efc_type[r] = 7;
+        real f0 = c->friction[0];
+        /* the cone's scale per row: mu = friction0 / sqrt(impratio) (the
+           regularised cone), friction_{j-1} for row j */
+        w->efc_fl[r] = e == 0 ? f0 / sqrt(m->impratio) : c->friction[e - 1];
+        if (e > 0) {
+          pos_aref = 0;
+          invw_r = invw / m->impratio;
+          if (e > 1) invw_r *= f0 * f0 / (c->friction[e - 1] * c->friction[e - 1]);
+        }
       } else {
         int k = e / 2 + 1;                           /* friction direction 1..dim-1 */
         const real* jt = k < 3 ? jf + k * nv : jf + (3 + k - 3) * nv; /* tangent (trans) or torsion/roll (rot) */
@@ -1148,7 +1168,7 @@ static void make_constraint(const or_model* m, int wi, ws_t* w) {
       w->efc_id[r] = ci;
       real jq = 0;
       for (int d = 0; d < nv; d++) jq += Jr[d] * w->qvel[d];
-      efc_row_params(m, w, r, pos, pos, invw, c->solref, c->solimp, c->includemargin, jq);
+      efc_row_params(m, w, r, pos_aref, pos, invw_r, c->solref, c->solimp, c->includemargin, jq);
     }
     free(jf);
   }
@@ -1176,17 +1196,99 @@ static real row_eval(const ws_t* w, int r, real jaref, real* force, real* cost) 
   *force = 0; *cost = 0; return 0;
 }
 
+/* elliptic cone contact at jar (its dim rows from r0): MuJoCo Warp solver.py
+   _update_constraint_efc (CONTACT_ELLIPTIC), MuJoCo engine_solver.c, restated.
+   U0 = mu jar0, Uj = friction_{j-1} jarj (the scales in efc_fl), N = U0,
+   T = |U1..|: the top zone (N >= mu T) is free; the bottom zone
+   (mu N + T <= 0) makes every row quadratic; between them the cone: cost
+   0.5 Dm (N - mu T)^2 with Dm = D0 / (mu^2 (1 + mu^2)). Writes the rows'
+   forces and, when H is given, the cost's Hessian in jar (dim x dim); returns
+   the cost. */
+static real cone_eval(const ws_t* w, int r0, int dim, const real* jar, real* force, real* H) {
+  const real mu = w->efc_fl[r0];
+  real U[6], TT = 0;
+  U[0] = jar[0] * mu;
+  for (int j = 1; j < dim; j++) {
+    U[j] = jar[j] * w->efc_fl[r0 + j];
+    TT += U[j] * U[j];
+  }
+  const real N = U[0], T = TT > 0 ? sqrt(TT) : 0;
+  if (H) memset(H, 0, sizeof(real) * dim * dim);
+  if (N >= mu * T || (T <= 0 && N >= 0)) { /* top zone */
+    for (int j = 0; j < dim; j++) force[j] = 0;
+    return 0;
+  }
+  if (mu * N + T <= 0 || (T <= 0 && N < 0)) { /* bottom zone */
+    real cost = 0;
+    for (int j = 0; j < dim; j++) {
+      const real D = w->efc_D[r0 + j];
+      force[j] = -D * jar[j];
+      cost += 0.5 * D * jar[j] * jar[j];
+      if (H) H[j * dim + j] = D;
+    }
+    return cost;
+  }
+  const real m2 = mu * mu * (1 + mu * mu);
+  const real Dm = w->efc_D[r0] / (m2 > MINVAL ? m2 : MINVAL), NmT = N - mu * T;
+  force[0] = -Dm * NmT * mu;
+  for (int j = 1; j < dim; j++) force[j] = -force[0] / T * U[j] * w->efc_fl[r0 + j];
+  if (H) {
+    /* in U: [1, -mu U^T / T; -mu U / T, mu N U U^T / T^3 + (mu^2 - mu N / T) I],
+       then scaled by Dm and the row scales on both sides */
+    real s[6];
+    s[0] = mu;
+    for (int j = 1; j < dim; j++) s[j] = w->efc_fl[r0 + j];
+    H[0] = 1;
+    for (int j = 1; j < dim; j++) H[j] = H[j * dim] = -mu * U[j] / T;
+    for (int j = 1; j < dim; j++)
+      for (int k = 1; k < dim; k++)
+        H[j * dim + k] = mu * N * U[j] * U[k] / (T * T * T) + (j == k ? mu * mu - mu * N / T : 0);
+    for (int j = 0; j < dim; j++)
+      for (int k = 0; k < dim; k++) H[j * dim + k] *= Dm * s[j] * s[k];
+  }
+  return 0.5 * Dm * NmT * NmT;
+}
+
+/* the rows' total cost at jar (cones per contact); sabs (if given) gathers
+   the magnitudes of the terms (the float32 evaluation's error scale) */
+static real rows_cost(const or_model* m, const ws_t* w, const real* jar, real* sabs) {
+  real cost = 0;
+  for (int r = 0; r < w->nefc; r++) {
+    real f[6], c;
+    if (w->efc_type[r] == 7) {
+      const int dim = w->con[w->efc_id[r]].dim;
+      c = cone_eval(w, r, dim, jar + r, f, NULL);
+      r += dim - 1;
+    } else {
+      row_eval(w, r, jar[r], f, &c);
+    }
+    cost += c;
+    if (sabs) *sabs += fabs(c);
+  }
+  (void)m;
+  return cost;
+}
+
 /* update forces/cost/qfrc_constraint at current jaref; returns total cost */
 static real update_constraint(const or_model* m, ws_t* w, const real* qacc_smooth) {
   int nv = m->nv;
   real cost = 0;
   memset(w->qfrc_constraint, 0, sizeof(real) * nv);
   for (int r = 0; r < w->nefc; r++) {
-    real f, c;
-    row_eval(w, r, w->jaref[r], &f, &c);
-    w->efc_force[r] = f;
+    real f[6], c;
+    int nr = 1;
+    if (w->efc_type[r] == 7) {
+      nr = w->con[w->efc_id[r]].dim;
+      c = cone_eval(w, r, nr, w->jaref + r, f, NULL);
+    } else {
+      row_eval(w, r, w->jaref[r], f, &c);
+    }
     cost += c;
-    for (int d = 0; d < nv; d++) w->qfrc_constraint[d] += w->J[(size_t)r * nv + d] * f;
+    for (int j = 0; j < nr; j++) {
+      w->efc_force[r + j] = f[j];
+      for (int d = 0; d < nv; d++) w->qfrc_constraint[d] += w->J[(size_t)(r + j) * nv + d] * f[j];
+    }
+    r += nr - 1;
   }
   real gauss = 0;
   for (int d = 0; d < nv; d++) gauss += 0.5 * (w->Ma[d] - w->qfrc_smooth[d]) * (w->qacc[d] - qacc_smooth[d]);
@@ -1226,6 +1328,24 @@ static void newton_direction(const or_model* m, ws_t* w) {
   for (int d = 0; d < nv; d++) w->grad[d] = w->Ma[d] - w->qfrc_smooth[d] - w->qfrc_constraint[d];
   memcpy(w->H, w->M, sizeof(real) * nv * nv);
   for (int r = 0; r < w->nefc; r++) {
+    if (w->efc_type[r] == 7) {
+      /* cone contact: J_c^T Hc J_c */
+      const int dim = w->con[w->efc_id[r]].dim;
+      real f[6], Hc[36];
+      cone_eval(w, r, dim, w->jaref + r, f, Hc);
+      for (int a = 0; a < dim; a++)
+        for (int b = 0; b < dim; b++) {
+          const real h = Hc[a * dim + b];
+          if (h == 0) continue;
+          const real *Ja = w->J + (size_t)(r + a) * nv, *Jb = w->J + (size_t)(r + b) * nv;
+          for (int i = 0; i < nv; i++) {
+            if (Ja[i] == 0) continue;
+            for (int j = 0; j <= i; j++) w->H[i * nv + j] += h * Ja[i] * Jb[j];
+          }
+        }
+      r += dim - 1;
+      continue;
+    }
     real f, c, h = row_eval(w, r, w->jaref[r], &f, &c);
     if (h == 0) continue;
     const real* Jr = w->J + (size_t)r * nv;
@@ -1274,6 +1394,28 @@ static void direction(const or_model* m, ws_t* w, int first) {
     newton_direction(m, w);
 }
 
+/* adds the rows' first and second derivatives along jv at step alpha */
+static void rows_derivs(ws_t* w, real alpha, real* d1, real* d2) {
+  for (int r = 0; r < w->nefc; r++) {
+    if (w->efc_type[r] == 7) {
+      const int dim = w->con[w->efc_id[r]].dim;
+      real jar[6], f[6], Hc[36];
+      for (int j = 0; j < dim; j++) jar[j] = w->jaref[r + j] + alpha * w->jv[r + j];
+      cone_eval(w, r, dim, jar, f, Hc);
+      for (int a = 0; a < dim; a++) {
+        *d1 -= f[a] * w->jv[r + a];
+        for (int b = 0; b < dim; b++) *d2 += w->jv[r + a] * Hc[a * dim + b] * w->jv[r + b];
+      }
+      r += dim - 1;
+      continue;
+    }
+    real ja = w->jaref[r] + alpha * w->jv[r], f, c;
+    real h = row_eval(w, r, ja, &f, &c);
+    *d1 -= f * w->jv[r];
+    *d2 += h * w->jv[r] * w->jv[r];
+  }
+}
+
 /* exact line search on the convex piecewise-quadratic cost along search */
 static real linesearch(const or_model* m, ws_t* w) {
   int nv = m->nv;
@@ -1306,12 +1448,8 @@ static real linesearch(const or_model* m, ws_t* w) {
       real a = exp(lmin + k * lstep), c = a * (g1 + 0.5 * a * g2);
       /* magnitude of the summed terms: the float32 evaluation's error scale */
       real s = fabs(a * g1) + fabs(0.5 * a * a * g2);
-      for (int r = 0; r < w->nefc; r++) {
-        real f, cr;
-        row_eval(w, r, w->jaref[r] + a * w->jv[r], &f, &cr);
-        c += cr;
-        s += fabs(cr);
-      }
+      for (int r = 0; r < w->nefc; r++) w->jtmp[r] = w->jaref[r] + a * w->jv[r];
+      c += rows_cost(m, w, w->jtmp, &s);
       if (k == fi) { cf = c; sf = s; }
       if (k < 64) g_dbg_scan_cost[k] = c;
       if (c < best) sb = s;
@@ -1360,12 +1498,7 @@ static real linesearch(const or_model* m, ws_t* w) {
   do {                                                                \
     d1 = g1 + (alpha) * g2;                                           \
     d2 = g2;                                                          \
-    for (int r = 0; r < w->nefc; r++) {                               \
-      real ja = w->jaref[r] + (alpha) * w->jv[r], f, c;               \
-      real h = row_eval(w, r, ja, &f, &c);                            \
-      d1 -= f * w->jv[r];                                             \
-      d2 += h * w->jv[r] * w->jv[r];                                  \
-    }                                                                 \
+    rows_derivs(w, alpha, &d1, &d2);                                  \
   } while (0)
   real d10, d20;
   DERIVS(0.0, d10, d20);
@@ -1403,13 +1536,12 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     w->jaref[r] = s - w->efc_aref[r];
   }
   real cost = update_constraint(m, w, w->qacc_smooth);
-  real cost_smooth = 0;
   for (int r = 0; r < w->nefc; r++) {
-    real s = 0, f, c;
+    real s = 0;
     for (int d = 0; d < nv; d++) s += w->J[(size_t)r * nv + d] * w->qacc_smooth[d];
-    row_eval(w, r, s - w->efc_aref[r], &f, &c);
-    cost_smooth += c;
+    w->jtmp[r] = s - w->efc_aref[r];
   }
+  real cost_smooth = rows_cost(m, w, w->jtmp, NULL);
   if (g_dbg_warm) {
     g_dbg_warm[2 * (size_t)w->wi] = cost;
     g_dbg_warm[2 * (size_t)w->wi + 1] = cost_smooth;
@@ -1485,8 +1617,11 @@ static void contact_force(const or_model* m, ws_t* w, int ci, real f[6]) {
   memset(f, 0, 6 * sizeof(real));
   if (c->efc_address < 0) return;
   const real* ef = w->efc_force + c->efc_address;
-  (void)m;
   if (c->dim == 1) { f[0] = ef[0]; return; }
+  if (m->cone == 1) { /* elliptic: the rows are the frame components */
+    for (int k = 0; k < c->dim; k++) f[k] = ef[k];
+    return;
+  }
   for (int e = 0; e < 2 * (c->dim - 1); e++) f[0] += ef[e];
   for (int k = 1; k < c->dim; k++) f[k] = c->friction[k - 1] * (ef[2 * k - 2] - ef[2 * k - 1]);
 }

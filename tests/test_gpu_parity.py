@@ -482,3 +482,72 @@ def test_box_on_box_carries_its_weight_on_gpu():
   assert np.allclose(fz[-100:].mean(axis=0), 2.0 * 9.81, rtol=0.01)
   q = sim.data.qpos.cpu().numpy()
   assert np.abs(q[:, 2] - 0.2).max() < 2e-3
+
+
+@pytest.mark.parametrize("ls_parallel", [True, False])
+def test_elliptic_cone_parity(ls_parallel):
+  """MujocoCfg(cone="elliptic") (reference sim.py:25-28,51 maps it to
+  mjCONE_ELLIPTIC; MuJoCo Warp solves it): one row per contact dimension, the
+  cone cost per contact, its Hessian block as virtual rows (csrc/mjh_step.hip
+  cone_eval / newton_direction), against the oracle's elliptic restatement
+  (oracle.c cone_eval: the block formed directly), both line searches, the
+  capped iteration count (follow mode for the parallel search)."""
+  n = 256
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(61))
+  cfg = dict(CFG, mujoco=MujocoCfg(timestep=0.005, iterations=10, ls_iterations=20, cone="elliptic"))
+  sim = Simulation(n, SimulationCfg(**cfg, ls_parallel=ls_parallel), m, DEV)
+  assert m.cone == 1
+  put(sim, st)
+  sim.step()
+  got = get(sim, n)
+  types = {int(t) for w in range(n) for t in got["efc_type"][w, : int(got["nefc"][w, 0])]}
+  assert 7 in types and 6 not in types, types
+  ref = Oracle(m).run(n, st, integrate=True, follow=got if ls_parallel else None)
+  assert_parity(got, ref, n, tag=f" elliptic ls_parallel={ls_parallel}")
+
+
+def test_elliptic_cone_converged_parity():
+  """Elliptic cones with the iteration cap lifted (exact line search,
+  iterations 100, tolerance 1e-10): the HIP solve and the float64 oracle reach
+  the same qacc in every world (the cone Hessian only shapes the path)."""
+  n = 256
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(63))
+  cfg = dict(CFG, mujoco=MujocoCfg(timestep=0.005, iterations=100, ls_iterations=50, tolerance=1e-10, cone="elliptic"))
+  sim = Simulation(n, SimulationCfg(**cfg, ls_parallel=False), m, DEV)
+  put(sim, st)
+  sim.forward()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=False)
+  rep = compare_step(got, ref, solve_rel=1e-4, solve_frac=1.0, solve_max=1e-4)
+  print("[elliptic converged]", rep["int_match_rate"], {k: f"{v:.2e}" for k, v in rep["maxerr"].items() if "/" in k},
+        "niter", got["solver_niter"].mean(), ref["solver_niter"].mean())
+  assert not rep["failures"], rep["failures"]
+
+
+@pytest.mark.parametrize("cone,factor", [("elliptic", 1.0), ("pyramidal", 2 ** -0.5)])
+def test_diagonal_sliding_by_cone_on_gpu(cone, factor):
+  """tests/test_oracle_known_answers.py::test_diagonal_sliding_by_cone on the
+  HIP step: a block on an incline (tan 0.8 > mu 0.65) tilted along the
+  frame's tangent diagonal slides with a = g (sin - factor mu cos), factor 1
+  for the elliptic cone and 1/sqrt(2) for the pyramidal one."""
+  from mjlab_amd.spec.compiler import compile_spec
+  from mjlab_amd.spec.mjcf import read_mjcf_string
+
+  mu, g = 0.65, 9.81
+  th = np.arctan(0.8)
+  gt = g * np.sin(th) / np.sqrt(2)
+  xml = f"""<mujoco><option timestep="0.002" gravity="{gt} {gt} {-g * np.cos(th)}"/><worldbody>
+  <geom name="floor" type="plane" size="5 5 0.1" friction="{mu} 0.005 0.0001"/>
+  <body name="blk" pos="0 0 0.05"><freejoint/><geom type="box" size="0.1 0.1 0.05" mass="1" friction="{mu} 0.005 0.0001"/></body>
+  </worldbody></mujoco>"""
+  m = compile_spec(read_mjcf_string(xml), 8, 64)
+  sim = Simulation(2, SimulationCfg(nconmax=8, njmax=64, mujoco=MujocoCfg(timestep=0.002, iterations=20, cone=cone)), m, DEV)
+  sp = []
+  for _ in range(500):
+    sim.step()
+    v = sim.data.qvel[0, :2].cpu().numpy()
+    sp.append(float(np.hypot(v[0], v[1])))
+  a = (sp[-1] - sp[249]) / (250 * 0.002)
+  assert a == pytest.approx(g * (np.sin(th) - factor * mu * np.cos(th)), rel=0.05)

@@ -332,3 +332,86 @@ def test_cg_and_newton_reach_the_same_minimiser():
   scale = 1 + np.abs(newton["qacc"]).max(axis=1, keepdims=True)
   assert (np.abs(cg["qacc"] - newton["qacc"]) / scale).max() < 1e-6
   assert cg["solver_niter"].mean() > newton["solver_niter"].mean()
+
+
+@pytest.mark.parametrize("tan_theta,slides", [(0.5, False), (0.8, True)])
+def test_elliptic_cone_incline_stick_slip_threshold(tan_theta, slides):
+  """The incline of test_block_on_incline_stick_slip_threshold with elliptic
+  cones (opt.cone = mjCONE_ELLIPTIC, impratio 1: the regularised cone's
+  mu = friction0): the same threshold tan(theta) = mu and sliding acceleration
+  g (sin(theta) - mu cos(theta)); the rows are the contact frame's
+  components (3 per contact instead of 4 pyramid edges)."""
+  mu, g = 0.65, 9.81
+  th = np.arctan(tan_theta)
+  grav = f"{g * np.sin(th)} 0 {-g * np.cos(th)}"
+  xml = _free_body_xml(
+    f"""<body name="blk" pos="0 0 0.05"><freejoint/><geom type="box" size="0.1 0.1 0.05" mass="1" friction="{mu} 0.005 0.0001"/></body>""",
+    gravity=grav, plane=f'<geom name="floor" type="plane" size="5 5 0.1" friction="{mu} 0.005 0.0001"/>')
+  m = _model(xml, cone=1)
+  orc = Oracle(m)
+  st = {"qpos": m.qpos0[None].copy()}
+  vx = []
+  for i in range(500):  # 1 s
+    out = orc.run(1, st, integrate=True)
+    if i == 10:
+      nc = int(out["ncon"][0, 0])
+      assert nc == 4 and int(out["nefc"][0, 0]) == 3 * nc
+      assert set(out["efc_type"][0, : 3 * nc].tolist()) == {7}
+    st = {k: out[k] for k in ("qpos", "qvel", "qacc_warmstart", "time")}
+    vx.append(st["qvel"][0, 0])
+  if slides:
+    a = (vx[-1] - vx[249]) / (250 * m.timestep)
+    assert a == pytest.approx(g * (np.sin(th) - mu * np.cos(th)), rel=0.05)
+  else:
+    assert abs(vx[-1]) < 5e-3 and abs(st["qpos"][0, 0]) < 5e-3
+
+
+@pytest.mark.parametrize("cone,factor", [(1, 1.0), (0, 2 ** -0.5)])
+def test_diagonal_sliding_by_cone(cone, factor):
+  """The incline of test_block_on_incline_stick_slip_threshold (tan(theta) =
+  0.8 > mu = 0.65) tilted along the diagonal of the contact frame's tangents:
+  an elliptic cone (the friction disc) resists the slide with mu N, the
+  pyramidal cone, whose edges lie along the tangents (each direction's
+  friction takes a share of the normal force), with mu N / sqrt(2) at most:
+  a = g (sin(theta) - factor mu cos(theta)). The two cone types apart."""
+  mu, g = 0.65, 9.81
+  th = np.arctan(0.8)
+  gt = g * np.sin(th) / np.sqrt(2)
+  xml = _free_body_xml(
+    f"""<body name="blk" pos="0 0 0.05"><freejoint/><geom type="box" size="0.1 0.1 0.05" mass="1" friction="{mu} 0.005 0.0001"/></body>""",
+    gravity=f"{gt} {gt} {-g * np.cos(th)}",
+    plane=f'<geom name="floor" type="plane" size="5 5 0.1" friction="{mu} 0.005 0.0001"/>')
+  m = _model(xml, cone=cone)
+  orc = Oracle(m)
+  st = {"qpos": m.qpos0[None].copy()}
+  sp = []
+  for _ in range(500):  # 1 s
+    out = orc.run(1, st, integrate=True)
+    st = {k: out[k] for k in ("qpos", "qvel", "qacc_warmstart", "time")}
+    sp.append(np.hypot(st["qvel"][0, 0], st["qvel"][0, 1]))
+  a = (sp[-1] - sp[249]) / (250 * m.timestep)
+  assert a == pytest.approx(g * (np.sin(th) - factor * mu * np.cos(th)), rel=0.05)
+  assert abs(st["qvel"][0, 0] - st["qvel"][0, 1]) < 1e-6  # stays on the diagonal
+
+
+def test_elliptic_newton_converges_fast_and_matches_cg():
+  """Elliptic cones on the G1 scene: Newton (with the cone's Hessian blocks)
+  and CG reach the same qacc with the iteration cap lifted, Newton in few
+  iterations (a wrong cone Hessian would still descend, but slowly)."""
+  from tests.scenes import random_states
+
+  n = 16
+  m = g1_scene_model(n)
+  m.cone = 1
+  m.iterations, m.tolerance, m.ls_iterations, m.ls_parallel = 300, 1e-14, 50, 0
+  st = random_states(m, n, np.random.default_rng(33))
+  m.solver = 2
+  newton = Oracle(m).run(n, st, integrate=False)
+  m.solver = 1
+  cg = Oracle(m).run(n, st, integrate=False)
+  assert (newton["ncon"] > 0).mean() > 0.8
+  types = {int(t) for w in range(n) for t in newton["efc_type"][w, : int(newton["nefc"][w, 0])]}
+  assert 7 in types and 6 not in types
+  scale = 1 + np.abs(newton["qacc"]).max(axis=1, keepdims=True)
+  assert (np.abs(cg["qacc"] - newton["qacc"]) / scale).max() < 1e-6
+  assert newton["solver_niter"].mean() < 20 < cg["solver_niter"].mean()
