@@ -543,7 +543,9 @@ def test_diagonal_sliding_by_cone_on_gpu(cone, factor):
   <body name="blk" pos="0 0 0.05"><freejoint/><geom type="box" size="0.1 0.1 0.05" mass="1" friction="{mu} 0.005 0.0001"/></body>
   </worldbody></mujoco>"""
   m = compile_spec(read_mjcf_string(xml), 8, 64)
-  sim = Simulation(2, SimulationCfg(nconmax=8, njmax=64, mujoco=MujocoCfg(timestep=0.002, iterations=20, cone=cone)), m, DEV)
+  # MujocoCfg.apply sets the gravity (as the reference's does), so the tilt goes there
+  sim = Simulation(2, SimulationCfg(nconmax=8, njmax=64, mujoco=MujocoCfg(timestep=0.002, iterations=20, cone=cone,
+                                                                           gravity=(gt, gt, -g * np.cos(th)))), m, DEV)
   sp = []
   for _ in range(500):
     sim.step()

@@ -10,6 +10,11 @@ O=gpurun_out/$TAG
 mkdir -p $O
 t() { echo "[$(date +%T)] $*"; }
 if [ -n "$DIAG" ]; then timeout -k 10 120 python $DIAG > $O/diag.log 2>&1; tail -30 $O/diag.log; fi
+if [ -n "$PHASE" ]; then
+  t phase
+  timeout -k 10 180 python tools/phase_profile.py 4096 > $O/phase.log 2>&1 || { tail -20 $O/phase.log; exit 1; }
+  tail -40 $O/phase.log
+fi
 t tests
 timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gputests.log 2>&1 || { tail -30 $O/gputests.log; exit 1; }
 tail -2 $O/gputests.log
