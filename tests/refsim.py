@@ -59,7 +59,7 @@ class Shadow:
     got = {k: v.detach().cpu().numpy().reshape(n, -1) for k, v in sim._data_flat.items()}
     ov = {f: sim._model_flat[f].detach().cpu().numpy() for f, s in sim._wstride.items() if s}
     ref = Oracle(sim.mj_model, "f64", overrides=ov).run(n, st, integrate=integrate, follow=got)
-    rep = compare_step(got, ref, dt=float(sim.mj_model.timestep))
+    rep = compare_step(got, ref, dt=float(sim.mj_model.timestep), skip=self.skip)
     self.nsteps += 1
     self.int_mismatch_worlds += len(rep["int_mismatch_worlds"])
     for k, v in rep["maxerr"].items():
