@@ -1091,12 +1091,157 @@ __device__ __noinline__ int box_box(Con* out, float margin, const float* pa, con
   return 1;
 }
 
+// plane (geom1) - cylinder (geom2): the oracle's raw_plane_cylinder (MuJoCo
+// mjc_PlaneCylinder) in float32: nearer-cap and farther-cap rim points, then
+// the nearer cap's rim points 120 degrees either side of the first
+__device__ __noinline__ int plane_cylinder(Con* out, float margin, const float* pp, const float* pm, const float* cp,
+                                           const float* cm, float r, float h) {
+  const float n[3] = {pm[2], pm[5], pm[8]};
+  float ax[3] = {cm[2], cm[5], cm[8]};
+  float prjaxis = dot3(n, ax);
+  if (prjaxis > 0.f) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) ax[k] = -ax[k];
+    prjaxis = -prjaxis;
+  }
+  const float dif[3] = {cp[0] - pp[0], cp[1] - pp[1], cp[2] - pp[2]};
+  const float dist0 = dot3(dif, n);
+  float vec[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) vec[k] = ax[k] * prjaxis - n[k];
+  const float len = sqrtf(dot3(vec, vec));
+  if (len < MJH_MINVAL) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) vec[k] = cm[3 * k] * r;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; k++) vec[k] *= r / len;
+  }
+  const float prjvec = dot3(vec, n);
+#pragma unroll
+  for (int k = 0; k < 3; k++) ax[k] *= h;
+  prjaxis *= h;
+  int cnt = 0;
+  for (int e = 0; e < 2; e++) {
+    const float sg = e == 0 ? 1.f : -1.f, dist = dist0 + sg * prjaxis + prjvec;
+    if (dist > margin) continue;
+    Con* c = out + cnt++;
+    c->dist = dist;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      c->pos[k] = cp[k] + vec[k] + sg * ax[k] - n[k] * 0.5f * dist;
+      c->frame[k] = n[k];
+      c->frame[3 + k] = 0.f;
+    }
+  }
+  const float dist = dist0 + prjaxis - 0.5f * prjvec;
+  if (dist <= margin) {
+    float side[3];
+    cross3(side, vec, ax);
+    const float sl = sqrtf(dot3(side, side));
+#pragma unroll
+    for (int k = 0; k < 3; k++) side[k] = sl > MJH_MINVAL ? side[k] * (r * 0.8660254037844386f / sl) : 0.f;
+    for (int e = 0; e < 2; e++) {
+      const float sg = e == 0 ? 1.f : -1.f;
+      Con* c = out + cnt++;
+      c->dist = dist;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        c->pos[k] = cp[k] + ax[k] - 0.5f * vec[k] + sg * side[k] - n[k] * 0.5f * dist;
+        c->frame[k] = n[k];
+        c->frame[3 + k] = 0.f;
+      }
+    }
+  }
+  return cnt;
+}
+
+// plane (geom1) - ellipsoid (geom2): the support point against the normal
+// (oracle raw_plane_ellipsoid, MuJoCo Warp plane_ellipsoid)
+__device__ __noinline__ int plane_ellipsoid(Con* c, float margin, const float* pp, const float* pm, const float* ep,
+                                            const float* em, const float* s) {
+  const float n[3] = {pm[2], pm[5], pm[8]};
+  float nl[3], u[3], pl[3], pw[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) nl[k] = em[k] * n[0] + em[3 + k] * n[1] + em[6 + k] * n[2];
+#pragma unroll
+  for (int k = 0; k < 3; k++) u[k] = s[k] * nl[k];
+  const float ul = fmaxf(sqrtf(dot3(u, u)), MJH_MINVAL);
+#pragma unroll
+  for (int k = 0; k < 3; k++) pl[k] = -s[k] * u[k] / ul;
+#pragma unroll
+  for (int k = 0; k < 3; k++) pw[k] = em[3 * k] * pl[0] + em[3 * k + 1] * pl[1] + em[3 * k + 2] * pl[2];
+  const float dif[3] = {ep[0] + pw[0] - pp[0], ep[1] + pw[1] - pp[1], ep[2] + pw[2] - pp[2]};
+  const float dist = dot3(dif, n);
+  if (dist > margin) return 0;
+  c->dist = dist;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    c->pos[k] = ep[k] + pw[k] - n[k] * 0.5f * dist;
+    c->frame[k] = n[k];
+    c->frame[3 + k] = 0.f;
+  }
+  return 1;
+}
+
+// sphere (geom1) - cylinder (geom2): side, cap or rim (oracle
+// raw_sphere_cylinder, MuJoCo Warp sphere_cylinder)
+__device__ __noinline__ int sphere_cylinder(Con* c, float margin, const float* sp, float rs, const float* cp, const float* cm,
+                                            float r, float h) {
+  const float ax[3] = {cm[2], cm[5], cm[8]};
+  const float v[3] = {sp[0] - cp[0], sp[1] - cp[1], sp[2] - cp[2]};
+  const float x = dot3(v, ax);
+  float pr[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) pr[k] = v[k] - ax[k] * x;
+  const float pr2 = dot3(pr, pr);
+  bool side = fabsf(x) < h, cap = pr2 < r * r;
+  if (side && cap) {
+    if (h - fabsf(x) < r - sqrtf(pr2)) side = false; else cap = false;
+  }
+  if (side) {
+    const float q[3] = {cp[0] + ax[0] * x, cp[1] + ax[1] * x, cp[2] + ax[2] * x};
+    return sphere_sphere(c, margin, sp, rs, q, r);
+  }
+  const float sg = x > 0.f ? 1.f : -1.f;
+  if (cap) {
+    float nrm[3], d[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      nrm[k] = -sg * ax[k];
+      d[k] = sp[k] - (cp[k] + sg * ax[k] * h);
+    }
+    const float dist = -dot3(d, nrm) - rs;
+    if (dist > margin) return 0;
+    c->dist = dist;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      c->pos[k] = sp[k] + nrm[k] * (rs + 0.5f * dist);
+      c->frame[k] = nrm[k];
+      c->frame[3 + k] = 0.f;
+    }
+    return 1;
+  }
+  const float prl = sqrtf(pr2);
+  float q[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) q[k] = cp[k] + sg * ax[k] * h + (prl > MJH_MINVAL ? pr[k] * (r / prl) : 0.f);
+  return sphere_sphere(c, margin, sp, rs, q, 0.f);
+}
+
 // Narrowphase for one pair (types ascending). Up to 4 contacts. `boxes`: the
-// model has pairs that need the box functions (Sizes::nboxpair; a compile-time
+// model has pairs that need the box, cylinder or ellipsoid functions
+// (Sizes::nboxpair; a compile-time
 // 0 in the model-specialised instances of models without such pairs, whose
 // code then carries none of them).
 __device__ MJH_COLL_INLINE int narrowphase(int t1, int t2, const float* p1, const float* m1, const float* s1, const float* p2,
                            const float* m2, const float* s2, float margin, Con* out, bool boxes) {
+  if (boxes && (t2 == 4 || t2 == 5)) {
+    if (t1 == 0 && t2 == 4) return plane_ellipsoid(out, margin, p1, m1, p2, m2, s2);
+    if (t1 == 0 && t2 == 5) return plane_cylinder(out, margin, p1, m1, p2, m2, s2[0], s2[1]);
+    if (t1 == 2 && t2 == 5) return sphere_cylinder(out, margin, p1, s1[0], p2, m2, s2[0], s2[1]);
+    return 0;
+  }
   if (boxes && t2 == 6 && t1 >= 2) {
     if (t1 == 2) return sphere_box(out, margin, p1, s1[0], p2, m2, s2);
     if (t1 == 3) {

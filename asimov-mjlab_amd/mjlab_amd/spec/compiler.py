@@ -32,9 +32,9 @@ from mjlab_amd.spec.spec import GEOM_TYPES, JOINT_TYPES, Spec
 from mjlab_amd.utils import rot
 
 MINVAL = 1e-15
-SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 6), (2, 2), (2, 3), (3, 3), (2, 6), (3, 6), (6, 6)}
-# pairs that need the box narrowphase functions (Model.nboxpair counts them)
-BOX_PAIRS = {(2, 6), (3, 6), (6, 6)}
+SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 4), (0, 5), (0, 6), (2, 2), (2, 3), (2, 5), (3, 3), (2, 6), (3, 6), (6, 6)}
+# pairs that need the box, cylinder or ellipsoid narrowphase functions (Model.nboxpair counts them)
+BOX_PAIRS = {(2, 6), (3, 6), (6, 6), (0, 4), (0, 5), (2, 5)}
 
 # Sensor type codes used by the kernels (order is ours; names follow mjtSensor).
 SENSOR_TYPES = {
@@ -236,8 +236,10 @@ def _geom_rbound(gtype: str, size: np.ndarray) -> float:
     return size[0] + size[1]
   if gtype == "cylinder":
     return math.hypot(size[0], size[1])
-  if gtype in ("box", "ellipsoid"):
+  if gtype == "box":
     return float(np.linalg.norm(size))
+  if gtype == "ellipsoid":
+    return float(np.max(size))
   return 0.0
 
 
@@ -748,8 +750,8 @@ def _compile_pairs(m: Model, spec: Spec) -> None:
       colgeoms.add(g1)
       colgeoms.add(g2)
   # geom-type pairs with a narrowphase in the HIP step (and the oracle):
-  # plane-{sphere,capsule,box}, sphere-{sphere,capsule,box}, capsule-{capsule,box},
-  # box-box.
+  # plane-{sphere,capsule,ellipsoid,cylinder,box}, sphere-{sphere,capsule,cylinder,box},
+  # capsule-{capsule,box}, box-box.
   # Other pairs stay in the table (the kernels return no contact for them)
   # and are reported here instead of being silently ignored.
   unsupported = sorted({(int(m.geom_type[a]), int(m.geom_type[b])) for a, b in pairs

@@ -864,6 +864,136 @@ static int raw_box_box(contact_t* out, real margin, const real pa[3], const real
   return 1;
 }
 
+/* plane (geom1) - cylinder (geom2, radius r, half height h): MuJoCo's
+   mjc_PlaneCylinder / MuJoCo Warp collision_primitive.plane_cylinder,
+   restated: the rim point of the nearer cap closest to the plane, the same rim
+   direction on the farther cap, then the nearer cap's rim points 120 degrees
+   either side of the first (a cylinder standing on the plane: 3 contacts;
+   lying on it: 2) */
+static int raw_plane_cylinder(contact_t* out, real margin, const real pp[3], const real pm[9], const real cp[3],
+                              const real cm[9], real r, real h) {
+  const real n[3] = {pm[2], pm[5], pm[8]};
+  real ax[3] = {cm[2], cm[5], cm[8]};
+  real prjaxis = dot3(n, ax);
+  if (prjaxis > 0) {
+    for (int k = 0; k < 3; k++) ax[k] = -ax[k];
+    prjaxis = -prjaxis;
+  }
+  const real dif[3] = {cp[0] - pp[0], cp[1] - pp[1], cp[2] - pp[2]};
+  const real dist0 = dot3(dif, n);
+  real vec[3];
+  for (int k = 0; k < 3; k++) vec[k] = ax[k] * prjaxis - n[k];
+  const real len = norm3(vec);
+  if (len < MINVAL) { /* axis along the normal: any rim direction */
+    for (int k = 0; k < 3; k++) vec[k] = cm[3 * k] * r;
+  } else {
+    for (int k = 0; k < 3; k++) vec[k] *= r / len;
+  }
+  const real prjvec = dot3(vec, n);
+  for (int k = 0; k < 3; k++) ax[k] *= h;
+  prjaxis *= h;
+  int cnt = 0;
+  for (int e = 0; e < 2; e++) {
+    const real sg = e == 0 ? 1 : -1, dist = dist0 + sg * prjaxis + prjvec;
+    if (dist > margin) continue;
+    contact_t* c = out + cnt++;
+    c->dist = dist;
+    for (int k = 0; k < 3; k++) {
+      c->pos[k] = cp[k] + vec[k] + sg * ax[k] - n[k] * 0.5 * dist;
+      c->frame[k] = n[k];
+      c->frame[3 + k] = 0;
+    }
+  }
+  const real dist = dist0 + prjaxis - 0.5 * prjvec;
+  if (dist <= margin) {
+    real side[3];
+    cross3(side, vec, ax);
+    const real sl = norm3(side);
+    for (int k = 0; k < 3; k++) side[k] = sl > MINVAL ? side[k] * (r * sqrt(3.0) * 0.5 / sl) : 0;
+    for (int e = 0; e < 2; e++) {
+      const real sg = e == 0 ? 1 : -1;
+      contact_t* c = out + cnt++;
+      c->dist = dist;
+      for (int k = 0; k < 3; k++) {
+        c->pos[k] = cp[k] + ax[k] - 0.5 * vec[k] + sg * side[k] - n[k] * 0.5 * dist;
+        c->frame[k] = n[k];
+        c->frame[3 + k] = 0;
+      }
+    }
+  }
+  return cnt;
+}
+
+/* plane (geom1) - ellipsoid (geom2, semi-axes s): the ellipsoid's support
+   point against the plane normal (MuJoCo Warp plane_ellipsoid, restated):
+   in the ellipsoid frame p = -S^2 n_l / |S n_l| */
+static int raw_plane_ellipsoid(contact_t* c, real margin, const real pp[3], const real pm[9], const real ep[3],
+                               const real em[9], const real s[3]) {
+  const real n[3] = {pm[2], pm[5], pm[8]};
+  real nl[3], u[3], pl[3], pw[3];
+  for (int k = 0; k < 3; k++) nl[k] = em[k] * n[0] + em[3 + k] * n[1] + em[6 + k] * n[2];
+  for (int k = 0; k < 3; k++) u[k] = s[k] * nl[k];
+  const real ul = norm3(u);
+  for (int k = 0; k < 3; k++) pl[k] = -s[k] * u[k] / (ul > MINVAL ? ul : MINVAL);
+  for (int k = 0; k < 3; k++) pw[k] = em[3 * k] * pl[0] + em[3 * k + 1] * pl[1] + em[3 * k + 2] * pl[2];
+  real dif[3];
+  for (int k = 0; k < 3; k++) dif[k] = ep[k] + pw[k] - pp[k];
+  const real dist = dot3(dif, n);
+  if (dist > margin) return 0;
+  c->dist = dist;
+  for (int k = 0; k < 3; k++) {
+    c->pos[k] = ep[k] + pw[k] - n[k] * 0.5 * dist;
+    c->frame[k] = n[k];
+    c->frame[3 + k] = 0;
+  }
+  return 1;
+}
+
+/* sphere (geom1, radius rs) - cylinder (geom2, radius r, half height h)
+   (MuJoCo Warp sphere_cylinder, restated): against the side when the centre
+   projects onto the shaft, against the cap when it lies over the cap disc
+   (inside: whichever surface is nearer), otherwise against the rim circle */
+static int raw_sphere_cylinder(contact_t* c, real margin, const real sp[3], real rs, const real cp[3], const real cm[9],
+                               real r, real h) {
+  const real ax[3] = {cm[2], cm[5], cm[8]};
+  const real v[3] = {sp[0] - cp[0], sp[1] - cp[1], sp[2] - cp[2]};
+  const real x = dot3(v, ax);
+  real pr[3];
+  for (int k = 0; k < 3; k++) pr[k] = v[k] - ax[k] * x;
+  const real pr2 = dot3(pr, pr);
+  int side = fabs(x) < h, cap = pr2 < r * r;
+  if (side && cap) { /* centre inside: the nearer surface */
+    if (h - fabs(x) < r - sqrt(pr2)) side = 0; else cap = 0;
+  }
+  if (side) { /* the shaft point level with the centre, as a sphere of radius r */
+    real q[3];
+    for (int k = 0; k < 3; k++) q[k] = cp[k] + ax[k] * x;
+    return raw_sphere_sphere(c, margin, sp, rs, q, r);
+  }
+  if (cap) { /* the cap plane, normal from the sphere into the cylinder */
+    const real sg = x > 0 ? 1 : -1;
+    real nrm[3], q[3];
+    for (int k = 0; k < 3; k++) { nrm[k] = -sg * ax[k]; q[k] = cp[k] + sg * ax[k] * h; }
+    real d[3];
+    for (int k = 0; k < 3; k++) d[k] = sp[k] - q[k];
+    const real dist = -dot3(d, nrm) - rs;
+    if (dist > margin) return 0;
+    c->dist = dist;
+    for (int k = 0; k < 3; k++) {
+      c->pos[k] = sp[k] + nrm[k] * (rs + 0.5 * dist);
+      c->frame[k] = nrm[k];
+      c->frame[3 + k] = 0;
+    }
+    return 1;
+  }
+  /* the rim: the circle point nearest the centre, as a sphere of radius 0 */
+  const real prl = sqrt(pr2);
+  real q[3];
+  const real sg = x > 0 ? 1 : -1;
+  for (int k = 0; k < 3; k++) q[k] = cp[k] + sg * ax[k] * h + (prl > MINVAL ? pr[k] * (r / prl) : 0);
+  return raw_sphere_sphere(c, margin, sp, rs, q, 0);
+}
+
 static int collide(const or_model* m, ws_t* w, int g1, int g2, real margin, contact_t* out) {
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   const real *p1 = w->gxpos + 3 * g1, *m1 = w->gxmat + 9 * g1, *s1 = m->geom_size + 3 * g1;
@@ -944,6 +1074,9 @@ static int collide(const or_model* m, ws_t* w, int g1, int g2, real margin, cont
     }
     return n;
   }
+  if (t1 == 0 && t2 == 4) return raw_plane_ellipsoid(out, margin, p1, m1, p2, m2, s2);
+  if (t1 == 0 && t2 == 5) return raw_plane_cylinder(out, margin, p1, m1, p2, m2, s2[0], s2[1]);
+  if (t1 == 2 && t2 == 5) return raw_sphere_cylinder(out, margin, p1, s1[0], p2, m2, s2[0], s2[1]);
   if (t1 == 2 && t2 == 6) return raw_sphere_box(out, margin, p1, s1[0], p2, m2, s2);
   if (t1 == 3 && t2 == 6) {
     real ax[3] = {m1[2], m1[5], m1[8]};

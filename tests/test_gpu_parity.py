@@ -553,3 +553,44 @@ def test_diagonal_sliding_by_cone_on_gpu(cone, factor):
     sp.append(float(np.hypot(v[0], v[1])))
   a = (sp[-1] - sp[249]) / (250 * 0.002)
   assert a == pytest.approx(g * (np.sin(th) - factor * mu * np.cos(th)), rel=0.05)
+
+
+CYL_SCENE = """<mujoco><compiler angle="radian"/><option timestep="0.002"/><worldbody>
+<geom name="floor" type="plane" size="5 5 0.1" contype="1" conaffinity="1"/>
+<geom name="post" type="cylinder" size="0.08 0.25" pos="0.3 0 0.25" contype="0" conaffinity="2"/>
+<body name="can" pos="0 0 0.3"><freejoint/><geom type="cylinder" size="0.1 0.15" mass="1.2" contype="1" conaffinity="2"/></body>
+<body name="egg" pos="-0.3 0 0.3"><freejoint/><geom type="ellipsoid" size="0.15 0.1 0.07" mass="0.8" contype="1" conaffinity="4"/></body>
+<body name="ball" pos="0.2 0.2 0.3"><freejoint/><geom type="sphere" size="0.07" mass="0.5" contype="2" conaffinity="0"/></body>
+</worldbody></mujoco>"""
+
+
+def test_cylinder_ellipsoid_pairs_parity():
+  """plane-cylinder, plane-ellipsoid and sphere-cylinder (against a moving
+  and a static cylinder) on the HIP step against the oracle: random poses,
+  one step, tests/scenes.py tolerances."""
+  from mjlab_amd.spec.compiler import compile_spec
+  from mjlab_amd.spec.mjcf import read_mjcf_string
+
+  n = 512
+  m = compile_spec(read_mjcf_string(CYL_SCENE), 50, 300)
+  assert m.nboxpair > 0 and not m.unsupported_pair_types
+  rng = np.random.default_rng(53)
+  q = np.zeros((n, m.nq))
+  for b, (lo, hi) in enumerate([([-0.3, -0.3, -0.05], [0.3, 0.3, 0.2]), ([-0.4, -0.3, -0.05], [0.0, 0.3, 0.15]),
+                                ([0.05, -0.3, -0.1], [0.55, 0.3, 0.6])]):
+    q[:, 7 * b : 7 * b + 3] = rng.uniform(lo, hi, (n, 3))
+    quat = rng.normal(size=(n, 4))
+    q[:, 7 * b + 3 : 7 * b + 7] = quat / np.linalg.norm(quat, axis=1, keepdims=True)
+  st = {"qpos": q, "qvel": rng.normal(scale=0.3, size=(n, m.nv)), "qacc_warmstart": np.zeros((n, m.nv))}
+  sim = Simulation(n, SimulationCfg(nconmax=50, njmax=300, mujoco=MujocoCfg(timestep=0.002, iterations=20,
+                                                                               ls_iterations=20)), m, DEV)
+  put(sim, st)
+  sim.step()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=True, follow=got)
+  rep = assert_parity(got, ref, n, min_int_rate=0.95, tag=" cylinder/ellipsoid pairs")
+  g = got["contact_geom"].reshape(n, -1, 2)
+  types = np.asarray(m.geom_type)
+  kinds = {(int(types[a]), int(types[b])) for w in range(n) for a, b in g[w, : int(got["ncon"][w, 0])]}
+  assert {(0, 4), (0, 5), (2, 5)} <= kinds, kinds
+  print("[cylinder/ellipsoid pairs] contact kinds", sorted(kinds), "int rate", rep["int_match_rate"])
