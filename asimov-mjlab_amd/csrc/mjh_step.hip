@@ -144,6 +144,7 @@ constexpr bool kPositionStageGlobal =
 #define SPI(name) reinterpret_cast<int*>((Rg::name ? G : S) + Lo.name)
 
 thread_local std::string g_err;
+thread_local bool g_keep_image = false;  // mjh_step_keep_image: no pack launch before this step
 bool g_disable_spec = false;  // mjh_set_specialization(0): always the generic instance
 bool g_auto_order = false;    // mjh_set_world_ordering(1): order the worlds in the pack launch
 bool g_pos_reuse = kPositionStageGlobal;  // mjh_set_position_reuse: reuse the position stage of unchanged worlds
@@ -4177,8 +4178,9 @@ int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, voi
   const int nvp = nvp_of(m->nv);
   const bool order = g_auto_order && d->world_order != nullptr && d->nworld > 1;
   // 1024 threads: the order workgroup's counting sort is the launch's long pole
-  hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields + (order ? 1 : 0)), dim3(1024), 0, s, *m, p.io, d->solver_niter, d->nefc,
-                     const_cast<long long*>(d->world_order), (long long)d->nworld);
+  if (!g_keep_image)
+    hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields + (order ? 1 : 0)), dim3(1024), 0, s, *m, p.io, d->solver_niter,
+                       d->nefc, const_cast<long long*>(d->world_order), (long long)d->nworld);
   // specialised instances assume the slab data layout (data_is_slab)
   const int k = (g_disable_spec || !data_is_slab(m, d)) ? -1 : find_spec(p, m);
   if (k >= 0)
@@ -4290,6 +4292,13 @@ int mjh_set_profile_buffer(void* ptr) {
 int mjh_step(const mjh_model* m, const mjh_data* d, void* stream) { return launch<true>(m, d, nullptr, stream); }
 
 int mjh_forward(const mjh_model* m, const mjh_data* d, void* stream) { return launch<false>(m, d, nullptr, stream); }
+
+int mjh_step_keep_image(const mjh_model* m, const mjh_data* d, void* stream) {
+  g_keep_image = true;
+  const int r = launch<true>(m, d, nullptr, stream);
+  g_keep_image = false;
+  return r;
+}
 
 int mjh_forward_gated(const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream) {
   if (!gate) { g_err = "null gate"; return 1; }

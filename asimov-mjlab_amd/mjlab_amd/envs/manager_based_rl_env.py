@@ -338,7 +338,9 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
       if i == 0 or not once:
         self.action_manager.apply_action()
       self.scene.write_data_to_sim()
-      self.sim.step()
+      # nothing between the substeps writes a model field (actions write ctrl),
+      # so substeps after the first reuse the packed model image
+      self.sim.step(keep_image=i > 0) if self.sim.use_cuda_graph else self.sim.step()
       self.scene.update(dt=self.physics_dt)
     if self.episode_length_buf.is_cuda:
       from mjlab_amd import envops

@@ -20,7 +20,7 @@ PKG = Path(__file__).resolve().parents[1]
 # MJH_LIB selects an alternative build of the same ABI (e.g. the phase-timing
 # build libmjh_prof.so used by tools/phase_profile.py).
 LIB_PATH = Path(os.environ.get("MJH_LIB", str(PKG / "libmjh.so")))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 EXPORTS = (
   "mjh_abi_version",
@@ -33,6 +33,7 @@ EXPORTS = (
   "mjh_set_profile_buffer",
   "mjh_efc_capacity",
   "mjh_lds_rows",
+  "mjh_step_keep_image",
   "mjh_plan_ints",
   "mjh_spec_index",
   "mjh_data_is_slab",
@@ -138,7 +139,7 @@ def lib() -> ctypes.CDLL:
   L.mjh_scratch_words.argtypes = [ctypes.c_void_p]
   L.mjh_scratch_words.restype = ctypes.c_longlong
   L.mjh_set_profile_buffer.argtypes = [ctypes.c_void_p]
-  for f in (L.mjh_step, L.mjh_forward):
+  for f in (L.mjh_step, L.mjh_forward, L.mjh_step_keep_image):
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     f.restype = ctypes.c_int
   L.mjh_forward_gated.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]

@@ -425,11 +425,10 @@ class Simulation:
                                                  ctypes.c_void_p(self._order.data_ptr()), self.num_envs, self._stream()),
                    "mjh_order_worlds")
 
-  def _launch_step(self) -> None:
+  def _launch_step(self, keep_image: bool = False) -> None:
     self._refresh_order()
-    native.check(
-      native.lib().mjh_step(ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), self._stream()), "mjh_step"
-    )
+    fn = native.lib().mjh_step_keep_image if keep_image else native.lib().mjh_step
+    native.check(fn(ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), self._stream()), "mjh_step")
 
   def _launch_forward(self) -> None:
     self._refresh_order()
@@ -472,11 +471,14 @@ class Simulation:
       "mjh_forward_gated",
     )
 
-  def step(self) -> None:
+  def step(self, keep_image: bool = False) -> None:
+    """One physics step. keep_image (inside an enclosing capture only): reuse
+    the model image packed for the previous launch on this stream — for
+    substeps between which no model field changes (the env's decimation loop)."""
     self._require_gpu()
     self.epoch.bump()
     if torch.cuda.is_current_stream_capturing():
-      self._launch_step()  # being captured into an enclosing (env-step) graph
+      self._launch_step(keep_image)  # being captured into an enclosing (env-step) graph
       return
     if self.step_graph is None:
       self.create_graph()

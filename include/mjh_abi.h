@@ -34,7 +34,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 9
+#define MJH_ABI_VERSION 10
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -187,6 +187,14 @@ int mjh_set_profile_buffer(void* ptr);
 /* One physics step (mj_step: forward + implicitfast/Euler integration) for all
  * nworld worlds. Replaces mjwarp.step (sim.py:193-199). */
 int mjh_step(const mjh_model* m, const mjh_data* d, void* stream);
+
+/* mjh_step without the model-image pack launch that precedes every other
+ * step / forward: the image (and the world order) of the previous launch on
+ * this stream are reused. For the env's decimation substeps after the first,
+ * between which nothing writes a model field (manager_based_rl_env.py:114-119:
+ * actions write ctrl, data). The caller guarantees that; results are then
+ * identical to mjh_step's. */
+int mjh_step_keep_image(const mjh_model* m, const mjh_data* d, void* stream);
 
 /* Forward dynamics only (no integration, time unchanged). Replaces
  * mjwarp.forward (sim.py:186-191). */

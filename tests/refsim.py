@@ -43,7 +43,7 @@ class Shadow:
     self.maxerr: dict[str, float] = {}
     self.int_mismatch_worlds = 0
     self._step, self._forward = sim.step, sim.forward
-    sim.step = lambda: self._run(True)
+    sim.step = lambda keep_image=False: self._run(True)  # (eager: every step packs the image anyway)
     sim.forward = lambda: self._run(False)
 
   def _snapshot(self) -> dict:
