@@ -398,9 +398,11 @@ __global__ __launch_bounds__(1024) void sum_ratios_kernel(const RatioArgs a, flo
   __shared__ float part[2][16];
   const int t = blockIdx.x;
   float x = 0.f, y = 0.f;
+  // den NULL: mean(sqrt(num)) (e.g. Metrics/angular_momentum_mean)
+  const float* dn = a.den[t];
   for (long long e = threadIdx.x; e < n; e += 1024) {
-    x += a.num[t][e];
-    y += a.den[t][e];
+    x += dn ? a.num[t][e] : sqrtf(a.num[t][e]);
+    y += dn ? dn[e] : 1.f;
   }
   x = wsum(x);
   y = wsum(y);

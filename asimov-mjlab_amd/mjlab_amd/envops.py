@@ -617,15 +617,16 @@ def masked_zero(tensors: list, mask) -> bool:
 
 
 def sum_ratios(pairs: list, out: torch.Tensor) -> bool:
-  """out[t] = sum(num_t) / max(sum(den_t), 1) for (num_t, den_t) (N,) float vectors, one launch."""
+  """out[t] = sum(num_t) / max(sum(den_t), 1) for (num_t, den_t) (N,) float vectors
+  (den_t None: mean(sqrt(num_t))), one launch."""
   T = len(pairs)
   if T == 0 or T > MAX_TERMS or not out.is_cuda or out.numel() < T:
     return False
   for a, b in pairs:
-    if not all(x.is_cuda and x.dtype == torch.float32 and x.dim() == 1 and x.is_contiguous() for x in (a, b)):
+    if not all(x.is_cuda and x.dtype == torch.float32 and x.dim() == 1 and x.is_contiguous() for x in (a, b) if x is not None):
       return False
   num = (ctypes.c_void_p * T)(*[a.data_ptr() for a, _ in pairs])
-  den = (ctypes.c_void_p * T)(*[b.data_ptr() for _, b in pairs])
+  den = (ctypes.c_void_p * T)(*[b.data_ptr() if b is not None else None for _, b in pairs])
   native.check(native.lib().mjh_sum_ratios(num, den, T, _ptr(out), pairs[0][0].shape[0], _stream()), "mjh_sum_ratios")
   return True
 
@@ -686,14 +687,21 @@ def rew_soft_landing(force, cct, cmd, first_lim: float, cmd_thr: float):
   return out, num, den
 
 
-def log_ratio(env, key: str, num: torch.Tensor, den: torch.Tensor) -> None:
-  """extras['log'][key] = sum(num) / max(sum(den), 1). Inside a reward pass the
-  reward manager evaluates every such log of the pass in one launch."""
+def log_ratio(env, key: str, num: torch.Tensor, den: torch.Tensor | None) -> None:
+  """extras['log'][key] = sum(num) / max(sum(den), 1), or mean(sqrt(num)) when
+  den is None. Inside a reward pass the reward manager evaluates every such log
+  of the pass in one launch."""
   pending = env.__dict__.get("_reward_log_ratios")
   if pending is not None:
     pending.append((key, num, den))
     return
-  env.extras["log"][key] = torch.sum(num) / torch.clamp(torch.sum(den), min=1)
+  env.extras["log"][key] = ratio_value(num, den)
+
+
+def ratio_value(num: torch.Tensor, den: torch.Tensor | None) -> torch.Tensor:
+  if den is None:
+    return torch.mean(torch.sqrt(num))
+  return torch.sum(num) / torch.clamp(torch.sum(den), min=1)
 
 
 def root_frame(xpos, xquat, com, cvel, grav, fwd) -> torch.Tensor | None:

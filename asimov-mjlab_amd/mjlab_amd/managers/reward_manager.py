@@ -95,7 +95,7 @@ class RewardManager:
           log[key] = self._log_buf[i]
       else:
         for key, a, b in pending:
-          log[key] = torch.sum(a) / torch.clamp(torch.sum(b), min=1)
+          log[key] = envops.ratio_value(a, b)
 
     if envops.reward_combine(vals, self._w, dt, self._reward_buf, self._step_reward, self._sums):
       return self._reward_buf

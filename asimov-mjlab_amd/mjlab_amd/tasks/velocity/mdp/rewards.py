@@ -84,7 +84,7 @@ def angular_momentum_penalty(env, sensor_name: str) -> torch.Tensor:
   h = env.scene[sensor_name].data
   sq = envops.rew_sqsum(h, 3) if h.dim() == 2 and h.shape[1] == 3 else None
   sq = sq if sq is not None else torch.sum(torch.square(h), dim=-1)
-  env.extras["log"]["Metrics/angular_momentum_mean"] = torch.mean(torch.sqrt(sq))
+  envops.log_ratio(env, "Metrics/angular_momentum_mean", sq, None)  # mean(sqrt(sq)), with the pass's other logs
   return sq
 
 

@@ -436,7 +436,8 @@ int mjh_masked_zero(float* const* ptrs, const long long* row_strides, const int*
                     const unsigned char* mask, long long n, void* stream);
 
 /* out[t] = sum(num[t]) / max(sum(den[t]), 1) over n envs (reward-term metric
- * logs, tasks/velocity/mdp/rewards.py). One workgroup. */
+ * logs, tasks/velocity/mdp/rewards.py); den[t] NULL: mean(sqrt(num[t]))
+ * (Metrics/angular_momentum_mean). One workgroup per term. */
 int mjh_sum_ratios(const float* const* num, const float* const* den, int nterms, float* out, long long n, void* stream);
 
 /* Contact-timing rewards of the velocity task (tasks/velocity/mdp/rewards.py),
