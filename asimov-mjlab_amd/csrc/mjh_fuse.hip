@@ -324,6 +324,16 @@ struct TermArgs {
   int nterms;
 };
 
+// bad_orientation (envs/mdp/terminations.py): acos(-g_z) > limit as
+// -cos(limit) < g_z <= 1, one launch (instead of two compares and an AND)
+__global__ void gz_above_kernel(const float* __restrict__ g, long long gs, float thr, unsigned char* __restrict__ out,
+                                long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float gz = g[e * gs];
+  out[e] = (gz > thr && gz <= 1.f) ? 1 : 0;
+}
+
 __global__ void term_combine_kernel(const TermArgs a, unsigned char* __restrict__ truncated,
                                     unsigned char* __restrict__ terminated, unsigned char* __restrict__ dones, long long n) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -923,6 +933,12 @@ int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, co
                    void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(event_mark_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, last, once, mask, step, n);
+  return finish();
+}
+
+int mjh_gz_above(const float* g, long long gs, float thr, unsigned char* out, long long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(gz_above_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, g, gs, thr, out, n);
   return finish();
 }
 

@@ -565,6 +565,17 @@ def event_mark(last: torch.Tensor, once: torch.Tensor, mask, step: torch.Tensor)
   return True
 
 
+def gz_above(gz: torch.Tensor, thr: float) -> torch.Tensor | None:
+  """(thr < gz) & (gz <= 1) as a bool vector in one launch (bad_orientation), or
+  None on CPU / an unsupported layout."""
+  if not (gz.is_cuda and gz.dtype == torch.float32 and gz.dim() == 1):
+    return None
+  n = gz.shape[0]
+  out = torch.empty(n, dtype=torch.bool, device=gz.device)
+  native.check(native.lib().mjh_gz_above(_ptr(gz), gz.stride(0), float(thr), _ptr(out), n, _stream()), "mjh_gz_above")
+  return out
+
+
 def term_combine(values: list, term_dones: list, time_out: list, truncated, terminated, dones) -> bool:
   """TerminationManager's copy / OR / dones chain over bool term vectors in one launch."""
   T = len(values)

@@ -26,7 +26,10 @@ def bad_orientation(env, limit_angle: float, asset_cfg: SceneEntityCfg = _DEFAUL
   g = env.scene[asset_cfg.name].data.projected_gravity_b
   if 0.0 <= limit_angle <= math.pi:
     gz = g[:, 2]
-    return (gz > -math.cos(limit_angle)) & (gz <= 1.0)
+    from mjlab_amd import envops
+
+    fused = envops.gz_above(gz, -math.cos(limit_angle))
+    return fused if fused is not None else (gz > -math.cos(limit_angle)) & (gz <= 1.0)
   return torch.acos(-g[:, 2]).abs() > limit_angle
 
 

@@ -79,6 +79,7 @@ EXPORTS = (
   "mjh_velocity_resample",
   "mjh_event_mark",
   "mjh_term_combine",
+  "mjh_gz_above",
   "mjh_velocity_rows",
   "mjh_masked_zero",
   "mjh_sum_ratios",
@@ -182,6 +183,7 @@ def lib() -> ctypes.CDLL:
   L.mjh_velocity_resample.argtypes = [vp, vp, cf, cf, cf, cf, ci, ci, vp, vp, vp, vp, vp, vp, u64, u64, vp, ll, vp]
   L.mjh_event_mark.argtypes = [vp, vp, vp, vp, ll, vp]
   L.mjh_term_combine.argtypes = [vp, vp, vp, ci, vp, vp, vp, ll, vp]
+  L.mjh_gz_above.argtypes = [vp, ll, ctypes.c_float, vp, ll, vp]
   L.mjh_velocity_rows.argtypes = [vp, ll, ll, vp, ll, vp, ll, vp, vp, ci, ll, vp]
   L.mjh_masked_zero.argtypes = [vp, vp, vp, ci, vp, ll, vp]
   L.mjh_sum_ratios.argtypes = [vp, vp, ci, vp, ll, vp]

@@ -419,6 +419,11 @@ int mjh_velocity_resample(const unsigned char* mask, const float* ranges, float 
 /* TerminationManager.compute's combination (termination_manager.py:54-82) for
  * nterms bool term vectors: term_dones[t] = values[t]; truncated = OR of the
  * time-out terms, terminated = OR of the others, dones = truncated | terminated. */
+/* out[e] = -cos(limit) < g[e * gs] <= 1 (thr = -cos(limit)): bad_orientation
+ * (envs/mdp/terminations.py, torch.acos(-g_z).abs() > limit_angle) on the
+ * projected gravity's z column, one launch. */
+int mjh_gz_above(const float* g, long long gs, float thr, unsigned char* out, long long n, void* stream);
+
 int mjh_term_combine(const unsigned char* const* values, unsigned char* const* term_dones, const int* time_out, int nterms,
                      unsigned char* truncated, unsigned char* terminated, unsigned char* dones, long long n,
                      void* stream);

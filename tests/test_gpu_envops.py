@@ -232,3 +232,19 @@ def test_obs_group_kernel_matches_per_term():
     (xs[2] + (u[:, 4:11] * 3.0 - 1.0)).clip(-1.0, 1.0) * 2.0,
   ], 1)
   torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)
+
+
+def test_gz_above_kernel_matches_torch():
+  """bad_orientation's fused test (-cos(limit) < g_z <= 1) equals the torch
+  formula on the same float32 values, including g_z just above 1 and at the
+  threshold."""
+  import math
+
+  from mjlab_amd import envops
+
+  g = torch.rand(4096, 3, device="cuda:0") * 2.2 - 1.1
+  thr = -math.cos(1.2)
+  g[:4, 2] = torch.tensor([1.0, 1.0000001, float(torch.tensor(thr, dtype=torch.float32)), -1.0])
+  got = envops.gz_above(g[:, 2], thr)
+  ref = (g[:, 2] > thr) & (g[:, 2] <= 1.0)
+  assert torch.equal(got, ref)
