@@ -113,7 +113,8 @@ __global__ void posture_kernel(const float* q, long long qs, const float* q0, lo
 //   slip:      sum_j |v_xy,j|^2 * [found_j > 0]                   (feet_slip)
 // both x [command total > threshold]; also writes sum_j |v_xy| * [found] and
 // sum_j [found] for the slip metric.
-__global__ void feet_kernel(const float* z, long long zs, const float* vel, long long vs, const float* found, long long fs,
+__global__ void feet_kernel(const float* z, long long zs, const float* vel, long long vs, long long vcs, const float* found,
+                            long long fs, long long fcs,
                             const float* cmd, long long cs, float target, float thr_clear, float thr_slip, int k,
                             float* clearance, float* slip, float* slip_vsum, float* slip_cnt, long long n) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -121,11 +122,11 @@ __global__ void feet_kernel(const float* z, long long zs, const float* vel, long
   const float tot = cmd_total(cmd + e * cs);
   float cl = 0.f, sl = 0.f, vs_ = 0.f, cnt = 0.f;
   for (int j = 0; j < k; j++) {
-    const float* v = vel + e * vs + 3 * j;
+    const float* v = vel + e * vs + vcs * j;
     const float vn = sqrtf(v[0] * v[0] + v[1] * v[1]);
     cl += fabsf(z[e * zs + 3 * j] - target) * vn;
     if (found) {
-      const float in = found[e * fs + j] > 0.f ? 1.f : 0.f;
+      const float in = found[e * fs + fcs * j] > 0.f ? 1.f : 0.f;
       sl += vn * vn * in;
       vs_ += vn * in;
       cnt += in;
@@ -185,12 +186,12 @@ int mjh_rew_posture(const float* q, long long qs, const float* q0, long long q0s
   return finish();
 }
 
-int mjh_rew_feet(const float* z, long long zs, const float* vel, long long vs, const float* found, long long fs,
-                 const float* cmd, long long cs, float target, float thr_clear, float thr_slip, int k, float* clearance,
-                 float* slip, float* slip_vsum, float* slip_cnt, long long n, void* stream) {
+int mjh_rew_feet(const float* z, long long zs, const float* vel, long long vs, long long vcs, const float* found, long long fs,
+                 long long fcs, const float* cmd, long long cs, float target, float thr_clear, float thr_slip, int k,
+                 float* clearance, float* slip, float* slip_vsum, float* slip_cnt, long long n, void* stream) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(feet_kernel, dim3(grid(n)), dim3(256), 0, (hipStream_t)stream, z, zs, vel, vs, found, fs, cmd, cs,
-                     target, thr_clear, thr_slip, k, clearance, slip, slip_vsum, slip_cnt, n);
+  hipLaunchKernelGGL(feet_kernel, dim3(grid(n)), dim3(256), 0, (hipStream_t)stream, z, zs, vel, vs, vcs, found, fs, fcs, cmd,
+                     cs, target, thr_clear, thr_slip, k, clearance, slip, slip_vsum, slip_cnt, n);
   return finish();
 }
 

@@ -197,18 +197,17 @@ def rew_feet(pos: torch.Tensor, vel: torch.Tensor, found, cmd: torch.Tensor, tar
   if vel.stride(1) != 3 and vel.stride(1) != 6:
     return None
   n, k = pos.shape[0], pos.shape[1]
-  if vel.stride(1) != 3:
-    vel = vel.contiguous()
-  if found is not None and found.dim() == 2 and found.stride(1) != 1:
-    found = found.contiguous()  # strided sensor-slot view
-  if found is not None and not (found.dim() == 2 and found.stride(1) == 1 and found.shape == (n, k) and found.dtype == torch.float32):
+  # strided views are read in place (velocity rows of 6, sensor-slot columns)
+  if found is not None and not (found.dim() == 2 and found.shape == (n, k) and found.dtype == torch.float32
+                                and found.is_cuda):
     return None
   z = pos[:, :, 2]
   cl = _vec_out(n, pos.device) if want == "clearance" else None
   outs = [_vec_out(n, pos.device) for _ in range(3)] if want == "slip" else [None, None, None]
   native.check(native.lib().mjh_rew_feet(
-    ctypes.c_void_p(pos.data_ptr() + 8), pos.stride(0), _ptr(vel), vel.stride(0),
-    _ptr(found) if want == "slip" else None, found.stride(0) if want == "slip" else 0, _ptr(cmd), cmd.stride(0),
+    ctypes.c_void_p(pos.data_ptr() + 8), pos.stride(0), _ptr(vel), vel.stride(0), vel.stride(1),
+    _ptr(found) if want == "slip" else None, found.stride(0) if want == "slip" else 0,
+    found.stride(1) if want == "slip" else 0, _ptr(cmd), cmd.stride(0),
     float(target), float(thr_clear), float(thr_slip), k, _ptr(cl) if cl is not None else None,
     *[_ptr(t) if t is not None else None for t in outs], n, _stream()), "mjh_rew_feet")
   del z

@@ -253,9 +253,9 @@ int mjh_rew_pos_limits(const float* q, long long qs, const float* lim, long long
 int mjh_rew_posture(const float* q, long long qs, const float* q0, long long q0s, const float* std_stand,
                     const float* std_walk, const float* std_run, const float* cmd, long long cs, float walk_thr,
                     float run_thr, int k, float* out, long long n, void* stream);
-int mjh_rew_feet(const float* z, long long zs, const float* vel, long long vs, const float* found, long long fs,
-                 const float* cmd, long long cs, float target, float thr_clear, float thr_slip, int k, float* clearance,
-                 float* slip, float* slip_vsum, float* slip_cnt, long long n, void* stream);
+int mjh_rew_feet(const float* z, long long zs, const float* vel, long long vs, long long vcs, const float* found, long long fs,
+                 long long fcs, const float* cmd, long long cs, float target, float thr_clear, float thr_slip, int k,
+                 float* clearance, float* slip, float* slip_vsum, float* slip_cnt, long long n, void* stream);
 
 /* UniformVelocityCommand.compute for all envs (velocity_command.py:65-101):
  * metrics, timers, masked resampling from u (N, 8) uniform draws (u NULL:
