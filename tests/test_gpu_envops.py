@@ -248,3 +248,17 @@ def test_gz_above_kernel_matches_torch():
   got = envops.gz_above(g[:, 2], thr)
   ref = (g[:, 2] > thr) & (g[:, 2] <= 1.0)
   assert torch.equal(got, ref)
+
+
+def test_sum_ratios_with_mean_sqrt_term():
+  """The reward pass's ratio-log launch: sum(num)/max(sum(den),1) terms and a
+  den-less term (mean(sqrt(num)): Metrics/angular_momentum_mean) against
+  torch, float32 summation-order tolerance."""
+  from mjlab_amd import envops
+
+  n = 4096
+  a, b, c = torch.rand(n, device="cuda:0"), (torch.rand(n, device="cuda:0") > 0.5).float(), torch.rand(n, device="cuda:0")
+  out = torch.zeros(2, device="cuda:0")
+  assert envops.sum_ratios([(a, b), (c, None)], out)
+  ref = torch.stack([a.sum() / b.sum().clamp(min=1), torch.sqrt(c).mean()])
+  torch.testing.assert_close(out, ref, rtol=1e-5, atol=0)
