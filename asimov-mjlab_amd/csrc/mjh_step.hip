@@ -205,22 +205,33 @@ struct ImgOff {
   int nfields;
 };
 
-// Worlds per workgroup by padded dof count: one-world workgroups up to 36 dofs
-// (G1, Go1): each wave retires on its own, the model image is read in place from
-// global memory, and MJH_WPCU (16) of them share a CU — 4 waves per SIMD, so all
-// 4,096 G1 worlds are resident at once (one round instead of two; G1 step
-// launch 0.605 -> 0.505 ms, Go1 8192 0.559 -> 0.522 ms, env bench 1.37M ->
-// 1.57M env-steps/s, profiles/r04m_*). 8-world workgroups sharing an LDS copy of
-// the image for larger models. MJH_WPB overrides it for A/B builds.
+#ifndef MJH_WPCU
+#define MJH_WPCU 16  // resident worlds per CU (see MJH_MINWAVES)
+#endif
+// Worlds per workgroup by padded dof count. 21-36 dofs (G1): one-world
+// workgroups; each wave retires on its own, the model image is read in place
+// from global memory, and MJH_WPCU (16) of them share a CU — 4 waves per SIMD, so
+// all 4,096 G1 worlds are resident at once (one round instead of two; G1 step
+// launch 0.605 -> 0.505 ms, env bench 1.37M -> 1.57M env-steps/s,
+// profiles/r04m_*). Up to 20 dofs (Go1): one workgroup of MJH_WPCU worlds per CU
+// sharing an LDS copy of the image (Go1 8192 0.523 -> 0.501 ms; for G1 the
+// smaller per-world LDS costs more than the image reads save,
+// profiles/r04s_wg16_kb.log). 8-world workgroups sharing the image for larger
+// models. MJH_WPB overrides it for A/B builds.
 __host__ __device__ constexpr int wpb_of_nvp(int nvp) {
 #ifdef MJH_WPB
   return (void)nvp, MJH_WPB;
 #else
-  return nvp <= 36 ? 1 : 8;
+  return nvp <= 20 ? MJH_WPCU : (nvp <= 36 ? 1 : 8);
 #endif
 }
 // the image lives in global memory for workgroups of fewer than 8 worlds
 __host__ __device__ constexpr bool img_global(int wpb) { return wpb < 8; }
+// one-world workgroups, and workgroups of a whole CU's MJH_WPCU worlds (one
+// LDS copy of the image for all of them): per-world layouts sized for MJH_WPCU
+// worlds per CU, with the packed factor, constraint rows beyond the LDS in
+// global scratch (two tiers) and the world index in a scalar register
+__host__ __device__ constexpr bool cu_worlds(int wpb) { return wpb == 1 || wpb == MJH_WPCU; }
 template <bool G>
 __device__ __forceinline__ const float* img_base(const float* g, const float* l) {
   if constexpr (G) return g; else return l;
@@ -491,7 +502,7 @@ __host__ __device__ constexpr int llen(int i) { return ((i >> 2) + 1) << 2; }
 static_assert(lrow(0) == 0 && lrow(1) == 4 && lrow(4) == 16 && lrow(5) == 24 && lrow(36) == 720, "packed rows");
 template <bool PK> __device__ __forceinline__ int lofs(int i, int ld) { return PK ? lrow(i) : i * ld; }
 template <bool PK> __device__ __forceinline__ int lspan(int i, int ld) { return PK ? llen(i) : ld; }
-__host__ __device__ constexpr bool pack_l(int wpb) { return wpb == 1; }
+__host__ __device__ constexpr bool pack_l(int wpb) { return cu_worlds(wpb); }
 
 #ifndef MJH_HESS_PF
 #define MJH_HESS_PF 4  // k-steps of J loads in flight in the Hessian
@@ -1554,9 +1565,6 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 // workgroups: MJH_WPCU / 4 waves per SIMD); it sets the launch bound's wave
 // target (the VGPR budget: 8 -> 256, 12 -> 168, 16 -> 128) and the per-world
 // LDS budget alike
-#ifndef MJH_WPCU
-#define MJH_WPCU 16
-#endif
 #ifndef MJH_MINWAVES
 #define MJH_MINWAVES(wpb) ((wpb) < 8 ? MJH_WPCU / 4 : 1)
 #endif
@@ -1644,8 +1652,11 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   // ~20 64-bit scratch pointers in VGPR pairs, live across the whole step).
   // One-world workgroups only: the 8-world instance is not VGPR-bound and the
   // SGPR pairs spill there (Go1 0.551 -> 0.559 ms)
-  const int w0 = (MODE != 1 && d.world_order) ? (int)d.world_order[slot] : slot;
-  const int w = WPB == 1 ? __builtin_amdgcn_readfirstlane(w0) : w0;
+  // whole-CU workgroups take the cost order's ranks b, b + nblocks, ... so each
+  // CU gets a mix of expensive and cheap worlds
+  const int rank = (WPB > 1 && cu_worlds(WPB) && d.nworld % WPB == 0) ? wave * (int)gridDim.x + (int)blockIdx.x : slot;
+  const int w0 = (MODE != 1 && d.world_order) ? (int)d.world_order[rank] : slot;
+  const int w = cu_worlds(WPB) ? __builtin_amdgcn_readfirstlane(w0) : w0;
   const int tid = threadIdx.x & 63;
   // mj_step (integration) or mj_forward: a runtime flag, not a template
   // parameter, so both run the very same code up to the integration (a step
@@ -2227,7 +2238,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   // addresses, so its results are the same. Its row count is known before any
   // row is written: the counts of the rows make_constraint emits (frictionloss
   // dofs, active limits, contacts within their margin) or the handoff's.
-  constexpr bool kTwoTier = WPB == 1 && MODE != 1;
+  constexpr bool kTwoTier = cu_worlds(WPB) && MODE != 1;
   bool big = false;
   if constexpr (kTwoTier) {
     if (Lo.lcap < Lo.rcap) {
@@ -4000,11 +4011,11 @@ Layout make_layout(const mjh_model* m, int budget, int wpb) {
     const int r = (budget - off - 64) / per_row_lds;
     if (r < lcap) lcap = r;
   }
-  if (wpb == 1 && g_lds_row_cap > 0 && g_lds_row_cap < lcap) lcap = g_lds_row_cap;
+  if (cu_worlds(wpb) && g_lds_row_cap > 0 && g_lds_row_cap < lcap) lcap = g_lds_row_cap;
   if (lcap < 1) lcap = 1;
   // 8-world workgroups: rows beyond the LDS are dropped (flagged as overflow);
-  // one-world workgroups: up to njmax, beyond lcap in global scratch (BIG)
-  if (wpb > 1) rcap = lcap;
+  // one-world and whole-CU workgroups: up to njmax, beyond lcap in global scratch (BIG)
+  if (!cu_worlds(wpb)) rcap = lcap;
   L.rcap = rcap;
   L.lcap = lcap;
   // LDS-resident row arrays take lcap rows, global ones rcap
@@ -4026,7 +4037,7 @@ Layout make_layout(const mjh_model* m, int budget, int wpb) {
   auto gt = [&](int n) { const int o = goff; goff += al(n); return o; };
   // the BIG worlds' row arrays (one-world workgroups with lcap < rcap)
   {
-    const bool two = wpb == 1;  // allocated whatever lcap is: the scratch size does not depend on it
+    const bool two = cu_worlds(wpb);  // allocated whatever lcap is: the scratch size does not depend on it
     L.g_efc_D = two ? gt(rcap) : 0; L.g_efc_R = two ? gt(rcap) : 0; L.g_efc_aref = two ? gt(rcap) : 0;
     L.g_efc_jaref = two ? gt(rcap) : 0; L.g_efc_jv = two ? gt(rcap) : 0; L.g_efc_force = two ? gt(rcap) : 0;
     L.g_efc_fl = two ? gt(rcap) : 0; L.g_efc_type = two ? gt(rcap) : 0; L.g_efc_h = two ? gt(rcap) : 0;
