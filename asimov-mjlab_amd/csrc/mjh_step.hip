@@ -504,8 +504,11 @@ template <bool PK> __device__ __forceinline__ int lofs(int i, int ld) { return P
 template <bool PK> __device__ __forceinline__ int lspan(int i, int ld) { return PK ? llen(i) : ld; }
 __host__ __device__ constexpr bool pack_l(int wpb) { return cu_worlds(wpb); }
 
+// k-steps of J loads in flight in the Hessian, by padded dof count. Measured
+// (profiles/r04pf_hess_pf_kb.log): G1 (36 dofs) flat across 2/4/6/8; Go1
+// (20 dofs, ~14 rows: 6 covers all of them) 0.502 -> 0.457 ms per launch
 #ifndef MJH_HESS_PF
-#define MJH_HESS_PF 4  // k-steps of J loads in flight in the Hessian
+#define MJH_HESS_PF(nvp) ((nvp) <= 20 ? 6 : 4)
 #endif
 // H (lower triangle of Hout, packed rows) = M + sum_k ash[k]^2 J[arow[k]] J[arow[k]]^T over the
 // nact compacted active rows, on the f32 matrix cores (v_mfma_f32_16x16x4_f32:
@@ -547,7 +550,7 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
   };
   // PF k-steps of J loads in flight (a ring unrolled by PF so every register
   // index is static); same k order as a plain loop, so the sums are unchanged
-  constexpr int PF = MJH_HESS_PF;
+  constexpr int PF = MJH_HESS_PF(NVP);
   float v[PF][NB];
 #pragma unroll
   for (int s = 0; s < PF; s++) load(4 * s + kq, v[s]);
