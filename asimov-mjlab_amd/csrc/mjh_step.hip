@@ -1561,6 +1561,9 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 #ifndef MJH_PMINWAVES
 #define MJH_PMINWAVES 1
 #endif
+#ifndef MJH_PRIO
+#define MJH_PRIO 0
+#endif
 #ifndef MJH_PERSIST
 #define MJH_PERSIST 0
 #endif
@@ -3100,6 +3103,13 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
 
     for (int it = 0; it < m.iterations; it++) {
       unsigned long long t_ls = PROF_NOW();
+#if MJH_PRIO == 1
+      // A/B: a world still iterating raises its wave's issue priority (the
+      // launch ends with its slowest world; the SIMD's other waves fill in)
+      if (it == 2) __builtin_amdgcn_s_setprio(1);
+      if (it == 4) __builtin_amdgcn_s_setprio(2);
+      if (it == 6) __builtin_amdgcn_s_setprio(3);
+#endif
       // ---- exact line search along `search`
       symv_u<NT, NVP>(Mm, nv, ldm, search, Mv);
       for (int r = tid; r < nefc; r += NT) {
@@ -4235,6 +4245,9 @@ int mjh_model_check(const mjh_model* m) {
   if (!m->image || m->image_words < p.io.img_words + 4) { g_err = "model image buffer missing or too small (mjh_image_words)"; return 1; }
   if (p.shmem > (size_t)kLdsBytes) { g_err = "model image + per-world scratch exceed LDS"; return 1; }
   if (p.lo.rcap < 8) { g_err = "too little LDS left for constraint rows"; return 1; }
+  // elliptic rows need the constraint Jacobian in global scratch (a preset that
+  // keeps J in LDS builds pyramidal rows only)
+  if (m->cone == 1 && !Rg::J) { g_err = "elliptic cones need a build with J in global scratch (MJH_PRESET)"; return 1; }
   g_err.clear();
   return 0;
 }
@@ -4308,7 +4321,9 @@ int mjh_step(const mjh_model* m, const mjh_data* d, void* stream) { return launc
 int mjh_forward(const mjh_model* m, const mjh_data* d, void* stream) { return launch<false>(m, d, nullptr, stream); }
 
 int mjh_step_keep_image(const mjh_model* m, const mjh_data* d, void* stream) {
-  g_keep_image = true;
+  // a persistent build (MJH_PERSIST) resets its world-claim counter in the pack
+  // launch, so it always packs (the image is rebuilt: same results, one launch more)
+  g_keep_image = MJH_PERSIST == 0;
   const int r = launch<true>(m, d, nullptr, stream);
   g_keep_image = false;
   return r;

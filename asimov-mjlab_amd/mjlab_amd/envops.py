@@ -201,6 +201,8 @@ def rew_feet(pos: torch.Tensor, vel: torch.Tensor, found, cmd: torch.Tensor, tar
   if found is not None and not (found.dim() == 2 and found.shape == (n, k) and found.dtype == torch.float32
                                 and found.is_cuda):
     return None
+  if want == "slip" and found is None:  # the slip reward needs the contact flags: torch path
+    return None
   z = pos[:, :, 2]
   cl = _vec_out(n, pos.device) if want == "clearance" else None
   outs = [_vec_out(n, pos.device) for _ in range(3)] if want == "slip" else [None, None, None]

@@ -29,6 +29,8 @@ from typing import Any
 import numpy as np
 import torch
 
+from mjlab_amd.utils.capture import GraphSlot
+
 from mjlab_amd.envs.mdp.events import reset_scene_to_default
 from mjlab_amd.managers.action_manager import ActionManager
 from mjlab_amd.managers.command_manager import CommandManager, NullCommandManager
@@ -152,7 +154,7 @@ class ManagerBasedEnv:
     self.__dict__["_rng_calls"] = 0
     self._reset_epoch = 0
     self._rng_ctr.zero_()
-    self.__dict__["_graph"] = None
+    self._graph = None
 
   def _begin_rng_phase(self, outside_step: bool) -> None:
     """Call keys restart at every env step (draws differ per step through the
@@ -206,6 +208,7 @@ class ManagerBasedEnv:
 
 class ManagerBasedRlEnv(ManagerBasedEnv):
   is_vector_env = True
+  _graph = GraphSlot()  # the captured env step (utils/capture.py: capture-safe release)
   metadata = {"render_modes": [None]}
 
   def __init__(self, cfg: ManagerBasedRlEnvCfg, device: str, render_mode: str | None = None, use_graph: bool | None = None, **kwargs) -> None:
@@ -244,6 +247,7 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     [obs groups in key order | reward | terminated | truncated]
     (mjlab_amd.distributed.pack_step_outputs): the multi-GPU exchange then
     all-gathers this buffer with no per-step allocation."""
+
     from mjlab_amd.distributed import packed_width
 
     if self._pack_buf is None:

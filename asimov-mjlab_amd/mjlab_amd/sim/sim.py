@@ -30,6 +30,7 @@ import numpy as np
 import torch
 
 from mjlab_amd.sim import abi, native
+from mjlab_amd.utils.capture import GraphSlot
 from mjlab_amd.sim.sim_data import Epoch, BATCHED_STATIC, DATA_SHAPES, MODEL_SHAPES, Bridge, make_opt, shape_of
 from mjlab_amd.spec.compiler import Model
 
@@ -192,6 +193,10 @@ _TORCH_DT = {"float": torch.float32, "int": torch.int32, "mjh_i64": torch.int64}
 
 
 class Simulation:
+  # captured graphs live outside the instance (utils/capture.py: capture-safe release)
+  step_graph = GraphSlot()
+  forward_graph = GraphSlot()
+
   def __init__(self, num_envs: int, cfg: SimulationCfg, model: Model, device: str) -> None:
     self.cfg = cfg
     self.device = device
@@ -332,6 +337,7 @@ class Simulation:
 
   def set_option(self, **kw) -> None:
     """Change solver/integrator options after construction (re-captures graphs)."""
+
     for k, v in kw.items():
       setattr(self._mj_model, k, v)
     self._build_structs()
@@ -425,13 +431,28 @@ class Simulation:
                                                  ctypes.c_void_p(self._order.data_ptr()), self.num_envs, self._stream()),
                    "mjh_order_worlds")
 
+  def model_version(self) -> int:
+    """Sum of the model buffers' torch version counters: changes whenever a
+    model field is written in place through torch (views share their base's
+    counter). Host state, read when a launch is issued (or captured)."""
+    return sum(t._version for t in self._model_flat.values())
+
   def _launch_step(self, keep_image: bool = False) -> None:
     self._refresh_order()
+    # the packed image is reused only while no model field has been written
+    # since the launch that packed it (ADVICE r4: an action term that writes
+    # gains between decimation substeps must not be ignored)
+    ver = self.model_version()
+    if keep_image and ver != getattr(self, "_packed_version", None):
+      keep_image = False
+    if not keep_image:
+      self._packed_version = ver
     fn = native.lib().mjh_step_keep_image if keep_image else native.lib().mjh_step
     native.check(fn(ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), self._stream()), "mjh_step")
 
   def _launch_forward(self) -> None:
     self._refresh_order()
+    self._packed_version = self.model_version()
     native.check(
       native.lib().mjh_forward(ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), self._stream()),
       "mjh_forward",
@@ -464,6 +485,7 @@ class Simulation:
     if gate.dtype not in (torch.bool, torch.uint8) or gate.numel() != 1 or not gate.is_cuda:
       raise ValueError("gate must be a one-element bool/uint8 device tensor")
     self._refresh_order()
+    self._packed_version = self.model_version()
     native.check(
       native.lib().mjh_forward_gated(
         ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), ctypes.c_void_p(gate.data_ptr()), self._stream()

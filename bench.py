@@ -19,12 +19,17 @@ one HIP graph. Actions come from the random agent of the reference's
 `play --agent random` (2*U[0,1)-1, torch.Generator seeded 1234 + rank).
 
 Steady state. Episode lengths start uniformly random (rsl_rl's
-`init_at_random_ep_len=True`, which the reference's train.py:121 passes), and
-`--settle` untimed env steps (default 150) run before the W warmup steps, so
-the timed window sees the steady reset rate (and with it the forward pass that
-the reference runs over all worlds whenever any env resets,
-manager_based_rl_env.py:133-137) whatever --warmup the caller picks. The line
-reports resets per step and the fraction of timed steps that ran that forward.
+`init_at_random_ep_len=True`, which the reference's train.py:121 passes), but
+every env starts standing, so the random agent's falls come in waves that take
+many episodes of fall time to dephase. The settle (untimed, before the W warmup
+steps) therefore runs at least one episode (--settle-min 1000 env steps,
+velocity_env_cfg.py:383) and then continues in 100-step blocks until the last
+two 250-step reset rates agree within 5 % (--settle-max 4000). The timed window
+then sees the stationary reset rate (and with it the forward pass that the
+reference runs over all worlds whenever any env resets,
+manager_based_rl_env.py:133-137) whatever --steps and --warmup the caller picks.
+The line reports the window's resets per step next to the settle tail's, and
+the fraction of timed steps that ran that forward.
 
 Rank 0 prints ONE JSON line with, in addition to the contract fields:
   roofline      — the dominant kernel (the fused physics step) measured live
@@ -74,7 +79,10 @@ def parse() -> argparse.Namespace:
   p.add_argument("--gpus", type=int, default=1)
   p.add_argument("--steps", type=int, default=300)
   p.add_argument("--warmup", type=int, default=30)
-  p.add_argument("--settle", type=int, default=150, help="untimed env steps before warmup (steady reset rate)")
+  p.add_argument("--settle", type=int, default=-1,
+                 help="untimed env steps before warmup; -1 (default): adaptive, until the reset rate is stationary")
+  p.add_argument("--settle-min", type=int, default=1000, help="adaptive settle: at least this many env steps (one episode)")
+  p.add_argument("--settle-max", type=int, default=4000, help="adaptive settle: at most this many env steps")
   p.add_argument("--num-envs", type=int, default=0, help="envs per GPU (default: the task's BASELINE config)")
   p.add_argument("--task", default=TASK)
   p.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL all-gather (N > 1)")
@@ -304,9 +312,39 @@ def main(env_hook=None) -> None:
       gather.gather_packed(packed)
 
   # graph capture happens on the 2nd step; settle + warmup steps are untimed
-  for _ in range(2 + args.settle + args.warmup):
-    o, r, te, tr, _ = env.step(agent())
-    exchange(o, r, te, tr)
+  def run(k: int) -> None:
+    for _ in range(k):
+      o, r, te, tr, _ = env.step(agent())
+      exchange(o, r, te, tr)
+
+  run(2)
+  settle_log, tail_rate = [], None
+  if args.settle >= 0:
+    run(args.settle)
+    settled = args.settle
+  else:
+    # adaptive: per-block reset counts (one host read per 50-step block, untimed)
+    blk, win = 50, 5  # two windows of 5 blocks = 250 steps each
+    counts, settled = [], 0
+    last = int(env.step_stats()[0].item())
+    while settled < args.settle_max:
+      run(blk)
+      settled += blk
+      cur = int(env.step_stats()[0].item())
+      counts.append(cur - last)
+      last = cur
+      if settled >= args.settle_min and len(counts) >= 2 * win and settled % 100 == 0:
+        a, b = sum(counts[-2 * win:-win]) / (win * blk), sum(counts[-win:]) / (win * blk)
+        done = int(abs(a - b) <= 0.05 * max(a, b, 1e-9))
+        if world > 1:  # every rank stops at the same step (the per-step gather is collective)
+          t = torch.tensor([done], device=dev, dtype=torch.long)
+          dist.all_reduce(t, op=dist.ReduceOp.MIN)
+          done = int(t.item())
+        if done:
+          break
+    settle_log = [c / blk for c in counts[-20:]]
+    tail_rate = sum(counts[-2 * win:]) / (2 * win * blk)
+  run(args.warmup)
   sync()
   stats0 = env.step_stats().clone()
   flags0 = env.sim.flag_stats()[3:].clone()  # running totals of worlds that overflowed / went non-finite
@@ -442,8 +480,10 @@ def main(env_hook=None) -> None:
         "physics_steps_per_s": value * env.cfg.decimation,
         "parallelism": f"env-sharded x{world}" + ("" if not use_gather else " + RCCL all-gather of obs/reward/dones"),
         "world_size": world,
-        "settle_steps": args.settle,
+        "settle_steps": settled,
         "resets_per_step": resets_per_step,
+        "settle_tail_resets_per_step": tail_rate,
+        "settle_block_resets_per_step": settle_log,
         "forward_gate_rate": gate_rate,
         "gather_ms_per_step": gather_ms,
         "mean_nefc": nefc,

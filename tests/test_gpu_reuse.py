@@ -150,3 +150,34 @@ def test_env_steps_bitwise_with_and_without_reuse():
       assert torch.equal(oa[grp], ob[grp]), (k, grp)
     assert torch.equal(ra, rb) and torch.equal(ta, tb) and torch.equal(tra, trb), k
   assert torch.equal(a.sim.data.qpos, b.sim.data.qpos)
+
+
+def test_keep_image_repacks_after_a_model_write():
+  """mjh_step_keep_image reuses the packed model image only while no model
+  field has changed since the launch that packed it (Simulation tracks the
+  model buffers' torch version counters at launch/capture time). A captured
+  sequence step -> in-place model write -> step(keep_image=True) must equal
+  the eager sequence bitwise (a stale image would keep the old masses)."""
+  from mjlab_amd.utils.capture import no_gc
+
+  n = 32
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(13))
+  eager, graphed = make_sim(m, n, ("body_mass",)), make_sim(m, n, ("body_mass",))
+  for s in (eager, graphed):
+    put(s, st)
+  eager.step()
+  eager.model.body_mass.mul_(1.5)
+  eager.step()
+  g = torch.cuda.CUDAGraph()
+  torch.cuda.synchronize()
+  with no_gc(), torch.cuda.graph(g):
+    graphed.step()
+    graphed.model.body_mass.mul_(1.5)
+    graphed.step(keep_image=True)
+  g.replay()
+  _same(get(eager, n), get(graphed, n), "keep_image after a model write")
+  # and without a write in between the image is reused (same results as packing)
+  v = graphed.model_version()
+  graphed.step()
+  assert graphed.model_version() == v
