@@ -47,6 +47,7 @@ struct Layout {
   int efc_h, arow, ash;
   int sidx;  // contact sensor: kept matches (contact index, ~index if flipped)
   int cg_g, cg_mg;  // CG solver: the previous iteration's gradient and M^-1 gradient
+  int pgs_ar, pgs_mj;  // PGS solver (global scratch): AR = J M^-1 J' + R (rcap x rcap), rows M^-1 J_r'
   int red, ints;
   int total, gtotal;  // per-world words: LDS, global scratch
   int ncap, rcap;
@@ -62,7 +63,7 @@ struct Layout {
 };
 
 enum { I_NCON = 0, I_NEFC, I_FLAGS, I_NITER, I_MISC, I_COUNT = 8 };
-constexpr int kSolverCG = 1;  // mjtSolver: mjSOL_PGS 0, mjSOL_CG 1, mjSOL_NEWTON 2
+constexpr int kSolverPGS = 0, kSolverCG = 1;  // mjtSolver: mjSOL_PGS 0, mjSOL_CG 1, mjSOL_NEWTON 2
 
 // Where each per-world array lives: LDS (fast, but it bounds how many worlds
 // share a CU) or the per-world global scratch (L1/L2-resident; coalesced since
@@ -3056,6 +3057,93 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         newton_direction();
     };
 
+    // PGS (opt.solver == mjSOL_PGS; generic instances only): MuJoCo's projected
+    // Gauss-Seidel on the dual (engine_solver.c mj_solPGS with the dual warm
+    // start of engine_forward.c; MuJoCo Warp has no PGS). The oracle's
+    // solve_pgs is the restatement this follows: minimise 0.5 f'AR f + f'b,
+    // AR = J M^-1 J' + diag(R), b = J qacc_smooth - aref (kept in jv), one row
+    // at a time with projection and the undo of a cost-increasing update; the
+    // sweep's improvement ends the solve. AR and the rows M^-1 J_r' live in
+    // global scratch (Lo.pgs_ar, Lo.pgs_mj), M's factor is still in Lm.
+    bool pgs = false;
+    if constexpr (SPEC < 0) pgs = m.solver == kSolverPGS;
+    if (pgs) {
+      float* const AR = G + Lo.pgs_ar;
+      float* const MJ = G + Lo.pgs_mj;
+      const int lda = Lo.rcap;
+      const float* const Lf = MODE == 2 ? G + Lo.h_L : Lm;
+      for (int r = 0; r < nefc; r++) {
+        for (int i = tid; i < nv; i += NT) tmp[i] = J[r * ldj + i];
+        ldl_solve_reg<NVP, PKL>(Lf, nv, ldm, tmp);
+        for (int i = tid; i < ldj; i += NT) MJ[r * ldj + i] = i < nv ? tmp[i] : 0.f;
+      }
+      wsync();
+      for (int i = 0; i < nefc; i++)
+        for (int j = tid; j < nefc; j += NT) AR[i * lda + j] = rowdot_u<NVP>(J + i * ldj, MJ + j * ldj, nv) + (j == i ? efc_R[i] : 0.f);
+      for (int r = tid; r < nefc; r += NT) jv[r] = rowdot_u<NVP>(J + r * ldj, qacc_smooth, nv) - efc_aref[r];
+      // warm start: the forces of qacc_warmstart's constraint state, zero when
+      // their dual cost is positive
+      for (int i = tid; i < nv; i += NT) qacc[i] = DP(qacc_warmstart)[W * nv + i];
+      wsync();
+      for (int r = tid; r < nefc; r += NT) {
+        float f, cr;
+        row_state(efc_type[r], efc_D[r], efc_R[r], efc_fl[r], rowdot_u<NVP>(J + r * ldj, qacc, nv) - efc_aref[r], &f, &cr);
+        efc_force[r] = f;
+      }
+      wsync();
+      float wc = 0.f;
+      for (int r = tid; r < nefc; r += NT) {
+        float af = 0.f;
+        for (int j = 0; j < nefc; j++) af += AR[r * lda + j] * efc_force[j];
+        wc += efc_force[r] * (jv[r] + 0.5f * af);
+      }
+      wc = bsum<NT>(wc, red);
+      if (wc > 0.f) {
+        lstr0 |= 1u << 30;
+        for (int r = tid; r < nefc; r += NT) efc_force[r] = 0.f;
+      }
+      wsync();
+      for (int it = 0; it < m.iterations; it++) {
+        float improvement = 0.f;
+        for (int i = 0; i < nefc; i++) {
+          float sres = 0.f;
+          for (int j = tid; j < nefc; j += NT) sres += AR[i * lda + j] * efc_force[j];
+          const float res = jv[i] + bsum<NT>(sres, red);
+          const float aii = AR[i * lda + i], old = efc_force[i];
+          float fi = old - res / fmaxf(aii, MJH_MINVAL);
+          if (efc_type[i] == MJH_CNSTR_FRICTION_DOF) {
+            const float fl = efc_fl[i];
+            fi = fi < -fl ? -fl : (fi > fl ? fl : fi);
+          } else if (fi < 0.f) {
+            fi = 0.f;
+          }
+          const float dl = fi - old;
+          float change = 0.5f * dl * dl * aii + dl * res;
+          if (change > 1e-10f) {
+            fi = old;
+            change = 0.f;
+          }
+          improvement -= change;
+          wsync();
+          if (tid == 0) efc_force[i] = fi;
+          wsync();
+        }
+        niter++;
+        if (improvement * scale < m.tolerance) {
+          lstr1 |= 1u << 30;
+          break;
+        }
+      }
+      for (int i = tid; i < nv; i += NT) {
+        float sf = 0.f;
+        for (int r = 0; r < nefc; r++) sf += J[r * ldj + i] * efc_force[r];
+        qfrc_con[i] = sf;
+        tmp[i] = sf;
+      }
+      ldl_solve_reg<NVP, PKL>(Lf, nv, ldm, tmp);
+      for (int i = tid; i < nv; i += NT) qacc[i] = qacc_smooth[i] + tmp[i];
+      wsync();
+    } else {
     // warm start: the cheaper of qacc_warmstart and qacc_smooth, both
     // evaluated in one pass over M's and J's rows (each row loaded once; the
     // qacc_smooth values wait in Mv / jv in case they win)
@@ -3293,6 +3381,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       direction(false);
       PROF_ACC(14, t_nd);
     }
+    }  // Newton / CG
   }
   wsync();
 
@@ -4060,6 +4149,9 @@ Layout make_layout(const mjh_model* m, int budget, int wpb) {
   L.h_type = gt(rcap); L.h_fl = gt(rcap); L.h_D = gt(rcap); L.h_R = gt(rcap);
   L.h_aref = gt(rcap); L.h_b = gt(rcap); L.h_jv = gt(rcap);
   L.h_ints = gt(8);
+  // PGS only (the dual's matrices; a model solved by Newton or CG allocates nothing)
+  L.pgs_ar = m->solver == kSolverPGS ? gt(rcap * rcap) : 0;
+  L.pgs_mj = m->solver == kSolverPGS ? gt(rcap * L.ldj) : 0;
   L.h_snap = gt(7 + m->nq + 7 * m->nmocap);
   // the position kernel's LDS per world: qpos, reductions, counters
   L.pred = al(m->nq);
@@ -4124,6 +4216,7 @@ bool data_is_slab(const mjh_model* m, const mjh_data* d) {
 int find_spec(const Plan& p, const mjh_model* m) {
   if (MJH_NSPEC == 0) return -1;
   if (m->cone == 1) return -1;  // elliptic cones: generic instances only
+  if (m->solver == kSolverPGS) return -1;  // PGS: generic instances only
   int v[kPlanInts];
   plan_to_ints(p, m, v);
   for (int k = 0; k < MJH_NSPEC; k++)
@@ -4248,6 +4341,8 @@ int mjh_model_check(const mjh_model* m) {
   // elliptic rows need the constraint Jacobian in global scratch (a preset that
   // keeps J in LDS builds pyramidal rows only)
   if (m->cone == 1 && !Rg::J) { g_err = "elliptic cones need a build with J in global scratch (MJH_PRESET)"; return 1; }
+  if (m->solver == kSolverPGS && m->cone == 1) { g_err = "the PGS solver supports pyramidal cones only"; return 1; }
+  if (m->solver == kSolverPGS && (!Rg::J || !Rg::M)) { g_err = "the PGS solver needs a build with J and M in global scratch"; return 1; }
   g_err.clear();
   return 0;
 }

@@ -56,8 +56,12 @@ class MujocoCfg:
   def apply(self, model: Model) -> None:
     if self.cone not in _CONES:
       raise ValueError(f"unknown friction cone {self.cone!r}")
-    if self.solver == "pgs":
-      raise NotImplementedError("the PGS solver is not implemented (Newton and CG are)")
+    if self.solver not in _SOLVERS:
+      raise ValueError(f"unknown solver {self.solver!r}")
+    if self.solver == "pgs" and self.cone == "elliptic":
+      # MuJoCo C's PGS projects each elliptic contact with a small QCQP; the
+      # device PGS (mjh_step.hip) handles pyramidal cones, limits and friction loss
+      raise NotImplementedError("the PGS solver supports pyramidal cones only (use Newton or CG for elliptic)")
     model.cone = _CONES[self.cone]
     model.solver = _SOLVERS[self.solver]
     model.jacobian = {"dense": 0, "sparse": 1, "auto": 2}[self.jacobian]

@@ -1651,6 +1651,113 @@ static real linesearch(const or_model* m, ws_t* w) {
   return alpha;
 }
 
+/* PGS (opt.solver == mjSOL_PGS): MuJoCo's projected Gauss-Seidel on the dual
+   problem (engine_solver.c mj_solPGS and the dual warm start of
+   engine_forward.c, restated from MuJoCo's published algorithm; MuJoCo Warp
+   implements CG and Newton only, so this follows MuJoCo C):
+     minimise 0.5 f' AR f + f' b,  AR = J M^-1 J' + diag(R),  b = J qacc_smooth - aref,
+   one row at a time: res = b_i + AR_i f, f_i -= res / AR_ii, projected onto
+   the row's set (friction loss: [-fl, fl]; limits and contact rows: f >= 0);
+   a row update whose cost change 0.5 AR_ii d^2 + d res exceeds 1e-10 is undone.
+   An iteration is one sweep over the rows; stop when the sweep's improvement
+   (the summed cost decrease) times 1 / (meaninertia nv) is below tolerance.
+   Warm start: the forces of qacc_warmstart's constraint state (jar = J qacc_ws -
+   aref), replaced by zero when their dual cost is positive. Result:
+   qfrc_constraint = J' f, qacc = qacc_smooth + M^-1 qfrc_constraint. Elliptic
+   cones are not supported here (MuJoCo solves a small cone QCQP per contact;
+   the Python layer refuses that combination). */
+static void solve_pgs(const or_model* m, ws_t* w, const real* warm) {
+  const int nv = m->nv, n = w->nefc;
+  const real scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+  real* MJ = (real*)xcalloc((size_t)n * nv, sizeof(real)); /* rows: M^-1 J_r' */
+  real* A = (real*)xcalloc((size_t)n * n, sizeof(real));
+  real* b = (real*)xcalloc((size_t)n, sizeof(real));
+  real* f = w->efc_force;
+  for (int r = 0; r < n; r++) {
+    memcpy(MJ + (size_t)r * nv, w->J + (size_t)r * nv, sizeof(real) * nv);
+    solve_tree(m, w->LD, MJ + (size_t)r * nv);
+  }
+  for (int i = 0; i < n; i++) {
+    for (int j = 0; j < n; j++) {
+      real s = 0;
+      for (int d = 0; d < nv; d++) s += w->J[(size_t)i * nv + d] * MJ[(size_t)j * nv + d];
+      A[(size_t)i * n + j] = s;
+    }
+    A[(size_t)i * n + i] += w->efc_R[i];
+    real s = 0;
+    for (int d = 0; d < nv; d++) s += w->J[(size_t)i * nv + d] * w->qacc_smooth[d];
+    b[i] = s - w->efc_aref[i];
+  }
+  /* warm start */
+  for (int r = 0; r < n; r++) {
+    real s = 0, c;
+    for (int d = 0; d < nv; d++) s += w->J[(size_t)r * nv + d] * warm[d];
+    row_eval(w, r, s - w->efc_aref[r], f + r, &c);
+  }
+  real wc = 0;
+  for (int i = 0; i < n; i++) {
+    real af = 0;
+    for (int j = 0; j < n; j++) af += A[(size_t)i * n + j] * f[j];
+    wc += f[i] * (b[i] + 0.5 * af);
+  }
+  if (g_dbg_warm) {
+    g_dbg_warm[2 * (size_t)w->wi] = wc;
+    g_dbg_warm[2 * (size_t)w->wi + 1] = 0;
+  }
+  w->warm_smooth = wc > 0;
+  if (wc > 0) memset(f, 0, sizeof(real) * n);
+  for (int it = 0; it < m->iterations; it++) {
+    if (w->follow && it >= w->fniter) break;
+    real improvement = 0;
+    for (int i = 0; i < n; i++) {
+      real res = b[i];
+      for (int j = 0; j < n; j++) res += A[(size_t)i * n + j] * f[j];
+      const real aii = A[(size_t)i * n + i], old = f[i];
+      real fi = old - res / (aii < MINVAL ? MINVAL : aii);
+      if (w->efc_type[i] == 1) {
+        const real fl = w->efc_fl[i];
+        fi = fi < -fl ? -fl : (fi > fl ? fl : fi);
+      } else if (fi < 0) {
+        fi = 0;
+      }
+      const real dl = fi - old;
+      real change = 0.5 * dl * dl * aii + dl * res;
+      if (change > 1e-10) {
+        fi = old;
+        change = 0;
+      }
+      f[i] = fi;
+      improvement -= change;
+    }
+    w->niter++;
+    const int conv = improvement * scale < m->tolerance;
+    if (g_dbg_conv && it < 15) {
+      real* cv = g_dbg_conv + ((size_t)w->wi * 15 + it) * 4;
+      cv[0] = improvement * scale;
+      cv[1] = NAN;
+      cv[2] = NAN;
+      cv[3] = NAN;
+    }
+    w->conv = conv;
+    if (!w->follow && conv) break;
+    if (it == m->iterations - 1 && !conv) w->capped = 1;
+  }
+  memset(w->qfrc_constraint, 0, sizeof(real) * nv);
+  for (int r = 0; r < n; r++)
+    for (int d = 0; d < nv; d++) w->qfrc_constraint[d] += w->J[(size_t)r * nv + d] * f[r];
+  memcpy(w->qacc, w->qfrc_constraint, sizeof(real) * nv);
+  solve_tree(m, w->LD, w->qacc);
+  for (int d = 0; d < nv; d++) w->qacc[d] += w->qacc_smooth[d];
+  for (int r = 0; r < n; r++) {
+    real s = 0;
+    for (int d = 0; d < nv; d++) s += w->J[(size_t)r * nv + d] * w->qacc[d];
+    w->jaref[r] = s - w->efc_aref[r];
+  }
+  free(MJ);
+  free(A);
+  free(b);
+}
+
 static void solve(const or_model* m, ws_t* w, const real* warm) {
   int nv = m->nv;
   real scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
@@ -1658,6 +1765,10 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
   if (w->nefc == 0) {
     memcpy(w->qacc, w->qacc_smooth, sizeof(real) * nv);
     memset(w->qfrc_constraint, 0, sizeof(real) * nv);
+    return;
+  }
+  if (m->solver == 0) {
+    solve_pgs(m, w, warm);
     return;
   }
   /* warmstart: keep the lower-cost of qacc_warmstart and qacc_smooth */

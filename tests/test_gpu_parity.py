@@ -594,3 +594,70 @@ def test_cylinder_ellipsoid_pairs_parity():
   kinds = {(int(types[a]), int(types[b])) for w in range(n) for a, b in g[w, : int(got["ncon"][w, 0])]}
   assert {(0, 4), (0, 5), (2, 5)} <= kinds, kinds
   print("[cylinder/ellipsoid pairs] contact kinds", sorted(kinds), "int rate", rep["int_match_rate"])
+
+
+@pytest.mark.parametrize("iterations", [1, 5])
+def test_pgs_solver_parity(iterations):
+  """opt.solver = PGS (MuJoCo's projected Gauss-Seidel on the dual; the
+  reference's MujocoCfg maps solver="pgs" to mjSOL_PGS, sim.py:34-38,55):
+  the HIP sweeps against the oracle's (oracle.c solve_pgs) from the same dual
+  warm start, a fixed number of sweeps (a PGS solve rarely meets the 1e-8
+  tolerance in a few sweeps, so both run to the cap): the soft solve test, as
+  for the capped CG solves."""
+  n = 256
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(43))
+  cfg = dict(CFG, mujoco=MujocoCfg(timestep=0.005, iterations=iterations, solver="pgs"))
+  sim = Simulation(n, SimulationCfg(**cfg, ls_parallel=False), m, DEV)
+  assert m.solver == 0
+  put(sim, st)
+  sim.step()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=True)
+  assert (got["nefc"] > 0).mean() > 0.5
+  assert (got["solver_niter"] == ref["solver_niter"]).mean() > 0.95
+  rep = compare_step(got, ref)
+  print(f"[pgs iterations={iterations}]", {k: f"{v:.2e}" for k, v in rep["maxerr"].items() if "/" in k})
+  assert not [f for f in rep["failures"] if "unconverged at the iteration cap" not in f], rep["failures"]
+  # the warm-start decision (dual cost of the warm forces > 0 -> zero forces) agrees
+  warm_dev, warm_ref = (got["solver_lstrace"][:, 0] >> 30) & 1, (ref["solver_lstrace"][:, 0] >> 30) & 1
+  assert (warm_dev == warm_ref).mean() > 0.98
+
+
+def test_pgs_converged_matches_newton():
+  """PGS run long (3000 sweeps) on the HIP step reaches the minimiser the
+  float64 oracle's Newton finds (the dual and primal problems share it), to
+  the float32 resolution of a linearly converging iteration."""
+  n = 128
+  m = g1_scene_model(n)
+  st = random_states(m, n, np.random.default_rng(45))
+  cfg = dict(CFG, mujoco=MujocoCfg(timestep=0.005, iterations=3000, tolerance=1e-12, solver="pgs"))
+  sim = Simulation(n, SimulationCfg(**cfg, ls_parallel=False), m, DEV)
+  put(sim, st)
+  sim.forward()
+  got = get(sim, n)
+  m.solver, m.iterations, m.tolerance, m.ls_parallel, m.ls_iterations = 2, 200, 1e-15, 0, 50
+  ref = Oracle(m).run(n, st, integrate=False)
+  scale = 1 + np.abs(ref["qacc"]).max(axis=1, keepdims=True)
+  err = (np.abs(got["qacc"] - ref["qacc"]) / scale).max(axis=1)
+  print("[pgs converged] max/median rel err", err.max(), np.median(err), "sweeps", got["solver_niter"].mean())
+  assert np.median(err) < 1e-4 and err.max() < 2e-3, (np.median(err), err.max())
+
+
+def test_pgs_known_answers_on_gpu():
+  """The closed-form scenes on the HIP PGS: the condim-1 ball rests at the
+  documented r* (tests/test_soft_constraint.py) and carries m g."""
+  from tests.test_soft_constraint import G, MASS, PARAMS, RAD, ball_model, rest_penetration
+
+  solref, solimp = PARAMS["default"]
+  m = ball_model(solref, solimp)
+  n = 8
+  sim = Simulation(n, SimulationCfg(nconmax=8, njmax=32, mujoco=MujocoCfg(timestep=m.timestep, iterations=100,
+                                                                          tolerance=1e-10, solver="pgs")), m, DEV)
+  q = np.tile([0, 0, RAD + 0.002, 1, 0, 0, 0], (n, 1))
+  put(sim, {"qpos": q})
+  for _ in range(800):
+    sim.step()
+  z = sim.data.qpos[:, 2].double().cpu().numpy()
+  np.testing.assert_allclose(z - RAD, rest_penetration(solref, solimp, m.timestep), rtol=2e-3)
+  np.testing.assert_allclose(sim.data.qfrc_constraint[:, 2].double().cpu().numpy(), MASS * G, rtol=1e-4)

@@ -419,3 +419,72 @@ def test_elliptic_newton_converges_fast_and_matches_cg():
   scale = 1 + np.abs(newton["qacc"]).max(axis=1, keepdims=True)
   assert (np.abs(cg["qacc"] - newton["qacc"]) / scale).max() < 1e-6
   assert newton["solver_niter"].mean() < 20 < cg["solver_niter"].mean()
+
+
+@pytest.mark.parametrize("scene", ["g1", "box"])
+def test_pgs_newton_cg_reach_the_same_minimiser(scene):
+  """PGS (opt.solver = mjSOL_PGS: projected Gauss-Seidel on the dual
+  0.5 f'AR f + f'b) and Newton / CG (the primal) solve the same convex
+  problem, so with the iteration caps lifted the three reach the same qacc
+  (float64 oracle). PGS converges linearly: it needs far more iterations."""
+  from tests.scenes import random_states
+
+  if scene == "g1":
+    n = 8
+    m = g1_scene_model(n)
+    st = random_states(m, n, np.random.default_rng(35))
+  else:
+    from tests.test_gpu_parity import BOX_SCENE, _box_states
+
+    n = 16
+    m = _model(BOX_SCENE)
+    st = _box_states(m, n, np.random.default_rng(36))
+  m.tolerance, m.ls_iterations, m.ls_parallel = 1e-15, 50, 0
+  out = {}
+  for solver, iters in (("newton", 200), ("cg", 3000), ("pgs", 20000)):
+    m.solver, m.iterations = {"pgs": 0, "cg": 1, "newton": 2}[solver], iters
+    out[solver] = Oracle(m).run(n, st, integrate=False)
+  assert (out["newton"]["nefc"] > 0).mean() > 0.5
+  scale = 1 + np.abs(out["newton"]["qacc"]).max(axis=1, keepdims=True)
+  for s in ("cg", "pgs"):
+    err = (np.abs(out[s]["qacc"] - out["newton"]["qacc"]) / scale).max()
+    assert err < 1e-5, (s, err)
+  # the dual solution's forces satisfy the projections: contact/limit rows >= 0
+  f, ty = out["pgs"]["efc_force"], out["pgs"]["efc_type"]
+  for w in range(n):
+    k = int(out["pgs"]["nefc"][w, 0])
+    assert (f[w, :k][ty[w, :k] != 1] >= 0).all()
+  assert out["pgs"]["solver_niter"].mean() > out["newton"]["solver_niter"].mean()
+
+
+def test_pgs_resting_penetration_and_incline_threshold():
+  """PGS on the closed-form scenes: the condim-1 ball rests at MuJoCo's
+  documented r* (tests/test_soft_constraint.py), and the incline block sticks
+  below tan(theta) = mu and slides with a = g (sin - mu cos) above it."""
+  from tests.test_soft_constraint import PARAMS, RAD, ball_model, rest_penetration, rollout
+
+  solref, solimp = PARAMS["default"]
+  m = ball_model(solref, solimp)
+  m.solver, m.iterations, m.tolerance = 0, 200, 1e-14
+  zs, _ = rollout(Oracle(m), RAD + 0.002, 0.0, 800)
+  assert zs[-1] - RAD == pytest.approx(rest_penetration(solref, solimp, m.timestep), rel=1e-6)
+  mu, g = 0.65, 9.81
+  for tan_theta, slides in ((0.5, False), (0.8, True)):
+    th = np.arctan(tan_theta)
+    xml = _free_body_xml(
+      f"""<body name="blk" pos="0 0 0.05"><freejoint/><geom type="box" size="0.1 0.1 0.05" mass="1" friction="{mu} 0.005 0.0001"/></body>""",
+      gravity=f"{g * np.sin(th)} 0 {-g * np.cos(th)}",
+      plane=f'<geom name="floor" type="plane" size="5 5 0.1" friction="{mu} 0.005 0.0001"/>')
+    m = _model(xml, solver=0, iterations=100)
+    orc = Oracle(m)
+    st = {"qpos": m.qpos0[None].copy()}
+    vx = []
+    for _ in range(500):
+      out = orc.run(1, st, integrate=True)
+      st = {k: out[k] for k in ("qpos", "qvel", "qacc_warmstart", "time")}
+      vx.append(st["qvel"][0, 0])
+    if slides:
+      a = (vx[-1] - vx[249]) / (250 * m.timestep)
+      assert a == pytest.approx(g * (np.sin(th) - mu * np.cos(th)), rel=0.05)
+    else:
+      assert abs(vx[-1]) < 5e-3 and abs(st["qpos"][0, 0]) < 5e-3

@@ -757,11 +757,13 @@ SIM_ROBOT_XML = """
 </worldbody></mujoco>"""
 
 MJ_INT_EULER, MJ_SOL_CG = 0, 1
+MJ_SOL_PGS = 0
 
 
 def test_simulation_config_is_piped(backend):
-  """test_sim.py:43-82, as the reference writes it (solver="cg"); the PGS
-  solver is refused rather than silently replaced."""
+  """test_sim.py:43-82, as the reference writes it (solver="cg"); solver="pgs"
+  is piped too (MuJoCo's mjSOL_PGS, pyramidal cones), PGS with elliptic cones
+  is refused rather than silently replaced."""
   model = compile_spec(read_mjcf_string(SIM_ROBOT_XML))
   cfg = SimulationCfg(contact_sensor_maxmatch=128, ls_parallel=False,
                       mujoco=MujocoCfg(timestep=0.02, integrator="euler", solver="cg", iterations=7,
@@ -782,8 +784,12 @@ def test_simulation_config_is_piped(backend):
   # the piped options reach the step: one Euler step under +7.5 gravity
   sim.step()
   assert abs(float(sim.data.qvel[0, 2]) - 7.5 * 0.02) < 1e-5
+  pgs = make_sim(1, SimulationCfg(mujoco=MujocoCfg(solver="pgs")), compile_spec(read_mjcf_string(SIM_ROBOT_XML)), backend)
+  assert pgs.mj_model.opt.solver == MJ_SOL_PGS and pgs.model.opt.solver == MJ_SOL_PGS
+  pgs.step()
   with pytest.raises(NotImplementedError):
-    make_sim(1, SimulationCfg(mujoco=MujocoCfg(solver="pgs")), compile_spec(read_mjcf_string(SIM_ROBOT_XML)), backend)
+    make_sim(1, SimulationCfg(mujoco=MujocoCfg(solver="pgs", cone="elliptic")), compile_spec(read_mjcf_string(SIM_ROBOT_XML)),
+             backend)
 
 
 # ---------------------------------------------------------------------------
