@@ -1,0 +1,67 @@
+// mjh_batch.h — one launch for a pass of independent per-env env-layer kernels.
+//
+// A captured env step replays ~50 small env-layer kernels; each is a separate
+// dispatch whose cost (~5 us on 4,096 envs) is its launch and memory latency,
+// not its work. Kernels that the env layer evaluates as a group of mutually
+// independent per-env jobs (the reward terms of one reward pass) are written
+// as job structs whose run(e) is the kernel body; their C-ABI entry points
+// either launch the job's own kernel (no batch open) or append the job to the
+// open batch. mjh_batch_end launches every translation unit's batch kernel
+// once: blockIdx.y selects the job, blockIdx.x * blockDim.x + threadIdx.x the
+// env, so the batched pass runs the same arithmetic as the separate launches
+// (bit-identical outputs) in one dispatch per file. Jobs in a batch must not
+// read each other's outputs (the reward terms read sim state, EntityData and
+// commands only); anything launched while a batch is open runs before it.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace mjh_batch {
+
+constexpr int kArgBytes = 192;  // the largest job struct (static_assert in submit)
+constexpr int kMaxJobs = 10;    // per translation unit and launch (kernel arguments: ~2 KB)
+enum Unit { kMdp = 0, kFuse = 1, kUnits = 2 };
+
+struct Job {
+  int kind;
+  int pad;
+  long long n;
+  alignas(16) unsigned char a[kArgBytes];
+};
+
+struct Pack {
+  int njobs;
+  int pad;
+  long long nmax;
+  Job jobs[kMaxJobs];
+};
+
+typedef void (*Launcher)(const Pack&, hipStream_t);
+
+// host side (mjh_mgr.hip): register a unit's batch launcher; append a job to
+// the open batch (false: no batch open, the caller launches the job itself)
+bool register_unit(int unit, Launcher f);
+bool add(int unit, int kind, long long n, const void* args, size_t bytes, hipStream_t s);
+
+inline int grid1(long long n) { return (int)((n + 255) / 256); }
+
+// launch job J's own kernel, or append it to the open batch
+template <class J>
+int submit(int unit, const J& j, long long n, hipStream_t s, void (*kernel)(J, long long)) {
+  static_assert(sizeof(J) <= kArgBytes, "job struct exceeds the batch slot");
+  if (n <= 0) return 0;
+  if (add(unit, J::kKind, n, &j, sizeof(J), s)) return 0;
+  hipLaunchKernelGGL(kernel, dim3(grid1(n)), dim3(256), 0, s, j, n);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+}  // namespace mjh_batch
+
+// the per-job kernel of a job struct J (J::run(e) is the body)
+template <class J>
+__global__ void mjh_job_kernel(const J j, long long n) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) j.run(e);
+}

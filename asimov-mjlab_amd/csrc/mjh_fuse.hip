@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/mjh_abi.h"
+#include "mjh_batch.h"
 #include "mjh_rng.h"
 
 namespace {
@@ -442,71 +443,95 @@ __device__ __forceinline__ float cmd_active(const float* cmd, long long cs, long
   return (sqrtf(c[0] * c[0] + c[1] * c[1]) + fabsf(c[2])) > thr ? 1.f : 0.f;
 }
 
+// the contact-timing reward terms as batchable jobs (mjh_batch.h; run(e) is
+// the term for env e)
 // feet_air_time: sum((t > tmin) & (t < tmax)) * active; log air_time_mean
-__global__ void rew_air_time_kernel(const float* __restrict__ t, long long ts, const float* __restrict__ cmd, long long cs,
-                                    float tmin, float tmax, float cmd_thr, float* __restrict__ out,
-                                    float* __restrict__ num, float* __restrict__ den, int k, long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  float r = 0.f, a = 0.f, b = 0.f;
-  for (int j = 0; j < k; j++) {
-    const float x = t[e * ts + j];
-    r += (x > tmin && x < tmax) ? 1.f : 0.f;
-    const float in_air = x > 0.f ? 1.f : 0.f;
-    a += x * in_air;
-    b += in_air;
+struct AirTimeJob {
+  static constexpr int kKind = 101;
+  const float* t; long long ts; const float* cmd; long long cs; float tmin; float tmax; float cmd_thr;
+  float* out; float* num; float* den; int k;
+  __device__ __forceinline__ void run(long long e) const {
+    float r = 0.f, a = 0.f, b = 0.f;
+    for (int j = 0; j < k; j++) {
+      const float x = t[e * ts + j];
+      r += (x > tmin && x < tmax) ? 1.f : 0.f;
+      const float in_air = x > 0.f ? 1.f : 0.f;
+      a += x * in_air;
+      b += in_air;
+    }
+    out[e] = r * cmd_active(cmd, cs, e, cmd_thr);
+    num[e] = a;
+    den[e] = b;
   }
-  out[e] = r * cmd_active(cmd, cs, e, cmd_thr);
-  num[e] = a;
-  den[e] = b;
-}
+};
 
 // feet_swing_height: peak = in_air ? max(peak, h) : peak; first contact =
 // 0 < contact_time < first_lim; cost = sum((peak / target - 1)^2 * first) *
 // active; log peak_height_mean; peak cleared where first
-__global__ void rew_swing_height_kernel(float* __restrict__ peak, const float* __restrict__ h, long long hes,
-                                        long long hcs, const float* __restrict__ found, long long fes, long long fcs,
-                                        const float* __restrict__ cct, long long cts, const float* __restrict__ cmd,
-                                        long long cs, float first_lim, float target, float cmd_thr,
-                                        float* __restrict__ out, float* __restrict__ num, float* __restrict__ den, int k,
-                                        long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  float c = 0.f, a = 0.f, b = 0.f;
-  for (int j = 0; j < k; j++) {
-    float p = peak[e * k + j];
-    if (found[e * fes + j * fcs] == 0.f) p = fmaxf(p, h[e * hes + j * hcs]);
-    const float ct = cct[e * cts + j];
-    const float first = (ct > 0.f && ct < first_lim) ? 1.f : 0.f;
-    const float err = p / target - 1.f;
-    c += err * err * first;
-    a += p * first;
-    b += first;
-    peak[e * k + j] = first != 0.f ? 0.f : p;
+struct SwingHeightJob {
+  static constexpr int kKind = 102;
+  float* peak; const float* h; long long hes; long long hcs; const float* found; long long fes; long long fcs;
+  const float* cct; long long cts; const float* cmd; long long cs; float first_lim; float target; float cmd_thr;
+  float* out; float* num; float* den; int k;
+  __device__ __forceinline__ void run(long long e) const {
+    float c = 0.f, a = 0.f, b = 0.f;
+    for (int j = 0; j < k; j++) {
+      float p = peak[e * k + j];
+      if (found[e * fes + j * fcs] == 0.f) p = fmaxf(p, h[e * hes + j * hcs]);
+      const float ct = cct[e * cts + j];
+      const float first = (ct > 0.f && ct < first_lim) ? 1.f : 0.f;
+      const float err = p / target - 1.f;
+      c += err * err * first;
+      a += p * first;
+      b += first;
+      peak[e * k + j] = first != 0.f ? 0.f : p;
+    }
+    out[e] = c * cmd_active(cmd, cs, e, cmd_thr);
+    num[e] = a;
+    den[e] = b;
   }
-  out[e] = c * cmd_active(cmd, cs, e, cmd_thr);
-  num[e] = a;
-  den[e] = b;
-}
+};
 
 // soft_landing: sum(|force| * first) * active; log landing_force_mean
-__global__ void rew_soft_landing_kernel(const float* __restrict__ f, long long fes, long long fss,
-                                        const float* __restrict__ cct, long long cts, const float* __restrict__ cmd,
-                                        long long cs, float first_lim, float cmd_thr, float* __restrict__ out,
-                                        float* __restrict__ num, float* __restrict__ den, int k, long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  float c = 0.f, b = 0.f;
-  for (int j = 0; j < k; j++) {
-    const float* v = f + e * fes + j * fss;
-    const float ct = cct[e * cts + j];
-    const float first = (ct > 0.f && ct < first_lim) ? 1.f : 0.f;
-    c += sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]) * first;
-    b += first;
+struct SoftLandingJob {
+  static constexpr int kKind = 103;
+  const float* f; long long fes; long long fss; const float* cct; long long cts; const float* cmd; long long cs;
+  float first_lim; float cmd_thr; float* out; float* num; float* den; int k;
+  __device__ __forceinline__ void run(long long e) const {
+    float c = 0.f, b = 0.f;
+    for (int j = 0; j < k; j++) {
+      const float* v = f + e * fes + j * fss;
+      const float ct = cct[e * cts + j];
+      const float first = (ct > 0.f && ct < first_lim) ? 1.f : 0.f;
+      c += sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]) * first;
+      b += first;
+    }
+    out[e] = c * cmd_active(cmd, cs, e, cmd_thr);
+    num[e] = c;
+    den[e] = b;
   }
-  out[e] = c * cmd_active(cmd, cs, e, cmd_thr);
-  num[e] = c;
-  den[e] = b;
+};
+
+__global__ void fuse_batch_kernel(const mjh_batch::Pack p) {
+  const mjh_batch::Job& j = p.jobs[blockIdx.y];
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= j.n) return;
+  switch (j.kind) {
+    case AirTimeJob::kKind: reinterpret_cast<const AirTimeJob*>(j.a)->run(e); break;
+    case SwingHeightJob::kKind: reinterpret_cast<const SwingHeightJob*>(j.a)->run(e); break;
+    case SoftLandingJob::kKind: reinterpret_cast<const SoftLandingJob*>(j.a)->run(e); break;
+    default: break;
+  }
+}
+
+void fuse_batch_launch(const mjh_batch::Pack& p, hipStream_t s) {
+  hipLaunchKernelGGL(fuse_batch_kernel, dim3(mjh_batch::grid1(p.nmax), p.njobs), dim3(256), 0, s, p);
+}
+const bool kFuseRegistered = mjh_batch::register_unit(mjh_batch::kFuse, fuse_batch_launch);
+
+template <class J>
+int submit_job(const J& j, long long n, void* stream) {
+  return mjh_batch::submit(mjh_batch::kFuse, j, n, (hipStream_t)stream, mjh_job_kernel<J>);
 }
 
 // ActionManager.process_action with one JointAction term (action_manager.py:
@@ -999,29 +1024,21 @@ int mjh_sum_ratios(const float* const* num, const float* const* den, int nterms,
 
 int mjh_rew_air_time(const float* t, long long ts, const float* cmd, long long cs, float tmin, float tmax, float cmd_thr,
                      float* out, float* num, float* den, int k, long long n, void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(rew_air_time_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, t, ts, cmd, cs, tmin, tmax,
-                     cmd_thr, out, num, den, k, n);
-  return finish();
+  return submit_job(AirTimeJob{t, ts, cmd, cs, tmin, tmax, cmd_thr, out, num, den, k}, n, stream);
 }
 
 int mjh_rew_swing_height(float* peak, const float* h, long long hes, long long hcs, const float* found, long long fes,
                          long long fcs, const float* cct, long long cts, const float* cmd, long long cs, float first_lim,
                          float target, float cmd_thr, float* out, float* num, float* den, int k, long long n,
                          void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(rew_swing_height_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, peak, h, hes, hcs, found,
-                     fes, fcs, cct, cts, cmd, cs, first_lim, target, cmd_thr, out, num, den, k, n);
-  return finish();
+  return submit_job(SwingHeightJob{peak, h, hes, hcs, found, fes, fcs, cct, cts, cmd, cs, first_lim, target, cmd_thr, out, num,
+                                   den, k}, n, stream);
 }
 
 int mjh_rew_soft_landing(const float* f, long long fes, long long fss, const float* cct, long long cts, const float* cmd,
                          long long cs, float first_lim, float cmd_thr, float* out, float* num, float* den, int k,
                          long long n, void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(rew_soft_landing_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, f, fes, fss, cct, cts, cmd,
-                     cs, first_lim, cmd_thr, out, num, den, k, n);
-  return finish();
+  return submit_job(SoftLandingJob{f, fes, fss, cct, cts, cmd, cs, first_lim, cmd_thr, out, num, den, k}, n, stream);
 }
 
 int mjh_joint_action(const float* input, long long is, float* action, float* prev, float* raw, float* processed,

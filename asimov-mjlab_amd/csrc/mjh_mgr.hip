@@ -5,7 +5,10 @@
 // launch parameter (no host->device copy inside the env step).
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include "../../include/mjh_abi.h"
+#include "mjh_batch.h"
 #include "mjh_rng.h"
 
 namespace {
@@ -98,7 +101,67 @@ __global__ void reward_combine_kernel(const RewArgs a, const float* __restrict__
 
 }  // namespace
 
+// ---- the job batch's host side (mjh_batch.h) ----------------------------------
+namespace mjh_batch {
+namespace {
+struct State {
+  bool open = false;
+  hipStream_t stream = nullptr;
+  Pack pack[kUnits];
+};
+thread_local State g_state;
+Launcher g_launch[kUnits] = {};
+
+void flush_unit(State& st, int u) {
+  Pack& p = st.pack[u];
+  if (p.njobs > 0 && g_launch[u]) g_launch[u](p, st.stream);
+  p.njobs = 0;
+  p.nmax = 0;
+}
+}  // namespace
+
+bool register_unit(int unit, Launcher f) {
+  if (unit < 0 || unit >= kUnits) return false;
+  g_launch[unit] = f;
+  return true;
+}
+
+bool add(int unit, int kind, long long n, const void* args, size_t bytes, hipStream_t s) {
+  State& st = g_state;
+  if (!st.open || unit < 0 || unit >= kUnits || !g_launch[unit] || bytes > (size_t)kArgBytes) return false;
+  if (s != st.stream) {  // a job on another stream: everything recorded so far goes first
+    for (int u = 0; u < kUnits; u++) flush_unit(st, u);
+    st.stream = s;
+  }
+  Pack& p = st.pack[unit];
+  if (p.njobs == kMaxJobs) flush_unit(st, unit);
+  Job& j = p.jobs[p.njobs++];
+  j.kind = kind;
+  j.pad = 0;
+  j.n = n;
+  std::memcpy(j.a, args, bytes);
+  if (n > p.nmax) p.nmax = n;
+  return true;
+}
+}  // namespace mjh_batch
+
 extern "C" {
+
+int mjh_batch_begin(void) {
+  mjh_batch::g_state.open = true;
+  mjh_batch::g_state.stream = nullptr;
+  for (auto& p : mjh_batch::g_state.pack) p.njobs = 0, p.nmax = 0;
+  return 0;
+}
+
+int mjh_batch_end(void* stream) {
+  auto& st = mjh_batch::g_state;
+  if (!st.open) return 0;
+  if (!st.stream) st.stream = (hipStream_t)stream;
+  for (int u = 0; u < mjh_batch::kUnits; u++) mjh_batch::flush_unit(st, u);
+  st.open = false;
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 
 int mjh_obs_group(const mjh_obs_term_desc* terms, int nterms, const float* u, long long us, float* out, long long os,
                   long long n, unsigned long long seed, unsigned long long key, const mjh_i64* ctr, void* stream) {

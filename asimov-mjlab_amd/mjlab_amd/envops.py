@@ -27,6 +27,45 @@ def _stream() -> ctypes.c_void_p:
   return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+# ---- job batches (csrc/mjh_batch.h) ---------------------------------------------
+_OPEN_BATCH = None
+
+
+class JobBatch:
+  """Context for a pass of independent per-env fused kernels (the reward terms):
+  inside it the batchable entry points record their job (mjh_batch_begin) and
+  the exit launches them all at once (mjh_batch_end: one dispatch per kernel
+  source file instead of one per term). The jobs' outputs must not be read
+  before the exit. The inputs they were recorded with are kept alive until the
+  batch has been launched (a temporary freed earlier could be reused by a
+  later allocation on the stream before the batch reads it). CPU tensors: no-op."""
+
+  def __init__(self, like: torch.Tensor) -> None:
+    self.on = bool(like.is_cuda)
+    self.keep: list = []
+
+  def __enter__(self) -> "JobBatch":
+    global _OPEN_BATCH
+    if self.on and _OPEN_BATCH is None:
+      native.check(native.lib().mjh_batch_begin(), "mjh_batch_begin")
+      _OPEN_BATCH = self
+    return self
+
+  def __exit__(self, *exc) -> bool:
+    global _OPEN_BATCH
+    if _OPEN_BATCH is self:
+      _OPEN_BATCH = None
+      native.check(native.lib().mjh_batch_end(_stream()), "mjh_batch_end")
+      self.keep.clear()
+    return False
+
+
+def _keep(*ts) -> None:
+  """Inputs of a job recorded into the open batch stay referenced until it launches."""
+  if _OPEN_BATCH is not None:
+    _OPEN_BATCH.keep.extend(t for t in ts if isinstance(t, torch.Tensor))
+
+
 def _rotate(q: torch.Tensor, v: torch.Tensor, inverse: bool) -> torch.Tensor:
   n = q.shape[0]
   out = torch.empty((n, 3), dtype=torch.float32, device=q.device)
@@ -133,6 +172,7 @@ def rew_track(cmd: torch.Tensor, v: torch.Tensor, std: float, angular: bool):
   if not (_rows(cmd, 3) and _rows(v, 3) and cmd.shape[0] == v.shape[0]):
     return None
   out = _vec_out(cmd.shape[0], cmd.device)
+  _keep(cmd, v)
   native.check(native.lib().mjh_rew_track(_ptr(cmd), cmd.stride(0), _ptr(v), v.stride(0), 1.0 / (std * std), int(angular),
                                           _ptr(out), cmd.shape[0], _stream()), "mjh_rew_track")
   return out
@@ -142,6 +182,7 @@ def rew_flat_orientation(q: torch.Tensor, g: torch.Tensor, std: float):
   if not (_rows(q, 4) and _rows(g, 3) and q.shape[0] == g.shape[0]):
     return None
   out = _vec_out(q.shape[0], q.device)
+  _keep(q, g)
   native.check(native.lib().mjh_rew_flat_orientation(_ptr(q), q.stride(0), _ptr(g), g.stride(0), 1.0 / (std * std), _ptr(out),
                                                      q.shape[0], _stream()), "mjh_rew_flat_orientation")
   return out
@@ -151,6 +192,7 @@ def rew_sqsum(x: torch.Tensor, k: int):
   if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1 and x.shape[1] >= k):
     return None
   out = _vec_out(x.shape[0], x.device)
+  _keep(x)
   native.check(native.lib().mjh_rew_sqsum(_ptr(x), x.stride(0), k, _ptr(out), x.shape[0], _stream()), "mjh_rew_sqsum")
   return out
 
@@ -160,6 +202,7 @@ def rew_diffsq(a: torch.Tensor, b: torch.Tensor):
   if not ok or a.shape != b.shape:
     return None
   out = _vec_out(a.shape[0], a.device)
+  _keep(a, b)
   native.check(native.lib().mjh_rew_diffsq(_ptr(a), a.stride(0), _ptr(b), b.stride(0), a.shape[1], _ptr(out), a.shape[0],
                                            _stream()), "mjh_rew_diffsq")
   return out
@@ -170,6 +213,7 @@ def rew_pos_limits(q: torch.Tensor, lim: torch.Tensor):
           and lim.stride(2) == 1 and lim.stride(1) == 2 and q.dtype == lim.dtype == torch.float32):
     return None
   out = _vec_out(q.shape[0], q.device)
+  _keep(q, lim)
   native.check(native.lib().mjh_rew_pos_limits(_ptr(q), q.stride(0), _ptr(lim), lim.stride(0), q.shape[1], _ptr(out),
                                                q.shape[0], _stream()), "mjh_rew_pos_limits")
   return out
@@ -182,6 +226,7 @@ def rew_posture(q, q0, std_stand, std_walk, std_run, cmd, walk_thr, run_thr):
   if not all(t.is_contiguous() and t.numel() == q.shape[1] for t in (std_stand, std_walk, std_run)):
     return None
   out = _vec_out(q.shape[0], q.device)
+  _keep(q, q0, std_stand, std_walk, std_run, cmd)
   native.check(native.lib().mjh_rew_posture(
     _ptr(q), q.stride(0), _ptr(q0), q0.stride(0), _ptr(std_stand), _ptr(std_walk), _ptr(std_run), _ptr(cmd), cmd.stride(0),
     float(walk_thr), float(run_thr), q.shape[1], _ptr(out), q.shape[0], _stream()), "mjh_rew_posture")
@@ -206,6 +251,7 @@ def rew_feet(pos: torch.Tensor, vel: torch.Tensor, found, cmd: torch.Tensor, tar
   z = pos[:, :, 2]
   cl = _vec_out(n, pos.device) if want == "clearance" else None
   outs = [_vec_out(n, pos.device) for _ in range(3)] if want == "slip" else [None, None, None]
+  _keep(pos, vel, found, cmd)
   native.check(native.lib().mjh_rew_feet(
     ctypes.c_void_p(pos.data_ptr() + 8), pos.stride(0), _ptr(vel), vel.stride(0), vel.stride(1),
     _ptr(found) if want == "slip" else None, found.stride(0) if want == "slip" else 0,
@@ -664,6 +710,7 @@ def rew_air_time(t, cmd, tmin: float, tmax: float, cmd_thr: float):
     return None
   out, num, den = (_vec_out(n, t.device) for _ in range(3))
   cp, cs = _cmd_args(cmd)
+  _keep(t, cmd)
   native.check(native.lib().mjh_rew_air_time(_ptr(t), st[0], cp, cs, float(tmin), float(tmax), float(cmd_thr), _ptr(out),
                                              _ptr(num), _ptr(den), k, n, _stream()), "mjh_rew_air_time")
   return out, num, den
@@ -677,6 +724,7 @@ def rew_swing_height(peak, h, found, cct, cmd, first_lim: float, target: float, 
     return None
   out, num, den = (_vec_out(n, peak.device) for _ in range(3))
   cp, cs = _cmd_args(cmd)
+  _keep(peak, h, found, cct, cmd)
   native.check(native.lib().mjh_rew_swing_height(
     _ptr(peak), _ptr(h), sh[0], sh[1], _ptr(found), sf[0], sf[1], _ptr(cct), sc[0], cp, cs, float(first_lim), float(target),
     float(cmd_thr), _ptr(out), _ptr(num), _ptr(den), k, n, _stream()), "mjh_rew_swing_height")
@@ -693,6 +741,7 @@ def rew_soft_landing(force, cct, cmd, first_lim: float, cmd_thr: float):
     return None
   out, num, den = (_vec_out(n, force.device) for _ in range(3))
   cp, cs = _cmd_args(cmd)
+  _keep(force, cct, cmd)
   native.check(native.lib().mjh_rew_soft_landing(
     _ptr(force), force.stride(0), force.stride(1), _ptr(cct), sc[0], cp, cs, float(first_lim), float(cmd_thr), _ptr(out),
     _ptr(num), _ptr(den), k, n, _stream()), "mjh_rew_soft_landing")

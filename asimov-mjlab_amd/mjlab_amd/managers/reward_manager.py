@@ -76,15 +76,20 @@ class RewardManager:
     are skipped and report 0, as in the reference."""
     self._env.__dict__["_command_active_cache"] = {}  # shared command-activity masks, this pass only
     self._env.__dict__["_reward_log_ratios"] = []  # the terms' metric logs, evaluated together below
+    from mjlab_amd import envops
+
+    # the fused terms are independent per-env jobs: recorded and launched as one
+    # batch (mjh_batch_begin / mjh_batch_end); their outputs are read only below
+    batch = envops.JobBatch(self._reward_buf)
     try:
-      vals = [
-        tcfg.func(self._env, **tcfg.params).float() if tcfg.weight != 0.0 else None
-        for tcfg in self._term_cfgs
-      ]
+      with batch:
+        vals = [
+          tcfg.func(self._env, **tcfg.params).float() if tcfg.weight != 0.0 else None
+          for tcfg in self._term_cfgs
+        ]
     finally:
       self._env.__dict__.pop("_command_active_cache", None)
       pending = self._env.__dict__.pop("_reward_log_ratios", [])
-    from mjlab_amd import envops
 
     if pending:
       if self._log_buf.numel() < len(pending):

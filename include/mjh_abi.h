@@ -34,7 +34,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 10
+#define MJH_ABI_VERSION 11
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -337,6 +337,20 @@ int mjh_obs_group(const mjh_obs_term_desc* terms, int nterms, const float* u, lo
  * step_reward[e, t] = v * w[t]; sums[e, t] += v * (w[t] * dt); reward[e] = sum_t. */
 int mjh_reward_combine(const float* const* values, const long long* strides, int nterms, const float* weights, float dt,
                        float* reward, float* step_reward, float* sums, long long n, void* stream);
+
+/* One dispatch per reward pass for the per-term kernels (replaces the reward
+ * terms' separate launches inside RewardManager.compute, reward_manager.py:
+ * 76-88, where every term is an independent per-env function). Between
+ * mjh_batch_begin and mjh_batch_end the batchable term entry points
+ * (mjh_rew_track, _flat_orientation, _sqsum, _diffsq, _pos_limits, _posture,
+ * _feet, _air_time, _swing_height, _soft_landing) record their job instead of
+ * launching it; mjh_batch_end launches the recorded jobs, one kernel per source
+ * file (blockIdx.y = job), on the stream they were recorded with (or `stream`).
+ * The jobs must not read each other's outputs; other launches made while the
+ * batch is open run before it. Outputs are bit-identical to the separate
+ * launches. Per thread (not shared across host threads). */
+int mjh_batch_begin(void);
+int mjh_batch_end(void* stream);
 
 /* Capacity/NaN statistics from the sticky per-world flags (data->flags_acc),
  * one workgroup, no host sync: stats[0..2] = worlds with contacts dropped /

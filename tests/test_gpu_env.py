@@ -189,3 +189,56 @@ def test_config1_single_env_zero_agent_against_oracle():
   assert torch.isfinite(obs["policy"]).all() and torch.isfinite(rew).all()
   # the zero agent holds the default pose: still standing after 30 env steps
   assert not bool(term.any())
+
+
+def test_batched_reward_pass_equals_separate_launches():
+  """The reward pass's job batch (mjh_batch_begin / mjh_batch_end: the fused
+  term kernels recorded and launched as one dispatch per source file) against
+  the same terms launched one by one: over K env steps from identical seeds,
+  rewards, episode sums, logs, observations and the simulation state agree
+  bitwise (the jobs run the same arithmetic; the batch only merges dispatches)."""
+  from mjlab_amd import envops
+  from mjlab_amd.sim import native
+
+  class _NoBatch:
+    def __init__(self, like):
+      pass
+
+    def __enter__(self):
+      return self
+
+    def __exit__(self, *exc):
+      return False
+
+  n, K = 64, 6
+  envs = []
+  for _ in range(2):
+    cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+    cfg.scene.num_envs = n
+    cfg.seed = 5
+    envs.append(ManagerBasedRlEnv(cfg, device="cuda:0", use_graph=False))
+  eb, es = envs
+  for e in envs:
+    e.reset()
+    e.episode_length_buf[:8] = e.max_episode_length - 1
+  g = torch.Generator(device="cuda:0").manual_seed(3)
+  orig = envops.JobBatch
+  for k in range(K):
+    a = 2 * torch.rand(n, eb.action_manager.total_action_dim, device="cuda:0", generator=g) - 1
+    before = native.CALLS["mjh_batch_end"]
+    ob, rb, tb, trb, xb = eb.step(a)
+    assert native.CALLS["mjh_batch_end"] > before  # the batched pass ran
+    envops.JobBatch = _NoBatch
+    try:
+      os_, rs, ts, trs, xs = es.step(a)
+    finally:
+      envops.JobBatch = orig
+    assert torch.equal(rb, rs), f"step {k}: reward"
+    assert torch.equal(eb.reward_manager._sums, es.reward_manager._sums), f"step {k}: episode sums"
+    assert torch.equal(eb.reward_manager._step_reward, es.reward_manager._step_reward), f"step {k}: step reward"
+    for name in ("policy", "critic"):
+      assert torch.equal(ob[name], os_[name]), f"step {k}: obs {name}"
+    for key, v in xb["log"].items():
+      assert torch.equal(torch.as_tensor(v), torch.as_tensor(xs["log"][key])), f"step {k}: log {key}"
+    for f in _STATE:
+      assert torch.equal(getattr(eb.sim.data, f), getattr(es.sim.data, f)), f"step {k}: sim.data.{f}"
