@@ -122,13 +122,13 @@ struct PostureJob {
 };
 
 // per-foot terms on k sites (site z, site linear velocity (N, k, 3)):
-//   clearance: sum_j |z_j - target| * |v_xy,j|                     (feet_clearance)
+//   clearance: sum_j |z_j - target| * |v_xy,j|                     (feet_clearance; z_j at column stride zcs)
 //   slip:      sum_j |v_xy,j|^2 * [found_j > 0]                   (feet_slip)
 // both x [command total > threshold]; also writes sum_j |v_xy| * [found] and
 // sum_j [found] for the slip metric.
 struct FeetJob {
   static constexpr int kKind = 7;
-  const float* z; long long zs; const float* vel; long long vs; long long vcs; const float* found; long long fs;
+  const float* z; long long zs; long long zcs; const float* vel; long long vs; long long vcs; const float* found; long long fs;
   long long fcs; const float* cmd; long long cs; float target; float thr_clear; float thr_slip; int k;
   float* clearance; float* slip; float* slip_vsum; float* slip_cnt;
   __device__ __forceinline__ void run(long long e) const {
@@ -137,7 +137,7 @@ struct FeetJob {
     for (int j = 0; j < k; j++) {
       const float* v = vel + e * vs + vcs * j;
       const float vn = sqrtf(v[0] * v[0] + v[1] * v[1]);
-      cl += fabsf(z[e * zs + 3 * j] - target) * vn;
+      cl += fabsf(z[e * zs + zcs * j] - target) * vn;
       if (found) {
         const float in = found[e * fs + fcs * j] > 0.f ? 1.f : 0.f;
         sl += vn * vn * in;
@@ -214,10 +214,10 @@ int mjh_rew_posture(const float* q, long long qs, const float* q0, long long q0s
   return submit(PostureJob{q, qs, q0, q0s, std_stand, std_walk, std_run, cmd, cs, walk_thr, run_thr, k, out}, n, stream);
 }
 
-int mjh_rew_feet(const float* z, long long zs, const float* vel, long long vs, long long vcs, const float* found, long long fs,
+int mjh_rew_feet(const float* z, long long zs, long long zcs, const float* vel, long long vs, long long vcs, const float* found, long long fs,
                  long long fcs, const float* cmd, long long cs, float target, float thr_clear, float thr_slip, int k,
                  float* clearance, float* slip, float* slip_vsum, float* slip_cnt, long long n, void* stream) {
-  return submit(FeetJob{z, zs, vel, vs, vcs, found, fs, fcs, cmd, cs, target, thr_clear, thr_slip, k, clearance, slip,
+  return submit(FeetJob{z, zs, zcs, vel, vs, vcs, found, fs, fcs, cmd, cs, target, thr_clear, thr_slip, k, clearance, slip,
                         slip_vsum, slip_cnt}, n, stream);
 }
 

@@ -19,6 +19,7 @@
 // cones, exact line search, tolerance scaled by meaninertia.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -3445,6 +3446,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         }
       }
     };
+    // the previous contact sensor's match parameters and count: mjlab declares
+    // one sensor per (primary, field), so consecutive sensors (found, force of
+    // the same foot) repeat the same scan; the kept matches are still in sx
+    int p_ot = -9, p_id = -9, p_rt = -9, p_rid = -9, p_cnt = 0;
     for (int s = 0; s < Z.nsensor; s++) {
       const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
       if (type == 40) {
@@ -3487,23 +3492,35 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           }
         }
         int cnt = 0;
-        for (int base = 0; base < ncon; base += NT) {
-          const int ci = base + tid;
-          int match = 0, flip = 0;
-          if (ci < ncon) {
-            const int g1 = creg ? cg1 : con_geom[2 * ci], g2 = creg ? cg2 : con_geom[2 * ci + 1];
-            if (om(otype, id, g1) && om(rtype, rid, g2)) match = 1;
-            else if (om(otype, id, g2) && om(rtype, rid, g1)) { match = 1; flip = 1; }
+        if (otype == p_ot && id == p_id && rtype == p_rt && rid == p_rid) {
+          cnt = p_cnt;  // same matches as the previous contact sensor (sx unchanged)
+        } else {
+          for (int base = 0; base < ncon; base += NT) {
+            const int ci = base + tid;
+            int match = 0, flip = 0;
+            if (ci < ncon) {
+              const int g1 = creg ? cg1 : con_geom[2 * ci], g2 = creg ? cg2 : con_geom[2 * ci + 1];
+              if (om(otype, id, g1) && om(rtype, rid, g2)) match = 1;
+              else if (om(otype, id, g2) && om(rtype, rid, g1)) { match = 1; flip = 1; }
+            }
+            int total;
+            const int off = bscan<NT>(match, &total, redi);
+            if (match && cnt + off < cap) sx[cnt + off] = flip ? ~ci : ci;
+            cnt += total;
           }
-          int total;
-          const int off = bscan<NT>(match, &total, redi);
-          if (match && cnt + off < cap) sx[cnt + off] = flip ? ~ci : ci;
-          cnt += total;
+          wsync();
+          p_ot = otype; p_id = id; p_rt = rtype; p_rid = rid; p_cnt = cnt;
         }
-        wsync();
         const int nm = min(cnt, cap);
         if (nm == 0) {
           for (int k = tid; k < dim; k += NT) sd[adr + k] = 0.f;
+          continue;
+        }
+        if (bits == 1) {
+          // found only: the match count in the first min(nm, nslot) slots (one
+          // record for netforce), zeros after — what the general path writes
+          for (int k = tid; k < dim; k += NT) sd[adr + k] = (reduce == 3 ? k == 0 : k < nm) ? (float)nm : 0.f;
+          wsync();
           continue;
         }
         // lane k < nm: match k. F = contact force/torque in the contact frame
@@ -3919,7 +3936,24 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     wsync();
     for (int i = tid; i < nq; i += NT) DP(qpos)[W * nq + i] = qpos[i];
     for (int i = tid; i < nv; i += NT) DP(qvel)[W * nv + i] = qvel[i];
-    if (tid == 0) DP(time)[W] += dt;
+    const float now = DP(time)[W] + dt;  // every lane: the value lane 0 stores
+    if (tid == 0) DP(time)[W] = now;
+    // fused contact-sensor timers (mjh_data.at_*; ContactSensor.
+    // _update_air_time_tracking, contact_sensor.py:327-367): lane j, slot j
+    if (d.at_cur_air != nullptr && tid < d.at_k) {
+      const long long t = (long long)W * d.at_k + tid;
+      const float el = now - d.at_last_time[W];
+      const bool is_c = DP(sensordata)[W * Z.nsensordata + d.at_cols[tid]] > 0.f;
+      const float ca = d.at_cur_air[t], cc = d.at_cur_con[t];
+      if (ca > 0.f && is_c) d.at_last_air[t] = ca + el;
+      d.at_cur_air[t] = is_c ? 0.f : ca + el;
+      if (cc > 0.f && !is_c) d.at_last_con[t] = cc + el;
+      d.at_cur_con[t] = is_c ? cc + el : 0.f;
+    }
+    if (d.at_cur_air != nullptr) {
+      wsync();
+      if (tid == 0) d.at_last_time[W] = now;
+    }
   }
 
   // non-finite check on the new state
@@ -4233,7 +4267,7 @@ unsigned long long launch_key(const mjh_model* m, const mjh_data* d) {
     for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
   };
   eat(m, sizeof(*m));
-  eat(d, sizeof(*d));
+  eat(d, offsetof(mjh_data, at_last_time));  // the fused sensor timers do not affect the position stage
   return h;
 }
 

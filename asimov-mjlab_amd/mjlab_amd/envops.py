@@ -237,9 +237,7 @@ def rew_feet(pos: torch.Tensor, vel: torch.Tensor, found, cmd: torch.Tensor, tar
              thr_slip: float, want: str):
   """want = "clearance" -> (N,) cost; "slip" -> (cost, sum |v_xy|*found, sum found)."""
   if not (pos.is_cuda and pos.dim() == 3 and vel.dim() == 3 and pos.stride(2) == 1 and vel.stride(2) == 1
-          and pos.stride(1) == 3 and vel.stride(1) >= 3 and pos.shape[:2] == vel.shape[:2] and _rows(cmd, 3)):
-    return None
-  if vel.stride(1) != 3 and vel.stride(1) != 6:
+          and pos.stride(1) >= 3 and vel.stride(1) >= 3 and pos.shape[:2] == vel.shape[:2] and _rows(cmd, 3)):
     return None
   n, k = pos.shape[0], pos.shape[1]
   # strided views are read in place (velocity rows of 6, sensor-slot columns)
@@ -253,7 +251,7 @@ def rew_feet(pos: torch.Tensor, vel: torch.Tensor, found, cmd: torch.Tensor, tar
   outs = [_vec_out(n, pos.device) for _ in range(3)] if want == "slip" else [None, None, None]
   _keep(pos, vel, found, cmd)
   native.check(native.lib().mjh_rew_feet(
-    ctypes.c_void_p(pos.data_ptr() + 8), pos.stride(0), _ptr(vel), vel.stride(0), vel.stride(1),
+    ctypes.c_void_p(pos.data_ptr() + 8), pos.stride(0), pos.stride(1), _ptr(vel), vel.stride(0), vel.stride(1),
     _ptr(found) if want == "slip" else None, found.stride(0) if want == "slip" else 0,
     found.stride(1) if want == "slip" else 0, _ptr(cmd), cmd.stride(0),
     float(target), float(thr_clear), float(thr_slip), k, _ptr(cl) if cl is not None else None,

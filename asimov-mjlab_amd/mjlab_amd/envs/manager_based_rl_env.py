@@ -186,8 +186,11 @@ class ManagerBasedEnv:
       self._sim_step_counter += 1
       self.action_manager.apply_action()
       self.scene.write_data_to_sim()
-      self.sim.step()
-      self.scene.update(dt=self.physics_dt)
+      # inside the captured step, the contact-sensor timers ride on the physics
+      # launch (Simulation.attach_air_time) instead of a launch per substep
+      fused = self._air_sensor is not None and torch.cuda.is_current_stream_capturing()
+      self.sim.step(air_time=True) if fused else self.sim.step()
+      self.scene.update(dt=self.physics_dt, skip=self._air_sensor if fused else None)
     if "interval" in self.event_manager.available_modes:
       self.event_manager.apply(mode="interval", dt=self.step_dt)
     self.obs_buf = self.observation_manager.compute(update_history=True)
@@ -240,6 +243,14 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     self._eager_steps = 0
     self._pack_buf: torch.Tensor | None = None
     self.metadata = dict(self.metadata, render_fps=1.0 / self.step_dt)
+    # one air-time contact sensor may have its timers fused into the physics step
+    self._air_sensor = None
+    if self.use_graph:
+      for sen in getattr(self.scene, "_sensors", {}).values():
+        attach = getattr(sen, "attach_air_time_to", None)
+        if attach is not None and attach(self.sim):
+          self._air_sensor = sen
+          break
 
   def enable_step_pack(self) -> torch.Tensor:
     """Learner-facing outputs packed at the end of every env step, inside the
@@ -342,10 +353,15 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
       if i == 0 or not once:
         self.action_manager.apply_action()
       self.scene.write_data_to_sim()
-      # nothing between the substeps writes a model field (actions write ctrl),
-      # so substeps after the first reuse the packed model image
-      self.sim.step(keep_image=i > 0) if self.sim.use_cuda_graph else self.sim.step()
-      self.scene.update(dt=self.physics_dt)
+      # every substep repacks: the pack launch also re-sorts the worlds by the
+      # previous substep's cost, which pays more than the launch costs (same-box
+      # A/B, profiles/r05f_keep_image_ab.log: 1.597M vs 1.570M env-steps/s with
+      # substeps 2-4 reusing the image, mjh_step_keep_image, and its stale order)
+      # inside the captured step, the contact-sensor timers ride on the physics
+      # launch (Simulation.attach_air_time) instead of a launch per substep
+      fused = self._air_sensor is not None and torch.cuda.is_current_stream_capturing()
+      self.sim.step(air_time=True) if fused else self.sim.step()
+      self.scene.update(dt=self.physics_dt, skip=self._air_sensor if fused else None)
     if self.episode_length_buf.is_cuda:
       from mjlab_amd import envops
 

@@ -64,6 +64,9 @@ class SceneEntityCfg:
         idx = slice(None)
       elif len(ids) > 0 and list(ids) == list(range(ids[0], ids[0] + len(ids))):
         idx = slice(ids[0], ids[0] + len(ids))  # a contiguous range: reads are views, no gather launch
+      elif len(ids) > 1 and ids[1] > ids[0] and list(ids) == list(range(ids[0], ids[-1] + 1, ids[1] - ids[0])):
+        # an increasing arithmetic progression (e.g. two feet): a strided view, no gather launch
+        idx = slice(ids[0], ids[-1] + 1, ids[1] - ids[0])
       else:
         idx = torch.tensor(ids, dtype=torch.long, device=scene.device)
       setattr(self, ids_attr.replace("_ids", "_idx"), idx)

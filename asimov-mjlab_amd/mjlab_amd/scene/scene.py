@@ -153,11 +153,14 @@ class Scene:
     for s in self._sensors.values():
       s.reset(env_ids)
 
-  def update(self, dt: float) -> None:
+  def update(self, dt: float, skip=None) -> None:
+    """skip: a sensor whose update the physics step already made (the env's
+    fused contact-sensor timers, ContactSensor.attach_air_time_to)."""
     for ent in self._entities.values():
       ent.update(dt)
     for s in self._sensors.values():
-      s.update(dt)
+      if s is not skip:
+        s.update(dt)
 
   def write_data_to_sim(self) -> None:
     for ent in self._entities.values():

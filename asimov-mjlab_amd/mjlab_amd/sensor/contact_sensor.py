@@ -193,11 +193,24 @@ class ContactSensor:
     # sensordata columns of the `found` slots, for the fused timer kernel
     fcols = [int(model.sensor(sl.sensor_name).adr[0]) for sl in self._slots if sl.field_name == "found"]
     self._found_cols = torch.tensor(fcols, dtype=torch.int32, device=device)
+    self._found_cols_host = fcols
     if self.cfg.track_air_time:
       n = data.time.shape[0]
       k = len({s.primary_name for s in self._slots})
       z = lambda: torch.zeros((n, k), device=device)  # noqa: E731
       self._air_time_state = _AirTimeState(z(), z(), z(), z(), torch.zeros((n,), device=device))
+
+  def attach_air_time_to(self, sim) -> bool:
+    """Fuse this sensor's timer update into the physics step of an env's
+    decimation loop (Simulation.attach_air_time): the step updates the timers
+    with the arithmetic of _update_air_time_tracking, so Scene.update skips
+    this sensor there. False when the sensor has no timers or the layout does
+    not fit the fused path."""
+    st = self._air_time_state
+    if st is None or len(self._found_cols_host) != st.current_air_time.shape[1]:
+      return False
+    return sim.attach_air_time(self._found_cols_host, st.last_time, st.current_air_time, st.last_air_time,
+                               st.current_contact_time, st.last_contact_time)
 
   @property
   def data(self) -> ContactData:

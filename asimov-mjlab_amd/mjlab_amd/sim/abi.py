@@ -89,6 +89,9 @@ def data_struct(real=ctypes.c_float, device: bool = True):
       members.append((f.name, ctypes.c_void_p))
   if device:  # device descriptor: per-world global scratch
     members += [("scratch", ctypes.c_void_p), ("scratch_words", ctypes.c_longlong), ("world_order", ctypes.c_void_p)]
+    # optional fused contact-sensor timers (mjh_data.at_*)
+    members += [(f"at_{n}", ctypes.c_void_p) for n in ("last_time", "cur_air", "last_air", "cur_con", "last_con")]
+    members += [("at_k", ctypes.c_int), ("at_cols", ctypes.c_int * 7)]
   return type("mjh_data" if device else "or_data", (ctypes.Structure,), {"_fields_": members})
 
 

@@ -163,7 +163,7 @@ def lib() -> ctypes.CDLL:
   L.mjh_rew_posture.argtypes = [vp, ll, vp, ll, vp, vp, vp, vp, ll, cf, cf, ci, vp, ll, vp]
   L.mjh_velocity_command.argtypes = [vp, ll, vp, ll, vp, ll, vp, ll, vp, cf, cf, cf, cf, cf, cf, cf, ci, vp, vp, vp, vp, vp,
                                      vp, vp, vp, vp, ctypes.c_ulonglong, ctypes.c_ulonglong, vp, ll, vp]
-  L.mjh_rew_feet.argtypes = [vp, ll, vp, ll, ll, vp, ll, ll, vp, ll, cf, cf, cf, ci, vp, vp, vp, vp, ll, vp]
+  L.mjh_rew_feet.argtypes = [vp, ll, ll, vp, ll, ll, vp, ll, ll, vp, ll, cf, cf, cf, ci, vp, vp, vp, vp, ll, vp]
   L.mjh_quat_from_euler.argtypes = [vp, ll, vp, ll, vp]
   L.mjh_quat_error.argtypes = [vp, ll, vp, ll, vp, ll, vp]
   L.mjh_frame_subtract.argtypes = [vp, ll, vp, ll, vp, ll, ll, vp, ll, ll, ci, vp, vp, ci, ll, vp]

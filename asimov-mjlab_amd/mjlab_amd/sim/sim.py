@@ -324,6 +324,19 @@ class Simulation:
     for name, t in self._data_flat.items():
       setattr(ds, name, t.data_ptr())
     self._mstruct, self._dstruct = ms, ds
+    # the same descriptor with the fused contact-sensor timers (attach_air_time)
+    self._dstruct_at = None
+    at = getattr(self, "_air_time", None)
+    if at is not None:
+      dsa = DS()
+      ctypes.memmove(ctypes.addressof(dsa), ctypes.addressof(ds), ctypes.sizeof(DS))
+      cols, tensors = at
+      for name, t in zip(("last_time", "cur_air", "last_air", "cur_con", "last_con"), tensors):
+        setattr(dsa, "at_" + name, t.data_ptr())
+      dsa.at_k = len(cols)
+      for j, c in enumerate(cols):
+        dsa.at_cols[j] = int(c)
+      self._dstruct_at = dsa
     # bumped whenever the descriptors change: graphs that baked them are stale
     # and are re-captured lazily by the next step()/forward()
     self.struct_version = getattr(self, "struct_version", 0) + 1
@@ -435,24 +448,44 @@ class Simulation:
                                                  ctypes.c_void_p(self._order.data_ptr()), self.num_envs, self._stream()),
                    "mjh_order_worlds")
 
+  def attach_air_time(self, cols, last_time, cur_air, last_air, cur_con, last_con) -> bool:
+    """Fuse a contact sensor's air/contact timers into the physics step: a step
+    launched with ``step(air_time=True)`` updates them at its end (mjh_data.at_*,
+    the arithmetic of ContactSensor._update_air_time_tracking), replacing the
+    timer launch of Scene.update after each decimation substep. cols: the
+    sensordata columns of the sensor's `found` slots (at most 7), one per timer
+    column. Returns False (nothing attached) for layouts the kernel does not
+    take. Plain ``step()`` never touches the timers."""
+    ts = (last_time, cur_air, last_air, cur_con, last_con)
+    if not self.use_cuda_graph or not (0 < len(cols) <= 7):
+      return False
+    if not all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() for t in ts):
+      return False
+    if last_time.numel() != self.num_envs or any(t.shape != (self.num_envs, len(cols)) for t in ts[1:]):
+      return False
+    self._air_time = (list(cols), ts)
+    self._build_structs()
+    return True
+
   def model_version(self) -> int:
     """Sum of the model buffers' torch version counters: changes whenever a
     model field is written in place through torch (views share their base's
     counter). Host state, read when a launch is issued (or captured)."""
     return sum(t._version for t in self._model_flat.values())
 
-  def _launch_step(self, keep_image: bool = False) -> None:
+  def _launch_step(self, keep_image: bool = False, air_time: bool = False) -> None:
     self._refresh_order()
     # the packed image is reused only while no model field has been written
     # since the launch that packed it (ADVICE r4: an action term that writes
     # gains between decimation substeps must not be ignored)
     ver = self.model_version()
-    if keep_image and ver != getattr(self, "_packed_version", None):
+    if keep_image and (ver != getattr(self, "_packed_version", None) or os.environ.get("MJH_KEEP_IMAGE") == "0"):
       keep_image = False
     if not keep_image:
       self._packed_version = ver
     fn = native.lib().mjh_step_keep_image if keep_image else native.lib().mjh_step
-    native.check(fn(ctypes.addressof(self._mstruct), ctypes.addressof(self._dstruct), self._stream()), "mjh_step")
+    ds = self._dstruct_at if (air_time and self._dstruct_at is not None) else self._dstruct
+    native.check(fn(ctypes.addressof(self._mstruct), ctypes.addressof(ds), self._stream()), "mjh_step")
 
   def _launch_forward(self) -> None:
     self._refresh_order()
@@ -497,14 +530,15 @@ class Simulation:
       "mjh_forward_gated",
     )
 
-  def step(self, keep_image: bool = False) -> None:
-    """One physics step. keep_image (inside an enclosing capture only): reuse
-    the model image packed for the previous launch on this stream — for
-    substeps between which no model field changes (the env's decimation loop)."""
+  def step(self, keep_image: bool = False, air_time: bool = False) -> None:
+    """One physics step. Inside an enclosing capture only: keep_image reuses
+    the model image packed for the previous launch on this stream (for
+    substeps between which no model field changes); air_time also updates the
+    attached contact-sensor timers (attach_air_time) at the end of the step."""
     self._require_gpu()
     self.epoch.bump()
     if torch.cuda.is_current_stream_capturing():
-      self._launch_step(keep_image)  # being captured into an enclosing (env-step) graph
+      self._launch_step(keep_image, air_time)  # being captured into an enclosing (env-step) graph
       return
     if self.step_graph is None:
       self.create_graph()

@@ -298,8 +298,9 @@ def main(env_hook=None) -> None:
   act = torch.empty(num_envs, env.action_manager.total_action_dim, device=dev)
 
   def agent():
-    act.uniform_(0.0, 1.0, generator=gen)
-    return act.mul_(2.0).sub_(1.0)
+    # 2 U[0,1) - 1 as one launch: uniform_(-1, 1) draws u * 2 + (-1) from the
+    # same generator state (2u is exact, so the values equal the three-op form)
+    return act.uniform_(-1.0, 1.0, generator=gen)
 
   gather = StepGather()
   use_gather = world > 1 and not args.no_gather

@@ -90,6 +90,21 @@ typedef struct mjh_data {
      by expected cost balances the waves of a workgroup (and, with one-world
      workgroups, starts the most expensive worlds first). */
   const long long* world_order;
+  /* optional fused contact-sensor timers (NULL at_cur_air = none): at the end
+     of every physics step (mjh_step; not forward) world w updates the timers
+     of ContactSensor._update_air_time_tracking (contact_sensor.py:327-367) for
+     its at_k slots from this step's contact flags sensordata[w, at_cols[j]] > 0
+     and time: at_cur_air / at_last_air / at_cur_con / at_last_con (nworld,
+     at_k), at_last_time (nworld). Replaces the per-substep timer launch of
+     Scene.update in the env's decimation loop. Not part of the launch key
+     (position reuse is unaffected). */
+  float* at_last_time;
+  float* at_cur_air;
+  float* at_last_air;
+  float* at_cur_con;
+  float* at_last_con;
+  int at_k;
+  int at_cols[7];
 } mjh_data;
 
 /* Version of this ABI (MJH_ABI_VERSION). */
@@ -253,7 +268,8 @@ int mjh_rew_pos_limits(const float* q, long long qs, const float* lim, long long
 int mjh_rew_posture(const float* q, long long qs, const float* q0, long long q0s, const float* std_stand,
                     const float* std_walk, const float* std_run, const float* cmd, long long cs, float walk_thr,
                     float run_thr, int k, float* out, long long n, void* stream);
-int mjh_rew_feet(const float* z, long long zs, const float* vel, long long vs, long long vcs, const float* found, long long fs,
+int mjh_rew_feet(const float* z, long long zs, long long zcs, const float* vel, long long vs, long long vcs, const float* found,
+                 long long fs,
                  long long fcs, const float* cmd, long long cs, float target, float thr_clear, float thr_slip, int k,
                  float* clearance, float* slip, float* slip_vsum, float* slip_cnt, long long n, void* stream);
 
