@@ -12,6 +12,10 @@
 // (bit-identical outputs) in one dispatch per file. Jobs in a batch must not
 // read each other's outputs (the reward terms read sim state, EntityData and
 // commands only); anything launched while a batch is open runs before it.
+// A sequential batch (mjh_batch_begin(1)) instead runs each env's jobs in the
+// order they were recorded, one thread per env (consecutive jobs of the same
+// file in one dispatch): for chains of per-env kernels where a job reads an
+// earlier job's output for the same env only.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -20,8 +24,8 @@
 
 namespace mjh_batch {
 
-constexpr int kArgBytes = 192;  // the largest job struct (static_assert in submit)
-constexpr int kMaxJobs = 10;    // per translation unit and launch (kernel arguments: ~2 KB)
+constexpr int kArgBytes = 240;  // the largest job struct (static_assert in submit)
+constexpr int kMaxJobs = 10;    // per translation unit and launch (kernel arguments: ~2.6 KB)
 enum Unit { kMdp = 0, kFuse = 1, kUnits = 2 };
 
 struct Job {
@@ -38,7 +42,9 @@ struct Pack {
   Job jobs[kMaxJobs];
 };
 
-typedef void (*Launcher)(const Pack&, hipStream_t);
+// seq = false: the jobs are independent (blockIdx.y = job); seq = true: thread
+// e runs the jobs in recorded order for env e (per-env dependencies kept)
+typedef void (*Launcher)(const Pack&, hipStream_t, bool seq);
 
 // host side (mjh_mgr.hip): register a unit's batch launcher; append a job to
 // the open batch (false: no batch open, the caller launches the job itself)
@@ -64,4 +70,34 @@ template <class J>
 __global__ void mjh_job_kernel(const J j, long long n) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e < n) j.run(e);
+}
+
+// a unit's batch kernels; D::run(job, e) switches on the job kind
+template <class D>
+__global__ void mjh_batch2d_kernel(const mjh_batch::Pack p) {
+  const mjh_batch::Job& j = p.jobs[blockIdx.y];
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < j.n) D::run(j, e);
+}
+template <class D>
+__global__ void mjh_batchseq_kernel(const mjh_batch::Pack p) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int k = 0; k < p.njobs; k++) {
+    const mjh_batch::Job& j = p.jobs[k];
+    if (e < j.n) D::run(j, e);
+  }
+}
+template <class D>
+void mjh_batch_launch(const mjh_batch::Pack& p, hipStream_t s, bool seq) {
+  if (seq)
+    hipLaunchKernelGGL(mjh_batchseq_kernel<D>, dim3(mjh_batch::grid1(p.nmax)), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(mjh_batch2d_kernel<D>, dim3(mjh_batch::grid1(p.nmax), p.njobs), dim3(256), 0, s, p);
+}
+// dispatch a job of kind J::kKind to J::run
+template <class J>
+__device__ __forceinline__ bool mjh_run_as(const mjh_batch::Job& j, long long e) {
+  if (j.kind != J::kKind) return false;
+  reinterpret_cast<const J*>(j.a)->run(e);
+  return true;
 }

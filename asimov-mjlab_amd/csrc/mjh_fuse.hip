@@ -179,15 +179,17 @@ __global__ void uniform_where_kernel(float* __restrict__ t, const unsigned char*
 
 // interval event timers (event_manager.py:120-145): t -= dt; due = t < 1e-6;
 // due timers are redrawn from U[lo, hi)
-__global__ void interval_tick_kernel(float* __restrict__ t, float dt, float lo, float hi, unsigned char* __restrict__ due,
-                                     unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  const float v = t[e] - dt;
-  const bool d = v < 1e-6f;
-  t[e] = d ? Rng(seed, key, ctr).u01(e) * (hi - lo) + lo : v;
-  due[e] = d ? 1 : 0;
-}
+struct IntervalTickJob {
+  static constexpr int kKind = 110;
+  float* t; float dt; float lo; float hi; unsigned char* due; unsigned long long seed; unsigned long long key;
+  const mjh_i64* ctr;
+  __device__ __forceinline__ void run(long long e) const {
+    const float v = t[e] - dt;
+    const bool d = v < 1e-6f;
+    t[e] = d ? Rng(seed, key, ctr).u01(e) * (hi - lo) + lo : v;
+    due[e] = d ? 1 : 0;
+  }
+};
 
 // ---- event terms ----------------------------------------------------------------
 struct Range6 {
@@ -258,25 +260,26 @@ __global__ void reset_joints_offset_kernel(float* __restrict__ qpos, long long q
 
 // push_by_setting_velocity (envs/mdp/events.py:124-137): root_link_vel_w + U6,
 // written as the free joint's qvel (angular part into the body frame)
-__global__ void push_velocity_kernel(const float* __restrict__ qpos, long long qs, int qadr, float* __restrict__ qvel,
-                                     long long vs, int vadr, const unsigned char* __restrict__ mask,
-                                     const float* __restrict__ vw, long long vws, const Range6 r,
-                                     unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n || !on(mask, e)) return;
-  const Rng rng(seed, key, ctr);
-  const float* v = vw + e * vws;
-  float u[6];
+struct PushVelocityJob {
+  static constexpr int kKind = 111;
+  const float* qpos; long long qs; int qadr; float* qvel; long long vs; int vadr; const unsigned char* mask;
+  const float* vw; long long vws; Range6 r; unsigned long long seed; unsigned long long key; const mjh_i64* ctr;
+  __device__ __forceinline__ void run(long long e) const {
+    if (!on(mask, e)) return;
+    const Rng rng(seed, key, ctr);
+    const float* v = vw + e * vws;
+    float u[6];
 #pragma unroll
-  for (int j = 0; j < 6; j++) u[j] = v[j] + (rng.u01(e * 6 + j) * (r.hi[j] - r.lo[j]) + r.lo[j]);
-  const float* qp = qpos + e * qs + qadr;
-  const float q[4] = {qp[3], qp[4], qp[5], qp[6]};
-  float wb[3];
-  qrot_inv(wb, q, u + 3);
-  float* qv = qvel + e * vs + vadr;
-  qv[0] = u[0]; qv[1] = u[1]; qv[2] = u[2];
-  qv[3] = wb[0]; qv[4] = wb[1]; qv[5] = wb[2];
-}
+    for (int j = 0; j < 6; j++) u[j] = v[j] + (rng.u01(e * 6 + j) * (r.hi[j] - r.lo[j]) + r.lo[j]);
+    const float* qp = qpos + e * qs + qadr;
+    const float q[4] = {qp[3], qp[4], qp[5], qp[6]};
+    float wb[3];
+    qrot_inv(wb, q, u + 3);
+    float* qv = qvel + e * vs + vadr;
+    qv[0] = u[0]; qv[1] = u[1]; qv[2] = u[2];
+    qv[3] = wb[0]; qv[4] = wb[1]; qv[5] = wb[2];
+  }
+};
 
 // ---- command terms --------------------------------------------------------------
 // CommandTerm.reset + UniformVelocityCommand._resample_command for the masked
@@ -327,14 +330,42 @@ struct TermArgs {
 
 // bad_orientation (envs/mdp/terminations.py): acos(-g_z) > limit as
 // -cos(limit) < g_z <= 1, one launch (instead of two compares and an AND)
-__global__ void gz_above_kernel(const float* __restrict__ g, long long gs, float thr, unsigned char* __restrict__ out,
-                                long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  const float gz = g[e * gs];
-  out[e] = (gz > thr && gz <= 1.f) ? 1 : 0;
-}
+struct GzAboveJob {
+  static constexpr int kKind = 112;
+  const float* g; long long gs; float thr; unsigned char* out;
+  __device__ __forceinline__ void run(long long e) const {
+    const float gz = g[e * gs];
+    out[e] = (gz > thr && gz <= 1.f) ? 1 : 0;
+  }
+};
+// time_out (envs/mdp/terminations.py): episode_length >= max
+struct TimeOutJob {
+  static constexpr int kKind = 113;
+  const mjh_i64* len; mjh_i64 max_len; unsigned char* out;
+  __device__ __forceinline__ void run(long long e) const { out[e] = len[e] >= max_len ? 1 : 0; }
+};
 
+// the combine for up to 6 terms as a batchable job (the kernel below takes any number)
+struct TermCombineJob {
+  static constexpr int kKind = 114;
+  const unsigned char* v[6]; unsigned char* d[6]; int time_out_mask; int nterms;
+  unsigned char* truncated; unsigned char* terminated; unsigned char* dones;
+  __device__ __forceinline__ void run(long long e) const {
+    unsigned char tr = 0, te = 0;
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+      if (t < nterms) {
+        const unsigned char x = v[t][e] ? 1 : 0;
+        d[t][e] = x;
+        if ((time_out_mask >> t) & 1) tr |= x;
+        else te |= x;
+      }
+    }
+    truncated[e] = tr;
+    terminated[e] = te;
+    dones[e] = tr | te;
+  }
+};
 __global__ void term_combine_kernel(const TermArgs a, unsigned char* __restrict__ truncated,
                                     unsigned char* __restrict__ terminated, unsigned char* __restrict__ dones, long long n) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -512,27 +543,6 @@ struct SoftLandingJob {
   }
 };
 
-__global__ void fuse_batch_kernel(const mjh_batch::Pack p) {
-  const mjh_batch::Job& j = p.jobs[blockIdx.y];
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= j.n) return;
-  switch (j.kind) {
-    case AirTimeJob::kKind: reinterpret_cast<const AirTimeJob*>(j.a)->run(e); break;
-    case SwingHeightJob::kKind: reinterpret_cast<const SwingHeightJob*>(j.a)->run(e); break;
-    case SoftLandingJob::kKind: reinterpret_cast<const SoftLandingJob*>(j.a)->run(e); break;
-    default: break;
-  }
-}
-
-void fuse_batch_launch(const mjh_batch::Pack& p, hipStream_t s) {
-  hipLaunchKernelGGL(fuse_batch_kernel, dim3(mjh_batch::grid1(p.nmax), p.njobs), dim3(256), 0, s, p);
-}
-const bool kFuseRegistered = mjh_batch::register_unit(mjh_batch::kFuse, fuse_batch_launch);
-
-template <class J>
-int submit_job(const J& j, long long n, void* stream) {
-  return mjh_batch::submit(mjh_batch::kFuse, j, n, (hipStream_t)stream, mjh_job_kernel<J>);
-}
 
 // ActionManager.process_action with one JointAction term (action_manager.py:
 // 107-116, joint_actions.py:90-108): prev = action; action = raw = input;
@@ -567,31 +577,31 @@ __device__ __forceinline__ void qrot(float o[3], const float q[4], const float v
   o[2] = (v[2] + sgn * w * tz) + (x * ty - y * tx);
 }
 
-__global__ void root_frame_kernel(const float* __restrict__ xpos, long long ps, const float* __restrict__ xquat,
-                                  long long qs, const float* __restrict__ com, long long cs, const float* __restrict__ cvel,
-                                  long long vs, const float* __restrict__ grav, long long gs, const float* __restrict__ fwd,
-                                  long long fs, float* __restrict__ out, long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  const float* p = xpos + e * ps;
-  const float* c = com + e * cs;
-  const float* v = cvel + e * vs;
-  const float q[4] = {xquat[e * qs], xquat[e * qs + 1], xquat[e * qs + 2], xquat[e * qs + 3]};
-  const float ox = c[0] - p[0], oy = c[1] - p[1], oz = c[2] - p[2];
-  const float ang[3] = {v[0], v[1], v[2]};
-  const float lin[3] = {v[3] - (ang[1] * oz - ang[2] * oy), v[4] - (ang[2] * ox - ang[0] * oz), v[5] - (ang[0] * oy - ang[1] * ox)};
-  float* o = out + 16 * e;
-  o[0] = lin[0]; o[1] = lin[1]; o[2] = lin[2];
-  o[3] = ang[0]; o[4] = ang[1]; o[5] = ang[2];
-  qrot(o + 6, q, lin, -1.f);
-  qrot(o + 9, q, ang, -1.f);
-  const float g[3] = {grav[e * gs], grav[e * gs + 1], grav[e * gs + 2]};
-  qrot(o + 12, q, g, -1.f);
-  const float f0[3] = {fwd[e * fs], fwd[e * fs + 1], fwd[e * fs + 2]};
-  float f[3];
-  qrot(f, q, f0, 1.f);
-  o[15] = atan2f(f[1], f[0]);
-}
+struct RootFrameJob {
+  static constexpr int kKind = 115;
+  const float* xpos; long long ps; const float* xquat; long long qs; const float* com; long long cs;
+  const float* cvel; long long vs; const float* grav; long long gs; const float* fwd; long long fs; float* out;
+  __device__ __forceinline__ void run(long long e) const {
+    const float* p = xpos + e * ps;
+    const float* c = com + e * cs;
+    const float* v = cvel + e * vs;
+    const float q[4] = {xquat[e * qs], xquat[e * qs + 1], xquat[e * qs + 2], xquat[e * qs + 3]};
+    const float ox = c[0] - p[0], oy = c[1] - p[1], oz = c[2] - p[2];
+    const float ang[3] = {v[0], v[1], v[2]};
+    const float lin[3] = {v[3] - (ang[1] * oz - ang[2] * oy), v[4] - (ang[2] * ox - ang[0] * oz), v[5] - (ang[0] * oy - ang[1] * ox)};
+    float* o = out + 16 * e;
+    o[0] = lin[0]; o[1] = lin[1]; o[2] = lin[2];
+    o[3] = ang[0]; o[4] = ang[1]; o[5] = ang[2];
+    qrot(o + 6, q, lin, -1.f);
+    qrot(o + 9, q, ang, -1.f);
+    const float g[3] = {grav[e * gs], grav[e * gs + 1], grav[e * gs + 2]};
+    qrot(o + 12, q, g, -1.f);
+    const float f0[3] = {fwd[e * fs], fwd[e * fs + 1], fwd[e * fs + 2]};
+    float f[3];
+    qrot(f, q, f0, 1.f);
+    o[15] = atan2f(f[1], f[0]);
+  }
+};
 
 // World order for the step kernel's workgroups (mjh_data.world_order): worlds
 // bucketed by their previous step's cost (solver_niter + 2) * nefc, most
@@ -821,11 +831,14 @@ __global__ void rew_exp_err_kernel(const float* __restrict__ a, long long aes, l
 
 // env-step bookkeeping (manager_based_rl_env.py:111-152): every episode
 // length += 1 and the env-step counter += 1 (the device random stream's counter)
-__global__ void step_counters_kernel(mjh_i64* __restrict__ episode_length, mjh_i64* __restrict__ step, long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < n) episode_length[e] += 1;
-  if (e == 0 && step) *step += 1;
-}
+struct StepCountersJob {
+  static constexpr int kKind = 116;
+  mjh_i64* episode_length; mjh_i64* step;
+  __device__ __forceinline__ void run(long long e) const {
+    episode_length[e] += 1;
+    if (e == 0 && step) *step += 1;
+  }
+};
 
 // after the terminations: any_reset = any(reset); stats[0] += count(reset),
 // stats[1] += any_reset (the gated forward's decision and its counters); one workgroup
@@ -848,6 +861,87 @@ __global__ __launch_bounds__(1024) void reset_stats_kernel(const unsigned char* 
   }
 }
 
+// ---- UniformVelocityCommand.compute (velocity_command.py:65-101 and
+// command_manager.py:53-67) for all envs in one launch: metric accumulation,
+// timer countdown, masked resampling from u (N, 8) uniform draws
+// [timer, lin_x, lin_y, ang_z, heading, heading-env, standing-env, unused],
+// heading control and standing override.
+
+__device__ __forceinline__ float wrap_to_pi_f(float a) {
+  const float two_pi = 6.283185307179586f, pi = 3.141592653589793f;
+  float r = fmodf(a, two_pi);  // torch.remainder: fmod, then shift into [0, 2pi)
+  if (r != 0.f && r < 0.f) r += two_pi;
+  return r > pi ? r - two_pi : r;
+}
+
+struct VelocityCommandJob {
+  static constexpr int kKind = 20;
+  const float* lin_b; long long ls; const float* ang_b; long long as; const float* root_q; long long qs;
+  const float* u; long long us; const float* ranges; float dt; float inv_max_step; float t_lo; float t_hi;
+  float rel_heading; float rel_standing; float stiffness; int heading_command; float* cmd; float* heading_target;
+  float* heading_error; bool* is_heading; bool* is_standing; float* time_left; long long* counter; float* err_xy;
+  float* err_yaw; unsigned long long seed; unsigned long long key; const mjh_i64* ctr;
+  __device__ __forceinline__ void run(long long e) const {
+    float* c = cmd + 3 * e;
+    const float* lv = lin_b + e * ls;
+    const float* av = ang_b + e * as;
+    // _update_metrics (before the resample, on the previous command)
+    const float dx = c[0] - lv[0], dy = c[1] - lv[1];
+    err_xy[e] += sqrtf(dx * dx + dy * dy) * inv_max_step;
+    err_yaw[e] += fabsf(c[2] - av[2]) * inv_max_step;
+    // countdown + resample
+    float tl = time_left[e] - dt;
+    float ud[8];
+    const float* ue = u ? u + e * us : ud;
+    if (tl <= 0.f) {
+      if (!u) {  // draws e*8 + j of the env's device stream (mjh_rng.h)
+        const mjh::Rng rng(seed, key, ctr);
+#pragma unroll
+        for (int j = 0; j < 8; j++) ud[j] = rng.u01(8 * e + j);
+      }
+      tl = ue[0] * (t_hi - t_lo) + t_lo;
+#pragma unroll
+      for (int k = 0; k < 3; k++) c[k] = ue[1 + k] * (ranges[2 * k + 1] - ranges[2 * k]) + ranges[2 * k];
+      if (heading_command) {
+        heading_target[e] = ue[4] * (ranges[7] - ranges[6]) + ranges[6];
+        is_heading[e] = ue[5] <= rel_heading;
+      }
+      is_standing[e] = ue[6] <= rel_standing;
+      counter[e] += 1;
+    }
+    time_left[e] = tl;
+    // _update_command
+    if (heading_command) {
+      const float* q = root_q + e * qs;
+      const float w = q[0], x = q[1], y = q[2], z = q[3];
+      // quat_apply(q, [1, 0, 0]) with the quat_rotate_kernel's operation order
+      const float tx = 2.f * (y * 0.f - z * 0.f), ty = 2.f * (z * 1.f - x * 0.f), tz = 2.f * (x * 0.f - y * 1.f);
+      const float fx = (1.f + w * tx) + (y * tz - z * ty);
+      const float fy = (0.f + w * ty) + (z * tx - x * tz);
+      const float herr = wrap_to_pi_f(heading_target[e] - atan2f(fy, fx));
+      heading_error[e] = herr;
+      if (is_heading[e]) c[2] = fminf(fmaxf(stiffness * herr, ranges[4]), ranges[5]);
+    }
+    if (is_standing[e]) c[0] = c[1] = c[2] = 0.f;
+  }
+};
+
+
+// this file's batchable jobs (mjh_batch.h)
+struct FuseJobs {
+  __device__ static void run(const mjh_batch::Job& j, long long e) {
+    mjh_run_as<AirTimeJob>(j, e) || mjh_run_as<SwingHeightJob>(j, e) || mjh_run_as<SoftLandingJob>(j, e) ||
+        mjh_run_as<IntervalTickJob>(j, e) || mjh_run_as<PushVelocityJob>(j, e) || mjh_run_as<GzAboveJob>(j, e) ||
+        mjh_run_as<TimeOutJob>(j, e) || mjh_run_as<TermCombineJob>(j, e) || mjh_run_as<RootFrameJob>(j, e) ||
+        mjh_run_as<StepCountersJob>(j, e) || mjh_run_as<VelocityCommandJob>(j, e);
+  }
+};
+const bool kFuseRegistered = mjh_batch::register_unit(mjh_batch::kFuse, mjh_batch_launch<FuseJobs>);
+
+template <class J>
+int submit_job(const J& j, long long n, void* stream) {
+  return mjh_batch::submit(mjh_batch::kFuse, j, n, (hipStream_t)stream, mjh_job_kernel<J>);
+}
 }  // namespace
 
 extern "C" {
@@ -894,10 +988,7 @@ int mjh_uniform_where(float* t, const unsigned char* mask, float lo, float hi, u
 
 int mjh_interval_tick(float* t, float dt, float lo, float hi, unsigned char* due, unsigned long long seed,
                       unsigned long long key, const mjh_i64* ctr, long long n, void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(interval_tick_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, t, dt, lo, hi, due, seed,
-                     key, ctr, n);
-  return finish();
+  return submit_job(IntervalTickJob{t, dt, lo, hi, due, seed, key, ctr}, n, stream);
 }
 
 int mjh_reset_root_uniform(float* qpos, long long qs, int qadr, float* qvel, long long vs, int vadr,
@@ -931,15 +1022,12 @@ int mjh_reset_joints_offset(float* qpos, long long qs, int qadr, float* qvel, lo
 int mjh_push_velocity(const float* qpos, long long qs, int qadr, float* qvel, long long vs, int vadr,
                       const unsigned char* mask, const float* vel_w, long long vws, const float* lo, const float* hi,
                       unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n, void* stream) {
-  if (n <= 0) return 0;
   Range6 r{};
   for (int j = 0; j < 6; j++) {
     r.lo[j] = lo[j];
     r.hi[j] = hi[j];
   }
-  hipLaunchKernelGGL(push_velocity_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, qpos, qs, qadr, qvel, vs,
-                     vadr, mask, vel_w, vws, r, seed, key, ctr, n);
-  return finish();
+  return submit_job(PushVelocityJob{qpos, qs, qadr, qvel, vs, vadr, mask, vel_w, vws, r, seed, key, ctr}, n, stream);
 }
 
 int mjh_velocity_resample(const unsigned char* mask, const float* ranges, float t_lo, float t_hi, float rel_heading,
@@ -962,9 +1050,11 @@ int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, co
 }
 
 int mjh_gz_above(const float* g, long long gs, float thr, unsigned char* out, long long n, void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(gz_above_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, g, gs, thr, out, n);
-  return finish();
+  return submit_job(GzAboveJob{g, gs, thr, out}, n, stream);
+}
+
+int mjh_time_out(const mjh_i64* episode_length, long long max_len, unsigned char* out, long long n, void* stream) {
+  return submit_job(TimeOutJob{episode_length, max_len, out}, n, stream);
 }
 
 int mjh_term_combine(const unsigned char* const* values, unsigned char* const* term_dones, const int* time_out, int nterms,
@@ -972,6 +1062,19 @@ int mjh_term_combine(const unsigned char* const* values, unsigned char* const* t
                      void* stream) {
   if (n <= 0) return 0;
   if (nterms > MJH_MAX_TERMS) return 1;
+  if (nterms <= 6) {
+    TermCombineJob j{};
+    for (int t = 0; t < nterms; t++) {
+      j.v[t] = values[t];
+      j.d[t] = term_dones[t];
+      j.time_out_mask |= time_out[t] ? 1 << t : 0;
+    }
+    j.nterms = nterms;
+    j.truncated = truncated;
+    j.terminated = terminated;
+    j.dones = dones;
+    return submit_job(j, n, stream);
+  }
   TermArgs a{};
   for (int t = 0; t < nterms; t++) {
     a.v[t] = values[t];
@@ -1053,10 +1156,7 @@ int mjh_joint_action(const float* input, long long is, float* action, float* pre
 int mjh_root_frame(const float* xpos, long long ps, const float* xquat, long long qs, const float* com, long long cs,
                    const float* cvel, long long vs, const float* grav, long long gs, const float* fwd, long long fs,
                    float* out, long long n, void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(root_frame_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, xpos, ps, xquat, qs, com, cs,
-                     cvel, vs, grav, gs, fwd, fs, out, n);
-  return finish();
+  return submit_job(RootFrameJob{xpos, ps, xquat, qs, com, cs, cvel, vs, grav, gs, fwd, fs, out}, n, stream);
 }
 
 int mjh_order_worlds(const int* solver_niter, const int* nefc, long long* order, long long n, void* stream) {
@@ -1112,9 +1212,7 @@ int mjh_rew_exp_err(const float* a, long long aes, long long ars, const int* ra,
 }
 
 int mjh_step_counters(mjh_i64* episode_length, mjh_i64* step, long long n, void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(step_counters_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, episode_length, step, n);
-  return finish();
+  return submit_job(StepCountersJob{episode_length, step}, n, stream);
 }
 
 int mjh_reset_stats(const unsigned char* reset, unsigned char* any_reset, mjh_i64* stats, long long n, void* stream) {
@@ -1124,3 +1222,16 @@ int mjh_reset_stats(const unsigned char* reset, unsigned char* any_reset, mjh_i6
 }
 
 }  // extern "C"
+extern "C" int mjh_velocity_command(const float* lin_b, long long ls, const float* ang_b, long long as, const float* root_q,
+                                    long long qs, const float* u, long long us, const float* ranges, float dt,
+                                    float inv_max_step, float t_lo, float t_hi, float rel_heading, float rel_standing,
+                                    float stiffness, int heading_command, float* cmd, float* heading_target,
+                                    float* heading_error, unsigned char* is_heading, unsigned char* is_standing,
+                                    float* time_left, long long* counter, float* err_xy, float* err_yaw,
+                                    unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n,
+                                    void* stream) {
+  return submit_job(VelocityCommandJob{lin_b, ls, ang_b, as, root_q, qs, u, us, ranges, dt, inv_max_step, t_lo, t_hi,
+                                   rel_heading, rel_standing, stiffness, heading_command, cmd, heading_target,
+                                   heading_error, reinterpret_cast<bool*>(is_heading), reinterpret_cast<bool*>(is_standing),
+                                   time_left, counter, err_xy, err_yaw, seed, key, ctr}, n, stream);
+}

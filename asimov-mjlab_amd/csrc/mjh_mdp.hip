@@ -154,27 +154,16 @@ struct FeetJob {
   }
 };
 
-// the reward pass's batch kernel for this file's jobs
-__global__ void mdp_batch_kernel(const mjh_batch::Pack p) {
-  const mjh_batch::Job& j = p.jobs[blockIdx.y];
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= j.n) return;
-  switch (j.kind) {
-    case TrackJob::kKind: reinterpret_cast<const TrackJob*>(j.a)->run(e); break;
-    case FlatJob::kKind: reinterpret_cast<const FlatJob*>(j.a)->run(e); break;
-    case SqsumJob::kKind: reinterpret_cast<const SqsumJob*>(j.a)->run(e); break;
-    case DiffsqJob::kKind: reinterpret_cast<const DiffsqJob*>(j.a)->run(e); break;
-    case PosLimitsJob::kKind: reinterpret_cast<const PosLimitsJob*>(j.a)->run(e); break;
-    case PostureJob::kKind: reinterpret_cast<const PostureJob*>(j.a)->run(e); break;
-    case FeetJob::kKind: reinterpret_cast<const FeetJob*>(j.a)->run(e); break;
-    default: break;
-  }
-}
 
-void mdp_batch_launch(const mjh_batch::Pack& p, hipStream_t s) {
-  hipLaunchKernelGGL(mdp_batch_kernel, dim3(mjh_batch::grid1(p.nmax), p.njobs), dim3(256), 0, s, p);
-}
-const bool kMdpRegistered = mjh_batch::register_unit(mjh_batch::kMdp, mdp_batch_launch);
+// this file's batchable jobs (mjh_batch.h)
+struct MdpJobs {
+  __device__ static void run(const mjh_batch::Job& j, long long e) {
+    mjh_run_as<TrackJob>(j, e) || mjh_run_as<FlatJob>(j, e) || mjh_run_as<SqsumJob>(j, e) ||
+        mjh_run_as<DiffsqJob>(j, e) || mjh_run_as<PosLimitsJob>(j, e) || mjh_run_as<PostureJob>(j, e) ||
+        mjh_run_as<FeetJob>(j, e);
+  }
+};
+const bool kMdpRegistered = mjh_batch::register_unit(mjh_batch::kMdp, mjh_batch_launch<MdpJobs>);
 
 template <class J>
 int submit(const J& j, long long n, void* stream) {
@@ -223,85 +212,3 @@ int mjh_rew_feet(const float* z, long long zs, long long zcs, const float* vel, 
 
 }  // extern "C"
 
-// ---- UniformVelocityCommand.compute (velocity_command.py:65-101 and
-// command_manager.py:53-67) for all envs in one launch: metric accumulation,
-// timer countdown, masked resampling from u (N, 8) uniform draws
-// [timer, lin_x, lin_y, ang_z, heading, heading-env, standing-env, unused],
-// heading control and standing override.
-namespace {
-__device__ __forceinline__ float wrap_to_pi_f(float a) {
-  const float two_pi = 6.283185307179586f, pi = 3.141592653589793f;
-  float r = fmodf(a, two_pi);  // torch.remainder: fmod, then shift into [0, 2pi)
-  if (r != 0.f && r < 0.f) r += two_pi;
-  return r > pi ? r - two_pi : r;
-}
-
-__global__ void velocity_command_kernel(const float* lin_b, long long ls, const float* ang_b, long long as,
-                                        const float* root_q, long long qs, const float* u, long long us,
-                                        const float* ranges, float dt, float inv_max_step, float t_lo, float t_hi,
-                                        float rel_heading, float rel_standing, float stiffness, int heading_command,
-                                        float* cmd, float* heading_target, float* heading_error, bool* is_heading,
-                                        bool* is_standing, float* time_left, long long* counter, float* err_xy,
-                                        float* err_yaw, unsigned long long seed, unsigned long long key,
-                                        const mjh_i64* ctr, long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  float* c = cmd + 3 * e;
-  const float* lv = lin_b + e * ls;
-  const float* av = ang_b + e * as;
-  // _update_metrics (before the resample, on the previous command)
-  const float dx = c[0] - lv[0], dy = c[1] - lv[1];
-  err_xy[e] += sqrtf(dx * dx + dy * dy) * inv_max_step;
-  err_yaw[e] += fabsf(c[2] - av[2]) * inv_max_step;
-  // countdown + resample
-  float tl = time_left[e] - dt;
-  float ud[8];
-  const float* ue = u ? u + e * us : ud;
-  if (tl <= 0.f) {
-    if (!u) {  // draws e*8 + j of the env's device stream (mjh_rng.h)
-      const mjh::Rng rng(seed, key, ctr);
-#pragma unroll
-      for (int j = 0; j < 8; j++) ud[j] = rng.u01(8 * e + j);
-    }
-    tl = ue[0] * (t_hi - t_lo) + t_lo;
-#pragma unroll
-    for (int k = 0; k < 3; k++) c[k] = ue[1 + k] * (ranges[2 * k + 1] - ranges[2 * k]) + ranges[2 * k];
-    if (heading_command) {
-      heading_target[e] = ue[4] * (ranges[7] - ranges[6]) + ranges[6];
-      is_heading[e] = ue[5] <= rel_heading;
-    }
-    is_standing[e] = ue[6] <= rel_standing;
-    counter[e] += 1;
-  }
-  time_left[e] = tl;
-  // _update_command
-  if (heading_command) {
-    const float* q = root_q + e * qs;
-    const float w = q[0], x = q[1], y = q[2], z = q[3];
-    // quat_apply(q, [1, 0, 0]) with the quat_rotate_kernel's operation order
-    const float tx = 2.f * (y * 0.f - z * 0.f), ty = 2.f * (z * 1.f - x * 0.f), tz = 2.f * (x * 0.f - y * 1.f);
-    const float fx = (1.f + w * tx) + (y * tz - z * ty);
-    const float fy = (0.f + w * ty) + (z * tx - x * tz);
-    const float herr = wrap_to_pi_f(heading_target[e] - atan2f(fy, fx));
-    heading_error[e] = herr;
-    if (is_heading[e]) c[2] = fminf(fmaxf(stiffness * herr, ranges[4]), ranges[5]);
-  }
-  if (is_standing[e]) c[0] = c[1] = c[2] = 0.f;
-}
-}  // namespace
-
-extern "C" int mjh_velocity_command(const float* lin_b, long long ls, const float* ang_b, long long as, const float* root_q,
-                                    long long qs, const float* u, long long us, const float* ranges, float dt,
-                                    float inv_max_step, float t_lo, float t_hi, float rel_heading, float rel_standing,
-                                    float stiffness, int heading_command, float* cmd, float* heading_target,
-                                    float* heading_error, unsigned char* is_heading, unsigned char* is_standing,
-                                    float* time_left, long long* counter, float* err_xy, float* err_yaw,
-                                    unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n,
-                                    void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(velocity_command_kernel, dim3(grid(n)), dim3(256), 0, (hipStream_t)stream, lin_b, ls, ang_b, as, root_q,
-                     qs, u, us, ranges, dt, inv_max_step, t_lo, t_hi, rel_heading, rel_standing, stiffness, heading_command,
-                     cmd, heading_target, heading_error, reinterpret_cast<bool*>(is_heading),
-                     reinterpret_cast<bool*>(is_standing), time_left, counter, err_xy, err_yaw, seed, key, ctr, n);
-  return finish();
-}

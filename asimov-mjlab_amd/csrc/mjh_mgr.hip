@@ -106,6 +106,8 @@ namespace mjh_batch {
 namespace {
 struct State {
   bool open = false;
+  bool seq = false;
+  int cur = -1;  // sequential batches: the unit of the jobs recorded last
   hipStream_t stream = nullptr;
   Pack pack[kUnits];
 };
@@ -114,7 +116,7 @@ Launcher g_launch[kUnits] = {};
 
 void flush_unit(State& st, int u) {
   Pack& p = st.pack[u];
-  if (p.njobs > 0 && g_launch[u]) g_launch[u](p, st.stream);
+  if (p.njobs > 0 && g_launch[u]) g_launch[u](p, st.stream, st.seq);
   p.njobs = 0;
   p.nmax = 0;
 }
@@ -130,9 +132,15 @@ bool add(int unit, int kind, long long n, const void* args, size_t bytes, hipStr
   State& st = g_state;
   if (!st.open || unit < 0 || unit >= kUnits || !g_launch[unit] || bytes > (size_t)kArgBytes) return false;
   if (s != st.stream) {  // a job on another stream: everything recorded so far goes first
-    for (int u = 0; u < kUnits; u++) flush_unit(st, u);
+    if (st.seq) {
+      if (st.cur >= 0) flush_unit(st, st.cur);
+    } else {
+      for (int u = 0; u < kUnits; u++) flush_unit(st, u);
+    }
     st.stream = s;
   }
+  if (st.seq && st.cur != unit && st.cur >= 0) flush_unit(st, st.cur);  // keep the recorded order
+  st.cur = unit;
   Pack& p = st.pack[unit];
   if (p.njobs == kMaxJobs) flush_unit(st, unit);
   Job& j = p.jobs[p.njobs++];
@@ -147,8 +155,10 @@ bool add(int unit, int kind, long long n, const void* args, size_t bytes, hipStr
 
 extern "C" {
 
-int mjh_batch_begin(void) {
+int mjh_batch_begin(int sequential) {
   mjh_batch::g_state.open = true;
+  mjh_batch::g_state.seq = sequential != 0;
+  mjh_batch::g_state.cur = -1;
   mjh_batch::g_state.stream = nullptr;
   for (auto& p : mjh_batch::g_state.pack) p.njobs = 0, p.nmax = 0;
   return 0;
@@ -158,7 +168,11 @@ int mjh_batch_end(void* stream) {
   auto& st = mjh_batch::g_state;
   if (!st.open) return 0;
   if (!st.stream) st.stream = (hipStream_t)stream;
-  for (int u = 0; u < mjh_batch::kUnits; u++) mjh_batch::flush_unit(st, u);
+  if (st.seq) {
+    if (st.cur >= 0) mjh_batch::flush_unit(st, st.cur);
+  } else {
+    for (int u = 0; u < mjh_batch::kUnits; u++) mjh_batch::flush_unit(st, u);
+  }
   st.open = false;
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -1564,7 +1564,7 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 #define MJH_PMINWAVES 1
 #endif
 #ifndef MJH_PRIO
-#define MJH_PRIO 0
+#define MJH_PRIO -1  // -1: by model size (see the Newton loop)
 #endif
 #ifndef MJH_PERSIST
 #define MJH_PERSIST 0
@@ -3192,13 +3192,15 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
 
     for (int it = 0; it < m.iterations; it++) {
       unsigned long long t_ls = PROF_NOW();
-#if MJH_PRIO == 1
-      // A/B: a world still iterating raises its wave's issue priority (the
-      // launch ends with its slowest world; the SIMD's other waves fill in)
-      if (it == 2) __builtin_amdgcn_s_setprio(1);
-      if (it == 4) __builtin_amdgcn_s_setprio(2);
-      if (it == 6) __builtin_amdgcn_s_setprio(3);
-#endif
+      // a world still iterating raises its wave's issue priority (the launch ends
+      // with its slowest world; the SIMD's other waves fill in). Measured
+      // (profiles/r05a_prio_kb.log): Go1 8192 0.457 -> 0.449 ms, G1 4096 0.501 ->
+      // 0.511 ms, so on for models up to 20 dofs only (MJH_PRIO: 1 all, 0 none)
+      if constexpr (MJH_PRIO == 1 || (MJH_PRIO < 0 && NVP <= 20)) {
+        if (it == 2) __builtin_amdgcn_s_setprio(1);
+        if (it == 4) __builtin_amdgcn_s_setprio(2);
+        if (it == 6) __builtin_amdgcn_s_setprio(3);
+      }
       // ---- exact line search along `search`
       symv_u<NT, NVP>(Mm, nv, ldm, search, Mv);
       for (int r = tid; r < nefc; r += NT) {

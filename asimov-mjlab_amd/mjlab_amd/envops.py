@@ -40,14 +40,15 @@ class JobBatch:
   batch has been launched (a temporary freed earlier could be reused by a
   later allocation on the stream before the batch reads it). CPU tensors: no-op."""
 
-  def __init__(self, like: torch.Tensor) -> None:
+  def __init__(self, like: torch.Tensor, sequential: bool = False) -> None:
     self.on = bool(like.is_cuda)
+    self.sequential = sequential
     self.keep: list = []
 
   def __enter__(self) -> "JobBatch":
     global _OPEN_BATCH
     if self.on and _OPEN_BATCH is None:
-      native.check(native.lib().mjh_batch_begin(), "mjh_batch_begin")
+      native.check(native.lib().mjh_batch_begin(int(self.sequential)), "mjh_batch_begin")
       _OPEN_BATCH = self
     return self
 
@@ -549,6 +550,7 @@ def interval_tick(env, site: str, t: torch.Tensor, dt: float, lo: float, hi: flo
   if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 1 and t.is_contiguous() and _bool_mask(due)):
     return False
   seed, key, ctr = rng_args(env, site)
+  _keep(t, due)
   native.check(native.lib().mjh_interval_tick(_ptr(t), float(dt), float(lo), float(hi), _ptr(due), seed, key, ctr,
                                               t.shape[0], _stream()), "mjh_interval_tick")
   return True
@@ -595,6 +597,7 @@ def push_velocity(env, site: str, qpos, qadr: int, qvel, vadr: int, mask, vel_w,
   if not ok or not _bool_mask(mask) or vel_w.shape != (qpos.shape[0], 6):
     return False
   seed, key, ctr = rng_args(env, site)
+  _keep(qpos, qvel, mask, vel_w)
   native.check(native.lib().mjh_push_velocity(
     _ptr(qpos), qpos.stride(0), int(qadr), _ptr(qvel), qvel.stride(0), int(vadr), _mptr(mask), _ptr(vel_w), vel_w.stride(0),
     _f6(lo6), _f6(hi6), seed, key, ctr, qpos.shape[0], _stream()), "mjh_push_velocity")
@@ -617,7 +620,20 @@ def gz_above(gz: torch.Tensor, thr: float) -> torch.Tensor | None:
     return None
   n = gz.shape[0]
   out = torch.empty(n, dtype=torch.bool, device=gz.device)
+  _keep(gz, out)
   native.check(native.lib().mjh_gz_above(_ptr(gz), gz.stride(0), float(thr), _ptr(out), n, _stream()), "mjh_gz_above")
+  return out
+
+
+def time_out(episode_length: torch.Tensor, max_len: int) -> torch.Tensor | None:
+  """episode_length >= max_len as a bool vector in one launch (batchable), or None."""
+  if not (episode_length.is_cuda and episode_length.dtype == torch.int64 and episode_length.dim() == 1
+          and episode_length.is_contiguous()):
+    return None
+  n = episode_length.shape[0]
+  out = torch.empty(n, dtype=torch.bool, device=episode_length.device)
+  _keep(episode_length, out)
+  native.check(native.lib().mjh_time_out(_ptr(episode_length), int(max_len), _ptr(out), n, _stream()), "mjh_time_out")
   return out
 
 
@@ -634,6 +650,7 @@ def term_combine(values: list, term_dones: list, time_out: list, truncated, term
   vp = (ctypes.c_void_p * T)(*[v.data_ptr() for v in values])
   dp = (ctypes.c_void_p * T)(*[d.data_ptr() for d in term_dones])
   to = (ctypes.c_int * T)(*[int(bool(x)) for x in time_out])
+  _keep(*values, *term_dones, truncated, terminated, dones)
   native.check(native.lib().mjh_term_combine(vp, dp, to, T, _ptr(truncated), _ptr(terminated), _ptr(dones), n, _stream()),
                "mjh_term_combine")
   return True
@@ -774,6 +791,7 @@ def root_frame(xpos, xquat, com, cvel, grav, fwd) -> torch.Tensor | None:
   if not all(t.shape[0] == n for t in ts):
     return None
   out = torch.empty((n, 16), dtype=torch.float32, device=xpos.device)
+  _keep(xpos, xquat, com, cvel, grav, fwd, out)
   native.check(native.lib().mjh_root_frame(_ptr(xpos), xpos.stride(0), _ptr(xquat), xquat.stride(0), _ptr(com), com.stride(0),
                                            _ptr(cvel), cvel.stride(0), _ptr(grav), grav.stride(0), _ptr(fwd), fwd.stride(0),
                                            _ptr(out), n, _stream()), "mjh_root_frame")
@@ -837,6 +855,7 @@ def rew_exp_err(a: torch.Tensor, b: torch.Tensor, std: float, quat: bool = False
 
 def step_counters(episode_length: torch.Tensor, step: torch.Tensor) -> None:
   """episode_length += 1; step += 1 (int64 device tensors) in one launch."""
+  _keep(episode_length, step)
   native.check(native.lib().mjh_step_counters(_ptr(episode_length), _ptr(step), episode_length.shape[0], _stream()),
                "mjh_step_counters")
 

@@ -45,6 +45,12 @@ from mjlab_amd.scene import Scene, SceneCfg
 from mjlab_amd.sim.sim import Simulation, SimulationCfg
 
 
+def _nullctx():
+  import contextlib
+
+  return contextlib.nullcontext()
+
+
 @dataclass
 class Box:
   """Shape-only stand-in for ``gym.spaces.Box`` (gymnasium is not a dependency)."""
@@ -243,6 +249,11 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     self._eager_steps = 0
     self._pack_buf: torch.Tensor | None = None
     self.metadata = dict(self.metadata, render_fps=1.0 / self.step_dt)
+    # sequential job batches (mjh_batch_begin(1)) for the per-env kernel chains
+    # of the termination pass and of the commands + interval events: only when
+    # every term in them is one whose fused kernels are batchable, so no torch
+    # op in the region reads a batched output before the batch launches
+    self._seq_term, self._seq_post = self._sequential_regions() if self.use_graph else (False, False)
     # one air-time contact sensor may have its timers fused into the physics step
     self._air_sensor = None
     if self.use_graph:
@@ -251,6 +262,21 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
         if attach is not None and attach(self.sim):
           self._air_sensor = sen
           break
+
+  def _sequential_regions(self) -> tuple[bool, bool]:
+    from mjlab_amd.envs.mdp import events as ev
+    from mjlab_amd.envs.mdp import terminations as tm
+
+    term_ok = all(c.func in (tm.time_out, tm.bad_orientation) for c in self.termination_manager._term_cfgs)
+    try:
+      from mjlab_amd.tasks.velocity.mdp.velocity_command import UniformVelocityCommand
+    except ImportError:  # pragma: no cover
+      return term_ok, False
+    cmds = [self.command_manager.get_term(n) for n in self.command_manager.active_terms]
+    cmd_ok = all(type(t) is UniformVelocityCommand and t.cfg.init_velocity_prob == 0.0 for t in cmds)
+    ivals = self.event_manager._mode_term_cfgs.get("interval", [])
+    ev_ok = all(c.func is ev.push_by_setting_velocity and not c.is_global_time for c in ivals)
+    return term_ok, cmd_ok and ev_ok
 
   def enable_step_pack(self) -> torch.Tensor:
     """Learner-facing outputs packed at the end of every env step, inside the
@@ -362,14 +388,17 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
       fused = self._air_sensor is not None and torch.cuda.is_current_stream_capturing()
       self.sim.step(air_time=True) if fused else self.sim.step()
       self.scene.update(dt=self.physics_dt, skip=self._air_sensor if fused else None)
-    if self.episode_length_buf.is_cuda:
-      from mjlab_amd import envops
+    from mjlab_amd import envops
 
-      envops.step_counters(self.episode_length_buf, self._env_step_t)
-    else:
-      self.episode_length_buf += 1
-      self._env_step_t += 1
-    self.termination_manager.compute()  # -> reset_buf / reset_terminated / reset_time_outs
+    # the termination pass: step counters, root frame, time_out, bad_orientation,
+    # combine — one per-env chain, one dispatch when batched sequentially
+    with envops.JobBatch(self.episode_length_buf, sequential=True) if self._seq_term else _nullctx():
+      if self.episode_length_buf.is_cuda:
+        envops.step_counters(self.episode_length_buf, self._env_step_t)
+      else:
+        self.episode_length_buf += 1
+        self._env_step_t += 1
+      self.termination_manager.compute()  # -> reset_buf / reset_terminated / reset_time_outs
     self.reward_manager.compute(dt=self.step_dt)  # -> reward_buf
     self._reset_idx(self.reset_buf)
     self.scene.write_data_to_sim()
@@ -389,9 +418,12 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     log["Sim/contact_overflow_worlds"] = fs[0]
     log["Sim/efc_overflow_worlds"] = fs[1]
     log["Sim/nonfinite_worlds"] = fs[2]
-    self.command_manager.compute(dt=self.step_dt)
-    if "interval" in self.event_manager.available_modes:
-      self.event_manager.apply(mode="interval", dt=self.step_dt)
+    # commands and interval events: root frame, velocity command, interval
+    # timers, pushes — one per-env chain (sequential batch when every term fuses)
+    with envops.JobBatch(self.episode_length_buf, sequential=True) if self._seq_post else _nullctx():
+      self.command_manager.compute(dt=self.step_dt)
+      if "interval" in self.event_manager.available_modes:
+        self.event_manager.apply(mode="interval", dt=self.step_dt)
     self.obs_buf = self.observation_manager.compute(update_history=True)
     if self._pack_buf is not None:
       from mjlab_amd.distributed import pack_step_outputs

@@ -13,6 +13,12 @@ _DEFAULT = SceneEntityCfg("robot")
 
 
 def time_out(env) -> torch.Tensor:
+  if env.episode_length_buf.is_cuda:
+    from mjlab_amd import envops
+
+    fused = envops.time_out(env.episode_length_buf, int(env.max_episode_length))
+    if fused is not None:
+      return fused
   return env.episode_length_buf >= env.max_episode_length
 
 

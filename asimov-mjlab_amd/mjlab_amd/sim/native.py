@@ -20,7 +20,7 @@ PKG = Path(__file__).resolve().parents[1]
 # MJH_LIB selects an alternative build of the same ABI (e.g. the phase-timing
 # build libmjh_prof.so used by tools/phase_profile.py).
 LIB_PATH = Path(os.environ.get("MJH_LIB", str(PKG / "libmjh.so")))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 EXPORTS = (
   "mjh_abi_version",
@@ -97,6 +97,7 @@ EXPORTS = (
   "mjh_reset_stats",
   "mjh_batch_begin",
   "mjh_batch_end",
+  "mjh_time_out",
 )
 
 
@@ -198,7 +199,8 @@ def lib() -> ctypes.CDLL:
   L.mjh_motion_adaptive.argtypes = [vp, vp, vp, vp, vp, vp, ci, ci, ll, cf, vp, vp, vp, u64, u64, vp, ll, vp]
   L.mjh_step_counters.argtypes = [vp, vp, ll, vp]
   L.mjh_reset_stats.argtypes = [vp, vp, vp, ll, vp]
-  L.mjh_batch_begin.argtypes = []
+  L.mjh_batch_begin.argtypes = [ci]
+  L.mjh_time_out.argtypes = [vp, ll, vp, ll, vp]
   L.mjh_batch_end.argtypes = [vp]
   L.mjh_rew_exp_err.argtypes = [vp, ll, ll, vp, vp, ll, ll, vp, ci, ci, ci, cf, vp, ll, vp]
   L.mjh_motion_frame.argtypes = [vp, vp, vp, ci, ci, ci, vp, vp, ll, ll, vp]

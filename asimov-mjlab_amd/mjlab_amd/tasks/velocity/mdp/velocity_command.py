@@ -82,6 +82,7 @@ class UniformVelocityCommand(CommandTerm):
     max_step = self.cfg.resampling_time_range[1] / self._env.step_dt
     seed, key, ctr = envops.rng_args(self._env, "velocity_command.compute") if u is None else (
       ctypes.c_ulonglong(0), ctypes.c_ulonglong(0), None)
+    envops._keep(lin, ang, q, u)
     native.check(native.lib().mjh_velocity_command(
       P(lin), lin.stride(0), P(ang), ang.stride(0), P(q), q.stride(0), P(u) if u is not None else None,
       u.stride(0) if u is not None else 0, P(self._ranges_t),

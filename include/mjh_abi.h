@@ -34,7 +34,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 11
+#define MJH_ABI_VERSION 12
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -364,8 +364,14 @@ int mjh_reward_combine(const float* const* values, const long long* strides, int
  * file (blockIdx.y = job), on the stream they were recorded with (or `stream`).
  * The jobs must not read each other's outputs; other launches made while the
  * batch is open run before it. Outputs are bit-identical to the separate
- * launches. Per thread (not shared across host threads). */
-int mjh_batch_begin(void);
+ * launches. Per thread (not shared across host threads).
+ * sequential != 0: each env's jobs run in the order they were recorded (one
+ * thread per env; consecutive jobs of one source file in one dispatch), for a
+ * chain of per-env kernels whose jobs read earlier jobs' outputs of the same
+ * env only (the env step's termination pass: mjh_step_counters, mjh_root_frame,
+ * mjh_time_out, mjh_gz_above, mjh_term_combine; the commands and interval
+ * events: mjh_velocity_command, mjh_interval_tick, mjh_push_velocity). */
+int mjh_batch_begin(int sequential);
 int mjh_batch_end(void* stream);
 
 /* Capacity/NaN statistics from the sticky per-world flags (data->flags_acc),
@@ -452,6 +458,10 @@ int mjh_velocity_resample(const unsigned char* mask, const float* ranges, float 
 /* out[e] = -cos(limit) < g[e * gs] <= 1 (thr = -cos(limit)): bad_orientation
  * (envs/mdp/terminations.py, torch.acos(-g_z).abs() > limit_angle) on the
  * projected gravity's z column, one launch. */
+/* time_out (envs/mdp/terminations.py): out[e] = episode_length[e] >= max_len
+ * (batchable). */
+int mjh_time_out(const mjh_i64* episode_length, long long max_len, unsigned char* out, long long n, void* stream);
+
 int mjh_gz_above(const float* g, long long gs, float thr, unsigned char* out, long long n, void* stream);
 
 int mjh_term_combine(const unsigned char* const* values, unsigned char* const* term_dones, const int* time_out, int nterms,

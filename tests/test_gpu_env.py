@@ -192,9 +192,10 @@ def test_config1_single_env_zero_agent_against_oracle():
 
 
 def test_batched_reward_pass_equals_separate_launches():
-  """The reward pass's job batch (mjh_batch_begin / mjh_batch_end: the fused
-  term kernels recorded and launched as one dispatch per source file) against
-  the same terms launched one by one: over K env steps from identical seeds,
+  """The job batches (mjh_batch_begin / mjh_batch_end: the reward terms as one
+  dispatch per source file; the termination pass and the commands + interval
+  events as sequential per-env chains) against the same kernels launched one
+  by one: over K captured env steps from identical seeds,
   rewards, episode sums, logs, observations and the simulation state agree
   bitwise (the jobs run the same arithmetic; the batch only merges dispatches)."""
   from mjlab_amd import envops
@@ -216,8 +217,9 @@ def test_batched_reward_pass_equals_separate_launches():
     cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
     cfg.scene.num_envs = n
     cfg.seed = 5
-    envs.append(ManagerBasedRlEnv(cfg, device="cuda:0", use_graph=False))
+    envs.append(ManagerBasedRlEnv(cfg, device="cuda:0"))  # captured steps: the sequential batches run too
   eb, es = envs
+  assert eb._seq_term and eb._seq_post
   for e in envs:
     e.reset()
     e.episode_length_buf[:8] = e.max_episode_length - 1
