@@ -170,12 +170,14 @@ __global__ void uniform_draws_kernel(float* __restrict__ out, long long n, unsig
   out[i] = Rng(seed, key, ctr).u01(i);
 }
 
-__global__ void uniform_where_kernel(float* __restrict__ t, const unsigned char* __restrict__ mask, float lo, float hi,
-                                     unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  if (on(mask, e)) t[e] = Rng(seed, key, ctr).u01(e) * (hi - lo) + lo;
-}
+struct UniformWhereJob {
+  static constexpr int kKind = 120;
+  float* t; const unsigned char* mask; float lo; float hi; unsigned long long seed; unsigned long long key;
+  const mjh_i64* ctr;
+  __device__ __forceinline__ void run(long long e) const {
+    if (on(mask, e)) t[e] = Rng(seed, key, ctr).u01(e) * (hi - lo) + lo;
+  }
+};
 
 // interval event timers (event_manager.py:120-145): t -= dt; due = t < 1e-6;
 // due timers are redrawn from U[lo, hi)
@@ -198,43 +200,65 @@ struct Range6 {
 
 // reset_root_state_uniform (envs/mdp/events.py:45-84): draws u[e, 0:6] for the
 // pose, u[e, 6:12] for the velocity (element index e * 12 + j)
-__global__ void reset_root_uniform_kernel(float* __restrict__ qpos, long long qs, int qadr, float* __restrict__ qvel,
-                                          long long vs, int vadr, const unsigned char* __restrict__ mask,
-                                          const float* __restrict__ rs, long long rss, const float* __restrict__ org,
-                                          long long os, const Range6 pose, const Range6 vel, int pose_rand, int vel_rand,
-                                          unsigned long long seed, unsigned long long key, const mjh_i64* ctr,
-                                          long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n || !on(mask, e)) return;
-  const Rng rng(seed, key, ctr);
-  const float* r = rs + e * rss;
-  float p6[6], v6[6];
+struct ResetRootJob {
+  static constexpr int kKind = 121;
+  float* qpos; long long qs; int qadr; float* qvel; long long vs; int vadr; const unsigned char* mask;
+  const float* rs; long long rss; const float* org; long long os; Range6 pose; Range6 vel; int pose_rand; int vel_rand;
+  unsigned long long seed; unsigned long long key; const mjh_i64* ctr;
+  __device__ __forceinline__ void run(long long e) const {
+    if (!on(mask, e)) return;
+    const Rng rng(seed, key, ctr);
+    const float* r = rs + e * rss;
+    float p6[6], v6[6];
 #pragma unroll
-  for (int j = 0; j < 6; j++) {
-    p6[j] = pose_rand ? rng.u01(e * 12 + j) * (pose.hi[j] - pose.lo[j]) + pose.lo[j] : 0.f;
-    v6[j] = vel_rand ? rng.u01(e * 12 + 6 + j) * (vel.hi[j] - vel.lo[j]) + vel.lo[j] : 0.f;
+    for (int j = 0; j < 6; j++) {
+      p6[j] = pose_rand ? rng.u01(e * 12 + j) * (pose.hi[j] - pose.lo[j]) + pose.lo[j] : 0.f;
+      v6[j] = vel_rand ? rng.u01(e * 12 + 6 + j) * (vel.hi[j] - vel.lo[j]) + vel.lo[j] : 0.f;
+    }
+    float qe[4], q[4];
+    qeuler(qe, p6[3], p6[4], p6[5]);
+    const float q0[4] = {r[3], r[4], r[5], r[6]};
+    qmul(q, q0, qe);
+    float* qp = qpos + e * qs + qadr;
+    const float* o = org + e * os;
+    qp[0] = r[0] + p6[0] + o[0];
+    qp[1] = r[1] + p6[1] + o[1];
+    qp[2] = r[2] + p6[2] + o[2];
+    qp[3] = q[0]; qp[4] = q[1]; qp[5] = q[2]; qp[6] = q[3];
+    // write_root_link_velocity: linear in the world frame, angular in the new body frame
+    const float w[3] = {r[10] + v6[3], r[11] + v6[4], r[12] + v6[5]};
+    float wb[3];
+    qrot_inv(wb, q, w);
+    float* qv = qvel + e * vs + vadr;
+    qv[0] = r[7] + v6[0]; qv[1] = r[8] + v6[1]; qv[2] = r[9] + v6[2];
+    qv[3] = wb[0]; qv[4] = wb[1]; qv[5] = wb[2];
   }
-  float qe[4], q[4];
-  qeuler(qe, p6[3], p6[4], p6[5]);
-  const float q0[4] = {r[3], r[4], r[5], r[6]};
-  qmul(q, q0, qe);
-  float* qp = qpos + e * qs + qadr;
-  const float* o = org + e * os;
-  qp[0] = r[0] + p6[0] + o[0];
-  qp[1] = r[1] + p6[1] + o[1];
-  qp[2] = r[2] + p6[2] + o[2];
-  qp[3] = q[0]; qp[4] = q[1]; qp[5] = q[2]; qp[6] = q[3];
-  // write_root_link_velocity: linear in the world frame, angular in the new body frame
-  const float w[3] = {r[10] + v6[3], r[11] + v6[4], r[12] + v6[5]};
-  float wb[3];
-  qrot_inv(wb, q, w);
-  float* qv = qvel + e * vs + vadr;
-  qv[0] = r[7] + v6[0]; qv[1] = r[8] + v6[1]; qv[2] = r[9] + v6[2];
-  qv[3] = wb[0]; qv[4] = wb[1]; qv[5] = wb[2];
-}
+};
 
 // reset_joints_by_offset (envs/mdp/events.py:87-121) for k consecutive joints:
 // draws u[e, 0:k] position offsets, u[e, k:2k] velocity offsets
+// the per-joint kernel below as a per-env job (sequential batches): the same
+// element arithmetic for j = 0..k-1
+struct ResetJointsJob {
+  static constexpr int kKind = 122;
+  float* qpos; long long qs; int qadr; float* qvel; long long vs; int vadr; int k; const unsigned char* mask;
+  const float* dp; long long dps; const float* dv; long long dvs; const float* lim; long long ls; float plo; float phi;
+  float vlo; float vhi; int prand; int vrand; unsigned long long seed; unsigned long long key; const mjh_i64* ctr;
+  __device__ __forceinline__ void run(long long e) const {
+    if (!on(mask, e)) return;
+    const Rng rng(seed, key, ctr);
+    for (int j = 0; j < k; j++) {
+      float p = dp[e * dps + j];
+      if (prand) p += rng.u01(e * 2 * k + j) * (phi - plo) + plo;
+      const float* l = lim + e * ls + 2 * j;
+      p = fminf(fmaxf(p, l[0]), l[1]);
+      float v = dv[e * dvs + j];
+      if (vrand) v += rng.u01(e * 2 * k + k + j) * (vhi - vlo) + vlo;
+      qpos[e * qs + qadr + j] = p;
+      qvel[e * vs + vadr + j] = v;
+    }
+  }
+};
 __global__ void reset_joints_offset_kernel(float* __restrict__ qpos, long long qs, int qadr, float* __restrict__ qvel,
                                            long long vs, int vadr, int k, const unsigned char* __restrict__ mask,
                                            const float* __restrict__ dp, long long dps, const float* __restrict__ dv,
@@ -287,36 +311,37 @@ struct PushVelocityJob {
 // u[e, 0] timer, u[e, 1:5] lin_x / lin_y / ang_z / heading, u[e, 5] heading env,
 // u[e, 6] standing env (element e * 8 + j). `reset` != 0: the counter restarts
 // (masked_fill 0, then += 1), else it is incremented.
-__global__ void velocity_resample_kernel(const unsigned char* __restrict__ mask, const float* __restrict__ ranges,
-                                         float t_lo, float t_hi, float rel_heading, float rel_standing,
-                                         int heading_command, int reset, float* __restrict__ cmd,
-                                         float* __restrict__ heading_target, unsigned char* __restrict__ is_heading,
-                                         unsigned char* __restrict__ is_standing, float* __restrict__ time_left,
-                                         mjh_i64* __restrict__ counter, unsigned long long seed, unsigned long long key,
-                                         const mjh_i64* ctr, long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n || !on(mask, e)) return;
-  const Rng rng(seed, key, ctr);
-  const long long b = e * 8;
-  time_left[e] = rng.u01(b) * (t_hi - t_lo) + t_lo;
+struct VelocityResampleJob {
+  static constexpr int kKind = 123;
+  const unsigned char* mask; const float* ranges; float t_lo; float t_hi; float rel_heading; float rel_standing;
+  int heading_command; int reset; float* cmd; float* heading_target; unsigned char* is_heading; unsigned char* is_standing;
+  float* time_left; mjh_i64* counter; unsigned long long seed; unsigned long long key; const mjh_i64* ctr;
+  __device__ __forceinline__ void run(long long e) const {
+    if (!on(mask, e)) return;
+    const Rng rng(seed, key, ctr);
+    const long long b = e * 8;
+    time_left[e] = rng.u01(b) * (t_hi - t_lo) + t_lo;
 #pragma unroll
-  for (int j = 0; j < 3; j++) cmd[e * 3 + j] = rng.u01(b + 1 + j) * (ranges[2 * j + 1] - ranges[2 * j]) + ranges[2 * j];
-  if (heading_command) {
-    heading_target[e] = rng.u01(b + 4) * (ranges[7] - ranges[6]) + ranges[6];
-    is_heading[e] = rng.u01(b + 5) <= rel_heading ? 1 : 0;
+    for (int j = 0; j < 3; j++) cmd[e * 3 + j] = rng.u01(b + 1 + j) * (ranges[2 * j + 1] - ranges[2 * j]) + ranges[2 * j];
+    if (heading_command) {
+      heading_target[e] = rng.u01(b + 4) * (ranges[7] - ranges[6]) + ranges[6];
+      is_heading[e] = rng.u01(b + 5) <= rel_heading ? 1 : 0;
+    }
+    is_standing[e] = rng.u01(b + 6) <= rel_standing ? 1 : 0;
+    counter[e] = reset ? 1 : counter[e] + 1;
   }
-  is_standing[e] = rng.u01(b + 6) <= rel_standing ? 1 : 0;
-  counter[e] = reset ? 1 : counter[e] + 1;
-}
+};
 
 // EventManager reset bookkeeping (event_manager.py:146-156): last = step, once = 1
-__global__ void event_mark_kernel(int* __restrict__ last, unsigned char* __restrict__ once,
-                                  const unsigned char* __restrict__ mask, const mjh_i64* __restrict__ step, long long n) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n || !on(mask, e)) return;
-  last[e] = step ? (int)*step : 0;
-  once[e] = 1;
-}
+struct EventMarkJob {
+  static constexpr int kKind = 124;
+  int* last; unsigned char* once; const unsigned char* mask; const mjh_i64* step;
+  __device__ __forceinline__ void run(long long e) const {
+    if (!on(mask, e)) return;
+    last[e] = step ? (int)*step : 0;
+    once[e] = 1;
+  }
+};
 
 // TerminationManager.compute's combination (termination_manager.py:54-82):
 // per-term done flags copied out, OR-ed into truncated (time-out terms) or
@@ -418,6 +443,31 @@ struct ZeroArgs {
   int ntensors, wmax;
 };
 
+// masked_zero for up to 6 tensors as a per-env job (sequential batches)
+struct MaskedZeroJob {
+  static constexpr int kKind = 125;
+  float* p[6]; long long rs[6]; int w[6]; int nt; const unsigned char* mask;
+  __device__ __forceinline__ void run(long long e) const {
+    if (!on(mask, e)) return;
+    for (int t = 0; t < nt; t++)
+      for (int j = 0; j < w[t]; j++) p[t][e * rs[t] + j] = 0.f;
+  }
+};
+// dst[e] = mask[e] ? src[e] : dst[e] (float); dst64[e] = mask[e] ? 0 : dst64[e] (int64)
+struct MaskedCopyJob {
+  static constexpr int kKind = 126;
+  float* dst; const float* src; const unsigned char* mask;
+  __device__ __forceinline__ void run(long long e) const {
+    if (mask[e]) dst[e] = src[e];
+  }
+};
+struct MaskedZeroI64Job {
+  static constexpr int kKind = 127;
+  mjh_i64* dst; const unsigned char* mask;
+  __device__ __forceinline__ void run(long long e) const {
+    if (mask[e]) dst[e] = 0;
+  }
+};
 __global__ void masked_zero_kernel(const ZeroArgs a, const unsigned char* __restrict__ mask, long long n) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int t = blockIdx.y;
@@ -933,7 +983,10 @@ struct FuseJobs {
     mjh_run_as<AirTimeJob>(j, e) || mjh_run_as<SwingHeightJob>(j, e) || mjh_run_as<SoftLandingJob>(j, e) ||
         mjh_run_as<IntervalTickJob>(j, e) || mjh_run_as<PushVelocityJob>(j, e) || mjh_run_as<GzAboveJob>(j, e) ||
         mjh_run_as<TimeOutJob>(j, e) || mjh_run_as<TermCombineJob>(j, e) || mjh_run_as<RootFrameJob>(j, e) ||
-        mjh_run_as<StepCountersJob>(j, e) || mjh_run_as<VelocityCommandJob>(j, e);
+        mjh_run_as<StepCountersJob>(j, e) || mjh_run_as<VelocityCommandJob>(j, e) || mjh_run_as<UniformWhereJob>(j, e) ||
+        mjh_run_as<ResetRootJob>(j, e) || mjh_run_as<ResetJointsJob>(j, e) || mjh_run_as<VelocityResampleJob>(j, e) ||
+        mjh_run_as<EventMarkJob>(j, e) || mjh_run_as<MaskedZeroJob>(j, e) || mjh_run_as<MaskedCopyJob>(j, e) ||
+        mjh_run_as<MaskedZeroI64Job>(j, e);
   }
 };
 const bool kFuseRegistered = mjh_batch::register_unit(mjh_batch::kFuse, mjh_batch_launch<FuseJobs>);
@@ -980,10 +1033,7 @@ int mjh_uniform_draws(float* out, long long n, unsigned long long seed, unsigned
 
 int mjh_uniform_where(float* t, const unsigned char* mask, float lo, float hi, unsigned long long seed,
                       unsigned long long key, const mjh_i64* ctr, long long n, void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(uniform_where_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, t, mask, lo, hi, seed, key,
-                     ctr, n);
-  return finish();
+  return submit_job(UniformWhereJob{t, mask, lo, hi, seed, key, ctr}, n, stream);
 }
 
 int mjh_interval_tick(float* t, float dt, float lo, float hi, unsigned char* due, unsigned long long seed,
@@ -996,15 +1046,13 @@ int mjh_reset_root_uniform(float* qpos, long long qs, int qadr, float* qvel, lon
                            long long os, const float* pose_lo, const float* pose_hi, const float* vel_lo,
                            const float* vel_hi, int pose_rand, int vel_rand, unsigned long long seed,
                            unsigned long long key, const mjh_i64* ctr, long long n, void* stream) {
-  if (n <= 0) return 0;
   Range6 p{}, v{};
   for (int j = 0; j < 6; j++) {
     p.lo[j] = pose_lo[j]; p.hi[j] = pose_hi[j];
     v.lo[j] = vel_lo[j]; v.hi[j] = vel_hi[j];
   }
-  hipLaunchKernelGGL(reset_root_uniform_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, qpos, qs, qadr, qvel,
-                     vs, vadr, mask, root_state, rss, origins, os, p, v, pose_rand, vel_rand, seed, key, ctr, n);
-  return finish();
+  return submit_job(ResetRootJob{qpos, qs, qadr, qvel, vs, vadr, mask, root_state, rss, origins, os, p, v, pose_rand, vel_rand,
+                                 seed, key, ctr}, n, stream);
 }
 
 int mjh_reset_joints_offset(float* qpos, long long qs, int qadr, float* qvel, long long vs, int vadr, int k,
@@ -1013,6 +1061,10 @@ int mjh_reset_joints_offset(float* qpos, long long qs, int qadr, float* qvel, lo
                             float vel_hi, int pos_rand, int vel_rand, unsigned long long seed, unsigned long long key,
                             const mjh_i64* ctr, long long n, void* stream) {
   if (n <= 0 || k <= 0) return 0;
+  // inside a batch: a per-env job; otherwise one thread per (env, joint)
+  const ResetJointsJob j{qpos, qs, qadr, qvel, vs, vadr, k, mask, def_pos, dps, def_vel, dvs, lim, ls, pos_lo, pos_hi, vel_lo,
+                         vel_hi, pos_rand, vel_rand, seed, key, ctr};
+  if (mjh_batch::add(mjh_batch::kFuse, ResetJointsJob::kKind, n, &j, sizeof(j), (hipStream_t)stream)) return 0;
   hipLaunchKernelGGL(reset_joints_offset_kernel, dim3(grid(n * k)), dim3(kBlock), 0, (hipStream_t)stream, qpos, qs, qadr,
                      qvel, vs, vadr, k, mask, def_pos, dps, def_vel, dvs, lim, ls, pos_lo, pos_hi, vel_lo, vel_hi,
                      pos_rand, vel_rand, seed, key, ctr, n);
@@ -1035,18 +1087,13 @@ int mjh_velocity_resample(const unsigned char* mask, const float* ranges, float 
                           unsigned char* is_heading, unsigned char* is_standing, float* time_left, mjh_i64* counter,
                           unsigned long long seed, unsigned long long key, const mjh_i64* ctr, long long n,
                           void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(velocity_resample_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, mask, ranges, t_lo,
-                     t_hi, rel_heading, rel_standing, heading_command, reset, cmd, heading_target, is_heading,
-                     is_standing, time_left, counter, seed, key, ctr, n);
-  return finish();
+  return submit_job(VelocityResampleJob{mask, ranges, t_lo, t_hi, rel_heading, rel_standing, heading_command, reset, cmd,
+                                        heading_target, is_heading, is_standing, time_left, counter, seed, key, ctr}, n, stream);
 }
 
 int mjh_event_mark(int* last, unsigned char* once, const unsigned char* mask, const mjh_i64* step, long long n,
                    void* stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(event_mark_kernel, dim3(grid(n)), dim3(kBlock), 0, (hipStream_t)stream, last, once, mask, step, n);
-  return finish();
+  return submit_job(EventMarkJob{last, once, mask, step}, n, stream);
 }
 
 int mjh_gz_above(const float* g, long long gs, float thr, unsigned char* out, long long n, void* stream) {
@@ -1099,6 +1146,17 @@ int mjh_masked_zero(float* const* ptrs, const long long* row_strides, const int*
                     const unsigned char* mask, long long n, void* stream) {
   if (n <= 0 || ntensors <= 0) return 0;
   if (ntensors > MJH_MAX_TERMS) return 1;
+  if (ntensors <= 6) {  // inside a batch: a per-env job
+    MaskedZeroJob j{};
+    for (int t = 0; t < ntensors; t++) {
+      j.p[t] = ptrs[t];
+      j.rs[t] = row_strides[t];
+      j.w[t] = widths[t];
+    }
+    j.nt = ntensors;
+    j.mask = mask;
+    if (mjh_batch::add(mjh_batch::kFuse, MaskedZeroJob::kKind, n, &j, sizeof(j), (hipStream_t)stream)) return 0;
+  }
   ZeroArgs a{};
   a.wmax = 0;
   for (int t = 0; t < ntensors; t++) {
@@ -1110,6 +1168,14 @@ int mjh_masked_zero(float* const* ptrs, const long long* row_strides, const int*
   a.ntensors = ntensors;
   hipLaunchKernelGGL(masked_zero_kernel, dim3(grid(n * a.wmax), ntensors), dim3(kBlock), 0, (hipStream_t)stream, a, mask, n);
   return finish();
+}
+
+int mjh_masked_copy(float* dst, const float* src, const unsigned char* mask, long long n, void* stream) {
+  return submit_job(MaskedCopyJob{dst, src, mask}, n, stream);
+}
+
+int mjh_masked_zero_i64(mjh_i64* dst, const unsigned char* mask, long long n, void* stream) {
+  return submit_job(MaskedZeroI64Job{dst, mask}, n, stream);
 }
 
 int mjh_sum_ratios(const float* const* num, const float* const* den, int nterms, float* out, long long n, void* stream) {

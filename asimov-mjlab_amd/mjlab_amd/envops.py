@@ -541,6 +541,7 @@ def uniform_where(env, site: str, t: torch.Tensor, mask, lo: float, hi: float) -
   if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 1 and t.is_contiguous() and _bool_mask(mask)):
     return False
   seed, key, ctr = rng_args(env, site)
+  _keep(t, mask)
   native.check(native.lib().mjh_uniform_where(_ptr(t), _mptr(mask), float(lo), float(hi), seed, key, ctr, t.shape[0],
                                               _stream()), "mjh_uniform_where")
   return True
@@ -569,6 +570,7 @@ def reset_root_uniform(env, site: str, qpos, qadr: int, qvel, vadr: int, mask, r
   if root_state.shape[0] != n or origins.shape[0] != n:
     return False
   seed, key, ctr = rng_args(env, site)
+  _keep(qpos, qvel, mask, root_state, origins)
   native.check(native.lib().mjh_reset_root_uniform(
     _ptr(qpos), qpos.stride(0), int(qadr), _ptr(qvel), qvel.stride(0), int(vadr), _mptr(mask), _ptr(root_state),
     root_state.stride(0), _ptr(origins), origins.stride(0), _f6(lo6), _f6(hi6), _f6(vlo6), _f6(vhi6), int(pose_rand),
@@ -585,6 +587,7 @@ def reset_joints_offset(env, site: str, qpos, qadr: int, qvel, vadr: int, mask, 
     return False
   seed, key, ctr = rng_args(env, site)
   pr, vr = tuple(prange) != (0.0, 0.0), tuple(vrange) != (0.0, 0.0)
+  _keep(qpos, qvel, mask, def_pos, def_vel, lim)
   native.check(native.lib().mjh_reset_joints_offset(
     _ptr(qpos), qpos.stride(0), int(qadr), _ptr(qvel), qvel.stride(0), int(vadr), k, _mptr(mask), _ptr(def_pos),
     def_pos.stride(0), _ptr(def_vel), def_vel.stride(0), _ptr(lim), lim.stride(0), float(prange[0]), float(prange[1]),
@@ -608,6 +611,7 @@ def event_mark(last: torch.Tensor, once: torch.Tensor, mask, step: torch.Tensor)
   if not (last.is_cuda and last.dtype == torch.int32 and once.dtype == torch.bool and _bool_mask(mask)
           and isinstance(step, torch.Tensor) and step.is_cuda and step.dtype == torch.int64 and step.numel() == 1):
     return False
+  _keep(last, once, mask, step)
   native.check(native.lib().mjh_event_mark(_ptr(last), _ptr(once), _mptr(mask), _ptr(step), last.shape[0], _stream()),
                "mjh_event_mark")
   return True
@@ -671,6 +675,26 @@ def velocity_rows(pos: torch.Tensor, com: torch.Tensor, cvel: torch.Tensor, body
   return out
 
 
+def masked_copy(dst: torch.Tensor, src: torch.Tensor, mask) -> bool:
+  """dst[mask] = src[mask] for contiguous float vectors in one launch (batchable)."""
+  if not (_bool_mask(mask) and mask is not None and all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 1
+                                                        and t.is_contiguous() and t.shape == mask.shape for t in (dst, src))):
+    return False
+  _keep(dst, src, mask)
+  native.check(native.lib().mjh_masked_copy(_ptr(dst), _ptr(src), _ptr(mask), dst.shape[0], _stream()), "mjh_masked_copy")
+  return True
+
+
+def masked_zero_i64(dst: torch.Tensor, mask) -> bool:
+  """dst[mask] = 0 for a contiguous int64 vector in one launch (batchable)."""
+  if not (_bool_mask(mask) and mask is not None and dst.is_cuda and dst.dtype == torch.int64 and dst.dim() == 1
+          and dst.is_contiguous() and dst.shape == mask.shape):
+    return False
+  _keep(dst, mask)
+  native.check(native.lib().mjh_masked_zero_i64(_ptr(dst), _ptr(mask), dst.shape[0], _stream()), "mjh_masked_zero_i64")
+  return True
+
+
 def masked_zero(tensors: list, mask) -> bool:
   """t[mask] = 0 for several float tensors (rows of unit column stride) in one launch."""
   T = len(tensors)
@@ -685,6 +709,7 @@ def masked_zero(tensors: list, mask) -> bool:
     if not (t2.is_cuda and t2.dtype == torch.float32 and t2.dim() == 2 and t2.shape[0] == n and (t2.shape[1] == 1 or t2.stride(1) == 1)):
       return False
     ptrs[i], rs[i], ws[i] = t2.data_ptr(), t2.stride(0), t2.shape[1]
+  _keep(*tensors, mask)
   native.check(native.lib().mjh_masked_zero(ptrs, rs, ws, T, _ptr(mask), n, _stream()), "mjh_masked_zero")
   return True
 

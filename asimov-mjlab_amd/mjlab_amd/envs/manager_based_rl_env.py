@@ -254,6 +254,7 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     # every term in them is one whose fused kernels are batchable, so no torch
     # op in the region reads a batched output before the batch launches
     self._seq_term, self._seq_post = self._sequential_regions() if self.use_graph else (False, False)
+    self._seq_reset = self._sequential_reset() if self.use_graph else False
     # one air-time contact sensor may have its timers fused into the physics step
     self._air_sensor = None
     if self.use_graph:
@@ -277,6 +278,46 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     ivals = self.event_manager._mode_term_cfgs.get("interval", [])
     ev_ok = all(c.func is ev.push_by_setting_velocity and not c.is_global_time for c in ivals)
     return term_ok, cmd_ok and ev_ok
+
+  def _sequential_reset(self) -> bool:
+    """Whether every reset in _reset_idx is a batchable per-env kernel (or a
+    cross-env reduction that reads nothing the batch writes: the episode-log
+    means and termination counts), so the masked reset runs as one sequential
+    job batch: EntityData.clear_state, the contact-sensor timers, the reset
+    events, the action / command / interval-event resets, episode_length."""
+    from mjlab_amd.entity.data import EntityData
+    from mjlab_amd.envs.mdp import events as ev
+    from mjlab_amd.envs.mdp.actions import JointAction
+    from mjlab_amd.sensor.contact_sensor import ContactSensor
+
+    sc = self.scene
+    for ent in getattr(sc, "_entities", {}).values():
+      d = getattr(ent, "data", None)
+      if not isinstance(d, EntityData) or not all(isinstance(d._cols.get(k), slice)
+                                                  for k in ("free_joint_v_adr", "xfrc_all", "ctrl_ids")):
+        return False
+    for sen in getattr(sc, "_sensors", {}).values():
+      if not isinstance(sen, ContactSensor):
+        return False
+    om, am, rm, em, tm = (self.observation_manager, self.action_manager, self.reward_manager, self.event_manager,
+                          self.termination_manager)
+    if getattr(om, "_history", None) or getattr(om, "_class_terms", None):
+      return False
+    if not all(type(t).reset is JointAction.reset for t in am._terms.values()):
+      return False
+    if rm._class_term_cfgs or tm._class_term_cfgs or any(em._mode_class_term_cfgs.values()):
+      return False
+    if not all(c.func in (ev.reset_root_state_uniform, ev.reset_joints_by_offset)
+               for c in em._mode_term_cfgs.get("reset", [])):
+      return False
+    if any(c.is_global_time for c in em._mode_term_cfgs.get("interval", [])):
+      return False
+    try:
+      from mjlab_amd.tasks.velocity.mdp.velocity_command import UniformVelocityCommand
+    except ImportError:  # pragma: no cover
+      return False
+    cmds = [self.command_manager.get_term(n) for n in self.command_manager.active_terms]
+    return all(type(t) is UniformVelocityCommand and t.cfg.init_velocity_prob == 0.0 for t in cmds)
 
   def enable_step_pack(self) -> torch.Tensor:
     """Learner-facing outputs packed at the end of every env step, inside the
@@ -400,7 +441,8 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
         self._env_step_t += 1
       self.termination_manager.compute()  # -> reset_buf / reset_terminated / reset_time_outs
     self.reward_manager.compute(dt=self.step_dt)  # -> reward_buf
-    self._reset_idx(self.reset_buf)
+    with envops.JobBatch(self.reset_buf, sequential=True) if self._seq_reset else _nullctx():
+      self._reset_idx(self.reset_buf)
     self.scene.write_data_to_sim()
     if self.reset_buf.is_cuda:
       from mjlab_amd import envops
@@ -455,7 +497,10 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     log.update(self.command_manager.reset(mask))
     log.update(self.event_manager.reset(mask))
     log.update(self.termination_manager.reset(mask))
-    self.episode_length_buf.masked_fill_(mask, 0)
+    from mjlab_amd import envops
+
+    if not envops.masked_zero_i64(self.episode_length_buf, mask):
+      self.episode_length_buf.masked_fill_(mask, 0)
 
   def step_stats(self) -> torch.Tensor:
     """Cumulative ``[envs reset, env steps whose gated forward ran]`` (device, long)."""

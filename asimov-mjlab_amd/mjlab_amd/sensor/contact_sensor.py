@@ -233,7 +233,8 @@ class ContactSensor:
       if not envops.masked_zero(list(timers), env_ids):  # one launch for the four timers
         for t in timers:
           t.masked_fill_(m, 0.0)
-      torch.where(env_ids, self._data.time, st.last_time, out=st.last_time)
+      if not envops.masked_copy(st.last_time, self._data.time, env_ids):
+        torch.where(env_ids, self._data.time, st.last_time, out=st.last_time)
       return
     ids = slice(None) if env_ids is None else env_ids
     st.current_air_time[ids] = 0.0

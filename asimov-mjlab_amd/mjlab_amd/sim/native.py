@@ -20,7 +20,7 @@ PKG = Path(__file__).resolve().parents[1]
 # MJH_LIB selects an alternative build of the same ABI (e.g. the phase-timing
 # build libmjh_prof.so used by tools/phase_profile.py).
 LIB_PATH = Path(os.environ.get("MJH_LIB", str(PKG / "libmjh.so")))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 EXPORTS = (
   "mjh_abi_version",
@@ -98,6 +98,8 @@ EXPORTS = (
   "mjh_batch_begin",
   "mjh_batch_end",
   "mjh_time_out",
+  "mjh_masked_copy",
+  "mjh_masked_zero_i64",
 )
 
 
@@ -201,6 +203,8 @@ def lib() -> ctypes.CDLL:
   L.mjh_reset_stats.argtypes = [vp, vp, vp, ll, vp]
   L.mjh_batch_begin.argtypes = [ci]
   L.mjh_time_out.argtypes = [vp, ll, vp, ll, vp]
+  L.mjh_masked_copy.argtypes = [vp, vp, vp, ll, vp]
+  L.mjh_masked_zero_i64.argtypes = [vp, vp, ll, vp]
   L.mjh_batch_end.argtypes = [vp]
   L.mjh_rew_exp_err.argtypes = [vp, ll, ll, vp, vp, ll, ll, vp, ci, ci, ci, cf, vp, ll, vp]
   L.mjh_motion_frame.argtypes = [vp, vp, vp, ci, ci, ci, vp, vp, ll, ll, vp]

@@ -124,6 +124,7 @@ class UniformVelocityCommand(CommandTerm):
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     lo, hi = self.cfg.resampling_time_range
     seed, key, ctr = envops.rng_args(self._env, "velocity_command.resample")
+    envops._keep(mask)
     native.check(native.lib().mjh_velocity_resample(
       P(mask), P(self._ranges_t), float(lo), float(hi), float(self.cfg.rel_heading_envs), float(self.cfg.rel_standing_envs),
       int(self.cfg.heading_command), int(reset), P(self.vel_command_b), P(self.heading_target), P(self.is_heading_env),

@@ -34,7 +34,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 12
+#define MJH_ABI_VERSION 13
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -370,7 +370,10 @@ int mjh_reward_combine(const float* const* values, const long long* strides, int
  * chain of per-env kernels whose jobs read earlier jobs' outputs of the same
  * env only (the env step's termination pass: mjh_step_counters, mjh_root_frame,
  * mjh_time_out, mjh_gz_above, mjh_term_combine; the commands and interval
- * events: mjh_velocity_command, mjh_interval_tick, mjh_push_velocity). */
+ * events: mjh_velocity_command, mjh_interval_tick, mjh_push_velocity; the
+ * masked resets: mjh_masked_zero, mjh_masked_copy, mjh_masked_zero_i64,
+ * mjh_event_mark, mjh_reset_root_uniform, mjh_reset_joints_offset,
+ * mjh_velocity_resample, mjh_uniform_where). */
 int mjh_batch_begin(int sequential);
 int mjh_batch_end(void* stream);
 
@@ -479,6 +482,13 @@ int mjh_velocity_rows(const float* pos, long long pes, long long prs, const floa
  * ptrs[t] + e * row_strides[t]) in one launch (managers' masked_fill_ chains). */
 int mjh_masked_zero(float* const* ptrs, const long long* row_strides, const int* widths, int ntensors,
                     const unsigned char* mask, long long n, void* stream);
+
+/* Masked per-env copies for the reset path (batchable): dst[e] = src[e] where
+ * mask[e] (ContactSensor.reset's last_time, contact_sensor.py:210-216), and
+ * dst64[e] = 0 where mask[e] (episode_length_buf.masked_fill_,
+ * manager_based_rl_env.py:245). */
+int mjh_masked_copy(float* dst, const float* src, const unsigned char* mask, long long n, void* stream);
+int mjh_masked_zero_i64(mjh_i64* dst, const unsigned char* mask, long long n, void* stream);
 
 /* out[t] = sum(num[t]) / max(sum(den[t]), 1) over n envs (reward-term metric
  * logs, tasks/velocity/mdp/rewards.py); den[t] NULL: mean(sqrt(num[t]))

@@ -202,7 +202,7 @@ def test_batched_reward_pass_equals_separate_launches():
   from mjlab_amd.sim import native
 
   class _NoBatch:
-    def __init__(self, like):
+    def __init__(self, like, sequential=False):
       pass
 
     def __enter__(self):
@@ -229,7 +229,8 @@ def test_batched_reward_pass_equals_separate_launches():
     a = 2 * torch.rand(n, eb.action_manager.total_action_dim, device="cuda:0", generator=g) - 1
     before = native.CALLS["mjh_batch_end"]
     ob, rb, tb, trb, xb = eb.step(a)
-    assert native.CALLS["mjh_batch_end"] > before  # the batched pass ran
+    if k < 2:  # eager step, then the capture (later steps replay the graph: no host calls)
+      assert native.CALLS["mjh_batch_end"] > before  # the batched passes ran
     envops.JobBatch = _NoBatch
     try:
       os_, rs, ts, trs, xs = es.step(a)
