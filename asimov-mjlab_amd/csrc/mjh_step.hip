@@ -1683,8 +1683,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   const long long W = w;
   const int nq = Z.nq, nv = Z.nv, nb = Z.nbody, nu = Z.nu, nj = Z.njnt;
   const int ldm = Lo.ldm, ldj = Lo.ldj;
-  // the factor's rows: packed lower-triangular for one-world workgroups
-  constexpr bool PKL = pack_l(WPB);
+  // the factor's rows: packed lower-triangular for one-world workgroups (the
+  // split position launch hands the factor to the velocity launch, whose
+  // workgroup shape decides the packing)
+  constexpr bool PKL = pack_l(MODE == 1 ? wpb_of_nvp(NVP) : WPB);
   const int kLWords = PKL ? lrow(NVP) : nv * ldm;
   // elliptic friction cones: the generic instances only (the model-specialised
   // ones are picked for pyramidal cones), J in global scratch (virtual rows of
