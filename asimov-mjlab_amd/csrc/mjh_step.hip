@@ -27,6 +27,7 @@
 #include <type_traits>
 
 #include "../../include/mjh_abi.h"
+#include "mjh_convex.h"
 #include "mjh_math.h"
 #include "mjh_rng.h"
 
@@ -1246,8 +1247,24 @@ __device__ __noinline__ int sphere_cylinder(Con* c, float margin, const float* s
   return sphere_sphere(c, margin, sp, rs, q, 0.f);
 }
 
+// the general convex pairs (sphere-ellipsoid, capsule-{ellipsoid,cylinder},
+// ellipsoid-{ellipsoid,cylinder,box}, cylinder-{cylinder,box}): GJK + EPA and
+// a Newton polish of the normal, one contact (mjh_convex.h, the oracle's
+// collide() compiles the same source in float64)
+__device__ __noinline__ int convex_pair(Con* c, int t1, const float* p1, const float* m1, const float* s1, int t2,
+                                        const float* p2, const float* m2, const float* s2, float margin) {
+  float n[3];
+  if (!cvx_collide(t1, p1, m1, s1, t2, p2, m2, s2, margin, &c->dist, c->pos, n)) return 0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    c->frame[k] = n[k];
+    c->frame[3 + k] = 0.f;
+  }
+  return 1;
+}
+
 // Narrowphase for one pair (types ascending). Up to 4 contacts. `boxes`: the
-// model has pairs that need the box, cylinder or ellipsoid functions
+// model has pairs that need the box, cylinder, ellipsoid or convex functions
 // (Sizes::nboxpair; a compile-time
 // 0 in the model-specialised instances of models without such pairs, whose
 // code then carries none of them).
@@ -1257,6 +1274,7 @@ __device__ MJH_COLL_INLINE int narrowphase(int t1, int t2, const float* p1, cons
     if (t1 == 0 && t2 == 4) return plane_ellipsoid(out, margin, p1, m1, p2, m2, s2);
     if (t1 == 0 && t2 == 5) return plane_cylinder(out, margin, p1, m1, p2, m2, s2[0], s2[1]);
     if (t1 == 2 && t2 == 5) return sphere_cylinder(out, margin, p1, s1[0], p2, m2, s2[0], s2[1]);
+    if (t1 >= 2) return convex_pair(out, t1, p1, m1, s1, t2, p2, m2, s2, margin);
     return 0;
   }
   if (boxes && t2 == 6 && t1 >= 2) {
@@ -1266,7 +1284,7 @@ __device__ MJH_COLL_INLINE int narrowphase(int t1, int t2, const float* p1, cons
       return capsule_box(out, margin, p1, ax, s1[1], s1[0], p2, m2, s2);
     }
     if (t1 == 6) return box_box(out, margin, p1, m1, s1, p2, m2, s2);
-    return 0;
+    return convex_pair(out, t1, p1, m1, s1, t2, p2, m2, s2, margin);
   }
   if (t1 == 0 && t2 == 2) return plane_sphere(out, margin, p1, m1, p2, s2[0]);
   if (t1 == 0 && t2 == 3) {

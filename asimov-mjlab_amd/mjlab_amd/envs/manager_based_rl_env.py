@@ -288,6 +288,7 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     from mjlab_amd.entity.data import EntityData
     from mjlab_amd.envs.mdp import events as ev
     from mjlab_amd.envs.mdp.actions import JointAction
+    from mjlab_amd.sensor.builtin_sensor import BuiltinSensor
     from mjlab_amd.sensor.contact_sensor import ContactSensor
 
     sc = self.scene
@@ -297,7 +298,7 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
                                                   for k in ("free_joint_v_adr", "xfrc_all", "ctrl_ids")):
         return False
     for sen in getattr(sc, "_sensors", {}).values():
-      if not isinstance(sen, ContactSensor):
+      if not isinstance(sen, ContactSensor) and type(sen).reset is not BuiltinSensor.reset:  # the latter: a no-op
         return False
     om, am, rm, em, tm = (self.observation_manager, self.action_manager, self.reward_manager, self.event_manager,
                           self.termination_manager)
@@ -305,7 +306,10 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
       return False
     if not all(type(t).reset is JointAction.reset for t in am._terms.values()):
       return False
-    if rm._class_term_cfgs or tm._class_term_cfgs or any(em._mode_class_term_cfgs.values()):
+    # class terms take part only through a reset method (their __call__ runs outside the reset)
+    if any(hasattr(c.func, "reset") for c in rm._class_term_cfgs + tm._class_term_cfgs):
+      return False
+    if any(em._mode_class_term_cfgs.values()):
       return False
     if not all(c.func in (ev.reset_root_state_uniform, ev.reset_joints_by_offset)
                for c in em._mode_term_cfgs.get("reset", [])):

@@ -32,9 +32,12 @@ from mjlab_amd.spec.spec import GEOM_TYPES, JOINT_TYPES, Spec
 from mjlab_amd.utils import rot
 
 MINVAL = 1e-15
-SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 4), (0, 5), (0, 6), (2, 2), (2, 3), (2, 5), (3, 3), (2, 6), (3, 6), (6, 6)}
-# pairs that need the box, cylinder or ellipsoid narrowphase functions (Model.nboxpair counts them)
-BOX_PAIRS = {(2, 6), (3, 6), (6, 6), (0, 4), (0, 5), (2, 5)}
+# the general convex pairs: GJK + EPA, one contact (csrc/mjh_convex.h; MuJoCo's mjc_Convex)
+CONVEX_PAIRS = {(2, 4), (3, 4), (4, 4), (3, 5), (4, 5), (5, 5), (4, 6), (5, 6)}
+SUPPORTED_PAIRS = {(0, 2), (0, 3), (0, 4), (0, 5), (0, 6), (2, 2), (2, 3), (2, 5), (3, 3), (2, 6), (3, 6),
+                   (6, 6)} | CONVEX_PAIRS
+# pairs that need the box, cylinder, ellipsoid or convex narrowphase functions (Model.nboxpair counts them)
+BOX_PAIRS = {(2, 6), (3, 6), (6, 6), (0, 4), (0, 5), (2, 5)} | CONVEX_PAIRS
 
 # Sensor type codes used by the kernels (order is ours; names follow mjtSensor).
 SENSOR_TYPES = {

@@ -994,6 +994,18 @@ static int raw_sphere_cylinder(contact_t* c, real margin, const real sp[3], real
   return raw_sphere_sphere(c, margin, sp, rs, q, 0);
 }
 
+/* the general convex pairs (sphere-ellipsoid, capsule-{ellipsoid,cylinder},
+   ellipsoid-{ellipsoid,cylinder,box}, cylinder-{cylinder,box}): GJK + EPA,
+   one contact (asimov-mjlab_amd/csrc/mjh_convex.h, shared with the kernel and
+   pinned by tests/test_convex.py's known answers) */
+#define CVX_REAL real
+#include "mjh_convex.h"
+
+static int convex_pair(int t1, int t2) {
+  if (t1 < 2 || t2 < 2) return 0;
+  return t2 == 4 || (t2 == 5 && t1 != 2) || (t2 == 6 && (t1 == 4 || t1 == 5));
+}
+
 static int collide(const or_model* m, ws_t* w, int g1, int g2, real margin, contact_t* out) {
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   const real *p1 = w->gxpos + 3 * g1, *m1 = w->gxmat + 9 * g1, *s1 = m->geom_size + 3 * g1;
@@ -1083,6 +1095,15 @@ static int collide(const or_model* m, ws_t* w, int g1, int g2, real margin, cont
     return raw_capsule_box(out, margin, p1, ax, s1[1], s1[0], p2, m2, s2);
   }
   if (t1 == 6 && t2 == 6) return raw_box_box(out, margin, p1, m1, s1, p2, m2, s2);
+  if (convex_pair(t1, t2)) {
+    real n[3];
+    if (!cvx_collide(t1, p1, m1, s1, t2, p2, m2, s2, margin, &out->dist, out->pos, n)) return 0;
+    for (int k = 0; k < 3; k++) {
+      out->frame[k] = n[k];
+      out->frame[3 + k] = 0;
+    }
+    return 1;
+  }
   return 0; /* unsupported pairs are rejected by the compiler */
 }
 

@@ -219,7 +219,7 @@ def test_batched_reward_pass_equals_separate_launches():
     cfg.seed = 5
     envs.append(ManagerBasedRlEnv(cfg, device="cuda:0"))  # captured steps: the sequential batches run too
   eb, es = envs
-  assert eb._seq_term and eb._seq_post
+  assert eb._seq_term and eb._seq_post and eb._seq_reset
   for e in envs:
     e.reset()
     e.episode_length_buf[:8] = e.max_episode_length - 1

@@ -104,10 +104,9 @@ def _entity(xml: str, **kw) -> Entity:
 def _init_entity_with_sim(entity: Entity, backend: str, num_envs: int = 1, skip: tuple[str, ...] = ()):
   """test_entity_data.py:35-41 / test_entity.py:130-136."""
   model = entity.compile()
-  # the one pair without a narrowphase in these scenes: FIXED_BASE_ARTICULATED's
-  # cylinder base against link2's box, which sit 0.3 m apart in every state the
-  # restated tests use (no contact either way); anything else must be supported
-  assert set(model.unsupported_pair_types) <= {(5, 6)}, model.unsupported_pair_types
+  # every pair of these scenes has a narrowphase (FIXED_BASE_ARTICULATED's
+  # cylinder base against link2's box: the general convex collider)
+  assert not model.unsupported_pair_types, model.unsupported_pair_types
   sim = make_sim(num_envs, SimulationCfg(), model, backend, skip=skip)
   entity.initialize(model, sim.model, sim.data, device_of(backend))
   return entity, sim
