@@ -83,6 +83,25 @@ __device__ __forceinline__ void axis_angle(float q[4], const float* axis, float 
   q[0] = c; q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
 }
 
+// the rotation vector (axis x angle, angle in (-pi, pi]) of a quaternion
+// (MuJoCo mju_quat2Vel with dt = 1); returns the angle
+__device__ __forceinline__ float quat2vel(float r[3], const float* q) {
+  float ax[3] = {q[1], q[2], q[3]};
+  const float s = normalize3(ax);
+  float ang = 2.f * atan2f(s, q[0]);
+  if (ang > 3.14159265358979f) ang -= 6.28318530717959f;
+  r[0] = ax[0] * ang; r[1] = ax[1] * ang; r[2] = ax[2] * ang;
+  return ang;
+}
+
+// r such that qa = qb * exp(r) (MuJoCo mju_subQuat)
+__device__ __forceinline__ void sub_quat(float r[3], const float* qa, const float* qb) {
+  const float qbc[4] = {qb[0], -qb[1], -qb[2], -qb[3]}, a[4] = {qa[0], qa[1], qa[2], qa[3]};
+  float d[4];
+  quat_mul(d, qbc, a);
+  quat2vel(r, d);
+}
+
 // spatial motion cross product r = v x m   ([ang; lin] convention)
 __device__ __forceinline__ void cross_motion(float r[6], const float* v, const float* m) {
   float t0 = -v[2] * m[1] + v[1] * m[2];

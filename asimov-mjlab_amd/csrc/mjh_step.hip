@@ -1247,6 +1247,27 @@ __device__ __noinline__ int sphere_cylinder(Con* c, float margin, const float* s
   return sphere_sphere(c, margin, sp, rs, q, 0.f);
 }
 
+// Joint limit of a limited joint (mj_instantiateLimit): true if active, with
+// pos = distance - margin and, for hinge/slide, sgn = +1 at the lower bound, -1
+// at the upper. Ball: the rotation angle of the joint's quaternion against the
+// larger range bound (the row's Jacobian is -(unit rotation axis)).
+__device__ __forceinline__ bool joint_limit(int t, const float* q, const float* rng, float margin, float* pos, float* sgn) {
+  if (t == 2 || t == 3) {
+    const float dlo = q[0] - rng[0], dhi = rng[1] - q[0];
+    *pos = fminf(dlo, dhi) - margin;
+    *sgn = dlo < dhi ? 1.f : -1.f;
+    return *pos < 0.f;
+  }
+  if (t == 1) {
+    float r[3];
+    const float ang = fabsf(quat2vel(r, q));
+    *pos = fmaxf(rng[0], rng[1]) - ang - margin;
+    *sgn = 1.f;
+    return *pos < 0.f;
+  }
+  return false;
+}
+
 // the general convex pairs (sphere-ellipsoid, capsule-{ellipsoid,cylinder},
 // ellipsoid-{ellipsoid,cylinder,box}, cylinder-{cylinder,box}): GJK + EPA and
 // a Newton polish of the normal, one contact (mjh_convex.h, the oracle's
@@ -1931,6 +1952,13 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           quat2mat(Rq, q);
           mat_vec(v, Rq, IMG_F(jnt_pos) + 3 * j);
           p[0] = anc[0] - v[0]; p[1] = anc[1] - v[1]; p[2] = anc[2] - v[2];
+        } else if (IMG_I(jnt_type)[j] == 1) {  // ball: the normalised qpos quaternion, about the anchor
+          float ql[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]}, v[3];
+          quat_normalize(ql);
+          quat_mul(q, q, ql);
+          quat2mat(Rq, q);
+          mat_vec(v, Rq, IMG_F(jnt_pos) + 3 * j);
+          p[0] = anc[0] - v[0]; p[1] = anc[1] - v[1]; p[2] = anc[2] - v[2];
         }
         if (k == b) {
           xanchor[3 * j] = anc[0]; xanchor[3 * j + 1] = anc[1]; xanchor[3 * j + 2] = anc[2];
@@ -2086,6 +2114,16 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       for (int k = 0; k < 6; k++)
 #pragma unroll
         for (int e = 0; e < 6; e++) cdof[6 * (da + k) + e] = rows[k][e];
+    } else if (t == 1) {  // ball: rotations about the body's axes
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const float ax[3] = {xmat[9 * b + k], xmat[9 * b + 3 + k], xmat[9 * b + 6 + k]};
+        float cr[3];
+        cross3(cr, ax, off);
+        float* cd = cdof + 6 * (da + k);
+        cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+        cd[3] = cr[0]; cd[4] = cr[1]; cd[5] = cr[2];
+      }
     } else {
       const float ax[3] = {xaxis[3 * j], xaxis[3 * j + 1], xaxis[3 * j + 2]};
       float* cd = cdof + 6 * da;
@@ -2281,10 +2319,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         for (int base = 0; base < nj; base += NT) {
           const int j = base + tid;
           bool f = false;
-          if (j < nj && IMG_I(jnt_limited)[j] && (IMG_I(jnt_type)[j] == 2 || IMG_I(jnt_type)[j] == 3)) {
-            const float q = qpos[IMG_I(jnt_qposadr)[j]];
-            const float dlo = q - jnt_range[2 * j], dhi = jnt_range[2 * j + 1] - q;
-            f = fminf(dlo, dhi) - IMG_F(jnt_margin)[j] < 0.f;
+          if (j < nj && IMG_I(jnt_limited)[j]) {
+            float pos, sgn;
+            f = joint_limit(IMG_I(jnt_type)[j], qpos + IMG_I(jnt_qposadr)[j], jnt_range + 2 * j, IMG_F(jnt_margin)[j],
+                            &pos, &sgn);
           }
           need += __popcll(__ballot(f));
         }
@@ -2354,13 +2392,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       const int j = base + tid;
       int f = 0;
       float pos = 0.f, sgn = 0.f;
-      if (j < nj && IMG_I(jnt_limited)[j] && (IMG_I(jnt_type)[j] == 2 || IMG_I(jnt_type)[j] == 3)) {
-        const float q = qpos[IMG_I(jnt_qposadr)[j]];
-        const float dlo = q - jnt_range[2 * j], dhi = jnt_range[2 * j + 1] - q;
-        pos = fminf(dlo, dhi) - IMG_F(jnt_margin)[j];
-        sgn = dlo < dhi ? 1.f : -1.f;
-        f = pos < 0.f ? 1 : 0;
-      }
+      if (j < nj && IMG_I(jnt_limited)[j])
+        f = joint_limit(IMG_I(jnt_type)[j], qpos + IMG_I(jnt_qposadr)[j], jnt_range + 2 * j, IMG_F(jnt_margin)[j], &pos,
+                        &sgn) ? 1 : 0;
       int total;
       const int off = bscan<NT>(f, &total, redi);
       if (f) {
@@ -2370,7 +2404,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           efc_type[r] = MJH_CNSTR_LIMIT_JOINT;
           efc_id[r] = j;
           efc_fl[r] = 0.f;
-          efc_mask[r] = 1ull << dof;
+          efc_mask[r] = (IMG_I(jnt_type)[j] == 1 ? 7ull : 1ull) << dof;  // a ball limit spans its three dofs
           efc_pos[r] = pos + IMG_F(jnt_margin)[j];
           jv[r] = sgn;  // temporarily hold the Jacobian sign
           row_params_pos(m.timestep, pos, pos, IMG_F(dof_invweight0)[dof], IMG_F(jnt_solref) + 2 * j,
@@ -2411,17 +2445,34 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     // it). Single-dof rows first, their (type, column, value) one per lane.
     for (int base = 0; base < nsimple; base += NT) {
       int col = -1;
-      float val = 0.f;
+      float val = 0.f, bv[3] = {0.f, 0.f, 0.f};
+      bool ball = false;
       if (base + tid < nsimple) {
         const int r = base + tid, t = efc_type[r];
         col = t == MJH_CNSTR_FRICTION_DOF ? efc_id[r] : IMG_I(jnt_dofadr)[efc_id[r]];
         val = t == MJH_CNSTR_FRICTION_DOF ? 1.f : jv[r];
+        if (t == MJH_CNSTR_LIMIT_JOINT && IMG_I(jnt_type)[efc_id[r]] == 1) {
+          // ball limit: -(unit rotation axis) on the joint's three dofs
+          ball = true;
+          quat2vel(bv, qpos + IMG_I(jnt_qposadr)[efc_id[r]]);
+          normalize3(bv);
+          val = -bv[0];
+        }
       }
       const int cnt = min(NT, nsimple - base);
-      for (int k = 0; k < cnt; k++) {
-        const int ck = __builtin_amdgcn_readlane(col, k);
-        const float vk = rl(val, k);
-        if (tid < ldj) J[(base + k) * ldj + tid] = tid == ck ? vk : 0.f;
+      if (__ballot(ball) == 0ull) {
+        for (int k = 0; k < cnt; k++) {
+          const int ck = __builtin_amdgcn_readlane(col, k);
+          const float vk = rl(val, k);
+          if (tid < ldj) J[(base + k) * ldj + tid] = tid == ck ? vk : 0.f;
+        }
+      } else {  // rows with up to three consecutive entries
+        const float b1 = ball ? -bv[1] : 0.f, b2 = ball ? -bv[2] : 0.f;
+        for (int k = 0; k < cnt; k++) {
+          const int ck = __builtin_amdgcn_readlane(col, k);
+          const float vk = rl(val, k), v1 = rl(b1, k), v2 = rl(b2, k);
+          if (tid < ldj) J[(base + k) * ldj + tid] = tid == ck ? vk : (tid == ck + 1 ? v1 : (tid == ck + 2 ? v2 : 0.f));
+        }
       }
     }
     // contact rows: lane = contact loads the contact's data, then per contact
@@ -2757,6 +2808,11 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     if ((t == 2 || t == 3) && jnt_stiffness[jnt] != 0.f) {
       const int qa = IMG_I(jnt_qposadr)[jnt];
       pas -= jnt_stiffness[jnt] * (qpos[qa] - IMG_F(qpos_spring)[qa]);
+    } else if (t == 1 && jnt_stiffness[jnt] != 0.f) {  // ball: the rotation vector from the spring pose
+      const int qa = IMG_I(jnt_qposadr)[jnt], k = i - IMG_I(jnt_dofadr)[jnt];
+      float dif[3];
+      sub_quat(dif, qpos + qa, IMG_F(qpos_spring) + qa);
+      pas -= jnt_stiffness[jnt] * (k == 0 ? dif[0] : (k == 1 ? dif[1] : dif[2]));
     }
     qfrc_passive[i] = pas;
     qfrc_act[i] = 0.f;
@@ -3951,6 +4007,16 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         quat_mul(q, q, qr);
         quat_normalize(q);
         qpos[q0 + 3] = q[0]; qpos[q0 + 4] = q[1]; qpos[q0 + 5] = q[2]; qpos[q0 + 6] = q[3];
+      } else if (IMG_I(jnt_type)[j] == 1) {  // ball: mju_quatIntegrate
+        float q[4] = {qpos[q0], qpos[q0 + 1], qpos[q0 + 2], qpos[q0 + 3]};
+        float om[3] = {qvel[v0], qvel[v0 + 1], qvel[v0 + 2]};
+        const float ang = dt * normalize3(om);
+        float qr[4];
+        axis_angle(qr, om, ang);
+        quat_normalize(q);
+        quat_mul(q, q, qr);
+        quat_normalize(q);
+        qpos[q0] = q[0]; qpos[q0 + 1] = q[1]; qpos[q0 + 2] = q[2]; qpos[q0 + 3] = q[3];
       } else {
         qpos[q0] += dt * qvel[v0];
       }

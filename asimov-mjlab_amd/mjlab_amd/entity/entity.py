@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from mjlab_amd.entity.data import EntityData
+from mjlab_amd.spec.compiler import DOF_WIDTH, QPOS_WIDTH
 from mjlab_amd.spec.spec import KeySpec, Spec
 from mjlab_amd.utils import spec_config as spec_cfg
 from mjlab_amd.utils.string import resolve_expr, resolve_matching_names
@@ -309,9 +310,9 @@ class Entity:
       if t == 0:
         fv += list(range(va, va + 6))
         fq += list(range(qa, qa + 7))
-      else:
-        jv.append(va)
-        jq.append(qa)
+      else:  # ball: 4 qpos, 3 dofs (reference entity.py:631-633, qpos_width / dof_width)
+        jv += list(range(va, va + DOF_WIDTH[t]))
+        jq += list(range(qa, qa + QPOS_WIDTH[t]))
 
     def T(x):
       return torch.tensor(x, dtype=torch.int, device=device)

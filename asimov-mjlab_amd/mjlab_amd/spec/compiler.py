@@ -8,7 +8,7 @@ algorithm, not vendored in the reference):
 1. depth-first body order, joint/dof/geom/site addresses;
 2. ``fromto`` capsules, inertia from geoms when a body has no ``<inertial>``;
 3. autolimits for joints, actuator ``inheritrange``/``ctrlrange``/``forcerange``;
-4. ``qpos0`` (free joint = body pose, hinge/slide = ``ref``);
+4. ``qpos0`` (free joint = body pose, ball = identity, hinge/slide = ``ref``);
 5. ``mj_setConst``: ``dof_invweight0``, ``body_invweight0``, ``meaninertia``
    from the mass matrix at ``qpos0``;
 6. the filtered geom-pair table (weld filter, parent filter, contype/conaffinity,
@@ -272,8 +272,6 @@ def compile_spec(spec: Spec, nconmax: int = 0, njmax: int = 0) -> Model:
       t = JOINT_TYPES[j.type]
       if t == 0 and (bi == 0 or len(b.joints) != 1 or parent[bi] != 0):
         raise ValueError("free joint must be the only joint of a world child body")
-      if t == 1:
-        raise NotImplementedError("ball joints are not supported on the HIP path")
       jid = len(jnt_list)
       dofadr = len(dof_list)
       if body_dofadr[bi] < 0:
@@ -435,6 +433,9 @@ def compile_spec(spec: Spec, nconmax: int = 0, njmax: int = 0) -> Model:
       qpos0[qa : qa + 3] = m.body_pos[bi]
       qpos0[qa + 3 : qa + 7] = m.body_quat[bi]
       qspring[qa : qa + 7] = qpos0[qa : qa + 7]
+    elif t == 1:  # ball: the identity rotation (MuJoCo ignores ref / springref here)
+      qpos0[qa : qa + 4] = [1.0, 0.0, 0.0, 0.0]
+      qspring[qa : qa + 4] = qpos0[qa : qa + 4]
     else:
       qpos0[qa] = j.ref
       qspring[qa] = j.springref
@@ -581,6 +582,8 @@ def _compile_sensors(m: Model, spec: Spec) -> None:
     m.sensor_type[i] = SENSOR_TYPES[s.type]
     m.sensor_objtype[i] = OBJ_CODES[s.objtype]
     m.sensor_objid[i] = m.names[lookup[s.objtype]].index(s.objname)
+    if s.type in ("jointpos", "jointvel") and m.jnt_type[m.sensor_objid[i]] not in (2, 3):
+      raise NotImplementedError(f"{s.type} sensor '{s.name}' needs a hinge or slide joint (MuJoCo: ballquat / ballangvel)")
     if s.reftype:
       m.sensor_reftype[i] = OBJ_CODES[s.reftype]
       m.sensor_refid[i] = m.names[lookup[s.reftype]].index(s.refname)
@@ -649,6 +652,11 @@ def _kinematics0(m: Model):
         ax = xmat[b][:, k]
         cdof[da + 3 + k, :3] = ax
         cdof[da + 3 + k, 3:] = np.cross(ax, off)
+    elif t == 1:  # ball: rotations about the body's axes
+      for k in range(3):
+        ax = xmat[b][:, k]
+        cdof[da + k, :3] = ax
+        cdof[da + k, 3:] = np.cross(ax, off)
     elif t == 3:
       cdof[da, :3] = xaxis[j]
       cdof[da, 3:] = np.cross(xaxis[j], off)
@@ -698,6 +706,8 @@ def _set_const(m: Model) -> None:
     if m.jnt_type[j] == 0:
       m.dof_invweight0[da : da + 3] = np.mean(np.diag(Minv)[da : da + 3])
       m.dof_invweight0[da + 3 : da + 6] = np.mean(np.diag(Minv)[da + 3 : da + 6])
+    elif m.jnt_type[j] == 1:  # ball: the mean over its three dofs (mj_setConst)
+      m.dof_invweight0[da : da + 3] = np.mean(np.diag(Minv)[da : da + 3])
     else:
       m.dof_invweight0[da] = Minv[da, da]
   for b in range(1, m.nbody):

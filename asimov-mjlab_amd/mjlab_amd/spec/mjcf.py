@@ -427,7 +427,7 @@ def model_to_mjcf(m) -> str:
           continue
         d = int(m.jnt_dofadr[j])
         lim = "true" if int(m.jnt_limited[j]) else "false"
-        out.append(f'{ind}  <joint name="{names["joint"][j]}" type="{ {2: "slide", 3: "hinge"}[t] }" pos="{_fmt(m.jnt_pos[j])}" '
+        out.append(f'{ind}  <joint name="{names["joint"][j]}" type="{ {1: "ball", 2: "slide", 3: "hinge"}[t] }" pos="{_fmt(m.jnt_pos[j])}" '
                    f'axis="{_fmt(m.jnt_axis[j])}" limited="{lim}" range="{_fmt(m.jnt_range[j])}" '
                    f'ref="{float(m.qpos0[int(m.jnt_qposadr[j])]):.9g}" springref="{float(m.qpos_spring[int(m.jnt_qposadr[j])]):.9g}" '
                    f'stiffness="{float(m.jnt_stiffness[j]):.9g}" armature="{float(m.dof_armature[d]):.9g}" '

@@ -21,6 +21,7 @@
 #endif
 
 #define MINVAL 1e-15
+#define PI 3.14159265358979323846
 #define MINIMP 0.0001
 #define MAXIMP 0.9999
 
@@ -90,6 +91,23 @@ static void axis_angle(real q[4], const real axis[3], real ang) {
   q[0] = cos(ang * 0.5); q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
 }
 /* spatial motion cross product  res = v x m  (v, m: [ang; lin]) */
+/* the rotation vector (axis x angle, angle in (-pi, pi]) of a quaternion (MuJoCo mju_quat2Vel, dt = 1) */
+static real quat2vel(real r[3], const real q[4]) {
+  real ax[3] = {q[1], q[2], q[3]};
+  const real s = normalize3(ax);
+  real ang = 2 * atan2(s, q[0]);
+  if (ang > PI) ang -= 2 * PI;
+  for (int k = 0; k < 3; k++) r[k] = ax[k] * ang;
+  return ang;
+}
+/* r such that qa = qb * exp(r) (MuJoCo mju_subQuat) */
+static void sub_quat(real r[3], const real qa[4], const real qb[4]) {
+  const real qbc[4] = {qb[0], -qb[1], -qb[2], -qb[3]};
+  real d[4];
+  mul_quat(d, qbc, qa);
+  quat2vel(r, d);
+}
+
 static void cross_motion(real r[6], const real v[6], const real m[6]) {
   real t[6];
   t[0] = -v[2] * m[1] + v[1] * m[2];
@@ -260,6 +278,12 @@ static void kinematics(const or_model* m, const or_data* d, int wi, ws_t* w) {
         mul_quat(xq, xq, ql);
         rot_quat(v, m->jnt_pos + 3 * j, xq);
         for (int k = 0; k < 3; k++) xp[k] = anc[k] - v[k];
+      } else if (m->jnt_type[j] == 1) { /* ball: the normalised qpos quaternion, about the anchor */
+        real ql[4] = {w->qpos[qa], w->qpos[qa + 1], w->qpos[qa + 2], w->qpos[qa + 3]}, v[3];
+        normalize4(ql);
+        mul_quat(xq, xq, ql);
+        rot_quat(v, m->jnt_pos + 3 * j, xq);
+        for (int k = 0; k < 3; k++) xp[k] = anc[k] - v[k];
       }
     }
     normalize4(xq);
@@ -358,6 +382,14 @@ static void com_pos(const or_model* m, int wi, ws_t* w) {
           cross3(cd + 3, ax, off);
         }
         break;
+      case 1: /* ball: rotations about the body's axes (mj_comPos) */
+        for (int k = 0; k < 3; k++) {
+          real* cd = w->cdof + 6 * (da + k);
+          real ax[3] = {w->xmat[9 * b + k], w->xmat[9 * b + 3 + k], w->xmat[9 * b + 6 + k]};
+          memcpy(cd, ax, 3 * sizeof(real));
+          cross3(cd + 3, ax, off);
+        }
+        break;
       case 2: {
         real* cd = w->cdof + 6 * da;
         memset(cd, 0, 3 * sizeof(real));
@@ -435,6 +467,10 @@ static void com_vel(const or_model* m, ws_t* w) {
         for (int k = 3; k < 6; k++) cross_motion(w->cdof_dot + 6 * (da + k), cv, w->cdof + 6 * (da + k));
         for (int k = 3; k < 6; k++)
           for (int c = 0; c < 6; c++) cv[c] += w->cdof[6 * (da + k) + c] * w->qvel[da + k];
+      } else if (m->jnt_type[j] == 1) { /* ball: all three from the parent's velocity (mj_comVel) */
+        for (int k = 0; k < 3; k++) cross_motion(w->cdof_dot + 6 * (da + k), cv, w->cdof + 6 * (da + k));
+        for (int k = 0; k < 3; k++)
+          for (int c = 0; c < 6; c++) cv[c] += w->cdof[6 * (da + k) + c] * w->qvel[da + k];
       } else {
         cross_motion(w->cdof_dot + 6 * da, cv, w->cdof + 6 * da);
         for (int c = 0; c < 6; c++) cv[c] += w->cdof[6 * da + c] * w->qvel[da];
@@ -511,6 +547,10 @@ static void passive_actuation(const or_model* m, int wi, ws_t* w, const real* ct
     if ((t == 2 || t == 3) && stiff[j] != 0) {
       int qa = m->jnt_qposadr[j];
       w->qfrc_passive[m->jnt_dofadr[j]] -= stiff[j] * (w->qpos[qa] - m->qpos_spring[qa]);
+    } else if (t == 1 && stiff[j] != 0) { /* ball: the rotation vector from the spring pose (mju_subQuat) */
+      real dif[3];
+      sub_quat(dif, w->qpos + m->jnt_qposadr[j], m->qpos_spring + m->jnt_qposadr[j]);
+      for (int k = 0; k < 3; k++) w->qfrc_passive[m->jnt_dofadr[j] + k] -= stiff[j] * dif[k];
     }
   }
   for (int d = 0; d < nv; d++) w->qfrc_passive[d] -= damping[d] * w->qvel[d];
@@ -1239,6 +1279,29 @@ static void make_constraint(const or_model* m, int wi, ws_t* w) {
   /* joint limits */
   for (int j = 0; j < m->njnt; j++) {
     int t = m->jnt_type[j];
+    if (m->jnt_limited[j] && t == 1) {
+      /* ball: the rotation angle against the larger range bound, J = -(rotation axis)
+         on the joint's three dofs (mj_instantiateLimit) */
+      real ax[3];
+      const real ang = fabs(quat2vel(ax, w->qpos + m->jnt_qposadr[j]));
+      normalize3(ax);
+      const real amax = rng[2 * j] > rng[2 * j + 1] ? rng[2 * j] : rng[2 * j + 1];
+      const real pos = amax - ang - m->jnt_margin[j];
+      if (pos >= 0) continue;
+      int r = new_row(m, w);
+      if (r < 0) return;
+      const int d = m->jnt_dofadr[j];
+      real jv = 0;
+      for (int k = 0; k < 3; k++) {
+        w->J[r * nv + d + k] = -ax[k];
+        jv -= ax[k] * w->qvel[d + k];
+      }
+      w->efc_type[r] = 3;
+      w->efc_id[r] = j;
+      efc_row_params(m, w, r, pos, pos, m->dof_invweight0[d], m->jnt_solref + 2 * j, m->jnt_solimp + 5 * j,
+                     m->jnt_margin[j], jv);
+      continue;
+    }
     if (!m->jnt_limited[j] || (t != 2 && t != 3)) continue;
     real q = w->qpos[m->jnt_qposadr[j]];
     real dlo = q - rng[2 * j], dhi = rng[2 * j + 1] - q;
@@ -2231,6 +2294,14 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
         for (int k = 0; k < 3; k++) w->qpos[q0 + k] += dt * w->qvel[v0 + k];
         real* q = w->qpos + q0 + 3;
         real om[3] = {w->qvel[v0 + 3], w->qvel[v0 + 4], w->qvel[v0 + 5]};
+        real ang = dt * normalize3(om), qr[4];
+        axis_angle(qr, om, ang);
+        normalize4(q);
+        mul_quat(q, q, qr);
+        normalize4(q);
+      } else if (m->jnt_type[j] == 1) { /* ball: mju_quatIntegrate */
+        real* q = w->qpos + q0;
+        real om[3] = {w->qvel[v0], w->qvel[v0 + 1], w->qvel[v0 + 2]};
         real ang = dt * normalize3(om), qr[4];
         axis_angle(qr, om, ang);
         normalize4(q);

@@ -643,6 +643,57 @@ def test_convex_pairs_parity():
   print("[convex pairs] contact kinds", sorted(kinds), "int rate", rep["int_match_rate"])
 
 
+BALL_SCENE = """<mujoco><compiler angle="radian"/><option timestep="0.002"/><worldbody>
+<geom name="floor" type="plane" size="5 5 0.1"/>
+<body name="torso" pos="0 0 0.4"><freejoint/><geom type="box" size="0.12 0.08 0.05" mass="3"/>
+  <body name="arm" pos="0.12 0 0"><joint name="shoulder" type="ball" range="0 1.0" limited="true" damping="0.05" stiffness="2"/>
+    <geom type="capsule" fromto="0 0 0 0.2 0 -0.05" size="0.03" mass="0.5"/>
+    <body name="fore" pos="0.2 0 -0.05"><joint name="elbow" type="hinge" axis="0 1 0" range="-1.5 1.5" limited="true"/>
+      <geom type="capsule" fromto="0 0 0 0.15 0 0" size="0.025" mass="0.3"/></body></body>
+  <body name="leg" pos="-0.12 0 -0.05"><joint name="hip" type="ball" damping="0.1"/>
+    <geom type="capsule" fromto="0 0 0 0 0 -0.25" size="0.035" mass="0.8"/></body>
+</body></worldbody></mujoco>"""
+
+
+def test_ball_joint_parity():
+  """Ball joints on the HIP step against the oracle: a free torso with a
+  limited, damped, sprung ball shoulder (a hinge elbow below it) and a free
+  ball hip, random poses touching the floor, one step (kinematics, the
+  three-dof cdof, cdof_dot from the parent velocity, the mju_subQuat spring,
+  the cone-limit row, mju_quatIntegrate); tests/scenes.py tolerances. The ball
+  joint itself is pinned by tests/test_ball_joint.py's closed forms."""
+  from mjlab_amd.spec.compiler import compile_spec
+  from mjlab_amd.spec.mjcf import read_mjcf_string
+  from mjlab_amd.utils import rot
+
+  n = 512
+  m = compile_spec(read_mjcf_string(BALL_SCENE), 50, 300)
+  assert list(m.jnt_type) == [0, 1, 3, 1] and m.nq == 7 + 4 + 1 + 4 and m.nv == 6 + 3 + 1 + 3
+  rng = np.random.default_rng(59)
+  q = np.zeros((n, m.nq))
+  q[:, :3] = rng.uniform([-0.2, -0.2, 0.1], [0.2, 0.2, 0.25], (n, 3))
+  for a in (3, 7, 12):
+    quat = rng.normal(size=(n, 4))
+    q[:, a : a + 4] = quat / np.linalg.norm(quat, axis=1, keepdims=True)
+  # the shoulder within 1.3 rad of its rest pose (its cone limit is 1.0 rad)
+  ax = rng.normal(size=(n, 3))
+  ang = rng.uniform(0, 1.3, n)
+  q[:, 7:11] = np.stack([rot.axis_angle_to_quat(ax[i] / np.linalg.norm(ax[i]), ang[i]) for i in range(n)])
+  q[:, 11] = rng.uniform(-1.6, 1.6, n)
+  st = {"qpos": q, "qvel": rng.normal(scale=0.5, size=(n, m.nv)), "qacc_warmstart": np.zeros((n, m.nv))}
+  sim = Simulation(n, SimulationCfg(nconmax=50, njmax=300, mujoco=MujocoCfg(timestep=0.002, iterations=20,
+                                                                               ls_iterations=20)), m, DEV)
+  put(sim, st)
+  sim.step()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=True, follow=got)
+  rep = assert_parity(got, ref, n, min_int_rate=0.95, tag=" ball joints")
+  lim = [(w, r) for w in range(n) for r in range(int(got["nefc"][w, 0])) if got["efc_type"][w, r] == 3]
+  assert len(lim) > 20  # shoulder / elbow limit rows were exercised
+  assert (got["ncon"] > 0).mean() > 0.5
+  print("[ball joints] limit rows", len(lim), "int rate", rep["int_match_rate"])
+
+
 @pytest.mark.parametrize("iterations", [1, 5])
 def test_pgs_solver_parity(iterations):
   """opt.solver = PGS (MuJoCo's projected Gauss-Seidel on the dual; the
