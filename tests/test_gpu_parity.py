@@ -135,14 +135,17 @@ def test_gated_forward():
 
 
 def test_overflow_is_flagged_not_fatal():
+  """Contacts beyond a world's slots (max(nconmax, njmax) = 16 here) are dropped
+  and flagged; the step stays finite."""
   n = 16
-  m = g1_scene_model(n, nconmax=4, njmax=300)
-  sim = Simulation(n, SimulationCfg(**dict(CFG, nconmax=4)), m, DEV)
+  m = g1_scene_model(n, nconmax=4, njmax=16)
+  sim = Simulation(n, SimulationCfg(**dict(CFG, nconmax=4, njmax=16)), m, DEV)
+  assert m.nconmax == 16 and m.ncon_share == 4
   st = random_states(m, n, np.random.default_rng(6), drop=0.06)
   put(sim, st)
   sim.step()
   got = get(sim, n)
-  assert (got["ncon"] <= 4).all()
+  assert (got["ncon"] <= 16).all()
   assert ((got["flags"] & 1) != 0).any()
   assert np.isfinite(got["qvel"]).all()
   # surfaced without a sync: sticky flags (OR over launches) counted and
@@ -158,6 +161,29 @@ def test_overflow_is_flagged_not_fatal():
   assert int(sim.data.flags_acc.abs().sum()) == 0
   st = sim.flag_stats().cpu().numpy()
   assert st[0] == 0 and st[3] == n_or  # running total kept
+
+
+def test_pooled_contacts_one_world_exceeds_nconmax():
+  """SimulationCfg.nconmax sizes a pool shared by the worlds, as the
+  reference's ("one world may have more than nconmax contacts",
+  /root/reference/src/mjlab/sim/sim.py:81-85): with nconmax 2 over 8 worlds a
+  world keeps up to min(max(2, njmax), 2 x 8) = 16 contacts, so the G1 worlds
+  lying on the floor keep all of theirs (as an uncapped float64 oracle run
+  finds them) while the airborne ones hold none, and nothing is flagged."""
+  n = 8
+  m = g1_scene_model(n, nconmax=2, njmax=300)
+  st = random_states(m, n, np.random.default_rng(6), drop=0.06)
+  full = Oracle(g1_scene_model(n, nconmax=64, njmax=300)).run(n, st, integrate=False)["ncon"][:, 0]
+  sim = Simulation(n, SimulationCfg(**dict(CFG, nconmax=2)), m, DEV)
+  assert m.nconmax == 16 and m.ncon_share == 2
+  put(sim, st)
+  sim.forward()
+  got = get(sim, n)
+  keep = np.minimum(full, 16)
+  np.testing.assert_array_equal(got["ncon"][:, 0], keep)
+  assert (keep > 2).sum() >= 3 and (keep <= 2).any()  # some worlds above their share, some below
+  sel = full <= 16
+  assert ((got["flags"][sel, 0] & 1) == 0).all()
 
 
 def test_full_size_determinism_and_world_independence():
