@@ -460,7 +460,10 @@ CVX_ENTRY int cvx_collide(int t1, const cvx_real* p1, const cvx_real* m1, const 
     }
   }
   cvx_face f[CVX_NF];
-  for (int i = 0; i < CVX_NF; i++) f[i].v[0] = -1;
+  for (int i = 0; i < CVX_NF; i++) {
+    f[i].v[0] = -1;
+    f[i].adj[0] = f[i].adj[1] = f[i].adj[2] = 0; /* every link stays a valid face index */
+  }
   {
     const int tri[4][3] = {{0, 1, 2}, {0, 3, 1}, {0, 2, 3}, {1, 3, 2}};
     for (int i = 0; i < 4; i++)
@@ -496,6 +499,10 @@ CVX_ENTRY int cvx_collide(int t1, const cvx_real* p1, const cvx_real* m1, const 
       const int fi = stack[--sp];
       for (int q = 0; q < 3 && ok; q++) {
         const int nb = f[fi].adj[q];
+        if (nb < 0 || nb >= CVX_NF || f[nb].v[0] < 0) { /* a dangling link: the polytope is torn */
+          ok = 0;
+          break;
+        }
         if (state[nb] == 0) {
           if (cvx_dot(f[nb].n, w.w) - f[nb].d > 0) {
             state[nb] = 1;
@@ -528,6 +535,7 @@ CVX_ENTRY int cvx_collide(int t1, const cvx_real* p1, const cvx_real* m1, const 
       if (!cvx_face_make(&f[slot], v, he[t][0], he[t][1], nv)) ok = 0; /* degenerate: torn */
       const int nb = he[t][2];
       f[slot].adj[0] = (signed char)nb;
+      f[slot].adj[1] = f[slot].adj[2] = -1; /* linked below; -1 if the horizon is not a simple loop */
       for (int r = 0; r < 3; r++)
         if (f[nb].v[r] == he[t][1] && f[nb].v[(r + 1) % 3] == he[t][0]) f[nb].adj[r] = (signed char)slot;
     }
@@ -538,7 +546,10 @@ CVX_ENTRY int cvx_collide(int t1, const cvx_real* p1, const cvx_real* m1, const 
           f[nf[t]].adj[1] = nf[u2];
           f[nf[u2]].adj[2] = nf[t];
         }
+    for (int t = 0; t < ne; t++)
+      if (f[nf[t]].adj[1] < 0 || f[nf[t]].adj[2] < 0) ok = 0;
     nv++;
+    if (!ok) break; /* a pinched horizon: keep the nearest face of the last closed polytope */
   }
 
   /* the origin's projection onto the nearest face, in barycentric coordinates */
