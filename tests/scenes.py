@@ -426,6 +426,7 @@ def check_iteration_counts(got: dict, model, state: dict, integrate: bool, nthre
 
 
 F32_SENSITIVITY = 4.0
+CONTACT_TOL = {"contact_dist": 5e-5, "contact_pos": 5e-5, "contact_frame": 1e-3}
 LS_NOISE_K = 4.0
 LS_TIE = 0.05
 LS_TIE_FRAC = 0.01
@@ -554,14 +555,26 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
   for k in SMOOTH:
     check_rel(k, 1e-4, sel)
   # contact geometry, aligned by geom pair, on every world
+  # Each difference is measured against max(tol, F32_SENSITIVITY x the float32
+  # oracle's own deviation at that contact): a contact whose placement is
+  # ill-conditioned (a nearly flat contact of the general convex collider,
+  # whose witness point may sit anywhere on the patch) moves as much under the
+  # oracle's own float32 rounding (same algorithm and choices), as for the
+  # other outputs' floors below.
+  f32 = ref.get("f32")
   cd, cp, cf = [0.0], [0.0], [0.0]
   for w in sel:
+    f32_ok = f32 is not None and "contact_pos" in f32 and int(f32["ncon"][w, 0]) == int(ref["ncon"][w, 0])
     for i, j in align_contacts(got, ref, int(w))[0]:
-      cd.append(abs(float(got["contact_dist"][w, i] - ref["contact_dist"][w, j])))
-      cp.append(float(np.abs(got["contact_pos"][w, 3 * i : 3 * i + 3] - ref["contact_pos"][w, 3 * j : 3 * j + 3]).max()))
-      # the normal is determined; the tangent basis follows it (make_frame)
-      cf.append(float(np.abs(got["contact_frame"][w, 9 * i : 9 * i + 9] - ref["contact_frame"][w, 9 * j : 9 * j + 9]).max()))
-  for name, v, tol in (("contact_dist", cd, 5e-5), ("contact_pos", cp, 5e-5), ("contact_frame", cf, 1e-3)):
+      for name, out, k in (("contact_dist", cd, 1), ("contact_pos", cp, 3), ("contact_frame", cf, 9)):
+        # the normal is determined; the tangent basis follows it (make_frame)
+        d = float(np.abs(got[name][w, k * i : k * i + k] - ref[name][w, k * j : k * j + k]).max())
+        if f32_ok:
+          fl = F32_SENSITIVITY * float(np.abs(f32[name][w, k * j : k * j + k] - ref[name][w, k * j : k * j + k]).max())
+          d = d * min(1.0, CONTACT_TOL[name] / fl) if fl > CONTACT_TOL[name] else d
+        out.append(d)
+  for name, v in (("contact_dist", cd), ("contact_pos", cp), ("contact_frame", cf)):
+    tol = CONTACT_TOL[name]
     maxerr[name] = max(v)
     if max(v) > tol:
       failures.append(f"{name}: max|d|={max(v):.3e} > {tol:.3e}")
