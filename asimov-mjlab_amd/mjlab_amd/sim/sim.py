@@ -212,12 +212,15 @@ class Simulation:
     # Contacts: the reference's nconmax sizes a pool shared by all worlds ("one
     # world may have more than nconmax contacts", sim.py:81-85; MuJoCo Warp
     # allocates nconmax x nworld). Each world here gets max(nconmax, njmax)
-    # slots, at most the whole pool: a world keeps more than nconmax contacts
-    # while others hold fewer (beyond njmax its rows overflow anyway). The
-    # pool's total is not enforced across worlds.
+    # slots: a world keeps more than nconmax contacts while others hold fewer
+    # (beyond njmax its rows overflow anyway). The slot count does not depend
+    # on the world count, so the model-specialised kernels' plans hold for any
+    # num_envs; the pool's total is not enforced across worlds.
     share = int(cfg.nconmax) if cfg.nconmax is not None else int(getattr(model, "ncon_share", model.nconmax))
     model.ncon_share = share
-    model.nconmax = min(max(share, int(model.njmax)), share * max(1, int(num_envs)))
+    model.nconmax = max(share, int(model.njmax))
+    if cfg.contact_sensor_maxmatch > 64:  # keep the exact-match guarantee below: at most 64 slots
+      model.nconmax = max(share, min(model.nconmax, 64))
     # the kernel keeps one wave lane per contact-sensor match (64): a cap above 64
     # is honoured exactly when no world can hold more than 64 contacts, since a
     # sensor never matches more contacts than the world has

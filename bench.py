@@ -49,6 +49,7 @@ Rank 0 prints ONE JSON line with, in addition to the contract fields:
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import socket
@@ -56,6 +57,13 @@ import subprocess
 import sys
 import time
 from pathlib import Path
+
+
+def _native():
+  from mjlab_amd.sim import native
+
+  return native.lib()
+
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "asimov-mjlab_amd"))
@@ -492,6 +500,9 @@ def main(env_hook=None) -> None:
         "efc_capacity": sim.efc_capacity(),
         "njmax": int(sim.mj_model.njmax),
         "nconmax": int(sim.mj_model.nconmax),
+        "nconmax_share": int(getattr(sim.mj_model, "ncon_share", sim.mj_model.nconmax)),
+        # the step kernel instance: >= 0 a model-specialised one (csrc/mjh_spec_table.h), -1 the generic
+        "spec_instance": int(_native().mjh_spec_index(ctypes.addressof(sim._mstruct))),
         "contact_overflow_worlds": int(flags[0]),
         "efc_overflow_worlds": int(flags[1]),
         "nonfinite_worlds": int(flags[2]),
