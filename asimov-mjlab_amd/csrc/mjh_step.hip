@@ -3882,12 +3882,17 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
 #pragma unroll
       for (int k = 0; k < 3; k++) { DP(xanchor)[3 * o + k] = vj[k]; DP(xaxis)[3 * o + k] = vj[3 + k]; }
     }
+    // sites: compact (nworld, nsite), or inside a wider per-world array after
+    // site_off static sites (mjh_data.site_wstride; the host wrote those once)
+    float* const o_sxpos = d.site_wstride ? d.site_xpos : DP(site_xpos);
+    float* const o_sxmat = d.site_wstride ? d.site_xmat : DP(site_xmat);
+    const long long s_row = d.site_wstride ? (long long)W * d.site_wstride + d.site_off : (long long)W * Z.nsite;
     for (int st = tid; sl; st += NT) {  // sites beyond the first 64: one more round each
-      const long long o = (long long)W * Z.nsite + st;
+      const long long o = s_row + st;
 #pragma unroll
-      for (int k = 0; k < 3; k++) DP(site_xpos)[3 * o + k] = vs[k];
+      for (int k = 0; k < 3; k++) o_sxpos[3 * o + k] = vs[k];
 #pragma unroll
-      for (int k = 0; k < 9; k++) DP(site_xmat)[9 * o + k] = vs[3 + k];
+      for (int k = 0; k < 9; k++) o_sxmat[9 * o + k] = vs[3 + k];
       if (st + NT >= Z.nsite) break;
 #pragma unroll
       for (int k = 0; k < 3; k++) vs[k] = sxpos[3 * (st + NT) + k];
@@ -4328,7 +4333,11 @@ bool data_is_slab(const mjh_model* m, const mjh_data* d) {
   const DataOff o = data_offsets(z);
   const char* base = reinterpret_cast<const char*>(d->qpos);
   bool ok = true;
-#define X_SL(type, name, count) ok = ok && reinterpret_cast<const char*>(d->name) == base + 4ll * o.name * d->nworld;
+  // site outputs in a wider array (site_wstride) are addressed through their pointers
+  const bool wide = d->site_wstride != 0;
+#define X_SL(type, name, count)                                                                  \
+  ok = ok && ((wide && (std::strcmp(#name, "site_xpos") == 0 || std::strcmp(#name, "site_xmat") == 0)) || \
+              reinterpret_cast<const char*>(d->name) == base + 4ll * o.name * d->nworld);
   MJH_DATA_ARRAYS(X_SL)
 #undef X_SL
   return ok;

@@ -7,11 +7,12 @@ Restates ``src/mjlab/scene/scene.py`` and the plane path of
   (``terrain_importer.py:154-163``), added before the entities so that body 1
   is ``terrain`` and geom 0 is the plane, as in the reference;
 * env origins follow the reference grid (``terrain_importer.py:225-240``);
-* the reference also adds one visual site per env origin to the *shared*
-  model (``terrain_importer.py:89-120``), which makes ``nsite = 6 + num_envs``
-  and its per-world site arrays O(num_envs^2). Those sites are group-4 visuals
-  never read by any MDP term; they are kept as ``env_origins`` only and not
-  compiled into the physics model ("Deliberate deviations").
+* one visual site per env origin, ``env_origin_{i}``, on the world body
+  (``terrain_importer.py:95-120``), so ``nsite = num_envs + (robot sites)``
+  and the robot's site ids start at num_envs, as in the reference model. The
+  compiled model records them as ``Model.nsite_origin``: static world sites
+  whose poses the Simulation writes once, so the step kernel sees only the
+  sites that move.
 """
 
 from __future__ import annotations
@@ -26,7 +27,7 @@ from mjlab_amd.entity import Entity, EntityCfg
 from mjlab_amd.entity.entity import merge_keyframes
 from mjlab_amd.sensor import BuiltinSensor, SensorCfg
 from mjlab_amd.spec.compiler import Model, compile_spec
-from mjlab_amd.spec.spec import BodySpec, GeomSpec, Spec
+from mjlab_amd.spec.spec import BodySpec, GeomSpec, SiteSpec, Spec
 
 
 @dataclass
@@ -50,6 +51,13 @@ class TerrainImporter:
     self.spec.worldbody.children.append(body)
     self.terrain_origins = None
     self.env_origins = self._grid(cfg.num_envs, cfg.env_spacing)
+    self._add_env_origin_sites()
+
+  def _add_env_origin_sites(self) -> None:
+    """terrain_importer.py:95-120: a transparent sphere site per env origin."""
+    for i, o in enumerate(self.env_origins.cpu().numpy()):
+      self.spec.worldbody.sites.append(SiteSpec(name=f"env_origin_{i}", type="sphere", pos=[float(x) for x in o],
+                                                size=[0.3, 0.3, 0.3], group=4, rgba=[0.2, 0.6, 0.2, 0.3]))
 
   def _grid(self, num_envs: int, spacing: float) -> torch.Tensor:
     origins = torch.zeros(num_envs, 3, device=self.device)
@@ -92,6 +100,11 @@ class Scene:
   def compile(self, nconmax: int | None = None, njmax: int | None = None) -> Model:
     m = compile_spec(self._spec, nconmax or 0, njmax or 0)
     merge_keyframes(m, self._entities.values())
+    # the env-origin sites lead the site list (the terrain's world sites are attached first)
+    n0 = self._cfg.num_envs if self._terrain is not None else 0
+    names = m.names["site"][:n0]
+    assert all(nm == f"env_origin_{i}" for i, nm in enumerate(names)) and (m.site_bodyid[:n0] == 0).all()
+    m.nsite_origin = n0
     return m
 
   @property

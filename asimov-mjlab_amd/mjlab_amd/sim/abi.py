@@ -92,6 +92,8 @@ def data_struct(real=ctypes.c_float, device: bool = True):
     # optional fused contact-sensor timers (mjh_data.at_*)
     members += [(f"at_{n}", ctypes.c_void_p) for n in ("last_time", "cur_air", "last_air", "cur_con", "last_con")]
     members += [("at_k", ctypes.c_int), ("at_cols", ctypes.c_int * 7)]
+    # optional site-output layout inside a wider per-world site array (env-origin sites)
+    members += [("site_wstride", ctypes.c_longlong), ("site_off", ctypes.c_int), ("_pad_site", ctypes.c_int)]
   return type("mjh_data" if device else "or_data", (ctypes.Structure,), {"_fields_": members})
 
 

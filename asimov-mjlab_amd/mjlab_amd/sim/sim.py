@@ -232,6 +232,17 @@ class Simulation:
     model.contact_sensor_maxmatch = cfg.contact_sensor_maxmatch
     model.ls_parallel = int(bool(cfg.ls_parallel))  # wp_model.opt.ls_parallel (sim.py:117)
     self.sizes = abi.model_sizes(model)
+    # A scene's env-origin sites (Model.nsite_origin, the leading world sites) are
+    # static: the kernel's model view starts after them (ksizes, offset site
+    # pointers, shifted sensor site ids) and writes its sites into the wide
+    # site_xpos / site_xmat rows after the static block written here once.
+    self._nsite0 = int(getattr(model, "nsite_origin", 0))
+    self.ksizes = dict(self.sizes, nsite=self.sizes["nsite"] - self._nsite0)
+    if self._nsite0:
+      site_obj = 6  # mjOBJ_SITE
+      for t, i in ((model.sensor_objtype, model.sensor_objid), (model.sensor_reftype, model.sensor_refid)):
+        if ((np.asarray(t) == site_obj) & (np.asarray(i) < self._nsite0)).any():
+          raise NotImplementedError("a sensor references an env-origin site (static, not simulated per world)")
 
     # ---- model buffers (torch-owned) ----
     host = abi.model_host_arrays(model)
@@ -250,7 +261,7 @@ class Simulation:
     # header order: specialised kernel instances derive every data pointer
     # from qpos with compile-time offsets (mjh_data_is_slab)
     self._data_flat: dict[str, torch.Tensor] = {}
-    counts = [(f, max(1, abi.count(f, self.sizes))) for f in abi.data_array_fields()]
+    counts = [(f, max(1, abi.count(f, self.ksizes))) for f in abi.data_array_fields()]
     self._slab = torch.zeros(num_envs * sum(c for _, c in counts), dtype=torch.float32, device=device)
     off = 0
     for f, c in counts:
@@ -262,6 +273,21 @@ class Simulation:
       mb = np.argsort(np.where(model.body_mocapid >= 0, model.body_mocapid, np.iinfo(np.int32).max))[: int(model.nmocap)]
       self._data_flat["mocap_pos"][:] = torch.as_tensor(np.asarray(model.body_pos)[mb].reshape(-1), dtype=torch.float32)
       self._data_flat["mocap_quat"][:] = torch.as_tensor(np.asarray(model.body_quat)[mb].reshape(-1), dtype=torch.float32)
+    if self._nsite0:
+      # the wide site outputs: (num_envs, nsite) with the static env-origin block
+      # (world body at the origin: xpos = site_pos, xmat = R(site_quat))
+      n0, ns = self._nsite0, self.sizes["nsite"]
+      sp = torch.as_tensor(np.asarray(model.site_pos)[:n0], dtype=torch.float32)
+      sq = np.asarray(model.site_quat)[:n0]
+      from mjlab_amd.utils import rot
+
+      sm = torch.as_tensor(np.stack([rot.quat_to_mat(q).reshape(-1) for q in sq]) if n0 else np.zeros((0, 9)),
+                           dtype=torch.float32)
+      xp = torch.zeros(num_envs, ns * 3, dtype=torch.float32, device=device)
+      xm = torch.zeros(num_envs, ns * 9, dtype=torch.float32, device=device)
+      xp[:, : n0 * 3] = sp.reshape(1, -1).to(device)
+      xm[:, : n0 * 9] = sm.reshape(1, -1).to(device)
+      self._data_flat["site_xpos"], self._data_flat["site_xmat"] = xp, xm
     data_views = {n: self._data_view(n) for n in self._data_flat}
     self.epoch = Epoch()
     self._data_bridge = Bridge(data_views, extra={"epoch": self.epoch}, nworld=num_envs)
@@ -301,12 +327,24 @@ class Simulation:
     MS = abi.model_struct()
     DS = abi.data_struct()
     ms = MS()
-    for k, v in self.sizes.items():
+    for k, v in self.ksizes.items():
       setattr(ms, k, v)
     for k, v in abi.model_options(self._mj_model).items():
       setattr(ms, k, v)
+    n0 = self._nsite0
+    # the kernel's site arrays start after the static env-origin sites
+    site_skip = {"site_bodyid": n0, "site_pos": 3 * n0, "site_quat": 4 * n0}
+    if n0 and not hasattr(self, "_ksensor"):
+      ids = {}
+      for tn, idn in (("sensor_objtype", "sensor_objid"), ("sensor_reftype", "sensor_refid")):
+        t, i = self._model_flat[tn], self._model_flat[idn]
+        ids[idn] = torch.where(t == 6, i - n0, i).contiguous()
+      self._ksensor = ids
     for name, t in self._model_flat.items():
-      setattr(ms, name, t.data_ptr())
+      ptr = t.data_ptr() + site_skip.get(name, 0) * t.element_size()
+      if n0 and name in ("sensor_objid", "sensor_refid"):
+        ptr = self._ksensor[name].data_ptr()
+      setattr(ms, name, ptr)
       if name in self._wstride:
         setattr(ms, name + "_wstride", self._wstride[name])
     # packed model image scratch (staged into LDS by every launch)
@@ -333,6 +371,9 @@ class Simulation:
     ds.world_order = self._order.data_ptr() if self.cfg.balance_worlds else None
     for name, t in self._data_flat.items():
       setattr(ds, name, t.data_ptr())
+    if n0:  # wide site outputs: world w's kernel site s at w * nsite + n0 + s
+      ds.site_wstride = self.sizes["nsite"]
+      ds.site_off = n0
     self._mstruct, self._dstruct = ms, ds
     # the same descriptor with the fused contact-sensor timers (attach_air_time)
     self._dstruct_at = None

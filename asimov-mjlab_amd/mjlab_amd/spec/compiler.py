@@ -94,6 +94,10 @@ class Model:
   (``src/mjlab/entity/entity.py:621-624``, ``contact_sensor.py:210-214``).
   """
 
+  # leading static world sites (a Scene's env-origin sites): the Simulation
+  # writes their poses once and the step kernel sees only the sites after them
+  nsite_origin = 0
+
   def __init__(self) -> None:
     self.names: dict[str, list[str]] = {}
 

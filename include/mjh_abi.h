@@ -34,7 +34,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 13
+#define MJH_ABI_VERSION 14
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -105,6 +105,16 @@ typedef struct mjh_data {
   float* at_last_con;
   int at_k;
   int at_cols[7];
+  /* optional site-output layout (site_wstride 0: compact, (nworld, nsite)):
+     world w's site s goes to element w * site_wstride + site_off + s of
+     site_xpos / site_xmat (counted in sites), so the outputs can sit inside a
+     wider per-world site array whose first site_off sites are static and
+     written once by the caller (a scene's env-origin sites; mjlab's
+     terrain_importer.py:95-120 puts one per env on the world body). The
+     model then describes only the sites after them. */
+  long long site_wstride;
+  int site_off;
+  int _pad_site;
 } mjh_data;
 
 /* Version of this ABI (MJH_ABI_VERSION). */

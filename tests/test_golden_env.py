@@ -115,7 +115,10 @@ def run_golden(task: str, device: str, tmp_path) -> None:
       env.action_manager.apply_action()
       _close(env.sim.data.ctrl, f("ctrl"), f"f{t} ctrl", atol=1e-6)
       for name in SIM_FIELDS:
-        getattr(env.sim.data, name).copy_(T(f("sim_" + name)).view_as(getattr(env.sim.data, name)))
+        dst = getattr(env.sim.data, name)
+        if name.startswith("site_"):  # the fixture holds the robot's sites; ours follow the env-origin sites
+          dst = dst[:, env.sim.mj_model.nsite_origin:]
+        dst.copy_(T(f("sim_" + name)).view_as(dst))
       env.sim.epoch.bump()
       if t == 0 and cname == "motion":  # relative targets of the initial phase (generator did the same)
         cmd._update_command()

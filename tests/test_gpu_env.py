@@ -245,3 +245,29 @@ def test_batched_reward_pass_equals_separate_launches():
       assert torch.equal(torch.as_tensor(v), torch.as_tensor(xs["log"][key])), f"step {k}: log {key}"
     for f in _STATE:
       assert torch.equal(getattr(eb.sim.data, f), getattr(es.sim.data, f)), f"step {k}: sim.data.{f}"
+
+
+def test_env_origin_sites_static_and_robot_sites_at_reference_ids():
+  """The reference's env-origin sites (terrain_importer.py:95-120) occupy site
+  ids 0..num_envs-1 of every world and never move; the robot's sites sit at
+  num_envs + k and are the ones the kernel writes (mjh_data.site_wstride /
+  site_off): after captured env steps the origin block still equals
+  scene.env_origins and the robot's feet sites lie at the feet."""
+  n = 16
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = n
+  env = ManagerBasedRlEnv(cfg, device="cuda:0")
+  env.reset()
+  for _ in range(3):
+    env.step(torch.zeros(n, env.action_manager.total_action_dim, device="cuda:0"))
+  torch.cuda.synchronize()
+  sx = env.sim.data.site_xpos
+  origins = env.scene.env_origins
+  assert tuple(sx.shape) == (n, n + 6, 3)
+  assert torch.equal(sx[:, :n], origins.unsqueeze(0).expand(n, n, 3))
+  robot = env.scene["robot"]
+  ids = robot.indexing.site_ids
+  assert ids.tolist() == list(range(n, n + 6))
+  torch.testing.assert_close(robot.data.site_pose_w[..., :3], sx[:, ids])
+  feet = [env.sim.mj_model.names["site"].index(f"robot/{s}") for s in ("left_foot", "right_foot")]
+  assert (sx[:, feet, 2] < 0.2).all() and (sx[:, feet, 2] > -0.05).all()  # on the ground, not at the origin block
