@@ -33,6 +33,25 @@ __device__ __forceinline__ void quat2mat(float m[9], const float q[4]) {
   m[6] = 2.f * (x * z - w * y); m[7] = 2.f * (y * z + w * x); m[8] = 1.f - 2.f * (x * x + y * y);
 }
 
+// rotation -> unit quaternion (mju_mat2Quat: the branch of the largest component, no sign normalisation)
+__device__ __forceinline__ void mat2quat(float q[4], const float* R) {
+  const float tr = R[0] + R[4] + R[8];
+  if (tr > 0.f) {
+    const float sq = sqrtf(tr + 1.f) * 2.f;
+    q[0] = 0.25f * sq; q[1] = (R[7] - R[5]) / sq; q[2] = (R[2] - R[6]) / sq; q[3] = (R[3] - R[1]) / sq;
+  } else if (R[0] > R[4] && R[0] > R[8]) {
+    const float sq = sqrtf(1.f + R[0] - R[4] - R[8]) * 2.f;
+    q[0] = (R[7] - R[5]) / sq; q[1] = 0.25f * sq; q[2] = (R[1] + R[3]) / sq; q[3] = (R[2] + R[6]) / sq;
+  } else if (R[4] > R[8]) {
+    const float sq = sqrtf(1.f + R[4] - R[0] - R[8]) * 2.f;
+    q[0] = (R[2] - R[6]) / sq; q[1] = (R[1] + R[3]) / sq; q[2] = 0.25f * sq; q[3] = (R[5] + R[7]) / sq;
+  } else {
+    const float sq = sqrtf(1.f + R[8] - R[0] - R[4]) * 2.f;
+    q[0] = (R[3] - R[1]) / sq; q[1] = (R[2] + R[6]) / sq; q[2] = (R[5] + R[7]) / sq; q[3] = 0.25f * sq;
+  }
+  quat_normalize(q);
+}
+
 __device__ __forceinline__ void mat_vec(float r[3], const float* m, const float v[3]) {
   float a = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
   float b = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];

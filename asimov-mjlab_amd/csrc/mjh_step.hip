@@ -3698,6 +3698,38 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         wsync();
         continue;
       }
+      if (type == 48 || type == 49) {
+        // e_potential (mj_energyPos: gravity over bodies + joint springs) /
+        // e_kinetic (mj_energyVel: qvel' M qvel / 2, M rows from the factor pass)
+        float e = 0.f, z = 0.f;
+        if (type == 48) {
+          for (int b = 1 + tid; b < nb; b += NT)
+            e -= cinert[10 * b + 9] * (m.gravity_x * xipos[3 * b] + m.gravity_y * xipos[3 * b + 1] + m.gravity_z * xipos[3 * b + 2]);
+          for (int j = tid; j < Z.njnt; j += NT) {
+            const float k = jnt_stiffness[j];
+            const int t = IMG_I(jnt_type)[j];
+            if (k == 0.f || t == 0) continue;
+            const int qa = IMG_I(jnt_qposadr)[j];
+            if (t == 1) {
+              float dif[3];
+              sub_quat(dif, qpos + qa, IMG_F(qpos_spring) + qa);
+              e += 0.5f * k * dot3(dif, dif);
+            } else {
+              const float dq = qpos[qa] - IMG_F(qpos_spring)[qa];
+              e += 0.5f * k * dq * dq;
+            }
+          }
+        } else {
+          for (int i = tid; i < nv; i += NT) {
+            float r = 0.f;
+            for (int j = 0; j < nv; j++) r += Mm[i * ldm + j] * qvel[j];
+            e += 0.5f * qvel[i] * r;
+          }
+        }
+        bsum2<NT>(e, z, red);
+        if (tid == 0) sd[adr] = e;
+        continue;
+      }
       if (type != 35 && type != 36) continue;
       // subtree linvel / angmom: lanes over bodies, wave reductions
       const unsigned long long* tmask = (const unsigned long long*)IMG_L(body_treemask);
@@ -3751,10 +3783,54 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         for (int k = 0; k < 3; k++) out[k] = cut > 0.f ? clampf(o3[k], -cut, cut) : o3[k];
       }
     }
+    // a sensor object's frame (mj_sensorPos): 1 body (inertial frame), 2 xbody,
+    // 5 geom (from its body's frame, as the geom pass computes it), 6 site; b:
+    // the body it moves with
+    auto obj_frame = [&](int ot, int oid, float (&p)[3], float (&R)[9], int& b) {
+      if (ot == 5) {
+        b = IMG_I(geom_bodyid)[oid];
+        float t[3], GR[9];
+        mat_vec(t, xmat + 9 * b, geom_pos + 3 * oid);
+        for (int k = 0; k < 3; k++) p[k] = xpos[3 * b + k] + t[k];
+        quat2mat(GR, geom_quat + 4 * oid);
+        mat_mul(R, xmat + 9 * b, GR);
+        return;
+      }
+      const float* sp = ot == 1 ? xipos + 3 * oid : (ot == 2 ? xpos + 3 * oid : sxpos + 3 * oid);
+      const float* sR = ot == 1 ? ximat + 9 * oid : (ot == 2 ? xmat + 9 * oid : sxmat + 9 * oid);
+      b = ot == 1 || ot == 2 ? oid : IMG_I(site_bodyid)[oid];
+      for (int k = 0; k < 3; k++) p[k] = sp[k];
+      for (int k = 0; k < 9; k++) R[k] = sR[k];
+    };
+    // its orientation: xbody copies xquat, body composes the inertial frame's
+    // quaternion, geom / site convert their matrix
+    auto obj_quat = [&](int ot, int oid, float (&q)[4]) {
+      if (ot == 2) {
+        for (int k = 0; k < 4; k++) q[k] = xquat[4 * oid + k];
+      } else if (ot == 1) {
+        float a[4] = {xquat[4 * oid], xquat[4 * oid + 1], xquat[4 * oid + 2], xquat[4 * oid + 3]};
+        quat_mul(q, a, body_iquat + 4 * oid);
+      } else {
+        float p[3], R[9];
+        int b;
+        obj_frame(ot, oid, p, R, b);
+        mat2quat(q, R);
+      }
+    };
+    // 6D world velocity [angular; linear at point p] of body b (mj_objectVelocity, flg_local 0)
+    auto obj_vel = [&](const float (&p)[3], int b, float (&v)[6]) {
+      const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
+      const float* cv = cvel + 6 * b;
+      const float dif[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]};
+      float t[3];
+      cross3(t, dif, cv);
+      v[0] = cv[0]; v[1] = cv[1]; v[2] = cv[2];
+      v[3] = cv[3] - t[0]; v[4] = cv[4] - t[1]; v[5] = cv[5] - t[2];
+    };
     // remaining sensors are independent and cheap: one lane each
     for (int s = tid; s < Z.nsensor; s += NT) {
       const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
-      if (type == 40 || type == 35 || type == 36) continue;
+      if (type == 40 || type == 35 || type == 36 || type == 48 || type == 49) continue;
       float* out = sd + adr;
       switch (type) {
         case 3: {  // gyro
@@ -3788,36 +3864,125 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           }
           break;
         }
-        case 30: out[0] = sxpos[3 * id]; out[1] = sxpos[3 * id + 1]; out[2] = sxpos[3 * id + 2]; break;
-        case 9: out[0] = qpos[IMG_I(jnt_qposadr)[id]]; break;
-        case 10: out[0] = qvel[IMG_I(jnt_dofadr)[id]]; break;
-        case 34: out[0] = subtree_com[3 * id]; out[1] = subtree_com[3 * id + 1]; out[2] = subtree_com[3 * id + 2]; break;
-        case 31: {
-          const float* R = sxmat + 9 * id;
-          float q[4], tr = R[0] + R[4] + R[8];
-          if (tr > 0.f) {
-            float sq = sqrtf(tr + 1.f) * 2.f;
-            q[0] = 0.25f * sq; q[1] = (R[7] - R[5]) / sq; q[2] = (R[2] - R[6]) / sq; q[3] = (R[3] - R[1]) / sq;
-          } else if (R[0] > R[4] && R[0] > R[8]) {
-            float sq = sqrtf(1.f + R[0] - R[4] - R[8]) * 2.f;
-            q[0] = (R[7] - R[5]) / sq; q[1] = 0.25f * sq; q[2] = (R[1] + R[3]) / sq; q[3] = (R[2] + R[6]) / sq;
-          } else if (R[4] > R[8]) {
-            float sq = sqrtf(1.f + R[4] - R[0] - R[8]) * 2.f;
-            q[0] = (R[2] - R[6]) / sq; q[1] = (R[1] + R[3]) / sq; q[2] = 0.25f * sq; q[3] = (R[5] + R[7]) / sq;
-          } else {
-            float sq = sqrtf(1.f + R[8] - R[0] - R[4]) * 2.f;
-            q[0] = (R[3] - R[1]) / sq; q[1] = (R[2] + R[6]) / sq; q[2] = (R[5] + R[7]) / sq; q[3] = 0.25f * sq;
+        case 30:
+        case 41:
+        case 42:
+        case 43: {  // framepos / frame{x,y,z}axis, optionally in the ref frame (mj_sensorPos)
+          float p[3], R[9], pr[3], Rr[9], v[3];
+          int b, br;
+          obj_frame(IMG_I(sensor_objtype)[s], id, p, R, b);
+          if (type == 30) { v[0] = p[0]; v[1] = p[1]; v[2] = p[2]; }
+          else { const int c = type - 41; v[0] = R[c]; v[1] = R[3 + c]; v[2] = R[6 + c]; }
+          const int rid = IMG_I(sensor_refid)[s];
+          if (rid >= 0) {
+            obj_frame(IMG_I(sensor_reftype)[s], rid, pr, Rr, br);
+            if (type == 30) { v[0] -= pr[0]; v[1] -= pr[1]; v[2] -= pr[2]; }
+            matT_vec(v, Rr, v);
           }
-          if (q[0] < 0.f) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+          out[0] = v[0]; out[1] = v[1]; out[2] = v[2];
+          break;
+        }
+        case 31: {  // framequat, relative to the ref frame when one is given: conj(q_ref) * q
+          float q[4];
+          obj_quat(IMG_I(sensor_objtype)[s], id, q);
+          const int rid = IMG_I(sensor_refid)[s];
+          if (rid >= 0) {
+            float qr[4];
+            obj_quat(IMG_I(sensor_reftype)[s], rid, qr);
+            qr[1] = -qr[1]; qr[2] = -qr[2]; qr[3] = -qr[3];
+            quat_mul(q, qr, q);
+          }
+          out[0] = q[0]; out[1] = q[1]; out[2] = q[2]; out[3] = q[3];
+          break;
+        }
+        case 44:
+        case 45: {  // framelinvel / frameangvel (mj_sensorVel): world frame, or relative to the ref frame and in it
+          float p[3], R[9], v[6];
+          int b;
+          obj_frame(IMG_I(sensor_objtype)[s], id, p, R, b);
+          obj_vel(p, b, v);
+          const int rid = IMG_I(sensor_refid)[s];
+          float r[3];
+          if (rid < 0) {
+            const float* o = type == 44 ? v + 3 : v;
+            r[0] = o[0]; r[1] = o[1]; r[2] = o[2];
+          } else {
+            float pr[3], Rr[9], vr[6], t[3];
+            int br;
+            obj_frame(IMG_I(sensor_reftype)[s], rid, pr, Rr, br);
+            obj_vel(pr, br, vr);
+            if (type == 44) {
+              const float dp[3] = {p[0] - pr[0], p[1] - pr[1], p[2] - pr[2]};
+              cross3(t, vr, dp);
+              r[0] = v[3] - vr[3] - t[0]; r[1] = v[4] - vr[4] - t[1]; r[2] = v[5] - vr[5] - t[2];
+            } else {
+              r[0] = v[0] - vr[0]; r[1] = v[1] - vr[1]; r[2] = v[2] - vr[2];
+            }
+            matT_vec(r, Rr, r);
+          }
+          out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
+          break;
+        }
+        case 46:
+        case 47: {  // framelinacc / frameangacc (mj_objectAcceleration, world frame): cacc at the frame origin + w x v
+          float p[3], R[9];
+          int b;
+          obj_frame(IMG_I(sensor_objtype)[s], id, p, R, b);
+          const float* a = cacc + 6 * b;
+          if (type == 47) { out[0] = a[0]; out[1] = a[1]; out[2] = a[2]; break; }
+          const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
+          const float dif[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]};
+          float v[6], t[3], al[3];
+          obj_vel(p, b, v);
+          cross3(t, dif, a);
+          al[0] = a[3] - t[0]; al[1] = a[4] - t[1]; al[2] = a[5] - t[2];
+          cross3(t, v, v + 3);
+          out[0] = al[0] + t[0]; out[1] = al[1] + t[1]; out[2] = al[2] + t[2];
+          break;
+        }
+        case 20:
+        case 21:
+        case 22: {  // jointlimitpos / vel / frc: the joint's limit row (efc_pos - margin, J qvel, force); 0 if inactive
+          float val = 0.f;
+          const int nr = min(nefc, Lo.rcap);
+          for (int r = 0; r < nr; r++) {
+            if (efc_type[r] != MJH_CNSTR_LIMIT_JOINT || efc_id[r] != id) continue;
+            val = type == 20 ? efc_pos[r] - IMG_F(jnt_margin)[id] : (type == 21 ? rowdot_u<NVP>(J + r * ldj, qvel, nv) : efc_force[r]);
+            break;
+          }
+          out[0] = val;
+          break;
+        }
+        case 13:  // actuatorpos / actuatorvel: gear * joint coordinate (joint transmission)
+        case 14: {
+          const int j = IMG_I(actuator_trnid)[id];
+          out[0] = IMG_F(actuator_gear)[id] * (type == 13 ? qpos[IMG_I(jnt_qposadr)[j]] : qvel[IMG_I(jnt_dofadr)[j]]);
+          break;
+        }
+        case 15: out[0] = act_force[id]; break;
+        case 16: out[0] = qfrc_act[IMG_I(jnt_dofadr)[id]]; break;
+        case 18: {  // ballquat: the normalised joint quaternion
+          float q[4];
+          const float* qp = qpos + IMG_I(jnt_qposadr)[id];
+          q[0] = qp[0]; q[1] = qp[1]; q[2] = qp[2]; q[3] = qp[3];
           quat_normalize(q);
           out[0] = q[0]; out[1] = q[1]; out[2] = q[2]; out[3] = q[3];
           break;
         }
+        case 19: {
+          const float* qv = qvel + IMG_I(jnt_dofadr)[id];
+          out[0] = qv[0]; out[1] = qv[1]; out[2] = qv[2];
+          break;
+        }
+        case 50: out[0] = DP(time)[W]; break;
+        case 9: out[0] = qpos[IMG_I(jnt_qposadr)[id]]; break;
+        case 10: out[0] = qvel[IMG_I(jnt_dofadr)[id]]; break;
+        case 34: out[0] = subtree_com[3 * id]; out[1] = subtree_com[3 * id + 1]; out[2] = subtree_com[3 * id + 2]; break;
         default:
           break;
       }
       const float cut = IMG_F(sensor_cutoff)[s];
-      if (cut > 0.f && type != 31)
+      if (cut > 0.f && type != 31 && type != 18 && (type < 41 || type > 43))  // quaternions and unit axes are not clipped
         for (int k = 0; k < IMG_I(sensor_dim)[s]; k++) out[k] = clampf(out[k], -cut, cut);
     }
   }

@@ -46,12 +46,31 @@ SENSOR_TYPES = {
   "gyro": 3,
   "jointpos": 9,
   "jointvel": 10,
+  "actuatorpos": 13,
+  "actuatorvel": 14,
+  "actuatorfrc": 15,
+  "jointactuatorfrc": 16,
+  "ballquat": 18,
+  "ballangvel": 19,
   "framepos": 30,
   "framequat": 31,
   "subtreecom": 34,
   "subtreelinvel": 35,
   "subtreeangmom": 36,
   "contact": 40,
+  "framexaxis": 41,
+  "frameyaxis": 42,
+  "framezaxis": 43,
+  "framelinvel": 44,
+  "frameangvel": 45,
+  "framelinacc": 46,
+  "frameangacc": 47,
+  "jointlimitpos": 20,
+  "jointlimitvel": 21,
+  "jointlimitfrc": 22,
+  "e_potential": 48,
+  "e_kinetic": 49,
+  "clock": 50,
 }
 SENSOR_DIMS = {
   "accelerometer": 3,
@@ -59,15 +78,36 @@ SENSOR_DIMS = {
   "gyro": 3,
   "jointpos": 1,
   "jointvel": 1,
+  "actuatorpos": 1,
+  "actuatorvel": 1,
+  "actuatorfrc": 1,
+  "jointactuatorfrc": 1,
+  "ballquat": 4,
+  "ballangvel": 3,
   "framepos": 3,
   "framequat": 4,
   "subtreecom": 3,
   "subtreelinvel": 3,
   "subtreeangmom": 3,
+  "framexaxis": 3,
+  "frameyaxis": 3,
+  "framezaxis": 3,
+  "framelinvel": 3,
+  "frameangvel": 3,
+  "framelinacc": 3,
+  "frameangacc": 3,
+  "jointlimitpos": 1,
+  "jointlimitvel": 1,
+  "jointlimitfrc": 1,
+  "e_potential": 1,
+  "e_kinetic": 1,
+  "clock": 1,
 }
+# sensors whose values are unit quaternions or axes: no cutoff (mjDATATYPE_QUATERNION / _AXIS)
+SENSOR_NO_CUTOFF = {"framequat", "ballquat", "framexaxis", "frameyaxis", "framezaxis"}
 # Contact sensor data fields: bit -> width (src/mjlab/sensor/contact_sensor.py:16-34).
 CONTACT_FIELD_DIMS = [1, 3, 3, 1, 3, 3, 3]
-OBJ_CODES = {"": 0, "body": 1, "xbody": 2, "joint": 3, "geom": 5, "site": 6}
+OBJ_CODES = {"": 0, "body": 1, "xbody": 2, "joint": 3, "geom": 5, "site": 6, "actuator": 19}
 QPOS_WIDTH = {0: 7, 1: 4, 2: 1, 3: 1}
 DOF_WIDTH = {0: 6, 1: 3, 2: 1, 3: 1}
 
@@ -428,6 +468,8 @@ def compile_spec(spec: Spec, nconmax: int = 0, njmax: int = 0) -> Model:
   m.jnt_solimp = np.array([j.solimp_limit for _, j, _, _, _ in jnt_list], np.float64).reshape(njnt, 5)
   m.jnt_margin = np.array([j.margin for _, j, _, _, _ in jnt_list], np.float64)
   m.jnt_stiffness = np.array([j.stiffness for _, j, _, _, _ in jnt_list], np.float64)
+  if any(t == 0 and j.stiffness != 0 for _, j, t, _, _ in jnt_list):
+    raise NotImplementedError("free-joint springs (stiffness on a free joint) are not supported")
 
   # qpos0 / qpos_spring
   qpos0 = np.zeros(nq)
@@ -580,14 +622,19 @@ def _compile_sensors(m: Model, spec: Spec) -> None:
     "site": "site",
     "geom": "geom",
     "joint": "joint",
+    "actuator": "actuator",
   }
   adr = 0
   for i, s in enumerate(spec.sensors):
     m.sensor_type[i] = SENSOR_TYPES[s.type]
     m.sensor_objtype[i] = OBJ_CODES[s.objtype]
-    m.sensor_objid[i] = m.names[lookup[s.objtype]].index(s.objname)
-    if s.type in ("jointpos", "jointvel") and m.jnt_type[m.sensor_objid[i]] not in (2, 3):
+    m.sensor_objid[i] = m.names[lookup[s.objtype]].index(s.objname) if s.objtype else -1
+    if s.type in ("jointpos", "jointvel", "jointactuatorfrc") and m.jnt_type[m.sensor_objid[i]] not in (2, 3):
       raise NotImplementedError(f"{s.type} sensor '{s.name}' needs a hinge or slide joint (MuJoCo: ballquat / ballangvel)")
+    if s.type in ("ballquat", "ballangvel") and m.jnt_type[m.sensor_objid[i]] != 1:
+      raise ValueError(f"{s.type} sensor '{s.name}' needs a ball joint")
+    if s.reftype and s.type in ("framelinacc", "frameangacc"):
+      raise ValueError(f"{s.type} sensor '{s.name}': MuJoCo's acceleration frame sensors take no reference frame")
     if s.reftype:
       m.sensor_reftype[i] = OBJ_CODES[s.reftype]
       m.sensor_refid[i] = m.names[lookup[s.reftype]].index(s.refname)

@@ -326,14 +326,23 @@ class MjcfReader:
       reduce = {"none": 0, "mindist": 1, "maxforce": 2, "netforce": 3}[a.get("reduce", "none")]
       s.intprm = [bits, reduce, int(a.get("num", 1))]
       return s
-    if node.tag in ("framequat", "framepos") and "objname" in a:
-      s.objtype, s.objname = a.get("objtype", "site"), a["objname"]
-    elif node.tag in ("gyro", "velocimeter", "accelerometer", "framequat", "framepos"):
+    frame = ("framepos", "framequat", "framexaxis", "frameyaxis", "framezaxis", "framelinvel", "frameangvel",
+             "framelinacc", "frameangacc")
+    if node.tag in frame:
+      s.objtype, s.objname = a["objtype"], a["objname"]
+      if "reftype" in a or "refname" in a:
+        s.reftype, s.refname = a["reftype"], a["refname"]
+    elif node.tag in ("gyro", "velocimeter", "accelerometer"):
       s.objtype, s.objname = "site", a["site"]
     elif node.tag in ("subtreeangmom", "subtreecom", "subtreelinvel"):
       s.objtype, s.objname = "body", a["body"]
-    elif node.tag in ("jointpos", "jointvel"):
+    elif node.tag in ("jointpos", "jointvel", "jointactuatorfrc", "ballquat", "ballangvel", "jointlimitpos",
+                      "jointlimitvel", "jointlimitfrc"):
       s.objtype, s.objname = "joint", a["joint"]
+    elif node.tag in ("actuatorpos", "actuatorvel", "actuatorfrc"):
+      s.objtype, s.objname = "actuator", a["actuator"]
+    elif node.tag in ("clock", "e_potential", "e_kinetic"):
+      pass
     else:
       raise NotImplementedError(f"sensor <{node.tag}> not supported")
     s.cutoff = float(a.get("cutoff", 0.0))
@@ -358,9 +367,13 @@ def read_mjcf_string(text: str, name: str = "inline.xml") -> Spec:
 
 # ---- writer: compiled model -> MJCF (for NaN dumps; MuJoCo's mj_saveModel is absent) ----
 _GEOM_NAMES = {0: "plane", 2: "sphere", 3: "capsule", 4: "ellipsoid", 5: "cylinder", 6: "box", 7: "mesh"}
-_SENSOR_TAGS = {1: "accelerometer", 2: "velocimeter", 3: "gyro", 9: "jointpos", 10: "jointvel", 30: "framepos",
-                31: "framequat", 34: "subtreecom", 35: "subtreelinvel", 36: "subtreeangmom"}
-_OBJ_NAMES = {1: "body", 2: "xbody", 3: "joint", 5: "geom", 6: "site"}
+_SENSOR_TAGS = {1: "accelerometer", 2: "velocimeter", 3: "gyro", 9: "jointpos", 10: "jointvel", 13: "actuatorpos",
+                14: "actuatorvel", 15: "actuatorfrc", 16: "jointactuatorfrc", 18: "ballquat", 19: "ballangvel",
+                20: "jointlimitpos", 21: "jointlimitvel", 22: "jointlimitfrc", 30: "framepos", 31: "framequat", 34: "subtreecom", 35: "subtreelinvel", 36: "subtreeangmom",
+                41: "framexaxis", 42: "frameyaxis", 43: "framezaxis", 44: "framelinvel", 45: "frameangvel",
+                46: "framelinacc", 47: "frameangacc", 48: "e_potential", 49: "e_kinetic", 50: "clock"}
+_FRAME_SENSORS = {30, 31, 41, 42, 43, 44, 45, 46, 47}
+_OBJ_NAMES = {1: "body", 2: "xbody", 3: "joint", 5: "geom", 6: "site", 19: "actuator"}
 _CONTACT_OBJ = {1: "body", 2: "subtree", 5: "geom"}
 
 
@@ -480,11 +493,19 @@ def model_to_mjcf(m) -> str:
         out.append(f'    <contact name="{nm}"{o1}{o2} data="{fields}" '
                    f'reduce="{ {0: "none", 1: "mindist", 2: "maxforce", 3: "netforce"}[red] }" num="{num}"/>')
         continue
+      if ot == 0:  # no object (clock, energies)
+        out.append(f'    <{_SENSOR_TAGS[t]} name="{nm}"{cut_a}/>')
+        continue
       kind = _OBJ_NAMES[ot]
-      attr = {"site": "site", "joint": "joint", "body": "body", "xbody": "body"}[kind]
-      obj = names["site" if kind == "site" else "joint" if kind == "joint" else "body"][oid]
-      if t in (30, 31):
-        out.append(f'    <{_SENSOR_TAGS[t]} name="{nm}" objtype="site" objname="{obj}"{cut_a}/>')
+      attr = {"site": "site", "joint": "joint", "body": "body", "xbody": "body", "actuator": "actuator"}.get(kind, kind)
+      obj = names[{"xbody": "body"}.get(kind, kind)][oid]
+      if t in _FRAME_SENSORS:
+        rt, rid = int(m.sensor_reftype[s]), int(m.sensor_refid[s])
+        ref = ""
+        if rid >= 0 and rt in _OBJ_NAMES:
+          rk = _OBJ_NAMES[rt]
+          ref = f' reftype="{rk}" refname="{names[{"xbody": "body"}.get(rk, rk)][rid]}"'
+        out.append(f'    <{_SENSOR_TAGS[t]} name="{nm}" objtype="{kind}" objname="{obj}"{ref}{cut_a}/>')
       else:
         out.append(f'    <{_SENSOR_TAGS[t]} name="{nm}" {attr}="{obj}"{cut_a}/>')
     out.append("  </sensor>")

@@ -1954,11 +1954,190 @@ static void contact_force(const or_model* m, ws_t* w, int ci, real f[6]) {
   for (int k = 1; k < c->dim; k++) f[k] = c->friction[k - 1] * (ef[2 * k - 2] - ef[2 * k - 1]);
 }
 
-static void sensors(const or_model* m, ws_t* w, real* sd) {
+/* rotation -> unit quaternion (mju_mat2Quat: branch of the largest component, no sign normalisation) */
+static void mat2quat(real q[4], const real* R) {
+  real tr = R[0] + R[4] + R[8];
+  if (tr > 0) {
+    real sq = sqrt(tr + 1) * 2;
+    q[0] = 0.25 * sq; q[1] = (R[7] - R[5]) / sq; q[2] = (R[2] - R[6]) / sq; q[3] = (R[3] - R[1]) / sq;
+  } else if (R[0] > R[4] && R[0] > R[8]) {
+    real sq = sqrt(1 + R[0] - R[4] - R[8]) * 2;
+    q[0] = (R[7] - R[5]) / sq; q[1] = 0.25 * sq; q[2] = (R[1] + R[3]) / sq; q[3] = (R[2] + R[6]) / sq;
+  } else if (R[4] > R[8]) {
+    real sq = sqrt(1 + R[4] - R[0] - R[8]) * 2;
+    q[0] = (R[2] - R[6]) / sq; q[1] = (R[1] + R[3]) / sq; q[2] = 0.25 * sq; q[3] = (R[5] + R[7]) / sq;
+  } else {
+    real sq = sqrt(1 + R[8] - R[0] - R[4]) * 2;
+    q[0] = (R[3] - R[1]) / sq; q[1] = (R[2] + R[6]) / sq; q[2] = (R[5] + R[7]) / sq; q[3] = 0.25 * sq;
+  }
+  normalize4(q);
+}
+
+/* a sensor object's frame (mj_sensorPos): body = inertial frame, xbody =
+   body frame, geom, site; *bd: the body it moves with */
+static void obj_frame(const or_model* m, const ws_t* w, int type, int id, const real** pos, const real** mat, int* bd) {
+  switch (type) {
+    case 1: *pos = w->xipos + 3 * id; *mat = w->ximat + 9 * id; *bd = id; break;
+    case 2: *pos = w->xpos + 3 * id; *mat = w->xmat + 9 * id; *bd = id; break;
+    case 5: *pos = w->gxpos + 3 * id; *mat = w->gxmat + 9 * id; *bd = m->geom_bodyid[id]; break;
+    default: *pos = w->sxpos + 3 * id; *mat = w->sxmat + 9 * id; *bd = m->site_bodyid[id]; break;
+  }
+}
+
+/* its orientation as a quaternion: xbody copies xquat, body composes the
+   inertial frame's quaternion, geom / site convert their matrix */
+static void obj_quat(const or_model* m, const ws_t* w, int wi, int type, int id, real q[4]) {
+  if (type == 2) {
+    memcpy(q, w->xquat + 4 * id, 4 * sizeof(real));
+  } else if (type == 1) {
+    mul_quat(q, w->xquat + 4 * id, WF(m, body_iquat, wi) + 4 * id);
+  } else {
+    const real *p, *R;
+    int b;
+    obj_frame(m, w, type, id, &p, &R, &b);
+    mat2quat(q, R);
+  }
+}
+
+/* its 6D velocity [angular; linear at the frame origin] in the world frame
+   (mj_objectVelocity, flg_local 0) */
+static void obj_vel(const or_model* m, const ws_t* w, int type, int id, real v[6]) {
+  const real *p, *R;
+  int b;
+  obj_frame(m, w, type, id, &p, &R, &b);
+  transform_motion(v, w->cvel + 6 * b, p, w->subtree_com + 3 * m->body_rootid[b], NULL);
+}
+
+static void sensors(const or_model* m, ws_t* w, int wi, real time, real* sd) {
   for (int s = 0; s < m->nsensor; s++) {
     int type = m->sensor_type[s], id = m->sensor_objid[s];
     real* out = sd + m->sensor_adr[s];
+    const int rtype = m->sensor_reftype[s], rid = m->sensor_refid[s];
     switch (type) {
+      case 30: case 41: case 42: case 43: { /* framepos / frame{x,y,z}axis, optionally in the ref frame */
+        const real *p, *R, *pr, *Rr;
+        int b, br;
+        obj_frame(m, w, m->sensor_objtype[s], id, &p, &R, &b);
+        real v[3];
+        if (type == 30) memcpy(v, p, sizeof(v));
+        else for (int k = 0; k < 3; k++) v[k] = R[3 * k + (type - 41)];
+        if (rid >= 0) {
+          obj_frame(m, w, rtype, rid, &pr, &Rr, &br);
+          if (type == 30) for (int k = 0; k < 3; k++) v[k] -= pr[k];
+          matT_vec(out, Rr, v);
+        } else {
+          memcpy(out, v, sizeof(v));
+        }
+        break;
+      }
+      case 31: { /* framequat, optionally relative to the ref frame: q_ref^-1 q */
+        real q[4];
+        obj_quat(m, w, wi, m->sensor_objtype[s], id, q);
+        if (rid >= 0) {
+          real qr[4], qc[4];
+          obj_quat(m, w, wi, rtype, rid, qr);
+          qc[0] = qr[0]; qc[1] = -qr[1]; qc[2] = -qr[2]; qc[3] = -qr[3];
+          mul_quat(out, qc, q);
+        } else {
+          memcpy(out, q, sizeof(q));
+        }
+        break;
+      }
+      case 44: case 45: { /* framelinvel / frameangvel (mj_sensorVel): world frame, or relative
+                             to the ref frame and expressed in it */
+        real v[6];
+        obj_vel(m, w, m->sensor_objtype[s], id, v);
+        if (rid < 0) {
+          memcpy(out, type == 44 ? v + 3 : v, 3 * sizeof(real));
+          break;
+        }
+        real vr[6], rel[3], dp[3], t[3];
+        const real *p, *R, *pr, *Rr;
+        int b, br;
+        obj_vel(m, w, rtype, rid, vr);
+        obj_frame(m, w, m->sensor_objtype[s], id, &p, &R, &b);
+        obj_frame(m, w, rtype, rid, &pr, &Rr, &br);
+        if (type == 44) {
+          for (int k = 0; k < 3; k++) dp[k] = p[k] - pr[k];
+          cross3(t, vr, dp);
+          for (int k = 0; k < 3; k++) rel[k] = v[3 + k] - vr[3 + k] - t[k];
+        } else {
+          for (int k = 0; k < 3; k++) rel[k] = v[k] - vr[k];
+        }
+        matT_vec(out, Rr, rel);
+        break;
+      }
+      case 46: case 47: { /* framelinacc / frameangacc (mj_objectAcceleration, world frame): cacc at
+                             the frame origin plus the Coriolis term w x v */
+        const real *p, *R;
+        int b;
+        obj_frame(m, w, m->sensor_objtype[s], id, &p, &R, &b);
+        const real* c = w->subtree_com + 3 * m->body_rootid[b];
+        real a[6], v[6], t[3];
+        transform_motion(a, w->cacc + 6 * b, p, c, NULL);
+        if (type == 47) { memcpy(out, a, 3 * sizeof(real)); break; }
+        transform_motion(v, w->cvel + 6 * b, p, c, NULL);
+        cross3(t, v, v + 3);
+        for (int k = 0; k < 3; k++) out[k] = a[3 + k] + t[k];
+        break;
+      }
+      case 20: case 21: case 22: { /* jointlimitpos / vel / frc: the joint's limit row, 0 when inactive */
+        out[0] = 0;
+        for (int r = 0; r < w->nefc; r++) {
+          if (w->efc_type[r] != 3 || w->efc_id[r] != id) continue;
+          if (type == 20) {
+            out[0] = w->efc_pos[r] - w->efc_margin[r];
+          } else if (type == 21) {
+            real v = 0;
+            for (int i = 0; i < m->nv; i++) v += w->J[r * m->nv + i] * w->qvel[i];
+            out[0] = v;
+          } else {
+            out[0] = w->efc_force[r];
+          }
+          break;
+        }
+        break;
+      }
+      case 13: out[0] = w->act_length[id]; break;
+      case 14: out[0] = w->act_vel[id]; break;
+      case 15: out[0] = w->act_force[id]; break;
+      case 16: out[0] = w->qfrc_actuator[m->jnt_dofadr[id]]; break;
+      case 18: { /* ballquat: the normalised joint quaternion */
+        real q[4];
+        memcpy(q, w->qpos + m->jnt_qposadr[id], sizeof(q));
+        normalize4(q);
+        memcpy(out, q, sizeof(q));
+        break;
+      }
+      case 19: memcpy(out, w->qvel + m->jnt_dofadr[id], 3 * sizeof(real)); break;
+      case 50: out[0] = time; break;
+      case 48: { /* e_potential (mj_energyPos): gravity and joint springs */
+        const real g[3] = {m->gravity_x, m->gravity_y, m->gravity_z};
+        const real* stiff = WF(m, jnt_stiffness, wi);
+        real e = 0;
+        for (int b = 1; b < m->nbody; b++) e -= w->cinert[10 * b + 9] * dot3(g, w->xipos + 3 * b);
+        for (int j = 0; j < m->njnt; j++) {
+          if (stiff[j] == 0) continue;
+          const int qa = m->jnt_qposadr[j], t = m->jnt_type[j];
+          if (t == 2 || t == 3) {
+            const real dq = w->qpos[qa] - m->qpos_spring[qa];
+            e += 0.5 * stiff[j] * dq * dq;
+          } else if (t == 1) {
+            real dif[3];
+            sub_quat(dif, w->qpos + qa, m->qpos_spring + qa);
+            e += 0.5 * stiff[j] * dot3(dif, dif);
+          }
+        }
+        out[0] = e;
+        break;
+      }
+      case 49: { /* e_kinetic (mj_energyVel): qvel' M qvel / 2 */
+        real e = 0;
+        for (int i = 0; i < m->nv; i++)
+          for (int j = 0; j < m->nv; j++) e += w->qvel[i] * w->M[i * m->nv + j] * w->qvel[j];
+        out[0] = 0.5 * e;
+        break;
+      }
       case 3: { /* gyro */
         int b = m->site_bodyid[id];
         matT_vec(out, w->sxmat + 9 * id, w->cvel + 6 * b);
@@ -1980,28 +2159,6 @@ static void sensors(const or_model* m, ws_t* w, real* sd) {
         transform_motion(v, w->cvel + 6 * b, w->sxpos + 3 * id, c, w->sxmat + 9 * id);
         cross3(t, v, v + 3);
         for (int k = 0; k < 3; k++) out[k] = a[3 + k] + t[k];
-        break;
-      }
-      case 30: memcpy(out, w->sxpos + 3 * id, 3 * sizeof(real)); break;
-      case 31: { /* framequat of site from its xmat */
-        const real* R = w->sxmat + 9 * id;
-        real q[4], tr = R[0] + R[4] + R[8];
-        if (tr > 0) {
-          real sq = sqrt(tr + 1) * 2;
-          q[0] = 0.25 * sq; q[1] = (R[7] - R[5]) / sq; q[2] = (R[2] - R[6]) / sq; q[3] = (R[3] - R[1]) / sq;
-        } else if (R[0] > R[4] && R[0] > R[8]) {
-          real sq = sqrt(1 + R[0] - R[4] - R[8]) * 2;
-          q[0] = (R[7] - R[5]) / sq; q[1] = 0.25 * sq; q[2] = (R[1] + R[3]) / sq; q[3] = (R[2] + R[6]) / sq;
-        } else if (R[4] > R[8]) {
-          real sq = sqrt(1 + R[4] - R[0] - R[8]) * 2;
-          q[0] = (R[2] - R[6]) / sq; q[1] = (R[1] + R[3]) / sq; q[2] = 0.25 * sq; q[3] = (R[5] + R[7]) / sq;
-        } else {
-          real sq = sqrt(1 + R[8] - R[0] - R[4]) * 2;
-          q[0] = (R[3] - R[1]) / sq; q[1] = (R[2] + R[6]) / sq; q[2] = (R[5] + R[7]) / sq; q[3] = 0.25 * sq;
-        }
-        if (q[0] < 0) for (int k = 0; k < 4; k++) q[k] = -q[k];
-        normalize4(q);
-        memcpy(out, q, sizeof(q));
         break;
       }
       case 9: out[0] = w->qpos[m->jnt_qposadr[id]]; break;
@@ -2128,7 +2285,8 @@ static void sensors(const or_model* m, ws_t* w, real* sd) {
         break;
       }
     }
-    if (m->sensor_cutoff[s] > 0 && type != 31 && type != 40)
+    /* cutoff: not for quaternions and axes (mjDATATYPE_QUATERNION / _AXIS) or contact records */
+    if (m->sensor_cutoff[s] > 0 && type != 31 && type != 18 && (type < 41 || type > 43) && type != 40)
       for (int k = 0; k < m->sensor_dim[s]; k++) {
         real cut = m->sensor_cutoff[s];
         out[k] = out[k] < -cut ? -cut : (out[k] > cut ? cut : out[k]);
@@ -2191,7 +2349,7 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   solve(m, w, d->qacc_warmstart + (size_t)wi * nv);
   rne(m, w, w->qacc, NULL); /* cacc with constraint accelerations (accelerometer) */
   real* sd = d->sensordata + (size_t)wi * m->nsensordata;
-  sensors(m, w, sd);
+  sensors(m, w, wi, d->time[wi], sd);
 
   /* outputs of the forward pass */
   memcpy(d->xpos + (size_t)wi * nb * 3, w->xpos, sizeof(real) * nb * 3);

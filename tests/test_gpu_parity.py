@@ -764,6 +764,37 @@ def test_ball_joint_parity():
   print("[ball joints] limit rows", len(lim), "int rate", rep["int_match_rate"])
 
 
+def test_builtin_sensor_parity():
+  """Every builtin sensor type outside the benchmark tasks' set on the HIP
+  step against the oracle (tests/test_sensors_builtin.py's scene: frame
+  sensors on body / xbody / geom / site objects with body / xbody / geom / site
+  reference frames, actuator and joint-actuator sensors, ball-joint sensors,
+  clock, e_potential, e_kinetic), random poses and velocities, one step; the
+  oracle's sensors are pinned by that file's closed forms."""
+  from tests import test_sensors_builtin as tsb
+
+  n = 256
+  m = tsb._model()
+  st = tsb._state(np.random.default_rng(61), n)
+  st["qacc_warmstart"] = np.zeros((n, m.nv))
+  sim = Simulation(n, SimulationCfg(nconmax=8, njmax=64, mujoco=MujocoCfg(timestep=0.002)), m, DEV)
+  put(sim, st)
+  sim.step()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=True, follow=got)
+  for s, name in enumerate(m.names["sensor"]):  # per sensor, so a mismatch names its sensor
+    a, d = int(m.sensor_adr[s]), int(m.sensor_dim[s])
+    err = np.abs(got["sensordata"][:, a:a + d] - ref["sensordata"][:, a:a + d])
+    print(f"[sensor {name}] max|d|={err.max():.3e} worst world {int(err.max(axis=1).argmax())}")
+  assert_parity(got, ref, n, tag=" builtin sensors")
+  # the quaternion sensors as rotations too (the sign of mju_mat2Quat's branch
+  # is part of the value compared above; this names the sensor on a mismatch)
+  for name in ("fq_body_in_base", "fq_site", "fq_geom_in_body", "bq"):
+    s = m.names["sensor"].index(name)
+    a = int(m.sensor_adr[s])
+    np.testing.assert_allclose(got["sensordata"][:, a:a + 4], ref["sensordata"][:, a:a + 4], atol=2e-5, err_msg=name)
+
+
 @pytest.mark.parametrize("iterations", [1, 5])
 def test_pgs_solver_parity(iterations):
   """opt.solver = PGS (MuJoCo's projected Gauss-Seidel on the dual; the
