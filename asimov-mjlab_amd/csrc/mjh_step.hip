@@ -1902,13 +1902,46 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   const unsigned long long r_tmk = bl ? tmk[tid] : 0ull;
   if (MODE == 1 || (MODE == 0 && !reused)) {
   float r_xipos[3] = {0.f, 0.f, 0.f}, r_ximat[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int b = tid; b < nb; b += NT) {
+  // Level-synchronous sweep: at level d the lanes of the bodies at depth d take
+  // their parent's final pose from its lane (ds_bpermute) and apply their own
+  // body offset and joints, whose inputs every lane loaded before the sweep. The
+  // operations per body are those of a root-to-body chain walk; the chain of
+  // dependent image loads per level is gone.
+  if (bl) {
+    const int b = tid;
     float p[3] = {0.f, 0.f, 0.f}, q[4] = {1.f, 0.f, 0.f, 0.f};
-    const int ca = IMG_I(body_chainadr)[b], cn = (b == 0) ? 0 : IMG_I(body_chainnum)[b];
-    for (int c = 0; c < cn; c++) {
-      const int k = IMG_I(body_chain)[ca + c];
-      const int ja = IMG_I(body_jntadr)[k], jn = IMG_I(body_jntnum)[k];
-      const int mid = Z.nmocap > 0 ? IMG_I(body_mocapid)[k] : -1;
+    const int cn = b == 0 ? 0 : IMG_I(body_chainnum)[b];  // depth (the chain ends at b)
+    const int par = cn > 0 ? IMG_I(body_parentid)[b] : 0;
+    const int ja = cn > 0 ? IMG_I(body_jntadr)[b] : 0, jn = cn > 0 ? IMG_I(body_jntnum)[b] : 0;
+    const int mid = (cn > 0 && Z.nmocap > 0) ? IMG_I(body_mocapid)[b] : -1;
+    const int jt0 = jn > 0 ? IMG_I(jnt_type)[ja] : -1, qa0 = jn > 0 ? IMG_I(jnt_qposadr)[ja] : 0;
+    float bp[3] = {0.f, 0.f, 0.f}, bq[4] = {1.f, 0.f, 0.f, 0.f}, ax0[3] = {0.f, 0.f, 0.f}, jp0[3] = {0.f, 0.f, 0.f};
+    if (cn > 0) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) bp[k] = body_pos[3 * b + k];
+#pragma unroll
+      for (int k = 0; k < 4; k++) bq[k] = body_quat[4 * b + k];
+    }
+    // the first joint's local rotation depends on qpos alone: every lane
+    // evaluates it (sincos, normalisation) once, off the level chain
+    float ql0[4] = {1.f, 0.f, 0.f, 0.f};
+    if (jn > 0) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) { ax0[k] = IMG_F(jnt_axis)[3 * ja + k]; jp0[k] = IMG_F(jnt_pos)[3 * ja + k]; }
+      if (jt0 == 3) {
+        axis_angle(ql0, ax0, qpos[qa0] - qpos0[qa0]);
+      } else if (jt0 == 1) {
+        ql0[0] = qpos[qa0]; ql0[1] = qpos[qa0 + 1]; ql0[2] = qpos[qa0 + 2]; ql0[3] = qpos[qa0 + 3];
+        quat_normalize(ql0);
+      }
+    }
+    for (int lev = 1; __any(cn >= lev); lev++) {  // wave-uniform: up to the tree depth
+      float pp[3], pq[4];
+#pragma unroll
+      for (int k = 0; k < 3; k++) pp[k] = shfl(p[k], par);
+#pragma unroll
+      for (int k = 0; k < 4; k++) pq[k] = shfl(q[k], par);
+      if (cn != lev) continue;
       if (mid >= 0) {  // mocap body (a child of the world): pose from mocap_pos / mocap_quat
         const float* mp = DP(mocap_pos) + (W * Z.nmocap + mid) * 3;
         const float* mq = DP(mocap_quat) + (W * Z.nmocap + mid) * 4;
@@ -1917,53 +1950,57 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         quat_normalize(q);
         continue;
       }
-      if (jn == 1 && IMG_I(jnt_type)[ja] == 0) {
-        const int qa = IMG_I(jnt_qposadr)[ja];
-        p[0] = qpos[qa]; p[1] = qpos[qa + 1]; p[2] = qpos[qa + 2];
-        q[0] = qpos[qa + 3]; q[1] = qpos[qa + 4]; q[2] = qpos[qa + 5]; q[3] = qpos[qa + 6];
+      if (jn == 1 && jt0 == 0) {  // free joint: the pose is the joint's coordinates
+        p[0] = qpos[qa0]; p[1] = qpos[qa0 + 1]; p[2] = qpos[qa0 + 2];
+        q[0] = qpos[qa0 + 3]; q[1] = qpos[qa0 + 4]; q[2] = qpos[qa0 + 5]; q[3] = qpos[qa0 + 6];
         quat_normalize(q);
-        if (k == b) {
-          float R[9];
-          quat2mat(R, q);
-          xanchor[3 * ja] = p[0]; xanchor[3 * ja + 1] = p[1]; xanchor[3 * ja + 2] = p[2];
-          xaxis[3 * ja] = R[2]; xaxis[3 * ja + 1] = R[5]; xaxis[3 * ja + 2] = R[8];
-        }
+        float R[9];
+        quat2mat(R, q);
+        xanchor[3 * ja] = p[0]; xanchor[3 * ja + 1] = p[1]; xanchor[3 * ja + 2] = p[2];
+        xaxis[3 * ja] = R[2]; xaxis[3 * ja + 1] = R[5]; xaxis[3 * ja + 2] = R[8];
         continue;
       }
-      float R[9], t[3];
-      quat2mat(R, q);
-      mat_vec(t, R, body_pos + 3 * k);
-      p[0] += t[0]; p[1] += t[1]; p[2] += t[2];
-      quat_mul(q, q, body_quat + 4 * k);
+      {
+        float R[9], t[3];
+        quat2mat(R, pq);
+        mat_vec(t, R, bp);
+        p[0] = pp[0] + t[0]; p[1] = pp[1] + t[1]; p[2] = pp[2] + t[2];
+        quat_mul(q, pq, bq);
+      }
       for (int j = ja; j < ja + jn; j++) {
+        const bool first = j == ja;
+        float ja_ax[3], ja_pos[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          ja_ax[k] = first ? ax0[k] : IMG_F(jnt_axis)[3 * j + k];
+          ja_pos[k] = first ? jp0[k] : IMG_F(jnt_pos)[3 * j + k];
+        }
+        const int jt = first ? jt0 : IMG_I(jnt_type)[j], qa = first ? qa0 : IMG_I(jnt_qposadr)[j];
         float Rq[9], ax[3], anc[3];
         quat2mat(Rq, q);
-        mat_vec(ax, Rq, IMG_F(jnt_axis) + 3 * j);
-        mat_vec(anc, Rq, IMG_F(jnt_pos) + 3 * j);
+        mat_vec(ax, Rq, ja_ax);
+        mat_vec(anc, Rq, ja_pos);
         anc[0] += p[0]; anc[1] += p[1]; anc[2] += p[2];
-        const int qa = IMG_I(jnt_qposadr)[j];
-        if (IMG_I(jnt_type)[j] == 2) {
+        if (jt == 2) {
           const float dd = qpos[qa] - qpos0[qa];
           p[0] += ax[0] * dd; p[1] += ax[1] * dd; p[2] += ax[2] * dd;
-        } else if (IMG_I(jnt_type)[j] == 3) {
-          float ql[4], v[3];
-          axis_angle(ql, IMG_F(jnt_axis) + 3 * j, qpos[qa] - qpos0[qa]);
+        } else if (jt == 3 || jt == 1) {  // hinge (axis-angle) / ball (the normalised qpos quaternion), about the anchor
+          float ql[4] = {ql0[0], ql0[1], ql0[2], ql0[3]}, v[3];
+          if (!first) {
+            if (jt == 3) {
+              axis_angle(ql, ja_ax, qpos[qa] - qpos0[qa]);
+            } else {
+              ql[0] = qpos[qa]; ql[1] = qpos[qa + 1]; ql[2] = qpos[qa + 2]; ql[3] = qpos[qa + 3];
+              quat_normalize(ql);
+            }
+          }
           quat_mul(q, q, ql);
           quat2mat(Rq, q);
-          mat_vec(v, Rq, IMG_F(jnt_pos) + 3 * j);
-          p[0] = anc[0] - v[0]; p[1] = anc[1] - v[1]; p[2] = anc[2] - v[2];
-        } else if (IMG_I(jnt_type)[j] == 1) {  // ball: the normalised qpos quaternion, about the anchor
-          float ql[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]}, v[3];
-          quat_normalize(ql);
-          quat_mul(q, q, ql);
-          quat2mat(Rq, q);
-          mat_vec(v, Rq, IMG_F(jnt_pos) + 3 * j);
+          mat_vec(v, Rq, ja_pos);
           p[0] = anc[0] - v[0]; p[1] = anc[1] - v[1]; p[2] = anc[2] - v[2];
         }
-        if (k == b) {
-          xanchor[3 * j] = anc[0]; xanchor[3 * j + 1] = anc[1]; xanchor[3 * j + 2] = anc[2];
-          xaxis[3 * j] = ax[0]; xaxis[3 * j + 1] = ax[1]; xaxis[3 * j + 2] = ax[2];
-        }
+        xanchor[3 * j] = anc[0]; xanchor[3 * j + 1] = anc[1]; xanchor[3 * j + 2] = anc[2];
+        xaxis[3 * j] = ax[0]; xaxis[3 * j + 1] = ax[1]; xaxis[3 * j + 2] = ax[2];
       }
       quat_normalize(q);
     }
