@@ -1624,6 +1624,103 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 // integration), starting from the handoff region. Split, the position stage
 // needs far fewer registers and LDS, so it runs at higher occupancy, and the
 // first physics step after a gated forward skips it.
+// force / torque sensor (mj_sensorAcc after mj_rnePostConstraint): cfrc_int of
+// the site's body sb -- over sb's subtree, I a + v x* I v minus the external
+// wrench (xfrc_applied at the com; contact forces at the contact point, - on
+// geom1's body and + on geom2's, the world body excluded), about the root's
+// subtree com -- moved to the site and rotated into its frame; lane 0 writes
+// out[3]. Out of line and recomputed per sensor: only models with these
+// sensors call it, and inlined it would cost the step kernel registers on
+// every path. Every lane of the wave calls it.
+#ifndef MJH_FT_ATTR
+#define MJH_FT_ATTR __noinline__
+#endif
+__device__ MJH_FT_ATTR void force_torque_sensor(int tid, int nb, int ncon, int type, int sb, const float* spos,
+                                              const float* smat, float cut, const float* cinert, const float* cacc,
+                                              const float* cvel, const float* xipos, const float* subtree_com,
+                                              const float* xfrc, const int* body_rootid, const int* geom_bodyid,
+                                              const float* con_frame, const float* con_pos, const int* con_geom,
+                                              const int* con_efcadr, const int* con_dim, const float* con_fric,
+                                              const float* efc_force, bool ell, unsigned long long r_tmk, float* out) {
+  const bool bl = tid < nb;
+  float fb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float rc[3] = {0.f, 0.f, 0.f};
+  if (bl && tid > 0) {
+    float t1[6], t2[6], t3[6];
+    inert_vec(t1, cinert + 10 * tid, cacc + 6 * tid);
+    inert_vec(t2, cinert + 10 * tid, cvel + 6 * tid);
+    cross_force(t3, cvel + 6 * tid, t2);
+    const float* xf = xfrc + 6 * tid;
+    const float* c = subtree_com + 3 * body_rootid[tid];
+    rc[0] = c[0]; rc[1] = c[1]; rc[2] = c[2];
+    const float r[3] = {xipos[3 * tid] - c[0], xipos[3 * tid + 1] - c[1], xipos[3 * tid + 2] - c[2]};
+    float rf[3];
+    cross3(rf, r, xf);
+    for (int k = 0; k < 3; k++) {
+      fb[k] = t1[k] + t3[k] - (xf[3 + k] + rf[k]);
+      fb[3 + k] = t1[3 + k] + t3[3 + k] - xf[k];
+    }
+  }
+  for (int c0 = 0; c0 < ncon; c0 += 64) {  // lane = contact, then each contact broadcast to its bodies' lanes
+    const int ci = c0 + tid;
+    float Fw[3] = {0.f, 0.f, 0.f}, Tw[3] = {0.f, 0.f, 0.f}, cp[3] = {0.f, 0.f, 0.f};
+    int b1 = 0, b2 = 0;
+    if (ci < ncon) {
+      float F[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // mj_contactForce, contact frame
+      const int r0 = con_efcadr[ci];
+      if (r0 >= 0) {
+        const int cdm = con_dim[ci];
+        if (cdm == 1) {
+          F[0] = efc_force[r0];
+        } else if (ell) {
+          for (int k = 0; k < cdm && k < 6; k++) F[k] = efc_force[r0 + k];
+        } else {
+          for (int e = 0; e < 2 * (cdm - 1); e++) F[0] += efc_force[r0 + e];
+          for (int k = 1; k < cdm && k < 6; k++) F[k] = con_fric[5 * ci + k - 1] * (efc_force[r0 + 2 * k - 2] - efc_force[r0 + 2 * k - 1]);
+        }
+      }
+      matT_vec(Fw, con_frame + 9 * ci, F);
+      matT_vec(Tw, con_frame + 9 * ci, F + 3);
+      cp[0] = con_pos[3 * ci]; cp[1] = con_pos[3 * ci + 1]; cp[2] = con_pos[3 * ci + 2];
+      b1 = geom_bodyid[con_geom[2 * ci]];
+      b2 = geom_bodyid[con_geom[2 * ci + 1]];
+    }
+    const int cnt = min(64, ncon - c0);
+    for (int k = 0; k < cnt; k++) {
+      const int k1 = __builtin_amdgcn_readlane(b1, k), k2 = __builtin_amdgcn_readlane(b2, k);
+      float f3[3], t3[3], p3[3];
+      for (int e = 0; e < 3; e++) { f3[e] = rl(Fw[e], k); t3[e] = rl(Tw[e], k); p3[e] = rl(cp[e], k); }
+      const float sg = (tid == k2 ? 1.f : 0.f) - (tid == k1 ? 1.f : 0.f);
+      if (bl && tid > 0 && sg != 0.f) {
+        const float r[3] = {p3[0] - rc[0], p3[1] - rc[1], p3[2] - rc[2]};
+        float t[3];
+        cross3(t, r, f3);
+        for (int e = 0; e < 3; e++) {
+          fb[e] -= sg * (t3[e] + t[e]);
+          fb[3 + e] -= sg * f3[e];
+        }
+      }
+    }
+  }
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = 1; k < nb; k++) {  // subtree sums, ascending k (as crb)
+    const float in = (tid > 0 && ((rl64(r_tmk, k) >> tid) & 1ull)) ? 1.f : 0.f;
+    for (int e = 0; e < 6; e++) acc[e] += in * rl(fb[e], k);
+  }
+  float f6[6];
+  for (int e = 0; e < 6; e++) f6[e] = rl(acc[e], sb);
+  if (tid == 0) {
+    const float* c = subtree_com + 3 * body_rootid[sb];
+    const float dif[3] = {spos[0] - c[0], spos[1] - c[1], spos[2] - c[2]};
+    float t[3], v[3], o[3];
+    cross3(t, dif, f6 + 3);
+    if (type == 4) { v[0] = f6[3]; v[1] = f6[4]; v[2] = f6[5]; }
+    else { v[0] = f6[0] - t[0]; v[1] = f6[1] - t[1]; v[2] = f6[2] - t[2]; }
+    matT_vec(o, smat, v);
+    for (int e = 0; e < 3; e++) out[e] = cut > 0.f ? clampf(o[e], -cut, cut) : o[e];
+  }
+}
+
 template <int WPB, int NVP, int SPEC = -1, bool SLAB = false, int MODE = 0>
 __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(WPB)) void step_kernel(const mjh_model m, const mjh_data d, const Layout Lo_,
                                                          const ImgOff Io_, const unsigned char* gate, int reuse,
@@ -1902,6 +1999,73 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   const unsigned long long r_tmk = bl ? tmk[tid] : 0ull;
   if (MODE == 1 || (MODE == 0 && !reused)) {
   float r_xipos[3] = {0.f, 0.f, 0.f}, r_ximat[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#ifdef MJH_KIN_CHAIN
+  for (int b = tid; b < nb; b += NT) {
+    float p[3] = {0.f, 0.f, 0.f}, q[4] = {1.f, 0.f, 0.f, 0.f};
+    const int ca = IMG_I(body_chainadr)[b], cn = (b == 0) ? 0 : IMG_I(body_chainnum)[b];
+    for (int c = 0; c < cn; c++) {
+      const int k = IMG_I(body_chain)[ca + c];
+      const int ja = IMG_I(body_jntadr)[k], jn = IMG_I(body_jntnum)[k];
+      const int mid = Z.nmocap > 0 ? IMG_I(body_mocapid)[k] : -1;
+      if (mid >= 0) {  // mocap body (a child of the world): pose from mocap_pos / mocap_quat
+        const float* mp = DP(mocap_pos) + (W * Z.nmocap + mid) * 3;
+        const float* mq = DP(mocap_quat) + (W * Z.nmocap + mid) * 4;
+        p[0] = mp[0]; p[1] = mp[1]; p[2] = mp[2];
+        q[0] = mq[0]; q[1] = mq[1]; q[2] = mq[2]; q[3] = mq[3];
+        quat_normalize(q);
+        continue;
+      }
+      if (jn == 1 && IMG_I(jnt_type)[ja] == 0) {
+        const int qa = IMG_I(jnt_qposadr)[ja];
+        p[0] = qpos[qa]; p[1] = qpos[qa + 1]; p[2] = qpos[qa + 2];
+        q[0] = qpos[qa + 3]; q[1] = qpos[qa + 4]; q[2] = qpos[qa + 5]; q[3] = qpos[qa + 6];
+        quat_normalize(q);
+        if (k == b) {
+          float R[9];
+          quat2mat(R, q);
+          xanchor[3 * ja] = p[0]; xanchor[3 * ja + 1] = p[1]; xanchor[3 * ja + 2] = p[2];
+          xaxis[3 * ja] = R[2]; xaxis[3 * ja + 1] = R[5]; xaxis[3 * ja + 2] = R[8];
+        }
+        continue;
+      }
+      float R[9], t[3];
+      quat2mat(R, q);
+      mat_vec(t, R, body_pos + 3 * k);
+      p[0] += t[0]; p[1] += t[1]; p[2] += t[2];
+      quat_mul(q, q, body_quat + 4 * k);
+      for (int j = ja; j < ja + jn; j++) {
+        float Rq[9], ax[3], anc[3];
+        quat2mat(Rq, q);
+        mat_vec(ax, Rq, IMG_F(jnt_axis) + 3 * j);
+        mat_vec(anc, Rq, IMG_F(jnt_pos) + 3 * j);
+        anc[0] += p[0]; anc[1] += p[1]; anc[2] += p[2];
+        const int qa = IMG_I(jnt_qposadr)[j];
+        if (IMG_I(jnt_type)[j] == 2) {
+          const float dd = qpos[qa] - qpos0[qa];
+          p[0] += ax[0] * dd; p[1] += ax[1] * dd; p[2] += ax[2] * dd;
+        } else if (IMG_I(jnt_type)[j] == 3) {
+          float ql[4], v[3];
+          axis_angle(ql, IMG_F(jnt_axis) + 3 * j, qpos[qa] - qpos0[qa]);
+          quat_mul(q, q, ql);
+          quat2mat(Rq, q);
+          mat_vec(v, Rq, IMG_F(jnt_pos) + 3 * j);
+          p[0] = anc[0] - v[0]; p[1] = anc[1] - v[1]; p[2] = anc[2] - v[2];
+        } else if (IMG_I(jnt_type)[j] == 1) {  // ball: the normalised qpos quaternion, about the anchor
+          float ql[4] = {qpos[qa], qpos[qa + 1], qpos[qa + 2], qpos[qa + 3]}, v[3];
+          quat_normalize(ql);
+          quat_mul(q, q, ql);
+          quat2mat(Rq, q);
+          mat_vec(v, Rq, IMG_F(jnt_pos) + 3 * j);
+          p[0] = anc[0] - v[0]; p[1] = anc[1] - v[1]; p[2] = anc[2] - v[2];
+        }
+        if (k == b) {
+          xanchor[3 * j] = anc[0]; xanchor[3 * j + 1] = anc[1]; xanchor[3 * j + 2] = anc[2];
+          xaxis[3 * j] = ax[0]; xaxis[3 * j + 1] = ax[1]; xaxis[3 * j + 2] = ax[2];
+        }
+      }
+      quat_normalize(q);
+    }
+#else
   // Level-synchronous sweep: at level d the lanes of the bodies at depth d take
   // their parent's final pose from its lane (ds_bpermute) and apply their own
   // body offset and joints, whose inputs every lane loaded before the sweep. The
@@ -2004,6 +2168,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       }
       quat_normalize(q);
     }
+#endif
     float R[9];
     quat2mat(R, q);
     xpos[3 * b] = p[0]; xpos[3 * b + 1] = p[1]; xpos[3 * b + 2] = p[2];
@@ -3735,6 +3900,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         wsync();
         continue;
       }
+#ifndef MJH_NO_EXT
       if (type == 48 || type == 49) {
         // e_potential (mj_energyPos: gravity over bodies + joint springs) /
         // e_kinetic (mj_energyVel: qvel' M qvel / 2, M rows from the factor pass)
@@ -3767,6 +3933,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         if (tid == 0) sd[adr] = e;
         continue;
       }
+#endif
       if (type != 35 && type != 36) continue;
       // subtree linvel / angmom: lanes over bodies, wave reductions
       const unsigned long long* tmask = (const unsigned long long*)IMG_L(body_treemask);
@@ -3820,6 +3987,19 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         for (int k = 0; k < 3; k++) out[k] = cut > 0.f ? clampf(o3[k], -cut, cut) : o3[k];
       }
     }
+#ifndef MJH_NO_FT
+    // force / torque sensors (mj_sensorAcc), in a pass of their own so that no
+    // state of theirs is live in the loop above
+    for (int s = 0; s < Z.nsensor; s++) {
+      const int type = IMG_I(sensor_type)[s];
+      if (type != 4 && type != 5) continue;
+      const int id = IMG_I(sensor_objid)[s];
+      force_torque_sensor(tid, nb, ncon, type, IMG_I(site_bodyid)[id], sxpos + 3 * id, sxmat + 9 * id, IMG_F(sensor_cutoff)[s],
+                          cinert, cacc, cvel, xipos, subtree_com, DP(xfrc_applied) + W * nb * 6, IMG_I(body_rootid),
+                          IMG_I(geom_bodyid), con_frame, con_pos, con_geom, con_efcadr, con_dim, con_fric, efc_force, ELL,
+                          r_tmk, sd + IMG_I(sensor_adr)[s]);
+    }
+#endif
     // a sensor object's frame (mj_sensorPos): 1 body (inertial frame), 2 xbody,
     // 5 geom (from its body's frame, as the geom pass computes it), 6 site; b:
     // the body it moves with
@@ -3867,7 +4047,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     // remaining sensors are independent and cheap: one lane each
     for (int s = tid; s < Z.nsensor; s += NT) {
       const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
-      if (type == 40 || type == 35 || type == 36 || type == 48 || type == 49) continue;
+      if (type == 40 || type == 35 || type == 36 || type == 48 || type == 49 || type == 4 || type == 5) continue;
       float* out = sd + adr;
       switch (type) {
         case 3: {  // gyro
@@ -3901,6 +4081,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           }
           break;
         }
+#ifndef MJH_NO_EXT
         case 30:
         case 41:
         case 42:
@@ -4012,6 +4193,14 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           break;
         }
         case 50: out[0] = DP(time)[W]; break;
+        case 6: {  // magnetometer: the global field in the site frame
+          const float mg[3] = {m.magnetic_x, m.magnetic_y, m.magnetic_z};
+          float r[3];
+          matT_vec(r, sxmat + 9 * id, mg);
+          out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
+          break;
+        }
+#endif
         case 9: out[0] = qpos[IMG_I(jnt_qposadr)[id]]; break;
         case 10: out[0] = qvel[IMG_I(jnt_dofadr)[id]]; break;
         case 34: out[0] = subtree_com[3 * id]; out[1] = subtree_com[3 * id + 1]; out[2] = subtree_com[3 * id + 2]; break;

@@ -122,6 +122,8 @@ def model_options(model) -> dict[str, float]:
   for f in option_fields():
     if f.name.startswith("gravity_"):
       out[f.name] = float(model.gravity["xyz".index(f.name[-1])])
+    elif f.name.startswith("magnetic_"):
+      out[f.name] = float(model.magnetic["xyz".index(f.name[-1])])
     else:
       out[f.name] = getattr(model, f.name)
   return out

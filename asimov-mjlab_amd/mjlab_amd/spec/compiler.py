@@ -44,6 +44,9 @@ SENSOR_TYPES = {
   "accelerometer": 1,
   "velocimeter": 2,
   "gyro": 3,
+  "force": 4,
+  "torque": 5,
+  "magnetometer": 6,
   "jointpos": 9,
   "jointvel": 10,
   "actuatorpos": 13,
@@ -76,6 +79,9 @@ SENSOR_DIMS = {
   "accelerometer": 3,
   "velocimeter": 3,
   "gyro": 3,
+  "force": 3,
+  "torque": 3,
+  "magnetometer": 3,
   "jointpos": 1,
   "jointvel": 1,
   "actuatorpos": 1,
@@ -137,6 +143,7 @@ class Model:
   # leading static world sites (a Scene's env-origin sites): the Simulation
   # writes their poses once and the step kernel sees only the sites after them
   nsite_origin = 0
+  magnetic = np.array([0.0, -0.5, 0.0])  # models built before the option existed
 
   def __init__(self) -> None:
     self.names: dict[str, list[str]] = {}
@@ -168,7 +175,8 @@ class Model:
     """``mjModel.opt`` view (mjtIntegrator / mjtSolver / mjtCone codes)."""
     from types import SimpleNamespace
 
-    return SimpleNamespace(timestep=self.timestep, gravity=np.asarray(self.gravity), impratio=self.impratio,
+    return SimpleNamespace(timestep=self.timestep, gravity=np.asarray(self.gravity), magnetic=np.asarray(self.magnetic),
+                           impratio=self.impratio,
                            tolerance=self.tolerance, ls_tolerance=self.ls_tolerance, iterations=self.iterations,
                            ls_iterations=self.ls_iterations, integrator=self.integrator, solver=self.solver,
                            cone=self.cone)
@@ -338,6 +346,7 @@ def compile_spec(spec: Spec, nconmax: int = 0, njmax: int = 0) -> Model:
   m.nmocap = 0
   m.timestep = opt.timestep
   m.gravity = np.array(opt.gravity, np.float64)
+  m.magnetic = np.array(opt.magnetic, np.float64)
   m.impratio = opt.impratio
   m.tolerance = opt.tolerance
   m.ls_tolerance = opt.ls_tolerance

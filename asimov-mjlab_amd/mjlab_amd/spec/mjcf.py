@@ -124,6 +124,8 @@ class MjcfReader:
           setattr(spec.option, k, int(v))
         elif k == "gravity":
           spec.option.gravity = _floats(v)
+        elif k == "magnetic":
+          spec.option.magnetic = _floats(v)
         elif k in ("integrator", "cone", "solver", "jacobian"):
           setattr(spec.option, k, v.lower())
     for tag in ("tendon", "equality"):
@@ -332,7 +334,7 @@ class MjcfReader:
       s.objtype, s.objname = a["objtype"], a["objname"]
       if "reftype" in a or "refname" in a:
         s.reftype, s.refname = a["reftype"], a["refname"]
-    elif node.tag in ("gyro", "velocimeter", "accelerometer"):
+    elif node.tag in ("gyro", "velocimeter", "accelerometer", "force", "torque", "magnetometer"):
       s.objtype, s.objname = "site", a["site"]
     elif node.tag in ("subtreeangmom", "subtreecom", "subtreelinvel"):
       s.objtype, s.objname = "body", a["body"]
@@ -367,7 +369,7 @@ def read_mjcf_string(text: str, name: str = "inline.xml") -> Spec:
 
 # ---- writer: compiled model -> MJCF (for NaN dumps; MuJoCo's mj_saveModel is absent) ----
 _GEOM_NAMES = {0: "plane", 2: "sphere", 3: "capsule", 4: "ellipsoid", 5: "cylinder", 6: "box", 7: "mesh"}
-_SENSOR_TAGS = {1: "accelerometer", 2: "velocimeter", 3: "gyro", 9: "jointpos", 10: "jointvel", 13: "actuatorpos",
+_SENSOR_TAGS = {1: "accelerometer", 2: "velocimeter", 3: "gyro", 4: "force", 5: "torque", 6: "magnetometer", 9: "jointpos", 10: "jointvel", 13: "actuatorpos",
                 14: "actuatorvel", 15: "actuatorfrc", 16: "jointactuatorfrc", 18: "ballquat", 19: "ballangvel",
                 20: "jointlimitpos", 21: "jointlimitvel", 22: "jointlimitfrc", 30: "framepos", 31: "framequat", 34: "subtreecom", 35: "subtreelinvel", 36: "subtreeangmom",
                 41: "framexaxis", 42: "frameyaxis", 43: "framezaxis", 44: "framelinvel", 45: "frameangvel",
@@ -401,7 +403,7 @@ def model_to_mjcf(m) -> str:
   for s in range(int(m.nsite)):
     sites_of[int(m.site_bodyid[s])].append(s)
   out = ['<mujoco model="mjlab_amd export">', '  <compiler angle="radian" autolimits="false" inertiafromgeom="false"/>',
-         f'  <option timestep="{m.timestep:.9g}" gravity="{_fmt(m.gravity)}" impratio="{m.impratio:.9g}" '
+         f'  <option timestep="{m.timestep:.9g}" gravity="{_fmt(m.gravity)}" magnetic="{_fmt(m.magnetic)}" impratio="{m.impratio:.9g}" '
          f'tolerance="{m.tolerance:.9g}" ls_tolerance="{m.ls_tolerance:.9g}" iterations="{int(m.iterations)}" '
          f'ls_iterations="{int(m.ls_iterations)}" integrator="{ {0: "Euler", 3: "implicitfast"}.get(int(m.integrator), "Euler") }" '
          f'cone="{ {0: "pyramidal", 1: "elliptic"}[int(m.cone)] }" solver="{ {0: "PGS", 1: "CG", 2: "Newton"}[int(m.solver)] }"/>',

@@ -167,6 +167,7 @@ class KeySpec:
 class OptionSpec:
   timestep: float = 0.002
   gravity: list[float] = field(default_factory=lambda: [0.0, 0.0, -9.81])
+  magnetic: list[float] = field(default_factory=lambda: [0.0, -0.5, 0.0])  # mjOption.magnetic (magnetometer)
   impratio: float = 1.0
   tolerance: float = 1e-8
   ls_tolerance: float = 0.01

@@ -35,7 +35,8 @@
   MO(float, ls_tolerance) MO(int, iterations) MO(int, ls_iterations)         \
   MO(int, integrator) MO(int, cone) MO(int, solver) MO(float, meaninertia)   \
   MO(int, contact_sensor_maxmatch) MO(int, disableflags)                     \
-  MO(int, ls_parallel) MO(float, ls_parallel_min_step)
+  MO(int, ls_parallel) MO(float, ls_parallel_min_step) MO(float, magnetic_x)  \
+  MO(float, magnetic_y) MO(float, magnetic_z)
 
 /* ---- static (shared) model arrays ---- */
 #define MJH_MODEL_ARRAYS(MA) \

@@ -152,6 +152,21 @@ static void transform_motion(real res[6], const real vec[6], const real p[3], co
   }
 }
 
+/* a spatial force [torque; force] about c moved to point p (torque - (p - c) x force),
+   optionally rotated into the frame rot (mju_transformSpatial, flg_force 1) */
+static void transform_force(real res[6], const real vec[6], const real p[3], const real c[3], const real* rot) {
+  real dif[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]}, t[3], out[6];
+  cross3(t, dif, vec + 3);
+  out[0] = vec[0] - t[0]; out[1] = vec[1] - t[1]; out[2] = vec[2] - t[2];
+  out[3] = vec[3]; out[4] = vec[4]; out[5] = vec[5];
+  if (rot) {
+    matT_vec(res, rot, out);
+    matT_vec(res + 3, rot, out + 3);
+  } else {
+    memcpy(res, out, sizeof(out));
+  }
+}
+
 /* ---------------------------------------------------------------- workspace */
 typedef struct {
   real dist, pos[3], frame[9], friction[5], solref[2], solimp[5], includemargin;
@@ -2008,7 +2023,55 @@ static void obj_vel(const or_model* m, const ws_t* w, int type, int id, real v[6
   transform_motion(v, w->cvel + 6 * b, p, w->subtree_com + 3 * m->body_rootid[b], NULL);
 }
 
-static void sensors(const or_model* m, ws_t* w, int wi, real time, real* sd) {
+/* cfrc_int (mj_rnePostConstraint): per body I a + v x* I v minus the external
+   wrench (xfrc_applied at the body com; contact forces at the contact point:
+   - on geom1's body, + on geom2's body, world body excluded), about the root's
+   subtree com, then accumulated from the leaves to the root (6 * nbody) */
+static void cfrc_interaction(const or_model* m, ws_t* w, const real* xfrc, real* fi) {
+  const int nb = m->nbody;
+  memset(fi, 0, 6 * sizeof(real) * nb);
+  for (int b = 1; b < nb; b++) {
+    real t1[6], t2[6], t3[6];
+    inert_vec(t1, w->cinert + 10 * b, w->cacc + 6 * b);
+    inert_vec(t2, w->cinert + 10 * b, w->cvel + 6 * b);
+    cross_force(t3, w->cvel + 6 * b, t2);
+    const real* f = xfrc + 6 * b;
+    const real* c = w->subtree_com + 3 * m->body_rootid[b];
+    real r[3] = {w->xipos[3 * b] - c[0], w->xipos[3 * b + 1] - c[1], w->xipos[3 * b + 2] - c[2]}, rf[3];
+    cross3(rf, r, f);
+    for (int k = 0; k < 3; k++) {
+      fi[6 * b + k] = t1[k] + t3[k] - (f[3 + k] + rf[k]);
+      fi[6 * b + 3 + k] = t1[3 + k] + t3[3 + k] - f[k];
+    }
+  }
+  for (int ci = 0; ci < w->ncon; ci++) {
+    const contact_t* con = w->con + ci;
+    real F[6], Fw[3], Tw[3];
+    contact_force(m, w, ci, F);
+    matT_vec(Fw, con->frame, F);
+    matT_vec(Tw, con->frame, F + 3);
+    for (int side = 0; side < 2; side++) {
+      const int b = m->geom_bodyid[con->geom[side]];
+      if (b == 0) continue;
+      const real sg = side ? 1 : -1;
+      const real* c = w->subtree_com + 3 * m->body_rootid[b];
+      real r[3] = {con->pos[0] - c[0], con->pos[1] - c[1], con->pos[2] - c[2]}, t[3];
+      cross3(t, r, Fw);
+      for (int k = 0; k < 3; k++) {
+        fi[6 * b + k] -= sg * (Tw[k] + t[k]);
+        fi[6 * b + 3 + k] -= sg * Fw[k];
+      }
+    }
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    const int p = m->body_parentid[b];
+    if (p > 0)
+      for (int k = 0; k < 6; k++) fi[6 * p + k] += fi[6 * b + k];
+  }
+}
+
+static void sensors(const or_model* m, ws_t* w, int wi, real time, const real* xfrc, real* sd) {
+  real* fint = NULL;  /* cfrc_int, computed at the first force / torque sensor */
   for (int s = 0; s < m->nsensor; s++) {
     int type = m->sensor_type[s], id = m->sensor_objid[s];
     real* out = sd + m->sensor_adr[s];
@@ -2096,6 +2159,22 @@ static void sensors(const or_model* m, ws_t* w, int wi, real time, real* sd) {
           }
           break;
         }
+        break;
+      }
+      case 4: case 5: { /* force / torque: cfrc_int of the site's body at the site, in the site frame */
+        if (!fint) {
+          fint = (real*)malloc(6 * sizeof(real) * m->nbody);
+          cfrc_interaction(m, w, xfrc, fint);
+        }
+        const int b = m->site_bodyid[id];
+        real v[6];
+        transform_force(v, fint + 6 * b, w->sxpos + 3 * id, w->subtree_com + 3 * m->body_rootid[b], w->sxmat + 9 * id);
+        memcpy(out, type == 4 ? v + 3 : v, 3 * sizeof(real));
+        break;
+      }
+      case 6: { /* magnetometer: the global field in the site frame */
+        const real mg[3] = {m->magnetic_x, m->magnetic_y, m->magnetic_z};
+        matT_vec(out, w->sxmat + 9 * id, mg);
         break;
       }
       case 13: out[0] = w->act_length[id]; break;
@@ -2292,6 +2371,7 @@ static void sensors(const or_model* m, ws_t* w, int wi, real time, real* sd) {
         out[k] = out[k] < -cut ? -cut : (out[k] > cut ? cut : out[k]);
       }
   }
+  free(fint);
 }
 
 /* ---------------------------------------------------------------- driver */
@@ -2349,7 +2429,7 @@ static void world_step(const or_model* m, or_data* d, int wi, int integrate, ws_
   solve(m, w, d->qacc_warmstart + (size_t)wi * nv);
   rne(m, w, w->qacc, NULL); /* cacc with constraint accelerations (accelerometer) */
   real* sd = d->sensordata + (size_t)wi * m->nsensordata;
-  sensors(m, w, wi, d->time[wi], sd);
+  sensors(m, w, wi, d->time[wi], xfrc, sd);
 
   /* outputs of the forward pass */
   memcpy(d->xpos + (size_t)wi * nb * 3, w->xpos, sizeof(real) * nb * 3);

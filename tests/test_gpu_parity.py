@@ -795,6 +795,35 @@ def test_builtin_sensor_parity():
     np.testing.assert_allclose(got["sensordata"][:, a:a + 4], ref["sensordata"][:, a:a + 4], atol=2e-5, err_msg=name)
 
 
+def test_force_torque_sensor_contact_parity():
+  """force / torque sensors with contacts on the HIP step against the oracle:
+  tests/test_sensors_builtin.py's box-and-ball stack in random poses against
+  the floor (the contact wrenches enter cfrc_int), one step; the oracle's
+  cfrc_int is pinned there by the resting stack's weights."""
+  from tests import test_sensors_builtin as tsb
+  from mjlab_amd.spec.compiler import compile_spec
+  from mjlab_amd.spec.mjcf import read_mjcf_string
+  from mjlab_amd.utils import rot
+
+  n = 256
+  m = compile_spec(read_mjcf_string(tsb.STACK_SCENE), 16, 64)
+  rng = np.random.default_rng(62)
+  q = np.zeros((n, 7))
+  q[:, :2] = rng.uniform(-0.3, 0.3, (n, 2))
+  q[:, 2] = rng.uniform(0.05, 0.2, n)
+  for w in range(n):
+    ax = rng.normal(size=3)
+    q[w, 3:7] = rot.axis_angle_to_quat(ax / np.linalg.norm(ax), rng.uniform(0, 0.6))
+  st = {"qpos": q, "qvel": rng.normal(scale=0.3, size=(n, 6)), "qacc_warmstart": np.zeros((n, 6))}
+  sim = Simulation(n, SimulationCfg(nconmax=16, njmax=64, mujoco=MujocoCfg(timestep=0.002)), m, DEV)
+  put(sim, st)
+  sim.step()
+  got = get(sim, n)
+  ref = Oracle(m).run(n, st, integrate=True, follow=got)
+  assert (got["ncon"] > 0).mean() > 0.5
+  assert_parity(got, ref, n, tag=" force/torque sensors")
+
+
 @pytest.mark.parametrize("iterations", [1, 5])
 def test_pgs_solver_parity(iterations):
   """opt.solver = PGS (MuJoCo's projected Gauss-Seidel on the dual; the

@@ -64,6 +64,9 @@ SENSOR_SCENE = """<mujoco><option timestep="0.002" gravity="0.3 -0.2 -9.81"/>
   <jointlimitpos name="jlp" joint="hinge"/>
   <jointlimitvel name="jlv" joint="hinge"/>
   <jointlimitfrc name="jlf" joint="hinge"/>
+  <force name="frc" site="armtip"/>
+  <torque name="trq" site="armtip"/>
+  <magnetometer name="mag" site="tip"/>
   <clock name="clk"/>
   <e_potential name="epot"/>
   <e_kinetic name="ekin"/>
@@ -233,6 +236,91 @@ def test_frame_acceleration_sensors():
     a_tip = a_org + np.cross(al_a, r2) + np.cross(om[arm], np.cross(om[arm], r2))
     np.testing.assert_allclose(_sensor(m, out, w, "fla_site"), a_tip - g, atol=1e-8)
     np.testing.assert_allclose(_sensor(m, out, w, "faa_body"), al_a, atol=1e-8)
+
+
+def test_force_torque_magnetometer_sensors():
+  """force / torque at a site = the wrench the site body's subtree receives
+  from its parent (Newton-Euler of the arm alone: m (a_com - g) - F_ext and
+  I alpha + w x I w + (com - site) x m (a_com - g) minus the external torque
+  about the site), in the site frame; an xfrc_applied on the arm is the
+  external wrench. magnetometer = the global field in the site frame."""
+  m = _model()
+  n = 3
+  rng = np.random.default_rng(10)
+  st = _state(rng, n)
+  arm = _id(m, "body", "arm")
+  xfrc = np.zeros((n, int(m.nbody), 6))
+  xfrc[:, arm] = rng.normal(size=(n, 6))
+  st["xfrc_applied"] = xfrc.reshape(n, -1)
+  out = Oracle(m).run(n, st, integrate=False)
+  g = np.asarray(m.gravity)
+  base = _id(m, "body", "base")
+  for w in range(n):
+    body, ibody, geom, site = _frames(m, out, w)
+    om, pvel = _velocities(m, st, out, w)
+    xpos = out["xpos"][w].reshape(-1, 3)
+    qv, qa = st["qvel"][w], out["qacc"][w]
+    Rb, Ra = body(base)[1], body(arm)[1]
+    al_b = Rb @ qa[3:6]
+    ax = Ra @ np.array([0, 1.0, 0])
+    al_a = al_b + ax * qa[6] + np.cross(om[base], ax * qv[6])
+    r = xpos[arm] - xpos[base]
+    a_org = qa[:3] + np.cross(al_b, r) + np.cross(om[base], np.cross(om[base], r))
+    pc, Ri = ibody(arm)
+    rc = pc - xpos[arm]
+    a_c = a_org + np.cross(al_a, rc) + np.cross(om[arm], np.cross(om[arm], rc))
+    mass = float(np.asarray(m.body_mass)[arm])
+    I = Ri @ np.diag(np.asarray(m.body_inertia).reshape(-1, 3)[arm]) @ Ri.T
+    F_ext, T_ext = xfrc[w, arm, :3], xfrc[w, arm, 3:]
+    ps, Rs = site(_id(m, "site", "armtip"))
+    f = mass * (a_c - g) - F_ext
+    t = I @ al_a + np.cross(om[arm], I @ om[arm]) + np.cross(pc - ps, mass * (a_c - g)) - (T_ext + np.cross(pc - ps, F_ext))
+    np.testing.assert_allclose(_sensor(m, out, w, "frc"), Rs.T @ f, atol=1e-8)
+    np.testing.assert_allclose(_sensor(m, out, w, "trq"), Rs.T @ t, atol=1e-8)
+    _, Rt = site(_id(m, "site", "tip"))
+    np.testing.assert_allclose(_sensor(m, out, w, "mag"), Rt.T @ np.array([0, -0.5, 0]), atol=1e-12)
+
+
+STACK_SCENE = """<mujoco><option timestep="0.002" gravity="0 0 -9.81"/>
+<worldbody>
+  <geom name="floor" type="plane" size="0 0 0.05"/>
+  <body name="box" pos="0 0 0.1">
+    <freejoint/>
+    <geom name="boxg" type="box" size="0.1 0.1 0.1" mass="2"/>
+    <site name="base_site" pos="0 0 -0.05"/>
+    <body name="top" pos="0 0 0.15">
+      <geom name="topg" type="sphere" size="0.05" mass="0.7" contype="0" conaffinity="0"/>
+      <site name="top_site" pos="0 0 -0.05"/>
+    </body>
+  </body>
+</worldbody>
+<sensor>
+  <force name="f_top" site="top_site"/>
+  <torque name="t_top" site="top_site"/>
+  <force name="f_box" site="base_site"/>
+  <torque name="t_box" site="base_site"/>
+</sensor>
+</mujoco>"""
+
+
+def test_force_sensor_carries_the_weight_above_it():
+  """A box with a welded ball on top, resting on the floor: the site under the
+  ball carries the ball's weight (0, 0, m_top g), the box's own site carries
+  nothing from a parent (the contact forces cancel the stack's weight: the
+  contact wrench enters cfrc_int with the right sign and point)."""
+  m = compile_spec(read_mjcf_string(STACK_SCENE), 8, 64)
+  orc = Oracle(m)
+  st = {"qpos": np.array([[0, 0, 0.1, 1, 0, 0, 0]])}
+  for _ in range(400):  # settle
+    out = orc.run(1, st, integrate=True)
+    st = {k: out[k] for k in ("qpos", "qvel", "qacc_warmstart", "time")}
+  out = orc.run(1, st, integrate=False)
+  assert out["ncon"][0, 0] >= 4
+  sens = {nm: _sensor(m, out, 0, nm) for nm in ("f_top", "t_top", "f_box", "t_box")}
+  np.testing.assert_allclose(sens["f_top"], [0, 0, 0.7 * 9.81], atol=1e-6)
+  np.testing.assert_allclose(sens["t_top"], [0, 0, 0], atol=1e-6)
+  np.testing.assert_allclose(sens["f_box"], [0, 0, 0], atol=2e-3)
+  np.testing.assert_allclose(sens["t_box"], [0, 0, 0], atol=2e-3)
 
 
 def test_joint_limit_sensors():
