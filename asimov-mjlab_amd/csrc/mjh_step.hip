@@ -3901,7 +3901,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         continue;
       }
 #ifndef MJH_NO_EXT
-      if (type == 48 || type == 49) {
+      if (Z.nsensor_ext > 0 && (type == 48 || type == 49)) {  // compile-time 0 in the benchmark models' instances
         // e_potential (mj_energyPos: gravity over bodies + joint springs) /
         // e_kinetic (mj_energyVel: qvel' M qvel / 2, M rows from the factor pass)
         float e = 0.f, z = 0.f;
@@ -3990,7 +3990,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
 #ifndef MJH_NO_FT
     // force / torque sensors (mj_sensorAcc), in a pass of their own so that no
     // state of theirs is live in the loop above
-    for (int s = 0; s < Z.nsensor; s++) {
+    for (int s = 0; s < (Z.nsensor_ext > 0 ? Z.nsensor : 0); s++) {
       const int type = IMG_I(sensor_type)[s];
       if (type != 4 && type != 5) continue;
       const int id = IMG_I(sensor_objid)[s];
@@ -4044,44 +4044,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       v[0] = cv[0]; v[1] = cv[1]; v[2] = cv[2];
       v[3] = cv[3] - t[0]; v[4] = cv[4] - t[1]; v[5] = cv[5] - t[2];
     };
-    // remaining sensors are independent and cheap: one lane each
-    for (int s = tid; s < Z.nsensor; s += NT) {
-      const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
-      if (type == 40 || type == 35 || type == 36 || type == 48 || type == 49 || type == 4 || type == 5) continue;
-      float* out = sd + adr;
+    // the sensor types outside the benchmark tasks' set (Sizes::nsensor_ext)
+    auto ext_sensor = [&](int s, int type, int id, float* out) {
       switch (type) {
-        case 3: {  // gyro
-          const int b = IMG_I(site_bodyid)[id];
-          float r[3];
-          matT_vec(r, sxmat + 9 * id, cvel + 6 * b);
-          out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
-          break;
-        }
-        case 2:
-        case 1: {  // velocimeter / accelerometer
-          const int b = IMG_I(site_bodyid)[id];
-          const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
-          const float* sp = sxpos + 3 * id;
-          float dif[3] = {sp[0] - c[0], sp[1] - c[1], sp[2] - c[2]}, t[3], lin[3], r[3];
-          const float* v = cvel + 6 * b;
-          cross3(t, dif, v);
-          lin[0] = v[3] - t[0]; lin[1] = v[4] - t[1]; lin[2] = v[5] - t[2];
-          matT_vec(r, sxmat + 9 * id, lin);
-          if (type == 2) {
-            out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
-          } else {
-            const float* a = cacc + 6 * b;
-            float al[3], ar[3], wl[3], cor[3];
-            cross3(t, dif, a);
-            al[0] = a[3] - t[0]; al[1] = a[4] - t[1]; al[2] = a[5] - t[2];
-            matT_vec(ar, sxmat + 9 * id, al);
-            matT_vec(wl, sxmat + 9 * id, v);
-            cross3(cor, wl, r);
-            out[0] = ar[0] + cor[0]; out[1] = ar[1] + cor[1]; out[2] = ar[2] + cor[2];
-          }
-          break;
-        }
-#ifndef MJH_NO_EXT
         case 30:
         case 41:
         case 42:
@@ -4200,11 +4165,52 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
           break;
         }
-#endif
+        default:
+          break;
+      }
+    };
+    // remaining sensors are independent and cheap: one lane each
+    for (int s = tid; s < Z.nsensor; s += NT) {
+      const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
+      if (type == 40 || type == 35 || type == 36 || type == 48 || type == 49 || type == 4 || type == 5) continue;
+      float* out = sd + adr;
+      switch (type) {
+        case 3: {  // gyro
+          const int b = IMG_I(site_bodyid)[id];
+          float r[3];
+          matT_vec(r, sxmat + 9 * id, cvel + 6 * b);
+          out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
+          break;
+        }
+        case 2:
+        case 1: {  // velocimeter / accelerometer
+          const int b = IMG_I(site_bodyid)[id];
+          const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
+          const float* sp = sxpos + 3 * id;
+          float dif[3] = {sp[0] - c[0], sp[1] - c[1], sp[2] - c[2]}, t[3], lin[3], r[3];
+          const float* v = cvel + 6 * b;
+          cross3(t, dif, v);
+          lin[0] = v[3] - t[0]; lin[1] = v[4] - t[1]; lin[2] = v[5] - t[2];
+          matT_vec(r, sxmat + 9 * id, lin);
+          if (type == 2) {
+            out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
+          } else {
+            const float* a = cacc + 6 * b;
+            float al[3], ar[3], wl[3], cor[3];
+            cross3(t, dif, a);
+            al[0] = a[3] - t[0]; al[1] = a[4] - t[1]; al[2] = a[5] - t[2];
+            matT_vec(ar, sxmat + 9 * id, al);
+            matT_vec(wl, sxmat + 9 * id, v);
+            cross3(cor, wl, r);
+            out[0] = ar[0] + cor[0]; out[1] = ar[1] + cor[1]; out[2] = ar[2] + cor[2];
+          }
+          break;
+        }
         case 9: out[0] = qpos[IMG_I(jnt_qposadr)[id]]; break;
         case 10: out[0] = qvel[IMG_I(jnt_dofadr)[id]]; break;
         case 34: out[0] = subtree_com[3 * id]; out[1] = subtree_com[3 * id + 1]; out[2] = subtree_com[3 * id + 2]; break;
         default:
+          if (Z.nsensor_ext > 0) ext_sensor(s, type, id, out);  // compile-time 0 in the benchmark models' instances
           break;
       }
       const float cut = IMG_F(sensor_cutoff)[s];

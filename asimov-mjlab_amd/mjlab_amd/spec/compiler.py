@@ -109,6 +109,9 @@ SENSOR_DIMS = {
   "e_kinetic": 1,
   "clock": 1,
 }
+# the sensor types the step kernel evaluates on every path (the benchmark tasks'
+# set); the others count into Model.nsensor_ext
+BASE_SENSOR_CODES = {1, 2, 3, 9, 10, 34, 35, 36, 40}
 # sensors whose values are unit quaternions or axes: no cutoff (mjDATATYPE_QUATERNION / _AXIS)
 SENSOR_NO_CUTOFF = {"framequat", "ballquat", "framexaxis", "frameyaxis", "framezaxis"}
 # Contact sensor data fields: bit -> width (src/mjlab/sensor/contact_sensor.py:16-34).
@@ -143,6 +146,7 @@ class Model:
   # leading static world sites (a Scene's env-origin sites): the Simulation
   # writes their poses once and the step kernel sees only the sites after them
   nsite_origin = 0
+  nsensor_ext = 0
   magnetic = np.array([0.0, -0.5, 0.0])  # models built before the option existed
 
   def __init__(self) -> None:
@@ -661,6 +665,10 @@ def _compile_sensors(m: Model, spec: Spec) -> None:
     m.sensor_cutoff[i] = s.cutoff
     adr += dim
   m.nsensordata = adr
+  # sensors outside the benchmark tasks' set (a size, so it is part of the
+  # specialised kernels' plans: an instance built for a model without them
+  # carries none of their code)
+  m.nsensor_ext = int(sum(1 for t in m.sensor_type if int(t) not in BASE_SENSOR_CODES))
 
 
 def _kinematics0(m: Model):

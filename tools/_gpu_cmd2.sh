@@ -1,6 +1,6 @@
 set -e
 cd "${GRAFT_REPO_ROOT:-.}"
-bash tools/gpu_libab.sh r05u chain
-MJH_LIB=asimov-mjlab_amd/mjlab_amd/variants/libmjh_chain.so timeout -k 10 120 python tools/kernel_bench.py 4096 40 Mjlab-Velocity-Flat-Unitree-G1 > gpurun_out/r05u/kb.log 2>&1
-timeout -k 10 120 python tools/kernel_bench.py 4096 40 Mjlab-Velocity-Flat-Unitree-G1 >> gpurun_out/r05u/kb.log 2>&1
-grep ms/launch gpurun_out/r05u/kb.log
+O=gpurun_out/r05w
+mkdir -p $O
+MJH_LIB=asimov-mjlab_amd/mjlab_amd/variants/libmjh_head.so timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "diagonal_sliding or elliptic" > $O/head.log 2>&1 || { tail -5 $O/head.log; exit 1; }
+tail -2 $O/head.log
