@@ -1632,6 +1632,85 @@ template <int K> __device__ __forceinline__ ImgOff spec_imgoff(const ImgOff& a) 
 // out[3]. Out of line and recomputed per sensor: only models with these
 // sensors call it, and inlined it would cost the step kernel registers on
 // every path. Every lane of the wave calls it.
+// ---- rays (mj_ray's primitive intersections): the distance along a unit ray
+// to the geom's surface, -1 for no hit; a x^2 + 2 b x + c = 0 gives the
+// smallest non-negative root. Out of line: only rangefinder models call it.
+__device__ __forceinline__ float ray_quad(float a, float b, float c, float (&x)[2]) {
+  float det = b * b - a * c;
+  if (det < MJH_MINVAL) { x[0] = x[1] = -1.f; return -1.f; }
+  det = sqrtf(det);
+  x[0] = (-b - det) / a;
+  x[1] = (-b + det) / a;
+  return x[0] >= 0.f ? x[0] : (x[1] >= 0.f ? x[1] : -1.f);
+}
+
+__device__ __noinline__ float ray_geom(int type, const float* size, const float* pos, const float* mat, const float* pnt,
+                                       const float* vec) {
+  const float dif[3] = {pnt[0] - pos[0], pnt[1] - pos[1], pnt[2] - pos[2]};
+  float lp[3], lv[3], xx[2];
+  matT_vec(lp, mat, dif);
+  matT_vec(lv, mat, vec);
+  float x = -1.f, sol;
+  switch (type) {
+    case 0: {  // plane: from the front side, within the rendered rectangle when sized
+      if (lv[2] > -MJH_MINVAL) return -1.f;
+      x = -lp[2] / lv[2];
+      if (x < 0.f) return -1.f;
+      const float p0 = lp[0] + x * lv[0], p1 = lp[1] + x * lv[1];
+      return ((size[0] <= 0.f || fabsf(p0) <= size[0]) && (size[1] <= 0.f || fabsf(p1) <= size[1])) ? x : -1.f;
+    }
+    case 2:
+      return ray_quad(dot3(lv, lv), dot3(lv, lp), dot3(lp, lp) - size[0] * size[0], xx);
+    case 3: {  // capsule: the round side between the flat ends, then the two caps
+      sol = ray_quad(lv[0] * lv[0] + lv[1] * lv[1], lv[0] * lp[0] + lv[1] * lp[1],
+                     lp[0] * lp[0] + lp[1] * lp[1] - size[0] * size[0], xx);
+      if (sol >= 0.f && fabsf(lp[2] + sol * lv[2]) <= size[1]) x = sol;
+      for (int side = -1; side <= 1; side += 2) {
+        const float ld[3] = {lp[0], lp[1], lp[2] - side * size[1]};
+        ray_quad(dot3(lv, lv), dot3(lv, ld), dot3(ld, ld) - size[0] * size[0], xx);
+        for (int i = 0; i < 2; i++)
+          if (xx[i] >= 0.f && side * (lp[2] + xx[i] * lv[2]) >= size[1] && (x < 0.f || xx[i] < x)) x = xx[i];
+      }
+      return x;
+    }
+    case 4: {  // ellipsoid
+      float a = 0.f, b = 0.f, c = -1.f;
+      for (int i = 0; i < 3; i++) {
+        const float si = 1.f / (size[i] * size[i]);
+        a += si * lv[i] * lv[i]; b += si * lv[i] * lp[i]; c += si * lp[i] * lp[i];
+      }
+      return ray_quad(a, b, c, xx);
+    }
+    case 5: {  // cylinder: the flat faces within the radius, then the round side
+      if (fabsf(lv[2]) > MJH_MINVAL)
+        for (int side = -1; side <= 1; side += 2) {
+          sol = (side * size[1] - lp[2]) / lv[2];
+          if (sol < 0.f) continue;
+          const float p0 = lp[0] + sol * lv[0], p1 = lp[1] + sol * lv[1];
+          if (p0 * p0 + p1 * p1 <= size[0] * size[0] && (x < 0.f || sol < x)) x = sol;
+        }
+      sol = ray_quad(lv[0] * lv[0] + lv[1] * lv[1], lv[0] * lp[0] + lv[1] * lp[1],
+                     lp[0] * lp[0] + lp[1] * lp[1] - size[0] * size[0], xx);
+      if (sol >= 0.f && fabsf(lp[2] + sol * lv[2]) <= size[1] && (x < 0.f || sol < x)) x = sol;
+      return x;
+    }
+    case 6:  // box: the six faces
+      for (int i = 0; i < 3; i++) {
+        if (fabsf(lv[i]) <= MJH_MINVAL) continue;
+        for (int side = -1; side <= 1; side += 2) {
+          sol = (side * size[i] - lp[i]) / lv[i];
+          if (sol < 0.f) continue;
+          const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+          if (fabsf(lp[i1] + sol * lv[i1]) <= size[i1] && fabsf(lp[i2] + sol * lv[i2]) <= size[i2] && (x < 0.f || sol < x))
+            x = sol;
+        }
+      }
+      return x;
+    default:
+      return -1.f;
+  }
+}
+
 #ifndef MJH_FT_ATTR
 #define MJH_FT_ATTR __noinline__
 #endif
@@ -4158,6 +4237,23 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           break;
         }
         case 50: out[0] = DP(time)[W]; break;
+        case 7: {  // rangefinder (mj_ray along the site's z axis; not the site body's geoms, not rgba alpha 0)
+          const float* R = sxmat + 9 * id;
+          const float vec[3] = {R[2], R[5], R[8]};
+          const float* rgba = WFIELD(geom_rgba);
+          const int bex = IMG_I(site_bodyid)[id];
+          float best = -1.f;
+          for (int g = 0; g < Z.ngeom; g++) {
+            if (IMG_I(geom_bodyid)[g] == bex || rgba[4 * g + 3] == 0.f) continue;
+            float gp[3], gR[9];
+            int gb;
+            obj_frame(5, g, gp, gR, gb);
+            const float dd = ray_geom(IMG_I(geom_type)[g], IMG_F(geom_size) + 3 * g, gp, gR, sxpos + 3 * id, vec);
+            if (dd >= 0.f && (best < 0.f || dd < best)) best = dd;
+          }
+          out[0] = best;
+          break;
+        }
         case 6: {  // magnetometer: the global field in the site frame
           const float mg[3] = {m.magnetic_x, m.magnetic_y, m.magnetic_z};
           float r[3];
@@ -4214,7 +4310,9 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           break;
       }
       const float cut = IMG_F(sensor_cutoff)[s];
-      if (cut > 0.f && type != 31 && type != 18 && (type < 41 || type > 43))  // quaternions and unit axes are not clipped
+      if (cut > 0.f && type == 7)  // rangefinder (mjDATATYPE_POSITIVE): clipped above only, a miss stays -1
+        out[0] = fminf(out[0], cut);
+      else if (cut > 0.f && type != 31 && type != 18 && (type < 41 || type > 43))  // quaternions and unit axes are not clipped
         for (int k = 0; k < IMG_I(sensor_dim)[s]; k++) out[k] = clampf(out[k], -cut, cut);
     }
   }

@@ -47,6 +47,7 @@ SENSOR_TYPES = {
   "force": 4,
   "torque": 5,
   "magnetometer": 6,
+  "rangefinder": 7,
   "jointpos": 9,
   "jointvel": 10,
   "actuatorpos": 13,
@@ -82,6 +83,7 @@ SENSOR_DIMS = {
   "force": 3,
   "torque": 3,
   "magnetometer": 3,
+  "rangefinder": 1,
   "jointpos": 1,
   "jointvel": 1,
   "actuatorpos": 1,

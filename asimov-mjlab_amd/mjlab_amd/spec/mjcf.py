@@ -334,7 +334,7 @@ class MjcfReader:
       s.objtype, s.objname = a["objtype"], a["objname"]
       if "reftype" in a or "refname" in a:
         s.reftype, s.refname = a["reftype"], a["refname"]
-    elif node.tag in ("gyro", "velocimeter", "accelerometer", "force", "torque", "magnetometer"):
+    elif node.tag in ("gyro", "velocimeter", "accelerometer", "force", "torque", "magnetometer", "rangefinder"):
       s.objtype, s.objname = "site", a["site"]
     elif node.tag in ("subtreeangmom", "subtreecom", "subtreelinvel"):
       s.objtype, s.objname = "body", a["body"]
@@ -369,7 +369,7 @@ def read_mjcf_string(text: str, name: str = "inline.xml") -> Spec:
 
 # ---- writer: compiled model -> MJCF (for NaN dumps; MuJoCo's mj_saveModel is absent) ----
 _GEOM_NAMES = {0: "plane", 2: "sphere", 3: "capsule", 4: "ellipsoid", 5: "cylinder", 6: "box", 7: "mesh"}
-_SENSOR_TAGS = {1: "accelerometer", 2: "velocimeter", 3: "gyro", 4: "force", 5: "torque", 6: "magnetometer", 9: "jointpos", 10: "jointvel", 13: "actuatorpos",
+_SENSOR_TAGS = {1: "accelerometer", 2: "velocimeter", 3: "gyro", 4: "force", 5: "torque", 6: "magnetometer", 7: "rangefinder", 9: "jointpos", 10: "jointvel", 13: "actuatorpos",
                 14: "actuatorvel", 15: "actuatorfrc", 16: "jointactuatorfrc", 18: "ballquat", 19: "ballangvel",
                 20: "jointlimitpos", 21: "jointlimitvel", 22: "jointlimitfrc", 30: "framepos", 31: "framequat", 34: "subtreecom", 35: "subtreelinvel", 36: "subtreeangmom",
                 41: "framexaxis", 42: "frameyaxis", 43: "framezaxis", 44: "framelinvel", 45: "frameangvel",

@@ -2070,6 +2070,100 @@ static void cfrc_interaction(const or_model* m, ws_t* w, const real* xfrc, real*
   }
 }
 
+/* ---- rays (mj_ray's primitive intersections, engine_ray.c): distance along a
+   unit ray to the geom's surface, -1 for no hit; a x^2 + 2 b x + c = 0 gives
+   the smallest non-negative root (ray_quad) */
+static real ray_quad(real a, real b, real c, real x[2]) {
+  real det = b * b - a * c;
+  if (det < MINVAL) { x[0] = x[1] = -1; return -1; }
+  det = sqrt(det);
+  x[0] = (-b - det) / a;
+  x[1] = (-b + det) / a;
+  return x[0] >= 0 ? x[0] : (x[1] >= 0 ? x[1] : -1);
+}
+
+static real ray_geom(int type, const real* size, const real* pos, const real* mat, const real* pnt, const real* vec) {
+  real dif[3] = {pnt[0] - pos[0], pnt[1] - pos[1], pnt[2] - pos[2]}, lp[3], lv[3], xx[2];
+  matT_vec(lp, mat, dif);
+  matT_vec(lv, mat, vec);
+  real x = -1, sol;
+  switch (type) {
+    case 0: { /* plane: from the front side, within the rendered rectangle when sized */
+      if (lv[2] > -MINVAL) return -1;
+      x = -lp[2] / lv[2];
+      if (x < 0) return -1;
+      const real p0 = lp[0] + x * lv[0], p1 = lp[1] + x * lv[1];
+      return ((size[0] <= 0 || fabs(p0) <= size[0]) && (size[1] <= 0 || fabs(p1) <= size[1])) ? x : -1;
+    }
+    case 2: /* sphere */
+      return ray_quad(dot3(lv, lv), dot3(lv, lp), dot3(lp, lp) - size[0] * size[0], xx);
+    case 3: { /* capsule: the round side between the flat ends, then the two caps */
+      sol = ray_quad(lv[0] * lv[0] + lv[1] * lv[1], lv[0] * lp[0] + lv[1] * lp[1],
+                     lp[0] * lp[0] + lp[1] * lp[1] - size[0] * size[0], xx);
+      if (sol >= 0 && fabs(lp[2] + sol * lv[2]) <= size[1]) x = sol;
+      for (int side = -1; side <= 1; side += 2) {
+        real ld[3] = {lp[0], lp[1], lp[2] - side * size[1]};
+        ray_quad(dot3(lv, lv), dot3(lv, ld), dot3(ld, ld) - size[0] * size[0], xx);
+        for (int i = 0; i < 2; i++)
+          if (xx[i] >= 0 && side * (lp[2] + xx[i] * lv[2]) >= size[1] && (x < 0 || xx[i] < x)) x = xx[i];
+      }
+      return x;
+    }
+    case 4: { /* ellipsoid */
+      real a = 0, b = 0, c = -1;
+      for (int i = 0; i < 3; i++) {
+        const real si = 1 / (size[i] * size[i]);
+        a += si * lv[i] * lv[i]; b += si * lv[i] * lp[i]; c += si * lp[i] * lp[i];
+      }
+      return ray_quad(a, b, c, xx);
+    }
+    case 5: { /* cylinder: the flat faces within the radius, then the round side */
+      if (fabs(lv[2]) > MINVAL)
+        for (int side = -1; side <= 1; side += 2) {
+          sol = (side * size[1] - lp[2]) / lv[2];
+          if (sol < 0) continue;
+          const real p0 = lp[0] + sol * lv[0], p1 = lp[1] + sol * lv[1];
+          if (p0 * p0 + p1 * p1 <= size[0] * size[0] && (x < 0 || sol < x)) x = sol;
+        }
+      sol = ray_quad(lv[0] * lv[0] + lv[1] * lv[1], lv[0] * lp[0] + lv[1] * lp[1],
+                     lp[0] * lp[0] + lp[1] * lp[1] - size[0] * size[0], xx);
+      if (sol >= 0 && fabs(lp[2] + sol * lv[2]) <= size[1] && (x < 0 || sol < x)) x = sol;
+      return x;
+    }
+    case 6: /* box: the six faces */
+      for (int i = 0; i < 3; i++) {
+        if (fabs(lv[i]) <= MINVAL) continue;
+        for (int side = -1; side <= 1; side += 2) {
+          sol = (side * size[i] - lp[i]) / lv[i];
+          if (sol < 0) continue;
+          const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+          if (fabs(lp[i1] + sol * lv[i1]) <= size[i1] && fabs(lp[i2] + sol * lv[i2]) <= size[i2] && (x < 0 || sol < x))
+            x = sol;
+        }
+      }
+      return x;
+    default:
+      return -1;
+  }
+}
+
+/* rangefinder (mj_sensorPos -> mj_ray): along the site's z axis, every geom but
+   the site body's and the invisible ones (rgba alpha 0), nearest hit or -1 */
+static real rangefinder(const or_model* m, const ws_t* w, int wi, int site) {
+  const real* R = w->sxmat + 9 * site;
+  const real vec[3] = {R[2], R[5], R[8]};
+  const real* rgba = WF(m, geom_rgba, wi);
+  const real* gsize = m->geom_size;
+  const int bex = m->site_bodyid[site];
+  real best = -1;
+  for (int g = 0; g < m->ngeom; g++) {
+    if (m->geom_bodyid[g] == bex || rgba[4 * g + 3] == 0) continue;
+    const real d = ray_geom(m->geom_type[g], gsize + 3 * g, w->gxpos + 3 * g, w->gxmat + 9 * g, w->sxpos + 3 * site, vec);
+    if (d >= 0 && (best < 0 || d < best)) best = d;
+  }
+  return best;
+}
+
 static void sensors(const or_model* m, ws_t* w, int wi, real time, const real* xfrc, real* sd) {
   real* fint = NULL;  /* cfrc_int, computed at the first force / torque sensor */
   for (int s = 0; s < m->nsensor; s++) {
@@ -2172,6 +2266,7 @@ static void sensors(const or_model* m, ws_t* w, int wi, real time, const real* x
         memcpy(out, type == 4 ? v + 3 : v, 3 * sizeof(real));
         break;
       }
+      case 7: out[0] = rangefinder(m, w, wi, id); break;
       case 6: { /* magnetometer: the global field in the site frame */
         const real mg[3] = {m->magnetic_x, m->magnetic_y, m->magnetic_z};
         matT_vec(out, w->sxmat + 9 * id, mg);
@@ -2365,7 +2460,9 @@ static void sensors(const or_model* m, ws_t* w, int wi, real time, const real* x
       }
     }
     /* cutoff: not for quaternions and axes (mjDATATYPE_QUATERNION / _AXIS) or contact records */
-    if (m->sensor_cutoff[s] > 0 && type != 31 && type != 18 && (type < 41 || type > 43) && type != 40)
+    if (m->sensor_cutoff[s] > 0 && type == 7) { /* mjDATATYPE_POSITIVE: clipped above only (a miss stays -1) */
+      if (out[0] > m->sensor_cutoff[s]) out[0] = m->sensor_cutoff[s];
+    } else if (m->sensor_cutoff[s] > 0 && type != 31 && type != 18 && (type < 41 || type > 43) && type != 40)
       for (int k = 0; k < m->sensor_dim[s]; k++) {
         real cut = m->sensor_cutoff[s];
         out[k] = out[k] < -cut ? -cut : (out[k] > cut ? cut : out[k]);

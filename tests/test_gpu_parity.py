@@ -824,6 +824,41 @@ def test_force_torque_sensor_contact_parity():
   assert_parity(got, ref, n, tag=" force/torque sensors")
 
 
+def test_rangefinder_parity():
+  """rangefinder (mj_ray over plane, sphere, box, capsule, cylinder and
+  ellipsoid geoms, the site body's and invisible geoms skipped) on the HIP
+  forward against the oracle: the probe of tests/test_sensors_builtin.py's ray
+  scene at random positions and orientations; distances to 1e-4 m, misses
+  (-1) identical. The oracle is pinned there by closed-form distances."""
+  from tests import test_sensors_builtin as tsb
+  from mjlab_amd.spec.compiler import compile_spec
+  from mjlab_amd.spec.mjcf import read_mjcf_string
+
+  n = 256
+  m = compile_spec(read_mjcf_string(tsb.RAY_SCENE), 8, 64)
+  rng = np.random.default_rng(63)
+  q = np.zeros((n, 7))
+  q[:, :3] = rng.uniform([-0.5, -0.5, 0.5], [0.5, 0.5, 1.5], (n, 3))
+  quat = rng.normal(size=(n, 4))
+  q[:, 3:] = quat / np.linalg.norm(quat, axis=1, keepdims=True)
+  st = {"qpos": q, "qvel": np.zeros((n, 6))}
+  sim = Simulation(n, SimulationCfg(nconmax=8, njmax=64, mujoco=MujocoCfg(timestep=0.002)), m, DEV)
+  put(sim, st)
+  sim.forward()
+  got = get(sim, n)["sensordata"]
+  ref = Oracle(m).run(n, st, integrate=False)["sensordata"]
+  ref32 = Oracle(m, precision="f32").run(n, st, integrate=False)["sensordata"]
+  # a grazing ray is ill-conditioned (a plane hit at incidence c moves by ~eps/c,
+  # a near-tangent sphere or capsule hit can flip to the geom behind it): an
+  # entry passes within 1e-4 m + 1e-3 relative of the float64 oracle, or of the
+  # float32 build of the same oracle code (the same flip at float32)
+  tol = 1e-4 + 1e-3 * np.abs(ref)
+  ok = (np.abs(got - ref) <= tol) | (np.abs(got - ref32) <= tol)
+  assert ok.all(), [(int(w), int(k), float(got[w, k]), float(ref[w, k]), float(ref32[w, k])) for w, k in np.argwhere(~ok)[:5]]
+  assert (np.abs(got - ref) <= tol).mean() > 0.99  # the float32 exemption stays rare
+  assert (ref > 0).mean() > 0.3 and (ref < 0).any()
+
+
 @pytest.mark.parametrize("iterations", [1, 5])
 def test_pgs_solver_parity(iterations):
   """opt.solver = PGS (MuJoCo's projected Gauss-Seidel on the dual; the

@@ -427,3 +427,56 @@ def test_sensor_object_checks():
   assert bad != SENSOR_SCENE
   with pytest.raises(ValueError, match="no reference frame"):
     compile_spec(read_mjcf_string(bad), 8, 64)
+
+
+C45 = np.cos(np.pi / 4)
+RAY_SCENE = f"""<mujoco><option timestep="0.002"/>
+<worldbody>
+  <geom name="floor" type="plane" size="0 0 0.05"/>
+  <geom name="ball" type="sphere" size="0.3" pos="2 0 1" contype="0" conaffinity="0"/>
+  <geom name="ghost" type="box" size="0.05 0.5 0.5" pos="1 0 1" rgba="1 1 1 0" contype="0" conaffinity="0"/>
+  <geom name="crate" type="box" size="0.2 0.3 0.4" pos="0 2 1" contype="0" conaffinity="0"/>
+  <geom name="pole" type="capsule" size="0.1 0.5" pos="-2 0 1" contype="0" conaffinity="0"/>
+  <geom name="drum" type="cylinder" size="0.25 0.3" pos="0 -2 1" contype="0" conaffinity="0"/>
+  <geom name="egg" type="ellipsoid" size="0.3 0.4 0.5" pos="0 0 3" contype="0" conaffinity="0"/>
+  <body name="probe" pos="0 0 1">
+    <freejoint/>
+    <geom name="probe_g" type="sphere" size="0.05" contype="0" conaffinity="0"/>
+    <site name="s_down" quat="0 1 0 0"/>
+    <site name="s_sphere" quat="{C45} 0 {C45} 0"/>
+    <site name="s_box" quat="{C45} {-C45} 0 0"/>
+    <site name="s_caps" quat="{C45} 0 {-C45} 0"/>
+    <site name="s_cyl" quat="{C45} {C45} 0 0"/>
+    <site name="s_up"/>
+    <site name="s_miss" pos="0 0 0.5" quat="{C45} 0 {C45} 0"/>
+  </body>
+</worldbody>
+<sensor>
+  <rangefinder name="r_down" site="s_down"/>
+  <rangefinder name="r_sphere" site="s_sphere"/>
+  <rangefinder name="r_box" site="s_box"/>
+  <rangefinder name="r_caps" site="s_caps"/>
+  <rangefinder name="r_cyl" site="s_cyl"/>
+  <rangefinder name="r_up" site="s_up"/>
+  <rangefinder name="r_miss" site="s_miss"/>
+  <rangefinder name="r_cut" site="s_sphere" cutoff="1"/>
+</sensor>
+</mujoco>"""
+
+
+def test_rangefinder_known_distances():
+  """mj_ray from each site along its z axis: the plane 1 m below, the sphere,
+  the box face, the capsule side, the cylinder side and the ellipsoid's pole at
+  their closed-form distances; the invisible box (rgba alpha 0) and the probe's
+  own geom are not hit; a ray that misses everything reads -1; cutoff clips
+  from above only."""
+  m = compile_spec(read_mjcf_string(RAY_SCENE), 8, 64)
+  out = Oracle(m).run(1, {"qpos": np.array([[0, 0, 1, 1, 0, 0, 0]])}, integrate=False)
+  got = {nm: _sensor(m, out, 0, nm)[0] for nm in ("r_down", "r_sphere", "r_box", "r_caps", "r_cyl", "r_up", "r_miss", "r_cut")}
+  want = {"r_down": 1.0, "r_sphere": 1.7, "r_box": 1.7, "r_caps": 1.9, "r_cyl": 1.75, "r_up": 1.5, "r_miss": -1.0, "r_cut": 1.0}
+  for k, v in want.items():
+    assert got[k] == pytest.approx(v, abs=1e-9), (k, got[k])
+  # tilted down by 30 degrees about y: the floor at 1 / cos(30 deg)
+  q = rot.quat_mul(rot.axis_angle_to_quat(np.array([0, 1.0, 0]), np.deg2rad(30)), np.array([1.0, 0, 0, 0]))
+  out = Oracle(m).run(1, {"qpos": np.array([[0, 0, 1, *q]])}, integrate=False)
+  assert _sensor(m, out, 0, "r_down")[0] == pytest.approx(1 / np.cos(np.deg2rad(30)), abs=1e-9)
