@@ -670,6 +670,44 @@ def test_accelerometer_sensor(backend):
   assert torch.allclose(sensor.data[:, 2], torch.full((2,), 9.81, device=sim.device), atol=0.2)
 
 
+def test_builtin_sensor_types_beyond_the_benchmark_set(backend):
+  """The remaining BuiltinSensorCfg types of builtin_sensor.py:30-110 through the
+  same Scene path (not in the reference's test file; numeric pins from the
+  scene): framepos of link1's site in the base frame is the joint offset
+  (0.3, 0, 0) whatever the hinge angle; e_potential of the 6 kg robot at
+  z = 1 m is m g z; e_kinetic at rest is 0; clock reads the data time before
+  the step; the base site's rangefinder (z up) sees nothing (-1); the force
+  at link1's site carries link1's weight while the robot falls freely (0 up to
+  rounding)."""
+  cfgs = (
+    BuiltinSensorCfg(name="l1_in_base", sensor_type="framepos", obj=ObjRef(type="site", name="link1_site", entity="robot"),
+                     ref=ObjRef(type="xbody", name="base", entity="robot")),
+    BuiltinSensorCfg(name="epot", sensor_type="e_potential"),
+    BuiltinSensorCfg(name="ekin", sensor_type="e_kinetic"),
+    BuiltinSensorCfg(name="clk", sensor_type="clock"),
+    BuiltinSensorCfg(name="range_up", sensor_type="rangefinder", obj=ObjRef(type="site", name="base_site", entity="robot")),
+    BuiltinSensorCfg(name="l1_force", sensor_type="force", obj=ObjRef(type="site", name="link1_site", entity="robot")),
+  )
+  dev = device_of(backend)
+  scene = Scene(SceneCfg(num_envs=2, env_spacing=3.0, entities={"robot": EntityCfg(
+    spec_fn=lambda: read_mjcf_string(ARTICULATED_ROBOT_XML))}, sensors=cfgs), dev)
+  model = scene.compile()
+  assert model.nsensor_ext == 6  # all outside the benchmark set: the generic kernel instance
+  sim = make_sim(2, SimulationCfg(njmax=20), model, backend)
+  scene.initialize(sim.mj_model, sim.model, sim.data)
+  sim.step()
+  d = {k: scene[k].data for k in ("robot/l1_in_base", "epot", "ekin", "clk", "robot/range_up", "robot/l1_force")}
+  assert d["robot/l1_in_base"].shape == (2, 3) and d["epot"].shape == (2, 1)
+  assert torch.allclose(d["robot/l1_in_base"], torch.tensor([[0.3, 0.0, 0.0]] * 2, device=dev), atol=1e-5)
+  assert torch.allclose(d["epot"][:, 0], torch.full((2,), 6 * 9.81, device=dev), rtol=1e-5)
+  assert torch.allclose(d["ekin"][:, 0], torch.zeros(2, device=dev), atol=1e-9)
+  assert torch.allclose(d["clk"][:, 0], torch.zeros(2, device=dev))
+  assert torch.equal(d["robot/range_up"][:, 0], torch.full((2,), -1.0, device=dev))
+  assert torch.allclose(d["robot/l1_force"], torch.zeros(2, 3, device=dev), atol=1e-3)
+  sim.step()
+  assert torch.allclose(scene["clk"].data[:, 0], torch.full((2,), float(model.timestep), device=dev), atol=1e-7)
+
+
 def test_builtin_sensor_cfg_validation():
   """builtin_sensor.py:206-259 (the reference's cfg checks)."""
   with pytest.raises(ValueError, match="requires obj.type='site'"):
