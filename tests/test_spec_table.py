@@ -21,3 +21,20 @@ def test_benchmark_tasks_select_a_specialised_kernel(task, num_envs):
   cfg.scene.num_envs = num_envs
   sim = Simulation(num_envs, cfg.sim, Scene(cfg.scene, device="cpu").compile(), "cpu")
   assert native.lib().mjh_spec_index(ctypes.addressof(sim._mstruct)) >= 0
+
+
+def test_a_sensor_outside_the_benchmark_set_selects_the_generic_kernel():
+  """Model.nsensor_ext is a model size, so part of the plan: the G1 task with
+  one extra framepos sensor no longer matches the specialised instance, whose
+  code has no framepos evaluation, and runs the generic one."""
+  from mjlab_amd.sensor.builtin_sensor import BuiltinSensorCfg, ObjRef
+
+  cfg = load_env_cfg(TASKS[0])
+  cfg.scene.num_envs = 2
+  assert Scene(cfg.scene, device="cpu").compile().nsensor_ext == 0
+  cfg.scene.sensors = tuple(cfg.scene.sensors) + (
+    BuiltinSensorCfg(name="pelvis_pos", sensor_type="framepos", obj=ObjRef(type="xbody", name="pelvis", entity="robot")),)
+  m = Scene(cfg.scene, device="cpu").compile()
+  assert m.nsensor_ext == 1
+  sim = Simulation(2, cfg.sim, m, "cpu")
+  assert native.lib().mjh_spec_index(ctypes.addressof(sim._mstruct)) == -1
