@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <type_traits>
 
 namespace mjh_batch {
 
@@ -46,10 +47,27 @@ struct Pack {
 // e runs the jobs in recorded order for env e (per-env dependencies kept)
 typedef void (*Launcher)(const Pack&, hipStream_t, bool seq);
 
+// Job flags (a job struct declares `static constexpr int kFlags`; a member
+// named `ctr` adds kReadsCounter):
+// * kProducer: other jobs or torch read the output within the same pass (the
+//   root frame), so in an independent batch the job launches at once instead
+//   of being recorded (the batch's jobs may not read each other's outputs);
+// * kWritesCounter: the job advances the device step counter from one thread
+//   (the step counters); kReadsCounter: the job reads that counter (the random
+//   streams, event marks). In a sequential batch a reader recorded after a
+//   writer starts a new dispatch, so every thread sees the advanced counter.
+enum Flags { kProducer = 1, kWritesCounter = 2, kReadsCounter = 4 };
+template <class J, class = void> struct declared_flags : std::integral_constant<int, 0> {};
+template <class J> struct declared_flags<J, std::void_t<decltype(J::kFlags)>> : std::integral_constant<int, J::kFlags> {};
+template <class J, class = void> struct has_ctr : std::false_type {};
+template <class J> struct has_ctr<J, std::void_t<decltype(&J::ctr)>> : std::true_type {};
+template <class J> constexpr int job_flags() { return declared_flags<J>::value | (has_ctr<J>::value ? kReadsCounter : 0); }
+
 // host side (mjh_mgr.hip): register a unit's batch launcher; append a job to
-// the open batch (false: no batch open, the caller launches the job itself)
+// the open batch (false: no batch open, or a producer in an independent batch:
+// the caller launches the job itself)
 bool register_unit(int unit, Launcher f);
-bool add(int unit, int kind, long long n, const void* args, size_t bytes, hipStream_t s);
+bool add(int unit, int kind, long long n, const void* args, size_t bytes, hipStream_t s, int flags);
 
 inline int grid1(long long n) { return (int)((n + 255) / 256); }
 
@@ -58,7 +76,7 @@ template <class J>
 int submit(int unit, const J& j, long long n, hipStream_t s, void (*kernel)(J, long long)) {
   static_assert(sizeof(J) <= kArgBytes, "job struct exceeds the batch slot");
   if (n <= 0) return 0;
-  if (add(unit, J::kKind, n, &j, sizeof(J), s)) return 0;
+  if (add(unit, J::kKind, n, &j, sizeof(J), s, job_flags<J>())) return 0;
   hipLaunchKernelGGL(kernel, dim3(grid1(n)), dim3(256), 0, s, j, n);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

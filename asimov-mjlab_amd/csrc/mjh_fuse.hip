@@ -335,6 +335,7 @@ struct VelocityResampleJob {
 // EventManager reset bookkeeping (event_manager.py:146-156): last = step, once = 1
 struct EventMarkJob {
   static constexpr int kKind = 124;
+  static constexpr int kFlags = mjh_batch::kReadsCounter;  // reads the step counter
   int* last; unsigned char* once; const unsigned char* mask; const mjh_i64* step;
   __device__ __forceinline__ void run(long long e) const {
     if (!on(mask, e)) return;
@@ -629,6 +630,7 @@ __device__ __forceinline__ void qrot(float o[3], const float q[4], const float v
 
 struct RootFrameJob {
   static constexpr int kKind = 115;
+  static constexpr int kFlags = mjh_batch::kProducer;  // read by reward / termination jobs and torch in the same pass
   const float* xpos; long long ps; const float* xquat; long long qs; const float* com; long long cs;
   const float* cvel; long long vs; const float* grav; long long gs; const float* fwd; long long fs; float* out;
   __device__ __forceinline__ void run(long long e) const {
@@ -883,6 +885,7 @@ __global__ void rew_exp_err_kernel(const float* __restrict__ a, long long aes, l
 // length += 1 and the env-step counter += 1 (the device random stream's counter)
 struct StepCountersJob {
   static constexpr int kKind = 116;
+  static constexpr int kFlags = mjh_batch::kWritesCounter;  // thread 0 advances the step counter
   mjh_i64* episode_length; mjh_i64* step;
   __device__ __forceinline__ void run(long long e) const {
     episode_length[e] += 1;
@@ -1064,7 +1067,9 @@ int mjh_reset_joints_offset(float* qpos, long long qs, int qadr, float* qvel, lo
   // inside a batch: a per-env job; otherwise one thread per (env, joint)
   const ResetJointsJob j{qpos, qs, qadr, qvel, vs, vadr, k, mask, def_pos, dps, def_vel, dvs, lim, ls, pos_lo, pos_hi, vel_lo,
                          vel_hi, pos_rand, vel_rand, seed, key, ctr};
-  if (mjh_batch::add(mjh_batch::kFuse, ResetJointsJob::kKind, n, &j, sizeof(j), (hipStream_t)stream)) return 0;
+  if (mjh_batch::add(mjh_batch::kFuse, ResetJointsJob::kKind, n, &j, sizeof(j), (hipStream_t)stream,
+                     mjh_batch::job_flags<ResetJointsJob>()))
+    return 0;
   hipLaunchKernelGGL(reset_joints_offset_kernel, dim3(grid(n * k)), dim3(kBlock), 0, (hipStream_t)stream, qpos, qs, qadr,
                      qvel, vs, vadr, k, mask, def_pos, dps, def_vel, dvs, lim, ls, pos_lo, pos_hi, vel_lo, vel_hi,
                      pos_rand, vel_rand, seed, key, ctr, n);
@@ -1155,7 +1160,9 @@ int mjh_masked_zero(float* const* ptrs, const long long* row_strides, const int*
     }
     j.nt = ntensors;
     j.mask = mask;
-    if (mjh_batch::add(mjh_batch::kFuse, MaskedZeroJob::kKind, n, &j, sizeof(j), (hipStream_t)stream)) return 0;
+    if (mjh_batch::add(mjh_batch::kFuse, MaskedZeroJob::kKind, n, &j, sizeof(j), (hipStream_t)stream,
+                       mjh_batch::job_flags<MaskedZeroJob>()))
+      return 0;
   }
   ZeroArgs a{};
   a.wmax = 0;

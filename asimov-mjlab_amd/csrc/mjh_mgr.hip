@@ -108,6 +108,7 @@ struct State {
   bool open = false;
   bool seq = false;
   int cur = -1;  // sequential batches: the unit of the jobs recorded last
+  bool counter_written = false;  // sequential batches: a recorded, not yet launched kWritesCounter job
   hipStream_t stream = nullptr;
   Pack pack[kUnits];
 };
@@ -128,9 +129,12 @@ bool register_unit(int unit, Launcher f) {
   return true;
 }
 
-bool add(int unit, int kind, long long n, const void* args, size_t bytes, hipStream_t s) {
+bool add(int unit, int kind, long long n, const void* args, size_t bytes, hipStream_t s, int flags) {
   State& st = g_state;
   if (!st.open || unit < 0 || unit >= kUnits || !g_launch[unit] || bytes > (size_t)kArgBytes) return false;
+  // a producer's output is read inside the pass: in an independent batch it
+  // runs now (ahead of the batch, on the same stream), never recorded
+  if (!st.seq && (flags & kProducer)) return false;
   if (s != st.stream) {  // a job on another stream: everything recorded so far goes first
     if (st.seq) {
       if (st.cur >= 0) flush_unit(st, st.cur);
@@ -140,9 +144,15 @@ bool add(int unit, int kind, long long n, const void* args, size_t bytes, hipStr
     st.stream = s;
   }
   if (st.seq && st.cur != unit && st.cur >= 0) flush_unit(st, st.cur);  // keep the recorded order
+  // a counter reader after the counter's writer: the writer's dispatch ends first
+  if (st.seq && (flags & kReadsCounter) && st.counter_written) {
+    for (int u = 0; u < kUnits; u++) flush_unit(st, u);
+    st.counter_written = false;
+  }
   st.cur = unit;
   Pack& p = st.pack[unit];
   if (p.njobs == kMaxJobs) flush_unit(st, unit);
+  if (flags & kWritesCounter) st.counter_written = true;
   Job& j = p.jobs[p.njobs++];
   j.kind = kind;
   j.pad = 0;
@@ -159,6 +169,7 @@ int mjh_batch_begin(int sequential) {
   mjh_batch::g_state.open = true;
   mjh_batch::g_state.seq = sequential != 0;
   mjh_batch::g_state.cur = -1;
+  mjh_batch::g_state.counter_written = false;
   mjh_batch::g_state.stream = nullptr;
   for (auto& p : mjh_batch::g_state.pack) p.njobs = 0, p.nmax = 0;
   return 0;

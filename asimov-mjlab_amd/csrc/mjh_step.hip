@@ -4860,6 +4860,9 @@ unsigned long long launch_key(const mjh_model* m, const mjh_data* d) {
   };
   eat(m, sizeof(*m));
   eat(d, offsetof(mjh_data, at_last_time));  // the fused sensor timers do not affect the position stage
+  // the site-output layout does (the position stage writes the sites there)
+  eat(&d->site_wstride, sizeof(d->site_wstride));
+  eat(&d->site_off, sizeof(d->site_off));
   return h;
 }
 

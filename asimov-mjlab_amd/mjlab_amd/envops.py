@@ -61,6 +61,15 @@ class JobBatch:
     return False
 
 
+def refuse_fallback_in_batch(name: str) -> None:
+  """A torch fallback inside an open sequential batch would read outputs of jobs
+  recorded before it, which have not run yet: refuse it loudly (the env enables
+  such batches only for term sets whose kernels all fuse)."""
+  if _OPEN_BATCH is not None and _OPEN_BATCH.sequential:
+    raise RuntimeError(f"{name}: torch fallback inside an open sequential job batch (its inputs are recorded, "
+                       "not yet launched jobs' outputs)")
+
+
 def _keep(*ts) -> None:
   """Inputs of a job recorded into the open batch stay referenced until it launches."""
   if _OPEN_BATCH is not None:
@@ -644,12 +653,16 @@ def time_out(episode_length: torch.Tensor, max_len: int) -> torch.Tensor | None:
 def term_combine(values: list, term_dones: list, time_out: list, truncated, terminated, dones) -> bool:
   """TerminationManager's copy / OR / dones chain over bool term vectors in one launch."""
   T = len(values)
-  if T == 0 or T > MAX_TERMS:
+  if T == 0:
+    return False
+  if T > MAX_TERMS:
+    refuse_fallback_in_batch("term_combine")
     return False
   n = dones.shape[0]
   for v in values + term_dones + [truncated, terminated, dones]:
     if not (isinstance(v, torch.Tensor) and v.is_cuda and v.dtype == torch.bool and v.dim() == 1 and v.shape[0] == n
             and v.stride(0) == 1):
+      refuse_fallback_in_batch("term_combine")
       return False
   vp = (ctypes.c_void_p * T)(*[v.data_ptr() for v in values])
   dp = (ctypes.c_void_p * T)(*[d.data_ptr() for d in term_dones])

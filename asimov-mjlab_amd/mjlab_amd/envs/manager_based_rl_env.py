@@ -107,6 +107,7 @@ def seed_rng(seed: int) -> None:
 class ManagerBasedEnv:
   def __init__(self, cfg: ManagerBasedEnvCfg, device: str) -> None:
     self.cfg = cfg
+    self._air_sensor = None  # a contact sensor whose timers ride on the physics launch (ManagerBasedRlEnv)
     if cfg.seed is not None:
       cfg.seed = self.seed(cfg.seed)
     self._sim_step_counter = 0
@@ -268,7 +269,11 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
     from mjlab_amd.envs.mdp import events as ev
     from mjlab_amd.envs.mdp import terminations as tm
 
-    term_ok = all(c.func in (tm.time_out, tm.bad_orientation) for c in self.termination_manager._term_cfgs)
+    # bad_orientation fuses only for a limit in [0, pi] (outside it, its torch acos
+    # path would read the root frame recorded in the batch before it launches)
+    term_ok = all(c.func is tm.time_out
+                  or (c.func is tm.bad_orientation and 0.0 <= float(c.params.get("limit_angle", -1.0)) <= math.pi)
+                  for c in self.termination_manager._term_cfgs)
     try:
       from mjlab_amd.tasks.velocity.mdp.velocity_command import UniformVelocityCommand
     except ImportError:  # pragma: no cover
@@ -302,7 +307,8 @@ class ManagerBasedRlEnv(ManagerBasedEnv):
         return False
     om, am, rm, em, tm = (self.observation_manager, self.action_manager, self.reward_manager, self.event_manager,
                           self.termination_manager)
-    if getattr(om, "_history", None) or getattr(om, "_class_terms", None):
+    if (any(getattr(om, "_group_obs_term_history_buffer", {}).values())
+        or any(getattr(om, "_group_obs_term_delay_buffer", {}).values()) or getattr(om, "_class_terms", None)):
       return False
     if not all(type(t).reset is JointAction.reset for t in am._terms.values()):
       return False

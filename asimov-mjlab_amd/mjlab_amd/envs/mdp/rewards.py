@@ -61,3 +61,22 @@ class posture:
     a = env.scene[asset_cfg.name]
     err = torch.square(a.data.joint_pos[:, asset_cfg.joint_idx] - self.default_joint_pos[:, asset_cfg.joint_idx])
     return torch.exp(-torch.mean(err / (self.std**2), dim=1))
+
+
+def electrical_power_cost(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
+  """Positive mechanical power sum(max(tau * qd, 0)) (``rewards.py:107-118``; regeneration is
+  not credited). ``actuator_force`` and ``joint_vel`` are the entity's actuator and joint
+  columns, paired by position as in the reference (one actuator per joint in mjlab robots)."""
+  a = env.scene[asset_cfg.name]
+  mech = a.data.actuator_force * a.data.joint_vel
+  return torch.sum(torch.clamp(mech, min=0.0), dim=1)
+
+
+def flat_orientation_l2(env, asset_cfg: SceneEntityCfg = _DEFAULT) -> torch.Tensor:
+  """sum(projected_gravity_b[:, :2]^2) (``rewards.py:121-126``); one fused job (the squared
+  sum of a row's first two entries, read in place from the root-frame record)."""
+  g = env.scene[asset_cfg.name].data.projected_gravity_b
+  fused = envops.rew_sqsum(g, 2)
+  if fused is not None:
+    return fused
+  return torch.sum(torch.square(g[:, :2]), dim=1)

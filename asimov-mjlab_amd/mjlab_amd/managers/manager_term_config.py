@@ -44,11 +44,18 @@ class EventTermCfg(ManagerTermBaseCfg):
 
 @dataclass
 class ObservationTermCfg(ManagerTermBaseCfg):
-  """Pipeline: compute -> noise -> clip -> scale (observation_manager.py:163-176)."""
+  """Pipeline: compute -> noise -> clip -> scale -> delay -> history
+  (observation_manager.py:163-188)."""
 
   noise: Any = None
   clip: tuple[float, float] | None = None
   scale: Any = None
+  delay_min_lag: int = 0
+  delay_max_lag: int = 0
+  delay_per_env: bool = True
+  delay_hold_prob: float = 0.0
+  delay_update_period: int = 0
+  delay_per_env_phase: bool = True
   history_length: int = 0
   flatten_history_dim: bool = True
 

@@ -1,14 +1,20 @@
-"""Observation manager (``src/mjlab/managers/observation_manager.py:147-260``).
+"""Observation manager (``src/mjlab/managers/observation_manager.py:147-278``).
 
 Pipeline per term: compute -> noise (only if the group enables corruption) ->
-clip -> scale -> history; groups concatenated along the last dim.
+clip -> scale -> delay (DelayBuffer) -> history (CircularBuffer, first frame
+back-filled after a reset); groups concatenated along ``concatenate_dim``.
+Groups without delay or history on the GPU run as one fused launch
+(``_compute_fused``); the buffers are device-resident and capturable
+(``utils/buffers``), so delayed / history terms run inside the captured env step.
 """
 
 from __future__ import annotations
 
+import numpy as np
 import torch
 
-from mjlab_amd.managers.manager_base import as_mask, resolve_params
+from mjlab_amd.managers.manager_base import resolve_params
+from mjlab_amd.utils.buffers import CircularBuffer, DelayBuffer
 
 
 class ObservationManager:
@@ -18,7 +24,9 @@ class ObservationManager:
     self._group_terms: dict[str, list[tuple[str, object]]] = {}
     self._group_concat: dict[str, bool] = {}
     self._group_concat_dim: dict[str, int] = {}
-    self._history: dict[tuple[str, str], torch.Tensor] = {}
+    # per group: term name -> DelayBuffer / CircularBuffer (the reference's attribute names)
+    self._group_obs_term_delay_buffer: dict[str, dict[str, DelayBuffer]] = {}
+    self._group_obs_term_history_buffer: dict[str, dict[str, CircularBuffer]] = {}
     self._class_terms = []
     for gname, gcfg in cfg.items():
       if gcfg is None:
@@ -40,19 +48,28 @@ class ObservationManager:
       self._group_terms[gname] = terms
       self._group_concat[gname] = gcfg.concatenate_terms
       self._group_concat_dim[gname] = gcfg.concatenate_dim
-    # resolve scales and dims by evaluating every term once (observation_manager.py:246)
+    # resolve scales, buffers and dims by evaluating every term once (observation_manager.py:246-278)
     self.group_obs_term_dim: dict[str, list[tuple[int, ...]]] = {}
     for gname, terms in self._group_terms.items():
-      dims = []
+      dims, delays, hists = [], {}, {}
       for tname, tcfg in terms:
         out = tcfg.func(env, **tcfg.params)
+        obs_dims = tuple(out.shape)
         if tcfg.scale is not None and not isinstance(tcfg.scale, torch.Tensor):
           tcfg.scale = torch.tensor(tcfg.scale, dtype=torch.float32, device=env.device)
+        if tcfg.delay_max_lag > 0:
+          delays[tname] = DelayBuffer(min_lag=tcfg.delay_min_lag, max_lag=tcfg.delay_max_lag, batch_size=env.num_envs,
+                                      device=env.device, per_env=tcfg.delay_per_env, hold_prob=tcfg.delay_hold_prob,
+                                      update_period=tcfg.delay_update_period, per_env_phase=tcfg.delay_per_env_phase)
         if tcfg.history_length > 0:
-          h = torch.zeros(env.num_envs, tcfg.history_length, *out.shape[1:], device=env.device)
-          self._history[(gname, tname)] = h
-        dims.append(tuple(out.shape[1:]))
+          hists[tname] = CircularBuffer(max_len=tcfg.history_length, batch_size=env.num_envs, device=env.device)
+          obs_dims = (obs_dims[0], tcfg.history_length, *obs_dims[1:])
+          if tcfg.flatten_history_dim:
+            obs_dims = (obs_dims[0], int(np.prod(obs_dims[1:])))
+        dims.append(tuple(obs_dims[1:]))
       self.group_obs_term_dim[gname] = dims
+      self._group_obs_term_delay_buffer[gname] = delays
+      self._group_obs_term_history_buffer[gname] = hists
     self._obs_buffer = None
     self._fused = {g: self._fused_plan(g) for g in self._group_terms}
     # optional fixed noise draws per group, (N, group width) in U[0,1): replaces
@@ -69,7 +86,7 @@ class ObservationManager:
       return None
     plan, off = [], 0
     for (tname, tcfg), dims in zip(self._group_terms[gname], self.group_obs_term_dim[gname]):
-      if tcfg.history_length > 0 or len(dims) > 1:
+      if tcfg.history_length > 0 or tcfg.delay_max_lag > 0 or len(dims) > 1:
         return None
       w = dims[0] if dims else 1
       noise = None
@@ -95,12 +112,23 @@ class ObservationManager:
 
   @property
   def group_obs_dim(self) -> dict:
+    """Concatenated groups: the term dims summed along the concatenation dim
+    (observation_manager.py:19-40); other groups: the per-term dims."""
     out = {}
     for g, dims in self.group_obs_term_dim.items():
-      if self._group_concat[g]:
-        out[g] = (sum(int(torch.tensor(d).prod()) for d in dims),)
-      else:
+      if not self._group_concat[g]:
         out[g] = dims
+        continue
+      if all(len(d) == 1 for d in dims):
+        out[g] = (sum(int(d[0]) for d in dims),)
+        continue
+      if len({len(d) for d in dims}) != 1:
+        raise RuntimeError(f"Unable to concatenate observation terms in group {g}.")
+      cd = self._group_concat_dim[g]
+      axis = cd - 1 if cd > 0 else cd  # the term dims exclude the env dim
+      first = list(dims[0])
+      first[axis] = sum(int(d[axis]) for d in dims)
+      out[g] = tuple(first)
     return out
 
   @property
@@ -108,9 +136,12 @@ class ObservationManager:
     return dict(self._group_concat)
 
   def reset(self, env_ids=None) -> dict:
-    m = as_mask(env_ids, self._env.num_envs, self._env.device)
-    for h in self._history.values():
-      h.masked_fill_(m.view(-1, *([1] * (h.dim() - 1))), 0.0)
+    ids = None if env_ids is None or isinstance(env_ids, slice) else env_ids
+    for gname in self._group_terms:
+      for buf in self._group_obs_term_delay_buffer[gname].values():
+        buf.reset(batch_ids=ids)
+      for buf in self._group_obs_term_history_buffer[gname].values():
+        buf.reset(batch_ids=ids)
     for c in self._class_terms:
       if hasattr(c, "reset"):
         c.reset(env_ids=env_ids)
@@ -136,11 +167,15 @@ class ObservationManager:
         obs = obs.clip_(min=tcfg.clip[0], max=tcfg.clip[1])
       if tcfg.scale is not None:
         obs = obs.mul_(tcfg.scale)
+      if tcfg.delay_max_lag > 0:
+        delay = self._group_obs_term_delay_buffer[group_name][tname]
+        delay.append(obs)
+        obs = delay.compute()
       if tcfg.history_length > 0:
-        h = self._history[(group_name, tname)]
-        if update_history:
-          h.copy_(torch.cat([h[:, 1:], obs.unsqueeze(1)], dim=1))
-        obs = h.reshape(self._env.num_envs, -1) if tcfg.flatten_history_dim else h
+        hist = self._group_obs_term_history_buffer[group_name][tname]
+        if update_history or not hist.is_initialized:
+          hist.append(obs)
+        obs = hist.buffer.reshape(self._env.num_envs, -1) if tcfg.flatten_history_dim else hist.buffer
       obs_terms[tname] = obs
     if self._group_concat[group_name]:
       return torch.cat(list(obs_terms.values()), dim=self._group_concat_dim[group_name])

@@ -3,7 +3,9 @@
 import pytest
 import torch
 
+from mjlab_amd.envs import mdp as gmdp
 from mjlab_amd.envs.manager_based_rl_env import ManagerBasedRlEnv
+from mjlab_amd.managers.manager_term_config import RewardTermCfg
 from mjlab_amd.sim import native
 from mjlab_amd.tasks import load_env_cfg
 
@@ -101,11 +103,21 @@ def test_vecenv_obs_survive_the_next_graph_replay():
 def _twin_envs(task: str, n: int, tmp_path=None):
   envs = []
   for use_graph in (True, False):
-    cfg = load_env_cfg(task)
+    cfg = load_env_cfg(task.split("+")[0])
     cfg.scene.num_envs = n
     cfg.seed = 7
     if "Tracking" in task:
       cfg.commands["motion"].motion_file = _gpu_motion(tmp_path)
+    if task.endswith("+delay_history"):
+      # observation delay and history inside the captured step (constant lags: the
+      # draws are deterministic, so graph and eager agree bitwise; no corruption noise)
+      pol = cfg.observations["policy"]
+      pol.enable_corruption = False
+      pol.terms["base_ang_vel"].delay_min_lag = pol.terms["base_ang_vel"].delay_max_lag = 2
+      pol.terms["projected_gravity"].history_length = 3
+      pol.terms["joint_vel"].delay_min_lag = pol.terms["joint_vel"].delay_max_lag = 1
+      pol.terms["joint_vel"].history_length = 2
+      pol.terms["joint_vel"].flatten_history_dim = True
     envs.append(ManagerBasedRlEnv(cfg, device="cuda:0", use_graph=use_graph))
   return envs
 
@@ -114,7 +126,8 @@ _STATE = ("qpos", "qvel", "qacc_warmstart", "ctrl", "time", "xpos", "xquat", "cv
           "qfrc_applied", "xfrc_applied", "actuator_force", "nefc", "ncon", "solver_niter")
 
 
-@pytest.mark.parametrize("task", ["Mjlab-Velocity-Flat-Unitree-G1", "Mjlab-Tracking-Flat-Unitree-G1"])
+@pytest.mark.parametrize("task", ["Mjlab-Velocity-Flat-Unitree-G1", "Mjlab-Tracking-Flat-Unitree-G1",
+                                  "Mjlab-Velocity-Flat-Unitree-G1+delay_history"])
 def test_graph_replay_equals_eager_step(task, tmp_path):
   """The benchmarked object — the captured env step — against the same step run
   eagerly, call by call: from identical state, counters and seeds, every
@@ -149,6 +162,11 @@ def test_graph_replay_equals_eager_step(task, tmp_path):
       assert torch.equal(getattr(ge.sim.data, f), getattr(ee.sim.data, f)), f"step {k}: sim.data.{f}"
     assert torch.equal(ge.episode_length_buf, ee.episode_length_buf)
   assert resets >= 12
+  if task.endswith("+delay_history"):
+    # the device ring pointer advanced on every replay: the history holds distinct frames
+    hb = ge.observation_manager._group_obs_term_history_buffer["policy"]["projected_gravity"]
+    assert int(hb._pointer) == K % 3  # 1 + K appends (reset, then one per env step)
+    assert not torch.equal(hb.buffer[:, 0], hb.buffer[:, -1])
 
 
 def test_reset_with_seed_reproduces_device_draws():
@@ -191,13 +209,18 @@ def test_config1_single_env_zero_agent_against_oracle():
   assert not bool(term.any())
 
 
-def test_batched_reward_pass_equals_separate_launches():
+@pytest.mark.parametrize("no_fell_over", [False, True])
+def test_batched_reward_pass_equals_separate_launches(no_fell_over):
   """The job batches (mjh_batch_begin / mjh_batch_end: the reward terms as one
   dispatch per source file; the termination pass and the commands + interval
   events as sequential per-env chains) against the same kernels launched one
   by one: over K captured env steps from identical seeds,
   rewards, episode sums, logs, observations and the simulation state agree
-  bitwise (the jobs run the same arithmetic; the batch only merges dispatches)."""
+  bitwise (the jobs run the same arithmetic; the batch only merges dispatches).
+  Without the fell_over termination nothing fills the root-frame cache before
+  the reward pass, so the reward terms' root-frame reads (the velocity-tracking
+  jobs and a flat_orientation_l2 term's torch sum) depend on the root frame
+  launching ahead of the independent batch (mjh_batch kProducer)."""
   from mjlab_amd import envops
   from mjlab_amd.sim import native
 
@@ -217,6 +240,9 @@ def test_batched_reward_pass_equals_separate_launches():
     cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
     cfg.scene.num_envs = n
     cfg.seed = 5
+    if no_fell_over:
+      del cfg.terminations["fell_over"]
+      cfg.rewards["flat_orientation_l2"] = RewardTermCfg(func=gmdp.flat_orientation_l2, weight=-0.5)
     envs.append(ManagerBasedRlEnv(cfg, device="cuda:0"))  # captured steps: the sequential batches run too
   eb, es = envs
   assert eb._seq_term and eb._seq_post and eb._seq_reset
