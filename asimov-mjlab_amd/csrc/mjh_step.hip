@@ -23,6 +23,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 #include <string>
 #include <type_traits>
 
@@ -4866,6 +4867,29 @@ unsigned long long launch_key(const mjh_model* m, const mjh_data* d) {
   return h;
 }
 
+// Launch plugins (mjh_register_spec_plugin): model-specialised instances built
+// for a plan after the library was (mjlab_amd/sim/jit.py compiles this file with
+// -DMJH_PLUGIN and a one-plan table when a Simulation's model matches no entry of
+// mjh_spec_table.h, and registers the library's mjh_plugin_step here). A plugin
+// is taken on the same conditions as a built-in specialisation: exact plan
+// match, slab data layout, pyramidal cones, Newton or CG.
+typedef int (*PluginFn)(int step, const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream, int reuse,
+                        unsigned long long key);
+struct PluginEntry {
+  int plan[kPlanInts];
+  PluginFn fn;
+};
+std::vector<PluginEntry> g_plugins;
+
+int find_plugin(const Plan& p, const mjh_model* m) {
+  if (g_plugins.empty() || MJH_SPLIT != 0 || m->cone == 1 || m->solver == kSolverPGS) return -1;
+  int v[kPlanInts];
+  plan_to_ints(p, m, v);
+  for (size_t k = 0; k < g_plugins.size(); k++)
+    if (std::memcmp(v, g_plugins[k].plan, sizeof(v)) == 0) return (int)k;
+  return -1;
+}
+
 // one step/forward launch of MODE (0 fused, 1 position, 2 velocity/solver)
 template <int WPB, bool STEP, int NVP, int SPEC, bool SLAB, int MODE>
 void launch_mode(const Plan& p, const mjh_model* m, const mjh_data* d, const unsigned char* gate, hipStream_t s,
@@ -4928,10 +4952,18 @@ int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, voi
     hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields + (order ? 1 : 0)), dim3(1024), 0, s, *m, p.io, d->solver_niter,
                        d->nefc, const_cast<long long*>(d->world_order), (long long)d->nworld);
   // specialised instances assume the slab data layout (data_is_slab)
-  const int k = (g_disable_spec || !data_is_slab(m, d)) ? -1 : find_spec(p, m);
-  if (k >= 0)
+  const bool slab = !g_disable_spec && data_is_slab(m, d);
+  const int k = slab ? find_spec(p, m) : -1;
+  const int kp = (slab && k < 0) ? find_plugin(p, m) : -1;
+  if (k >= 0) {
     launch_spec<STEP, 0>(k, p, m, d, gate, s);
-  else if (nvp == 20)
+  } else if (kp >= 0) {
+    const int r = g_plugins[kp].fn(STEP ? 1 : 0, m, d, gate, stream, g_pos_reuse ? 1 : 0, launch_key(m, d));
+    if (r != 0) {
+      g_err = "specialised plugin launch failed (code " + std::to_string(r) + ")";
+      return 2;
+    }
+  } else if (nvp == 20)
     launch_step<STEP, 20, -1, false>(p, m, d, gate, s);
   else if (nvp == 36)
     launch_step<STEP, 36, -1, false>(p, m, d, gate, s);
@@ -4947,9 +4979,61 @@ int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, voi
 
 }  // namespace
 
+#ifdef MJH_PLUGIN
+// ---- plugin build (-DMJH_PLUGIN, MJH_SPEC_TABLE = a one-plan table) ------------
+// Exports only the launch of its specialised instance; the main library
+// packs the model image and orders the worlds before calling it.
+extern "C" {
+int mjh_plugin_abi(void) { return MJH_ABI_VERSION; }
+
+int mjh_plugin_plan(int* out, int cap) {
+  if (MJH_NSPEC != 1 || cap < kPlanInts) return -1;
+  for (int i = 0; i < kPlanInts; i++) out[i] = kSpecPlan[0][i];
+  return kPlanInts;
+}
+
+int mjh_plugin_step(int step, const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream, int reuse,
+                    unsigned long long key) {
+  if constexpr (MJH_NSPEC == 1) {
+    const Plan p = make_plan(m);
+    if (find_spec(p, m) != 0 || !data_is_slab(m, d)) return 3;  // not this plugin's plan
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    constexpr int NVP = kSpecNvp[0];
+    if (step)
+      launch_mode<wpb_of_nvp(NVP), true, NVP, 0, true, 0>(p, m, d, gate, s, reuse, key);
+    else
+      launch_mode<wpb_of_nvp(NVP), false, NVP, 0, true, 0>(p, m, d, gate, s, reuse, key);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
+  return 4;
+}
+}  // extern "C"
+#else
 extern "C" {
 
 int mjh_abi_version(void) { return MJH_ABI_VERSION; }
+
+int mjh_register_spec_plugin(void* fn, const int* plan, int nplan) {
+  if (!fn || !plan || nplan != kPlanInts) {
+    g_err = "mjh_register_spec_plugin: null function or plan of the wrong length";
+    return -1;
+  }
+  for (size_t k = 0; k < g_plugins.size(); k++)
+    if (std::memcmp(plan, g_plugins[k].plan, sizeof(int) * kPlanInts) == 0) {
+      g_plugins[k].fn = reinterpret_cast<PluginFn>(fn);
+      return (int)k;
+    }
+  PluginEntry e;
+  std::memcpy(e.plan, plan, sizeof(e.plan));
+  e.fn = reinterpret_cast<PluginFn>(fn);
+  g_plugins.push_back(e);
+  return (int)g_plugins.size() - 1;
+}
+
+int mjh_plugin_index(const mjh_model* m) {
+  if (!m) return -1;
+  return find_spec(make_plan(m), m) >= 0 ? -1 : find_plugin(make_plan(m), m);
+}
 
 const char* mjh_last_error(void) { return g_err.c_str(); }
 
@@ -5083,3 +5167,4 @@ int mjh_repeat(float* dst, const float* src, long long nelem, int nworld, void* 
 }
 
 }  // extern "C"
+#endif  // MJH_PLUGIN

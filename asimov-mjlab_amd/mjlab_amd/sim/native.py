@@ -20,7 +20,7 @@ PKG = Path(__file__).resolve().parents[1]
 # MJH_LIB selects an alternative build of the same ABI (e.g. the phase-timing
 # build libmjh_prof.so used by tools/phase_profile.py).
 LIB_PATH = Path(os.environ.get("MJH_LIB", str(PKG / "libmjh.so")))
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 EXPORTS = (
   "mjh_abi_version",
@@ -36,6 +36,8 @@ EXPORTS = (
   "mjh_step_keep_image",
   "mjh_plan_ints",
   "mjh_spec_index",
+  "mjh_register_spec_plugin",
+  "mjh_plugin_index",
   "mjh_data_is_slab",
   "mjh_set_specialization",
   "mjh_set_world_ordering",
@@ -128,6 +130,8 @@ def lib() -> ctypes.CDLL:
   L.mjh_lds_rows.argtypes = [ctypes.c_void_p]
   L.mjh_plan_ints.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
   L.mjh_spec_index.argtypes = [ctypes.c_void_p]
+  L.mjh_register_spec_plugin.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+  L.mjh_plugin_index.argtypes = [ctypes.c_void_p]
   L.mjh_data_is_slab.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
   L.mjh_set_specialization.argtypes = [ctypes.c_int]
   L.mjh_set_world_ordering.argtypes = [ctypes.c_int]

@@ -189,6 +189,10 @@ class SimulationCfg:
   # worlds handed to workgroups in order of their previous step's cost (one counting-sort
   # launch before each physics launch): G1 4096 0.741 -> 0.700 ms per step launch
   balance_worlds: bool = True
+  # model-specialised step kernel for a model outside the built-in table
+  # (mjlab_amd/sim/jit.py): "auto" compiles a launch plugin once per launch plan
+  # (cached), "cached" only uses one already built, "off" keeps the generic instance
+  specialize: str = "auto"
   mujoco: MujocoCfg = field(default_factory=MujocoCfg)
   nan_guard: NanGuardCfg = field(default_factory=NanGuardCfg)
 
@@ -297,8 +301,10 @@ class Simulation:
     self.step_graph = None
     self.forward_graph = None
     self.nan_guard = NanGuard(cfg.nan_guard, num_envs, model)
+    self._kernel = {"kind": "generic", "index": -1, "reason": "not selected"}
     if self.use_cuda_graph:
       native.check(native.lib().mjh_model_check(ctypes.addressof(self._mstruct)), "mjh_model_check")
+      self._select_kernel()
       self._launch_forward()
       self.create_graph()
 
@@ -410,7 +416,25 @@ class Simulation:
       setattr(self._mj_model, k, v)
     self._build_structs()
     if self.use_cuda_graph:
+      self._select_kernel()
       self.create_graph()
+
+  def _select_kernel(self) -> None:
+    """The step-kernel instance of this model: a built-in specialisation, a launch
+    plugin (built once per plan, mjlab_amd/sim/jit.py) or the generic instance."""
+    from mjlab_amd.sim import jit
+
+    mode = getattr(self.cfg, "specialize", "auto")
+    if mode == "off":
+      k = int(native.lib().mjh_spec_index(ctypes.addressof(self._mstruct)))
+      self._kernel = {"kind": "builtin", "index": k} if k >= 0 else {"kind": "generic", "index": -1, "reason": "off"}
+      return
+    self._kernel = jit.ensure(ctypes.addressof(self._mstruct), self._mj_model, name=getattr(self._mj_model, "name", "model"),
+                              compile_missing=(mode == "auto"))
+
+  def kernel_instance(self) -> dict:
+    """Which step-kernel instance runs: {"kind": "builtin"|"plugin"|"generic", "index": ..}."""
+    return dict(self._kernel)
 
   # ---- reference API ----
   @property

@@ -441,6 +441,34 @@ def main(env_hook=None) -> None:
       valu = None
   nv = sim.mj_model.nv
   b_solve = niter * 4 * (nefc * nv + nv * nv + 6 * nefc + 4 * nv) + 4 * (nefc + 2 * nv)
+  # what limits the step launch, from the committed SQ counters of the same workload
+  # (profiles/step_kernel_sq.json): the share of wave-cycles spent waiting (SQ_WAIT_ANY)
+  limiter = None
+  if sqf.exists():
+    try:
+      sj = json.loads(sqf.read_text())
+      if "wait_any_frac" in sj:
+        limiter = {"kind": "latency", "sq_wait_any_frac": sj["wait_any_frac"], "source": sj.get("source", sqf.name),
+                   "note": "per-world dependent chains (LDS/L2 round trips, readlane-serial factor sweeps): "
+                           "SQ_WAIT_ANY / SQ_WAVE_CYCLES of the step kernel"}
+    except (ValueError, OSError):
+      limiter = None
+  # the north-star solver figure (BASELINE.json: >= 40% of HBM roofline in the
+  # constraint-solver kernel), measured on the split build's solver launch by
+  # tools/gpu_solver_pmc.sh -> profiles/solver_roofline.json (same task, 4096 envs)
+  solver_rl = None
+  srf = REPO / "profiles" / "solver_roofline.json"
+  if srf.exists():
+    try:
+      sr = json.loads(srf.read_text())
+      if int(sr.get("num_envs", -1)) == num_envs and sr.get("task", TASK) == args.task:
+        solver_rl = {"bound": "hbm", "kernel": sr.get("kernel"), "launch_us": sr.get("launch_us"),
+                     "algorithmic_frac": sr.get("algorithmic_frac"), "counter_frac": sr.get("counter_frac"),
+                     "achieved_algorithmic_gbs": sr.get("algorithmic_gbs"), "achieved_counter_gbs": sr.get("counter_gbs"),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "target_frac": 0.40, "head": sr.get("head"),
+                     "gap": sr.get("gap"), "source": "profiles/solver_roofline.json (" + sr.get("source", "") + ")"}
+    except (ValueError, OSError):
+      solver_rl = None
 
   # algorithmic FLOPs per env step (SURVEY §8d / BASELINE.md): smooth dynamics,
   # collision over the pair table, and per Newton iteration the Hessian
@@ -503,6 +531,9 @@ def main(env_hook=None) -> None:
         "nconmax_share": int(getattr(sim.mj_model, "ncon_share", sim.mj_model.nconmax)),
         # the step kernel instance: >= 0 a model-specialised one (csrc/mjh_spec_table.h), -1 the generic
         "spec_instance": int(_native().mjh_spec_index(ctypes.addressof(sim._mstruct))),
+        # which instance ran: "builtin" (the table above), "plugin" (compiled for this
+        # model's plan, mjlab_amd/sim/jit.py) or "generic"
+        "kernel_instance": sim.kernel_instance()["kind"],
         "contact_overflow_worlds": int(flags[0]),
         "efc_overflow_worlds": int(flags[1]),
         "nonfinite_worlds": int(flags[2]),
@@ -520,7 +551,9 @@ def main(env_hook=None) -> None:
         "launch_us": t_launch * 1e6,
         "bytes_per_launch": bytes_per_launch,
         "solver_streamed_model_gbs": b_solve * num_envs / t_launch / 1e9,
+        "limiter": limiter,
       },
+      "roofline_solver": solver_rl,
       "roofline_valu": valu,
       "cpu_baseline": cpu,
     }

@@ -34,7 +34,7 @@ typedef long long mjh_i64;
 extern "C" {
 #endif
 
-#define MJH_ABI_VERSION 16
+#define MJH_ABI_VERSION 17
 
 /* efc_type codes (mjtConstraint) */
 #define MJH_CNSTR_FRICTION_DOF 1
@@ -162,6 +162,28 @@ int mjh_plan_ints(const mjh_model* m, int* out, int cap);
 /* Index of the compiled model-specialised instance the step/forward launches
  * of model m use (-1: the generic instance). */
 int mjh_spec_index(const mjh_model* m);
+
+/* Registers a launch plugin: a model-specialised step instance compiled after
+ * this library for one launch plan (plan: mjh_plan_ints of the model, nplan
+ * ints; fn: the plugin library's mjh_plugin_step, see below). Step/forward
+ * launches of a model whose plan equals it, in the slab data layout, with
+ * pyramidal cones and the Newton or CG solver, run the plugin's instance
+ * after this library's model-image pack (which also orders the worlds).
+ * Replaces MuJoCo Warp's per-model kernel generation (mujoco_warp.put_model +
+ * the Warp JIT behind mjlab sim.py:116-147: whatever model is put is compiled
+ * for). Returns the plugin's index, or -1 on a null function / wrong length.
+ * Plugin libraries (mjh_step.hip built with -DMJH_PLUGIN and a one-plan
+ * table, mjlab_amd/sim/jit.py) export:
+ *   int mjh_plugin_abi(void);                    MJH_ABI_VERSION it was built at
+ *   int mjh_plugin_plan(int* out, int cap);      the plan it was built for
+ *   int mjh_plugin_step(int step, const mjh_model*, const mjh_data*,
+ *                       const unsigned char* gate, void* stream, int reuse,
+ *                       unsigned long long key); 0 on success */
+int mjh_register_spec_plugin(void* fn, const int* plan, int nplan);
+
+/* Index of the registered plugin the launches of model m use (-1: none; a
+ * built-in specialisation, mjh_spec_index >= 0, takes precedence). */
+int mjh_plugin_index(const mjh_model* m);
 
 /* 1 if every data array of d lies in one slab, array f at nworld * (words per
  * world of the arrays before f, MJH_DATA_ARRAYS order) from d->qpos — the

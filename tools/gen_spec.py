@@ -18,11 +18,8 @@ sys.path.insert(0, str(ROOT / "asimov-mjlab_amd"))
 OUT = ROOT / "asimov-mjlab_amd" / "csrc" / "mjh_spec_table.h"
 if "--out" in sys.argv:  # variant builds (tools/build_variant.py) write their own table
   OUT = Path(sys.argv[sys.argv.index("--out") + 1])
-EMPTY = """// Generated by tools/gen_spec.py --empty: no specialisations (first build stage).
-#define MJH_NSPEC 0
-static const int kSpecPlan[1][kPlanInts] = {};
-constexpr int kSpecNvp[1] = {36};
-"""
+from mjlab_amd.sim.spec_table import EMPTY, layout_ints, plan_of, render  # noqa: E402
+
 if "--empty" in sys.argv:  # before anything loads the (possibly stale) library
   OUT.write_text(EMPTY)
   sys.exit(0)
@@ -34,65 +31,24 @@ from mjlab_amd.tasks import load_env_cfg  # noqa: E402
 TASKS = ("Mjlab-Velocity-Flat-Unitree-G1", "Mjlab-Velocity-Flat-Unitree-Go1", "Mjlab-Tracking-Flat-Unitree-G1")
 
 
-def plan_of(task: str) -> list[int]:
+def task_plan(task: str) -> list[int]:
   cfg = load_env_cfg(task)
   cfg.scene.num_envs = 1
+  cfg.sim.specialize = "off"  # the plan only: no plugin lookup
   sim = Simulation(1, cfg.sim, Scene(cfg.scene, device="cpu").compile(), "cpu")
-  buf = (ctypes.c_int * 4096)()
-  n = native.lib().mjh_plan_ints(ctypes.addressof(sim._mstruct), buf, 4096)
-  assert n > 0
-  return list(buf[:n])
+  return plan_of(native.lib(), ctypes.addressof(sim._mstruct))
 
 
 def main() -> None:
   plans, names = [], []
   for t in TASKS:
-    p = plan_of(t)
+    p = task_plan(t)
     if p not in plans:
       plans.append(p)
       names.append(t)
-  nplan = len(plans[0])
-  lines = [
-    "// Generated by tools/gen_spec.py — model-specialised step-kernel constants.",
-    "// Plans: [nvp, sizes (MJH_MODEL_SIZES), Layout, ImgOff] of the benchmark models:",
-  ]
-  lines += [f"//   {k}: {n}" for k, n in enumerate(names)]
-  lines.append(f"#define MJH_NSPEC {len(plans)}")
-  lines.append(f"static_assert(kPlanInts == {nplan}, \"regenerate mjh_spec_table.h (tools/gen_spec.py)\");")
-  lines.append(f"static const int kSpecPlan[MJH_NSPEC][kPlanInts] = {{")
-  for p in plans:
-    lines.append("  {" + ", ".join(map(str, p)) + "},")
-  lines.append("};")
-  lines.append("constexpr int kSpecNvp[MJH_NSPEC] = {" + ", ".join(str(p[0]) for p in plans) + "};")
-  for k, p in enumerate(plans):
-    nsz = None
-    # sizes, layout and image offsets as aggregate initialisers (declaration order)
-    lines.append(f"template <> __device__ __forceinline__ Sizes spec_sizes<{k}>(const mjh_model&) {{")
-    lines.append(f"  return Sizes{{{', '.join(map(str, p[1:1 + SIZE_INTS]))}}};\n}}")
-    lines.append(f"template <> __device__ __forceinline__ Layout spec_layout<{k}>(const Layout&) {{")
-    lines.append(f"  return Layout{{{', '.join(map(str, p[1 + SIZE_INTS:1 + SIZE_INTS + LAYOUT_INTS]))}}};\n}}")
-    lines.append(f"template <> __device__ __forceinline__ ImgOff spec_imgoff<{k}>(const ImgOff&) {{")
-    lines.append(f"  return ImgOff{{{', '.join(map(str, p[1 + SIZE_INTS + LAYOUT_INTS:]))}}};\n}}")
-  OUT.write_text("\n".join(lines) + "\n")
+  OUT.write_text(render(plans, names, layout_ints(native.lib())))
   print(f"wrote {OUT.name}: {len(plans)} specialisations ({', '.join(names)})")
 
 
-def _counts() -> tuple[int, int]:
-  hdr = (ROOT / "include" / "mjh_fields.h").read_text()
-  import re
-
-  body = hdr[hdr.index("#define MJH_MODEL_SIZES"):]
-  body = body[: body.index("\n\n")]
-  sizes = len(re.findall(r"MS\((\w+)\)", body))
-  return sizes
-
-
-SIZE_INTS = _counts()
-LAYOUT_INTS = None  # filled from the plan length below
-
 if __name__ == "__main__":
-  # layout/image split: the library reports its total; the image part is the
-  # remainder after the layout, whose size the library also exports
-  n_layout = ctypes.c_int.in_dll(native.lib(), "mjh_layout_ints").value
-  LAYOUT_INTS = n_layout
   main()

@@ -17,7 +17,7 @@ S=$(find $O/st -name '*kernel_stats.csv' | head -1)
 F=$(find $O/pf -name '*counter_collection.csv' | head -1)
 W=$(find $O/pw -name '*counter_collection.csv' | head -1)
 cp $S $O/split_kernel_stats.csv
-python tools/solver_roofline.py $S $F $W $O/kb_split.log 4096 35 > $O/solver_roofline.json
+python tools/solver_roofline.py $S $F $W $O/kb_split.log 4096 35 "$TAG" > $O/solver_roofline.json
 cat $O/solver_roofline.json
 for P in pf pw; do
   C=$(find $O/$P -name '*counter_collection.csv' | head -1)

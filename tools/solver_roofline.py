@@ -58,6 +58,10 @@ print(json.dumps({
   "num_envs": n, "kernel": name, "launch_us": t_us, "mean_nefc": nefc, "mean_iters": iters,
   "b_solve_per_world": b_solve, "algorithmic_gbs": alg, "algorithmic_frac": alg / HBM,
   "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb, "counter_gbs": cnt, "counter_frac": cnt / HBM,
-  "launches": [nf, nw], "peak_gbs": HBM,
+  "launches": [nf, nw], "peak_gbs": HBM, "task": "Mjlab-Velocity-Flat-Unitree-G1",
+  "head": sys.argv[7] if len(sys.argv) > 7 else None,
+  "gap": f"40% of 8 TB/s on {b_solve * n / 1e6:.1f} MB is a {b_solve * n / (0.4 * HBM * 1e9) * 1e6:.0f} us launch, "
+         f"{t_us / (b_solve * n / (0.4 * HBM * 1e9) * 1e6):.1f}x faster than the measured {t_us:.0f} us: the solver is a "
+         "per-world serial chain over an LDS/L2-resident hot set (DESIGN.md §4), not an HBM stream",
   "source": "tools/gpu_solver_pmc.sh: MJH_SPLIT=1 build, tools/kernel_bench.py G1 4096, rocprofv3 --stats + --pmc FETCH_SIZE / WRITE_SIZE",
 }, indent=1))

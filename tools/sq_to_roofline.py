@@ -13,6 +13,10 @@ out = Path(sys.argv[5]) if len(sys.argv) > 5 else Path(__file__).resolve().paren
 s = json.load(open(src))
 pk = {k: v for k, v in s.get("per_kernel", {}).items() if "step_kernel" in k}
 ins = sum(v.get("SQ_INSTS_VALU", 0.0) for v in pk.values())
+# latency share: wave-cycles spent waiting (any dependency) over all wave-cycles
+wait = sum(v.get("SQ_WAIT_ANY", 0.0) for v in pk.values()) or s.get("SQ_WAIT_ANY", 0.0)
+cyc = sum(v.get("SQ_WAVE_CYCLES", 0.0) for v in pk.values()) or s.get("SQ_WAVE_CYCLES", 0.0)
 out.write_text(json.dumps({"task": task, "num_envs": n, "valu_insts_per_launch": ins, "kernels": sorted(pk),
+                           "wait_any_frac": (wait / cyc) if cyc else None, "sq_wait_any": wait, "sq_wave_cycles": cyc,
                            "source": tag}, indent=1) + "\n")
 print("wrote", out, ins)
