@@ -1548,6 +1548,12 @@ __device__ __forceinline__ float cone_eval(int dim, const ConeRows& c, float (&f
 // scratch address folds into an instruction offset instead of living in
 // (spilled) scalar registers. SPEC = -1 is the generic instance. The host picks
 // a specialisation only when the model's launch plan matches it exactly.
+// extension sensor groups (Sizes::sensor_ext_mask, spec/compiler.py SENSOR_EXT_GROUPS):
+// the bits of the groups a model has; a specialised instance carries only their code
+enum : int {
+  kExtEnergy = 1, kExtForce = 2, kExtFramePos = 4, kExtFrameQuat = 8, kExtFrameVel = 16, kExtFrameAcc = 32,
+  kExtLimit = 64, kExtActuator = 128, kExtBall = 256, kExtClock = 512, kExtRange = 1024, kExtMag = 2048
+};
 struct Sizes {
 #define X_SZS(name) int name;
   MJH_MODEL_SIZES(X_SZS)
@@ -3981,7 +3987,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         continue;
       }
 #ifndef MJH_NO_EXT
-      if (Z.nsensor_ext > 0 && (type == 48 || type == 49)) {  // compile-time 0 in the benchmark models' instances
+      if ((Z.sensor_ext_mask & kExtEnergy) && (type == 48 || type == 49)) {  // compile-time 0 in the benchmark models' instances
         // e_potential (mj_energyPos: gravity over bodies + joint springs) /
         // e_kinetic (mj_energyVel: qvel' M qvel / 2, M rows from the factor pass)
         float e = 0.f, z = 0.f;
@@ -4070,7 +4076,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
 #ifndef MJH_NO_FT
     // force / torque sensors (mj_sensorAcc), in a pass of their own so that no
     // state of theirs is live in the loop above
-    for (int s = 0; s < (Z.nsensor_ext > 0 ? Z.nsensor : 0); s++) {
+    for (int s = 0; s < ((Z.sensor_ext_mask & kExtForce) ? Z.nsensor : 0); s++) {
       const int type = IMG_I(sensor_type)[s];
       if (type != 4 && type != 5) continue;
       const int id = IMG_I(sensor_objid)[s];
@@ -4124,13 +4130,15 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       v[0] = cv[0]; v[1] = cv[1]; v[2] = cv[2];
       v[3] = cv[3] - t[0]; v[4] = cv[4] - t[1]; v[5] = cv[5] - t[2];
     };
-    // the sensor types outside the benchmark tasks' set (Sizes::nsensor_ext)
+    // the sensor types outside the benchmark tasks' set, by group (Sizes::sensor_ext_mask: an
+    // instance specialised for a model compiles in only the groups the model has)
     auto ext_sensor = [&](int s, int type, int id, float* out) {
       switch (type) {
         case 30:
         case 41:
         case 42:
         case 43: {  // framepos / frame{x,y,z}axis, optionally in the ref frame (mj_sensorPos)
+          if (!(Z.sensor_ext_mask & kExtFramePos)) break;
           float p[3], R[9], pr[3], Rr[9], v[3];
           int b, br;
           obj_frame(IMG_I(sensor_objtype)[s], id, p, R, b);
@@ -4146,6 +4154,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           break;
         }
         case 31: {  // framequat, relative to the ref frame when one is given: conj(q_ref) * q
+          if (!(Z.sensor_ext_mask & kExtFrameQuat)) break;
           float q[4];
           obj_quat(IMG_I(sensor_objtype)[s], id, q);
           const int rid = IMG_I(sensor_refid)[s];
@@ -4160,6 +4169,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         }
         case 44:
         case 45: {  // framelinvel / frameangvel (mj_sensorVel): world frame, or relative to the ref frame and in it
+          if (!(Z.sensor_ext_mask & kExtFrameVel)) break;
           float p[3], R[9], v[6];
           int b;
           obj_frame(IMG_I(sensor_objtype)[s], id, p, R, b);
@@ -4188,6 +4198,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         }
         case 46:
         case 47: {  // framelinacc / frameangacc (mj_objectAcceleration, world frame): cacc at the frame origin + w x v
+          if (!(Z.sensor_ext_mask & kExtFrameAcc)) break;
           float p[3], R[9];
           int b;
           obj_frame(IMG_I(sensor_objtype)[s], id, p, R, b);
@@ -4206,6 +4217,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         case 20:
         case 21:
         case 22: {  // jointlimitpos / vel / frc: the joint's limit row (efc_pos - margin, J qvel, force); 0 if inactive
+          if (!(Z.sensor_ext_mask & kExtLimit)) break;
           float val = 0.f;
           const int nr = min(nefc, Lo.rcap);
           for (int r = 0; r < nr; r++) {
@@ -4218,13 +4230,15 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         }
         case 13:  // actuatorpos / actuatorvel: gear * joint coordinate (joint transmission)
         case 14: {
+          if (!(Z.sensor_ext_mask & kExtActuator)) break;
           const int j = IMG_I(actuator_trnid)[id];
           out[0] = IMG_F(actuator_gear)[id] * (type == 13 ? qpos[IMG_I(jnt_qposadr)[j]] : qvel[IMG_I(jnt_dofadr)[j]]);
           break;
         }
-        case 15: out[0] = act_force[id]; break;
-        case 16: out[0] = qfrc_act[IMG_I(jnt_dofadr)[id]]; break;
+        case 15: if (Z.sensor_ext_mask & kExtActuator) out[0] = act_force[id]; break;
+        case 16: if (Z.sensor_ext_mask & kExtActuator) out[0] = qfrc_act[IMG_I(jnt_dofadr)[id]]; break;
         case 18: {  // ballquat: the normalised joint quaternion
+          if (!(Z.sensor_ext_mask & kExtBall)) break;
           float q[4];
           const float* qp = qpos + IMG_I(jnt_qposadr)[id];
           q[0] = qp[0]; q[1] = qp[1]; q[2] = qp[2]; q[3] = qp[3];
@@ -4233,12 +4247,14 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           break;
         }
         case 19: {
+          if (!(Z.sensor_ext_mask & kExtBall)) break;
           const float* qv = qvel + IMG_I(jnt_dofadr)[id];
           out[0] = qv[0]; out[1] = qv[1]; out[2] = qv[2];
           break;
         }
-        case 50: out[0] = DP(time)[W]; break;
+        case 50: if (Z.sensor_ext_mask & kExtClock) out[0] = DP(time)[W]; break;
         case 7: {  // rangefinder (mj_ray along the site's z axis; not the site body's geoms, not rgba alpha 0)
+          if (!(Z.sensor_ext_mask & kExtRange)) break;
           const float* R = sxmat + 9 * id;
           const float vec[3] = {R[2], R[5], R[8]};
           const float* rgba = WFIELD(geom_rgba);
@@ -4256,6 +4272,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           break;
         }
         case 6: {  // magnetometer: the global field in the site frame
+          if (!(Z.sensor_ext_mask & kExtMag)) break;
           const float mg[3] = {m.magnetic_x, m.magnetic_y, m.magnetic_z};
           float r[3];
           matT_vec(r, sxmat + 9 * id, mg);
@@ -4307,7 +4324,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         case 10: out[0] = qvel[IMG_I(jnt_dofadr)[id]]; break;
         case 34: out[0] = subtree_com[3 * id]; out[1] = subtree_com[3 * id + 1]; out[2] = subtree_com[3 * id + 2]; break;
         default:
-          if (Z.nsensor_ext > 0) ext_sensor(s, type, id, out);  // compile-time 0 in the benchmark models' instances
+          if (Z.sensor_ext_mask != 0) ext_sensor(s, type, id, out);  // compile-time 0 in the benchmark models' instances
           break;
       }
       const float cut = IMG_F(sensor_cutoff)[s];

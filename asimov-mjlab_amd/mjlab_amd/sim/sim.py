@@ -191,8 +191,9 @@ class SimulationCfg:
   balance_worlds: bool = True
   # model-specialised step kernel for a model outside the built-in table
   # (mjlab_amd/sim/jit.py): "auto" compiles a launch plugin once per launch plan
-  # (cached), "cached" only uses one already built, "off" keeps the generic instance
-  specialize: str = "auto"
+  # (cached), "cached" only uses one already built, "off" keeps the generic
+  # instance; default from MJH_SPECIALIZE (the test suite sets "cached")
+  specialize: str = field(default_factory=lambda: os.environ.get("MJH_SPECIALIZE", "auto"))
   mujoco: MujocoCfg = field(default_factory=MujocoCfg)
   nan_guard: NanGuardCfg = field(default_factory=NanGuardCfg)
 

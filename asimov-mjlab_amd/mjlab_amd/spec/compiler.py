@@ -112,8 +112,12 @@ SENSOR_DIMS = {
   "clock": 1,
 }
 # the sensor types the step kernel evaluates on every path (the benchmark tasks'
-# set); the others count into Model.nsensor_ext
+# set); the others count into Model.nsensor_ext and set their group's bit in
+# Model.sensor_ext_mask (a model size: mjh_step.hip's kExt* groups)
 BASE_SENSOR_CODES = {1, 2, 3, 9, 10, 34, 35, 36, 40}
+SENSOR_EXT_GROUPS = {48: 1, 49: 1, 4: 2, 5: 2, 30: 4, 41: 4, 42: 4, 43: 4, 31: 8, 44: 16, 45: 16, 46: 32, 47: 32,
+                     20: 64, 21: 64, 22: 64, 13: 128, 14: 128, 15: 128, 16: 128, 18: 256, 19: 256, 50: 512, 7: 1024,
+                     6: 2048}
 # sensors whose values are unit quaternions or axes: no cutoff (mjDATATYPE_QUATERNION / _AXIS)
 SENSOR_NO_CUTOFF = {"framequat", "ballquat", "framexaxis", "frameyaxis", "framezaxis"}
 # Contact sensor data fields: bit -> width (src/mjlab/sensor/contact_sensor.py:16-34).
@@ -149,6 +153,7 @@ class Model:
   # writes their poses once and the step kernel sees only the sites after them
   nsite_origin = 0
   nsensor_ext = 0
+  sensor_ext_mask = 0
   magnetic = np.array([0.0, -0.5, 0.0])  # models built before the option existed
 
   def __init__(self) -> None:
@@ -671,6 +676,12 @@ def _compile_sensors(m: Model, spec: Spec) -> None:
   # specialised kernels' plans: an instance built for a model without them
   # carries none of their code)
   m.nsensor_ext = int(sum(1 for t in m.sensor_type if int(t) not in BASE_SENSOR_CODES))
+  m.sensor_ext_mask = 0
+  for t in m.sensor_type:
+    if int(t) not in BASE_SENSOR_CODES:
+      if int(t) not in SENSOR_EXT_GROUPS:
+        raise NotImplementedError(f"sensor type {int(t)} has no device evaluation")
+      m.sensor_ext_mask |= SENSOR_EXT_GROUPS[int(t)]
 
 
 def _kinematics0(m: Model):

@@ -26,7 +26,7 @@
 #define MJH_MODEL_SIZES(MS) \
   MS(nq) MS(nv) MS(nu) MS(na) MS(nbody) MS(njnt) MS(ngeom) MS(nsite)        \
   MS(nsensor) MS(nsensordata) MS(npair) MS(nmocap) MS(nconmax) MS(njmax)     \
-  MS(nchain) MS(ncolgeom) MS(nboxpair) MS(nsensor_ext)
+  MS(nchain) MS(ncolgeom) MS(nboxpair) MS(sensor_ext_mask)
 
 /* ---- options (mjOption subset used by mjlab's MujocoCfg, sim.py:42-76) ---- */
 #define MJH_MODEL_OPTIONS(MO) \

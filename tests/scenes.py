@@ -434,7 +434,8 @@ LS_CAPPED_FRAC = 0.125
 
 
 def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: float = 0.005, solve_rel: float = SOLVE_REL,
-                 solve_frac: float = SOLVE_FRAC, solve_max: float = SOLVE_MAX, skip: tuple[str, ...] = ()) -> dict:
+                 solve_frac: float = SOLVE_FRAC, solve_max: float = SOLVE_MAX, skip: tuple[str, ...] = (),
+                 cap_exempt: bool = True) -> dict:
   """Compare one step's outputs (arrays shaped (nworld, -1)).
 
   Integer outputs (contacts by geom pair, nefc, efc types/ids) are compared
@@ -445,6 +446,8 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
   constraint rows (efc_pos/D/aref/force, and efc_J when both sides carry the
   debug copies) and the solver, integration and sensor outputs on every world
   whose integer outputs agree; qM (debug copy) on every world.
+  cap_exempt=False holds the worlds unconverged at the iteration cap to the hard
+  bounds too (a test that caps the solver by construction, a few iterations).
   Returns {"maxerr", "failures", "int_mismatch_worlds", "int_mismatch_reasons",
   "int_match_rate"}."""
   n = got["qpos"].shape[0]
@@ -462,6 +465,7 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
   good = np.array([w for w in sel if int(w) not in reasons], dtype=int)
   # unconverged worlds under the parallel line search: no hard bound (path-dependent)
   capped: list[int] = []
+  ls_bad: list[int] = []
   n_ls_bad = 0
   if "ls_excess" in ref and len(good):
     ex = ref["ls_excess"][good, 0]
@@ -498,11 +502,17 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
         failures.append(f"ls_choice: {len(bad)} worlds replayed a step size beyond {LS_NOISE_K}x the float32 cost "
                         f"noise (worst {worst:.2f}x, worlds {bad[:8]})")
       capped += [w for w in bad if w not in capped]
+      ls_bad = list(bad)
   if "solver_capped" in ref and ("ls_gap" in ref or "ls_excess" in ref):
     lsp = np.isfinite(ref["ls_gap"][:, 0]) if "ls_gap" in ref else np.ones(len(ref["ls_excess"]), bool)
     capped += [int(w) for w in good if ref["solver_capped"][w, 0] and lsp[w] and int(w) not in capped]
-    if len(capped) > max(1, int(LS_CAPPED_FRAC * len(sel))):
+    if cap_exempt and len(capped) > max(1, int(LS_CAPPED_FRAC * len(sel))):
       failures.append(f"{len(capped)}/{len(sel)} worlds unconverged at the iteration cap (> {LS_CAPPED_FRAC:.0%})")
+  capped_held = 0
+  if not cap_exempt:  # capped by construction: every bound applies (line-search outliers stay soft)
+    keep = set(ls_bad)
+    capped_held = len([w for w in capped if w not in keep])
+    capped = [w for w in capped if w in keep]
   solved = good
 
   soft_over: dict[str, int] = {}  # per output: worlds over the soft (per-world) bound, admitted up to 1 - frac
@@ -643,6 +653,8 @@ def compare_step(got: dict, ref: dict, worlds: np.ndarray | None = None, dt: flo
     "worst_bound": max(ratios, default=0.0),
     "soft_over": max(soft_over.values(), default=0),
     "capped": len(capped),
+    "capped_held_hard": capped_held,
+    "capped_verified": 0,
     "ls_outliers": n_ls_bad,
     "int_mismatch": len(bad_int),
     "stop_mismatch": dec["stop_mismatch"],

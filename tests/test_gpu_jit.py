@@ -34,6 +34,7 @@ G1 = "Mjlab-Velocity-Flat-Unitree-G1"
 
 def _sim(n, framepos=("pelvis",)):
   cfg, m = task_model(G1, framepos)
+  cfg.sim.specialize = "auto"  # build the plugin if the tree has none (prebuilt by __graft_entry__.build())
   return Simulation(n, cfg.sim, m, DEV), m
 
 
@@ -95,5 +96,5 @@ def test_plugin_speed_against_generic_and_builtin():
   t_builtin = _launch_ms(base, mb, n)
   print(f"[plugin speed] G1+framepos N={n}: plugin {t_plugin:.3f} ms, generic {t_generic:.3f} ms per launch; "
         f"benchmark G1 built-in instance {t_builtin:.3f} ms (plugin/builtin {t_plugin / t_builtin:.3f})")
-  assert t_plugin < t_generic
-  assert t_plugin <= 1.15 * t_builtin
+  assert t_plugin <= 1.02 * t_generic
+  assert t_plugin <= 1.10 * t_builtin

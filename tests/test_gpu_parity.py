@@ -33,15 +33,63 @@ def get(sim, n):
   return {k: getattr(sim.data, k).detach().cpu().numpy().reshape(n, -1) for k in sim.data.fields()}
 
 
-def assert_parity(got, ref, n, min_int_rate=0.98, tag=""):
+LIFTED_ITERATIONS = 100
+
+
+def recheck_capped(m, state, worlds, ls_parallel=True, integrate=True, cfg=None, overrides=None):
+  """The worlds a comparison held to the soft bound because the solver stopped
+  at the iteration cap (tests/scenes.py: unconverged, so a float32 and a float64
+  iterate drift apart) are solved again from the same state with the cap lifted
+  (LIFTED_ITERATIONS), device against the oracle (follow mode), and now held to
+  every hard bound; both must converge. A world that passes is no longer an
+  unverified exemption (the PARITY summary's capped_unverified)."""
+  import copy
+
+  from tests.scenes import PARITY_LOG
+
+  worlds = [int(w) for w in worlds]
+  k = len(worlds)
+  mc = copy.deepcopy(m)
+  base = dict(cfg or CFG)
+  mj = copy.deepcopy(base["mujoco"])
+  mj.iterations = LIFTED_ITERATIONS
+  base["mujoco"] = mj
+  sim = Simulation(k, SimulationCfg(**base, ls_parallel=ls_parallel), mc, DEV)
+  sub_over = None
+  if overrides:
+    sub_over = {name: np.asarray(a)[worlds] for name, a in overrides.items()}
+    sim.expand_model_fields(tuple(sub_over))
+    for name, a in sub_over.items():
+      t = getattr(sim.model, name)
+      t.copy_(torch.as_tensor(a, dtype=t.dtype, device=DEV).view_as(t))
+  sub = {f: np.asarray(v)[worlds] for f, v in state.items()}
+  put(sim, sub)
+  sim.step() if integrate else sim.forward()
+  got = get(sim, k)
+  ref = Oracle(mc, overrides=sub_over).run(k, sub, integrate=integrate, follow=got if ls_parallel else None)
+  rep = compare_step(got, ref, cap_exempt=False)
+  PARITY_LOG.pop()  # the re-run is recorded on the original comparison's entry
+  conv = got["solver_niter"][:, 0] < LIFTED_ITERATIONS
+  assert not rep["failures"] and conv.all(), ("capped worlds re-run with the cap lifted", worlds, rep["failures"],
+                                              got["solver_niter"][:, 0])
+  PARITY_LOG[-1]["capped_verified"] = k
+  return k
+
+
+def assert_parity(got, ref, n, min_int_rate=0.98, tag="", recheck=None):
   """compare_step must report no failure (every integer mismatch explained by
   a borderline contact/row; floats within tests/scenes.py tolerances), and at
-  least `min_int_rate` of the worlds must have bit-identical integer outputs."""
+  least `min_int_rate` of the worlds must have bit-identical integer outputs.
+  recheck (model, state and the run's options): the capped worlds are solved
+  again with the iteration cap lifted and held to the hard bounds."""
   rep = compare_step(got, ref)
   print(f"[parity{tag}] int_match_rate={rep['int_match_rate']:.4f} mismatches={rep['int_mismatch_reasons']} "
         f"maxerr={ {k: f'{v:.2e}' for k, v in rep['maxerr'].items()} }")
   assert not rep["failures"], (rep["failures"], rep["maxerr"])
   assert rep["int_match_rate"] >= min_int_rate, rep["int_mismatch_reasons"]
+  capped = [w for w in rep["capped_worlds"] if w not in rep["int_mismatch_reasons"]]
+  if recheck is not None and capped:
+    recheck_capped(worlds=capped, **recheck)
   return rep
 
 
@@ -62,7 +110,8 @@ def test_single_step_parity(name, integrate, ls_parallel):
   got = get(sim, n)
   got.update({k: v.cpu().numpy().reshape(n, -1) for k, v in sim.debug_fields().items()})
   ref = Oracle(m).run(n, st, integrate=integrate, debug=True, follow=got)
-  rep = assert_parity(got, ref, n, tag=f" {name} integrate={integrate}")
+  rep = assert_parity(got, ref, n, tag=f" {name} integrate={integrate}",
+                      recheck=dict(m=m, state=st, ls_parallel=ls_parallel, integrate=integrate))
   assert "qM" in rep["maxerr"] and "efc_J" in rep["maxerr"]  # the debug copies were compared
   assert (got["ncon"] > 0).mean() > 0.5  # the states exercise contacts
   it = check_iteration_counts(got, m, st, integrate)
@@ -86,7 +135,7 @@ def test_trajectory_parity_along_gpu_rollout():
     sim.step()
     nxt = get(sim, n)
     ref = orc.run(n, state, integrate=True, follow=nxt)
-    rep = assert_parity(nxt, ref, n, min_int_rate=0.95, tag=f" step {k}")
+    rep = assert_parity(nxt, ref, n, min_int_rate=0.95, tag=f" step {k}", recheck=dict(m=m, state=state))
     worst = max(worst, rep["maxerr"]["qvel"])
     worst32 = max(worst32, float(np.abs(ref["f32"]["qvel"] - ref["qvel"]).max()))
   # 0.05 m/s, or the float32 oracle's own deviation along the same choices (x4,
@@ -106,7 +155,7 @@ def test_per_world_randomized_friction():
   sim.step()
   got = get(sim, n)
   ref = Oracle(m, overrides={"geom_friction": fr.cpu().numpy()}).run(n, st, integrate=True, follow=got)
-  assert_parity(got, ref, n)
+  assert_parity(got, ref, n, recheck=dict(m=m, state=st, overrides={"geom_friction": fr.cpu().numpy()}))
 
 
 def test_gated_forward():
@@ -226,7 +275,7 @@ def test_full_size_integer_parity_rate():
   sim.step()
   got = get(sim, n)
   ref = Oracle(m).run(n, st, integrate=True, nthreads=8, follow=got)
-  assert_parity(got, ref, n, min_int_rate=0.999, tag=" N=4096")
+  assert_parity(got, ref, n, min_int_rate=0.999, tag=" N=4096", recheck=dict(m=m, state=st))
 
 
 def test_contact_sensor_reductions_and_fields():
@@ -368,7 +417,7 @@ def test_mocap_body_parity(integrate):
   sim.step() if integrate else sim.forward()
   got = get(sim, n)
   ref = Oracle(m).run(n, st, integrate=integrate, follow=got)
-  assert_parity(got, ref, n, tag=f" mocap integrate={integrate}")
+  assert_parity(got, ref, n, tag=f" mocap integrate={integrate}", recheck=dict(m=m, state=st, integrate=integrate))
   b = int(np.nonzero(m.body_mocapid >= 0)[0][0])
   np.testing.assert_allclose(got["xpos"].reshape(n, -1, 3)[:, b], st["mocap_pos"][:, :3], atol=1e-6)
   g = [i for i in range(m.ngeom) if m.geom_bodyid[i] == b][0]
@@ -439,10 +488,11 @@ def test_cg_solver_parity(ls_parallel, iterations):
   sim.step()
   got = get(sim, n)
   ref = Oracle(m).run(n, st, integrate=True, follow=got if ls_parallel else None)
-  # capped by construction (a few iterations): the soft solve test only
-  rep = compare_step(got, ref)
+  # capped by construction (a few iterations), and held to every hard bound: over
+  # 1-3 iterations float32 and float64 CG stay together along the same choices
+  rep = compare_step(got, ref, cap_exempt=False)
   print(f"[cg iterations={iterations}]", {k: f"{v:.2e}" for k, v in rep["maxerr"].items() if "/" in k})
-  assert not [f for f in rep["failures"] if "unconverged at the iteration cap" not in f], rep["failures"]
+  assert not rep["failures"], rep["failures"]
 
 
 BOX_SCENE = """<mujoco><compiler angle="radian"/><option timestep="0.002"/><worldbody>
@@ -528,7 +578,8 @@ def test_elliptic_cone_parity(ls_parallel):
   types = {int(t) for w in range(n) for t in got["efc_type"][w, : int(got["nefc"][w, 0])]}
   assert 7 in types and 6 not in types, types
   ref = Oracle(m).run(n, st, integrate=True, follow=got if ls_parallel else None)
-  assert_parity(got, ref, n, tag=f" elliptic ls_parallel={ls_parallel}")
+  assert_parity(got, ref, n, tag=f" elliptic ls_parallel={ls_parallel}",
+                recheck=dict(m=m, state=st, ls_parallel=ls_parallel, cfg=cfg))
 
 
 def test_elliptic_cone_converged_parity():
@@ -711,6 +762,55 @@ def test_convex_pairs_parity():
   kinds = {(int(types[a]), int(types[b])) for w in range(n) for a, b in g[w, : int(got["ncon"][w, 0])]}
   assert CONVEX_PAIRS <= kinds, sorted(CONVEX_PAIRS - kinds)  # every convex pair was exercised
   print("[convex pairs] contact kinds", sorted(kinds), "int rate", rep["int_match_rate"])
+  _check_convex_against_support_minimum(m, got, q, n)
+
+
+def _check_convex_against_support_minimum(m, got, q, n, per_kind=6):
+  """The HIP contacts of the convex pairs against an independent statement of
+  the answer (not the shared-source oracle): for each pair
+  kind, `per_kind` worlds' contact depth must equal -min over unit u of
+  h1(u) + h2(-u) (tests/test_convex.py's numpy support functions, Fibonacci sphere
+  + Nelder-Mead), the overlap along the HIP normal must attain that minimum, and
+  the contact point must lie midway between the two extreme points along it.
+  Tolerances are float32-level (5e-5 m on 0.05-0.2 m shapes)."""
+  from mjlab_amd.spec.compiler import CONVEX_PAIRS
+  from mjlab_amd.utils import rot
+  from tests.test_convex import _min_overlap, _overlap, _support
+
+  types, sizes = np.asarray(m.geom_type), np.asarray(m.geom_size)
+  gpos, gquat = np.asarray(m.geom_pos), np.asarray(m.geom_quat)
+  bid = np.asarray(m.geom_bodyid)
+
+  def shape(w, g):
+    b = int(bid[g])
+    if b == 0:  # a static geom: its own pose
+      R, c = rot.quat_to_mat(gquat[g]), np.asarray(gpos[g], dtype=np.float64)
+    else:  # one geom per body, at the body origin: the body's free-joint pose
+      j = 7 * (b - 1)
+      R, c = rot.quat_to_mat(q[w, j + 3 : j + 7]), q[w, j : j + 3]
+    return (int(types[g]), list(sizes[g]), R, np.asarray(c, dtype=np.float64))
+
+  checked = {}
+  geoms = got["contact_geom"].reshape(n, -1, 2)
+  for w in range(n):
+    for k in range(int(got["ncon"][w, 0])):
+      g1, g2 = (int(x) for x in geoms[w, k])
+      kind = (int(types[g1]), int(types[g2]))
+      if kind not in CONVEX_PAIRS or checked.get(kind, 0) >= per_kind:
+        continue
+      P, Q = shape(w, g1), shape(w, g2)
+      fmin, _ = _min_overlap(P, Q)
+      d = float(got["contact_dist"].reshape(n, -1)[w, k])
+      nrm = got["contact_frame"].reshape(n, -1, 9)[w, k, :3].astype(np.float64)
+      pos = got["contact_pos"].reshape(n, -1, 3)[w, k].astype(np.float64)
+      assert abs(d + fmin) <= 5e-5, (kind, w, d, -fmin)
+      assert _overlap(P, Q, nrm)[0] - fmin <= 5e-5, (kind, w, nrm)
+      lo = np.dot(_support(*Q, -nrm[None])[0], nrm)
+      hi = np.dot(_support(*P, nrm[None])[0], nrm)
+      assert abs(np.dot(pos, nrm) - 0.5 * (lo + hi)) <= 5e-5, (kind, w)
+      checked[kind] = checked.get(kind, 0) + 1
+  print("[convex pairs] checked against the support-function minimum:", dict(sorted(checked.items())))
+  assert set(checked) == set(CONVEX_PAIRS) and min(checked.values()) == per_kind, checked
 
 
 BALL_SCENE = """<mujoco><compiler angle="radian"/><option timestep="0.002"/><worldbody>
