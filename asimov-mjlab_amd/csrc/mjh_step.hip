@@ -84,6 +84,21 @@ constexpr int kSolverPGS = 0, kSolverCG = 1;  // mjtSolver: mjSOL_PGS 0, mjSOL_C
 #ifndef MJH_PRESET
 #define MJH_PRESET 5
 #endif
+// sensor-phase variants (contact sensors: metadata preload, match test from
+// registers, LDS-only fences): A/B switches, see the sensor phase. Measured
+// (profiles/r06f_sensor_ab.log, G1 4096 kernel_bench, two passes): preload packed
+// 0.495 / 0.492 vs 0.498 / 0.500 ms (adopted); LDS-only fences no change; the
+// match test from registers (6 more live registers) 0.514 ms; unpacked preload
+// (10 registers) 0.527 ms (profiles/r06e) — the allocator moved spills into the solver
+#ifndef MJH_SENS_PRELOAD
+#define MJH_SENS_PRELOAD 2
+#endif
+#ifndef MJH_SENS_OMREG
+#define MJH_SENS_OMREG 0
+#endif
+#ifndef MJH_SENS_LSYNC
+#define MJH_SENS_LSYNC 0
+#endif
 #define MJH_REGIONS(X)                                                                              \
   X(qpos, 0) X(qvel, 0) X(qacc, 0) X(qacc_smooth, 0) X(qfrc_smooth, 0) X(qfrc_bias, 1) X(qfrc_con, 0)  \
   X(qfrc_passive, 1) X(qfrc_act, 1) X(grad, 0) X(search, 0) X(Ma, 0) X(Mv, 0) X(tmp, 0) X(tmp2, 0)    \
@@ -194,6 +209,10 @@ __device__ float* g_lsdbg;  // (nworld, 32) candidate costs of the parallel line
 // a workgroup share the CU's L1, so draining vmcnt makes a lane's stores
 // visible to the wave's other lanes (workgroup scope, non-tgsplit).
 __device__ __forceinline__ void wsync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
+// LDS-only fence (and a compiler barrier): a wave's LDS operations execute in
+// issue order, so this orders its LDS traffic without waiting for its
+// outstanding global stores as wsync does (vmcnt counts stores on gfx9)
+__device__ __forceinline__ void lsync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Word offsets of every model array inside the LDS model image, and of the
 // per-world copies of expanded (domain-randomised) fields (-1: shared).
@@ -3784,6 +3803,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     }
   }
   wsync();
+  PROF(26);
 
   // ---------------------------------------------------------------- sensors
   {
@@ -3795,7 +3815,33 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     const bool creg = ncon <= 64;
     bool cloaded = false;
     float cF[6], cfr[9], cps[3], cds = 0.f;
-    int cg1 = 0, cg2 = 0;
+    int cg1 = 0, cg2 = 0, cb1 = 0, cb2 = 0;  // contact tid's geoms and their bodies
+    unsigned long long ct1 = 0ull, ct2 = 0ull;  // the bodies' subtree masks (body_treemask)
+    // the sensors' metadata, lane s = sensor s (< 64), loaded in one round instead
+    // of a dependent chain of loads per sensor; read back by readlane (uniform s)
+    // (MJH_SENS_PRELOAD: 0 per-sensor loads, 1 one register per field, 2 packed
+    // into four registers; measured in profiles/r06*_ab)
+#if MJH_SENS_PRELOAD == 1
+    int q_type = -1, q_id = 0, q_adr = 0, q_bits = 0, q_red = 0, q_nslot = 0, q_ot = 0, q_rt = 0, q_rid = 0, q_dim = 0;
+    if (tid < Z.nsensor) {
+      q_type = IMG_I(sensor_type)[tid]; q_id = IMG_I(sensor_objid)[tid]; q_adr = IMG_I(sensor_adr)[tid];
+      q_bits = IMG_I(sensor_intprm)[3 * tid]; q_red = IMG_I(sensor_intprm)[3 * tid + 1];
+      q_nslot = IMG_I(sensor_intprm)[3 * tid + 2]; q_ot = IMG_I(sensor_objtype)[tid];
+      q_rt = IMG_I(sensor_reftype)[tid]; q_rid = IMG_I(sensor_refid)[tid]; q_dim = IMG_I(sensor_dim)[tid];
+    }
+    auto sq = [&](int v, const int* p, int s) -> int { return s < NT ? __builtin_amdgcn_readlane(v, s) : p[s]; };
+#elif MJH_SENS_PRELOAD == 2
+    // [type | objtype << 8 | reftype << 12 | bits << 16 | reduce << 24], adr,
+    // [objid | (refid + 1) << 16], [nslot | dim << 16] (field ranges checked by the compiler)
+    int q_a = -1, q_b = 0, q_c = 0, q_d = 0;
+    if (tid < Z.nsensor) {
+      q_a = IMG_I(sensor_type)[tid] | IMG_I(sensor_objtype)[tid] << 8 | IMG_I(sensor_reftype)[tid] << 12 |
+            IMG_I(sensor_intprm)[3 * tid] << 16 | IMG_I(sensor_intprm)[3 * tid + 1] << 24;
+      q_b = IMG_I(sensor_adr)[tid];
+      q_c = IMG_I(sensor_objid)[tid] | (IMG_I(sensor_refid)[tid] + 1) << 16;
+      q_d = IMG_I(sensor_intprm)[3 * tid + 2] | IMG_I(sensor_dim)[tid] << 16;
+    }
+#endif
     auto contact_force = [&](int ci, float (&F)[6]) {
 #pragma unroll
       for (int k = 0; k < 6; k++) F[k] = 0.f;
@@ -3817,27 +3863,67 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     // the same foot) repeat the same scan; the kept matches are still in sx
     int p_ot = -9, p_id = -9, p_rt = -9, p_rid = -9, p_cnt = 0;
     for (int s = 0; s < Z.nsensor; s++) {
+#if MJH_SENS_PRELOAD == 1
+      const int type = sq(q_type, IMG_I(sensor_type), s), id = sq(q_id, IMG_I(sensor_objid), s);
+      const int adr = sq(q_adr, IMG_I(sensor_adr), s);
+#elif MJH_SENS_PRELOAD == 2
+      const bool qr = s < NT;
+      const int qa = qr ? __builtin_amdgcn_readlane(q_a, s) : 0, qc = qr ? __builtin_amdgcn_readlane(q_c, s) : 0;
+      const int type = qr ? (qa & 255) : IMG_I(sensor_type)[s];
+      const int id = qr ? (qc & 0xffff) : IMG_I(sensor_objid)[s];
+      const int adr = qr ? __builtin_amdgcn_readlane(q_b, s) : IMG_I(sensor_adr)[s];
+#else
       const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
+#endif
       if (type == 40) {
         // contact sensor (MuJoCo mjSENS_CONTACT with mjlab's intprm encoding,
         // contact_sensor.py:472-496): matches in contact order, capped at
         // min(maxmatch, 64); then one lane per kept match.
-        const int bits = IMG_I(sensor_intprm)[3 * s], reduce = IMG_I(sensor_intprm)[3 * s + 1], nslot = IMG_I(sensor_intprm)[3 * s + 2];
+        const int* ip = IMG_I(sensor_intprm);
+#if MJH_SENS_PRELOAD == 1
+        const int bits = s < NT ? __builtin_amdgcn_readlane(q_bits, s) : ip[3 * s];
+        const int reduce = s < NT ? __builtin_amdgcn_readlane(q_red, s) : ip[3 * s + 1];
+        const int nslot = s < NT ? __builtin_amdgcn_readlane(q_nslot, s) : ip[3 * s + 2];
+        const int otype = sq(q_ot, IMG_I(sensor_objtype), s), rtype = sq(q_rt, IMG_I(sensor_reftype), s);
+        const int rid = sq(q_rid, IMG_I(sensor_refid), s);
+        const int dim = sq(q_dim, IMG_I(sensor_dim), s);
+#elif MJH_SENS_PRELOAD == 2
+        const int qd = qr ? __builtin_amdgcn_readlane(q_d, s) : 0;
+        const int bits = qr ? (qa >> 16) & 255 : ip[3 * s];
+        const int reduce = qr ? (qa >> 24) & 255 : ip[3 * s + 1];
+        const int nslot = qr ? (qd & 0xffff) : ip[3 * s + 2];
+        const int otype = qr ? (qa >> 8) & 15 : IMG_I(sensor_objtype)[s], rtype = qr ? (qa >> 12) & 15 : IMG_I(sensor_reftype)[s];
+        const int rid = qr ? (qc >> 16) - 1 : IMG_I(sensor_refid)[s];
+        const int dim = qr ? (qd >> 16) : IMG_I(sensor_dim)[s];
+#else
+        const int bits = ip[3 * s], reduce = ip[3 * s + 1], nslot = ip[3 * s + 2];
         const int otype = IMG_I(sensor_objtype)[s], rtype = IMG_I(sensor_reftype)[s], rid = IMG_I(sensor_refid)[s];
         const int dim = IMG_I(sensor_dim)[s];
+#endif
         const int cap = min(m.contact_sensor_maxmatch, 64);
         // kept matches in the solver's (now dead) LDS row-index array when it is
         // large enough (always for the benchmark models), else in global scratch.
         // The record is zeroed where it is written (below), so no store precedes
         // this sensor's scratch loads.
         int* const sx = acap + 4 >= 64 ? arow : sidx;
-        auto om = [&](int ty, int oid, int g) -> bool {
+        // the match list lives in LDS for the benchmark models (then only LDS
+        // ordering matters between its writes and reads: no wait for the
+        // sensordata stores in flight), else in global scratch
+        const bool sx_lds = MJH_SENS_LSYNC && (acap + 4 >= 64 ? (!BIG && !Rg::arow) : !Rg::sidx);
+        auto sx_fence = [&]() {
+          if (sx_lds) lsync(); else wsync();
+        };
+        // geom g (body gb, subtree mask tm) matches object (ty, oid)
+        auto om_b = [&](int ty, int oid, int g, int gb, unsigned long long tm) -> bool {
           if (oid < 0) return true;
-          const int gb = IMG_I(geom_bodyid)[g];
           if (ty == 5) return g == oid;
           if (ty == 1) return gb == oid;
-          if (ty == 2) return oid == 0 || (((unsigned long long)IMG_L(body_treemask)[gb] >> oid) & 1ull);
+          if (ty == 2) return oid == 0 || ((tm >> oid) & 1ull);
           return false;
+        };
+        auto om = [&](int ty, int oid, int g) -> bool {
+          const int gb = IMG_I(geom_bodyid)[g];
+          return om_b(ty, oid, g, gb, (unsigned long long)IMG_L(body_treemask)[gb]);
         };
         if (creg && !cloaded) {
           cloaded = true;
@@ -3855,6 +3941,12 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
             for (int k = 0; k < 3; k++) cps[k] = con_pos[3 * tid + k];
             cds = con_dist[tid];
             contact_force(tid, cF);
+            if (MJH_SENS_OMREG) {
+              cb1 = IMG_I(geom_bodyid)[cg1];
+              cb2 = IMG_I(geom_bodyid)[cg2];
+              ct1 = (unsigned long long)IMG_L(body_treemask)[cb1];
+              ct2 = (unsigned long long)IMG_L(body_treemask)[cb2];
+            }
           }
         }
         int cnt = 0;
@@ -3864,8 +3956,11 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           for (int base = 0; base < ncon; base += NT) {
             const int ci = base + tid;
             int match = 0, flip = 0;
-            if (ci < ncon) {
-              const int g1 = creg ? cg1 : con_geom[2 * ci], g2 = creg ? cg2 : con_geom[2 * ci + 1];
+            if (MJH_SENS_OMREG && ci < ncon && creg) {  // bodies and subtree masks in registers
+              if (om_b(otype, id, cg1, cb1, ct1) && om_b(rtype, rid, cg2, cb2, ct2)) match = 1;
+              else if (om_b(otype, id, cg2, cb2, ct2) && om_b(rtype, rid, cg1, cb1, ct1)) { match = 1; flip = 1; }
+            } else if (ci < ncon) {
+              const int g1 = con_geom[2 * ci], g2 = con_geom[2 * ci + 1];
               if (om(otype, id, g1) && om(rtype, rid, g2)) match = 1;
               else if (om(otype, id, g2) && om(rtype, rid, g1)) { match = 1; flip = 1; }
             }
@@ -3874,7 +3969,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
             if (match && cnt + off < cap) sx[cnt + off] = flip ? ~ci : ci;
             cnt += total;
           }
-          wsync();
+          sx_fence();
           p_ot = otype; p_id = id; p_rt = rtype; p_rid = rid; p_cnt = cnt;
         }
         const int nm = min(cnt, cap);
@@ -3886,7 +3981,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           // found only: the match count in the first min(nm, nslot) slots (one
           // record for netforce), zeros after — what the general path writes
           for (int k = tid; k < dim; k += NT) sd[adr + k] = (reduce == 3 ? k == 0 : k < nm) ? (float)nm : 0.f;
-          wsync();
+          sx_fence();  // only the match list needs ordering (the sensordata stores need none)
           continue;
         }
         // lane k < nm: match k. F = contact force/torque in the contact frame
@@ -3956,7 +4051,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
             if (bits & 32) { o[q++] = 0.f; o[q++] = 0.f; o[q++] = 0.f; }
             if (bits & 64) { o[q++] = 0.f; o[q++] = 0.f; o[q++] = 0.f; }
           }
-          wsync();
+          sx_fence();  // only the match list needs ordering (the sensordata stores need none)
           continue;
         }
         // none: contact order; mindist: dist ascending; maxforce: |F| descending
@@ -3983,7 +4078,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           if (bits & 64) { o[q++] = sg * fr[3]; o[q++] = sg * fr[4]; o[q++] = sg * fr[5]; }
         }
         for (int k = nm * (dim / nslot) + tid; k < dim; k += NT) sd[adr + k] = 0.f;  // slots without a match
-        wsync();
+        sx_fence();  // only the match list needs ordering (the sensordata stores need none)
         continue;
       }
 #ifndef MJH_NO_EXT
@@ -4283,6 +4378,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           break;
       }
     };
+    PROF(11);
     // remaining sensors are independent and cheap: one lane each
     for (int s = tid; s < Z.nsensor; s += NT) {
       const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];

@@ -7,7 +7,7 @@ library here ships specialised instances for the benchmark models only
 addresses and sizes are runtime values (far more registers, spills and private
 scratch). This module closes that gap the MI355X way: when a Simulation's launch
 plan matches no built-in specialisation, it renders a one-plan table, compiles
-``csrc/mjh_step.hip`` with ``-DMJH_PLUGIN`` for gfx950 (hipcc, ~1-2 min, once per
+``csrc/mjh_step.hip`` with ``-DMJH_PLUGIN`` for gfx950 (hipcc, ~20 s, once per
 plan: the library is cached under ``mjlab_amd/_jit/`` keyed by the plan, the
 kernel sources and the compile flags) and registers the plugin's launch entry
 with the main library (``mjh_register_spec_plugin``). The main library still
@@ -41,19 +41,34 @@ _SOURCES = ("mjh_step.hip", "mjh_math.h", "mjh_convex.h", "mjh_rng.h")
 _LOADED: dict[str, ctypes.CDLL] = {}  # plugin libraries stay loaded (their entry points are registered)
 
 
-def _key(plan: list[int]) -> str:
+def _source_key() -> str:
+  """The kernel sources, headers and flags a plugin is compiled from."""
   h = hashlib.sha256()
-  h.update(" ".join(map(str, plan)).encode())
   h.update(" ".join(FLAGS).encode())
   for name in _SOURCES:
     h.update((CSRC / name).read_bytes())
   for hdr in sorted(INCLUDE.glob("*.h")):
     h.update(hdr.read_bytes())
-  return h.hexdigest()[:20]
+  return h.hexdigest()[:10]
+
+
+def _key(plan: list[int]) -> str:
+  return hashlib.sha256(" ".join(map(str, plan)).encode()).hexdigest()[:14] + "_" + _source_key()
 
 
 def plugin_path(plan: list[int]) -> Path:
   return JIT_DIR / f"libmjh_spec_{_key(plan)}.so"
+
+
+def prune_stale() -> list[Path]:
+  """Remove cached plugins compiled from other kernel sources (never loadable again)."""
+  cur = _source_key()
+  gone = []
+  for f in JIT_DIR.glob("libmjh_spec_*"):
+    if not f.name.split(".")[0].endswith("_" + cur):
+      f.unlink(missing_ok=True)
+      gone.append(f)
+  return gone
 
 
 def compile_plugin(plan: list[int], name: str = "model", log=print) -> Path:
@@ -74,6 +89,7 @@ def compile_plugin(plan: list[int], name: str = "model", log=print) -> Path:
     raise RuntimeError(f"plugin compile failed: {' '.join(cmd)}\n{r.stderr[-4000:]}")
   os.replace(tmp, out)  # atomic: a concurrent builder of the same plan sees a whole file
   log(f"[mjlab_amd.jit] built {out.name} in {time.time() - t0:.0f} s")
+  prune_stale()
   return out
 
 

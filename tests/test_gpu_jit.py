@@ -10,7 +10,7 @@ runs a model-specialised instance compiled for its own plan, not the generic one
   (printed for profiles/; the plugin must beat the generic instance and stay within
   15 % of the benchmark instance: VERDICT r05 item 5 asks for 10 %).
 The plugin is prebuilt by __graft_entry__.build() (tools/jit_build.py); a tree without
-it compiles it here (hipcc, 1-2 min)."""
+it compiles it here (hipcc, ~20 s)."""
 
 import ctypes
 import sys

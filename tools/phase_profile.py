@@ -64,6 +64,7 @@ def seg(a, b):
   return (p[:, b] - p[:, a]).mean()
 print(f"  kinematics: bodies {seg(0,27):.0f} geoms {seg(27,28):.0f} sites {seg(28,1):.0f}")
 print(f"  com: subtree+cinert {seg(1,18):.0f} cdof {seg(18,19):.0f} crb {seg(19,20):.0f} M-fill {seg(20,10):.0f} factor {seg(10,2):.0f}")
+print(f"  cacc {seg(6,26):.0f}  contact/subtree/ft sensors {seg(26,11):.0f}  lane sensors {seg(11,7):.0f}")
 print(f"  rne: cvel {seg(5,21):.0f} cdof_dot {seg(21,22):.0f} rne {seg(22,23):.0f} cfrc-sum+bias {seg(23,24):.0f} "
       f"passive/act/smooth {seg(24,25):.0f} qacc_smooth solve {seg(25,3):.0f}")
 niter = sim.data.solver_niter.cpu().numpy()
