@@ -213,6 +213,18 @@ __device__ __forceinline__ void wsync() { asm volatile("s_waitcnt vmcnt(0) lgkmc
 // issue order, so this orders its LDS traffic without waiting for its
 // outstanding global stores as wsync does (vmcnt counts stores on gfx9)
 __device__ __forceinline__ void lsync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Bounds-check builds (-DMJH_BOUNDS=1, tools/bounds_check.py): an index outside its
+// array's capacity skips the access and sets MJH_FLAG_BOUNDS in the world's flags
+// (an LDS atomic on the world's counters, no trap); other builds compile to true.
+#ifndef MJH_BOUNDS
+#define MJH_BOUNDS 0
+#endif
+#if MJH_BOUNDS
+#define MJH_BOK(idx, cap) \
+  (((unsigned)(idx) < (unsigned)(cap)) ? true : (atomicOr(&ints[I_FLAGS], MJH_FLAG_BOUNDS), false))
+#else
+#define MJH_BOK(idx, cap) true
+#endif
 
 // Word offsets of every model array inside the LDS model image, and of the
 // per-world copies of expanded (domain-randomised) fields (-1: shared).
@@ -2668,6 +2680,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
 #undef SPRI
 #undef SPR
   const int acap = (BIG || Rg::arow) ? Lo.rcap : Lo.lcap;  // arow's entries
+  const int tcap = (BIG || Rg::efc_type) ? Lo.rcap : Lo.lcap;  // the row arrays' entries (efc_type's region)
   if (MODE == 1 || (MODE == 0 && !reused)) {  // position stage, part 2
 
   // ---------------------------------------------------------------- make_constraint
@@ -2682,7 +2695,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       const int off = bscan<NT>(f, &total, redi);
       if (f) {
         const int r = nefc + off;
-        if (r < rcap) {
+        if (r < rcap && MJH_BOK(r, tcap)) {
           efc_type[r] = MJH_CNSTR_FRICTION_DOF;
           efc_id[r] = i;
           efc_fl[r] = dof_frictionloss[i];
@@ -2706,7 +2719,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       const int off = bscan<NT>(f, &total, redi);
       if (f) {
         const int r = nefc + off;
-        if (r < rcap) {
+        if (r < rcap && MJH_BOK(r, tcap)) {
           const int dof = IMG_I(jnt_dofadr)[j];
           efc_type[r] = MJH_CNSTR_LIMIT_JOINT;
           efc_id[r] = j;
@@ -2877,6 +2890,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           (unsigned long long)IMG_L(body_dofmask)[b1] ^ (unsigned long long)IMG_L(body_dofmask)[b2];
       for (int e = 0; e < nr; e++) {
         const int r = r0 + e;
+        if (!MJH_BOK(r, tcap)) break;
         efc_type[r] = dim == 1 ? MJH_CNSTR_CONTACT_FRICTIONLESS
                                : (ell ? MJH_CNSTR_CONTACT_ELLIPTIC : MJH_CNSTR_CONTACT_PYRAMIDAL);
         efc_id[r] = ci;
@@ -3293,8 +3307,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         int total;
         const int off = bscan<NT>(a, &total, redi);
         if (a) {
-          arow[nact + off] = r;
-          ash[nact + off] = sqrtf(h);
+          if (MJH_BOK(nact + off, acap + 4)) {
+            arow[nact + off] = r;
+            ash[nact + off] = sqrtf(h);
+          }
         }
         nact += total;
       }
@@ -3350,11 +3366,13 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
 #pragma unroll
                 for (int j = 0; j < 6; j++)
                   if (j < dim) val += cf[j] * J[(r0 + j) * ldj + tid];
-                J[vr * ldj + tid] = val;
+                if (MJH_BOK(vr, m.cone == 1 ? 2 * Lo.rcap : Lo.rcap)) J[vr * ldj + tid] = val;
               }
               if (tid == 0) {
-                arow[nact] = vr;
-                ash[nact] = 1.f;
+                if (MJH_BOK(nact, acap + 4)) {
+                  arow[nact] = vr;
+                  ash[nact] = 1.f;
+                }
               }
               nact++;
               ncone++;

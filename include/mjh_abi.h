@@ -47,6 +47,9 @@ extern "C" {
 #define MJH_FLAG_CONTACT_OVERFLOW 1
 #define MJH_FLAG_EFC_OVERFLOW 2
 #define MJH_FLAG_NONFINITE 4
+/* bounds-check builds only (-DMJH_BOUNDS=1): an array index out of its capacity
+   was skipped (never set by release builds) */
+#define MJH_FLAG_BOUNDS 8
 
 /* integrator codes (mjtIntegrator) */
 #define MJH_INT_EULER 0

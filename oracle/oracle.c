@@ -178,6 +178,7 @@ static int g_dbg_lscost_it;
 static real* g_dbg_conv;
 static real* g_dbg_warm;
 static int g_ls_scan = 0;
+static int g_stop_mode = 0;  /* 0: MuJoCo's Newton/CG stop test; 1: improvement test only */
 static _Thread_local real g_dbg_scan_cost[64];
 
 typedef struct {
@@ -1919,7 +1920,10 @@ static void solve(const or_model* m, ws_t* w, const real* warm) {
     real gn = 0;
     for (int d = 0; d < nv; d++) gn += w->grad[d] * w->grad[d];
     real improvement = scale * (old - cost), gradient = scale * sqrt(gn);
-    int conv = improvement < m->tolerance || gradient < m->tolerance;
+    /* g_stop_mode 1 (diagnostics, tools/iteration_analysis.py): the improvement
+       test alone -- what a float32 solver is left with when its gradient's
+       rounding floor lies above the tolerance */
+    int conv = improvement < m->tolerance || (g_stop_mode == 0 && gradient < m->tolerance);
     if (g_dbg_conv && it < 15) {
       real* cv = g_dbg_conv + ((size_t)w->wi * 15 + it) * 4;
       real gm = 0;
@@ -2678,6 +2682,8 @@ int oracle_run(const or_model* m, or_data* d, int w0, int w1, int integrate, int
 void oracle_set_follow(int on) { g_follow = on; }
 
 void oracle_set_ls_scan(int on) { g_ls_scan = on; }
+
+void oracle_set_stop_mode(int mode) { g_stop_mode = mode; }
 
 void oracle_set_lscost(real* cost, int iteration) {
   g_dbg_lscost = cost;

@@ -79,6 +79,9 @@ void oracle_set_follow(int on);
  * (nworld, 64), or with iteration = -1 at every iteration < 15, (nworld, 15, 64)
  * (NULL: off). */
 void oracle_set_ls_scan(int on);
+/* diagnostics: 0 MuJoCo's Newton/CG stop test (improvement or gradient below
+   tolerance), 1 the improvement test only (tools/iteration_analysis.py) */
+void oracle_set_stop_mode(int mode);
 void oracle_set_lscost(real* cost, int iteration);
 size_t oracle_sizeof_model(void);
 size_t oracle_sizeof_data(void);
