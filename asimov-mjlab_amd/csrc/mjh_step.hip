@@ -5004,8 +5004,8 @@ unsigned long long launch_key(const mjh_model* m, const mjh_data* d) {
 // mjh_spec_table.h, and registers the library's mjh_plugin_step here). A plugin
 // is taken on the same conditions as a built-in specialisation: exact plan
 // match, slab data layout, pyramidal cones, Newton or CG.
-typedef int (*PluginFn)(int step, const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream, int reuse,
-                        unsigned long long key);
+typedef int (*PluginFn)(int step, const int* plan, const mjh_model* m, const mjh_data* d, const unsigned char* gate,
+                        void* stream, int reuse, unsigned long long key);
 struct PluginEntry {
   int plan[kPlanInts];
   PluginFn fn;
@@ -5089,7 +5089,8 @@ int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, voi
   if (k >= 0) {
     launch_spec<STEP, 0>(k, p, m, d, gate, s);
   } else if (kp >= 0) {
-    const int r = g_plugins[kp].fn(STEP ? 1 : 0, m, d, gate, stream, g_pos_reuse ? 1 : 0, launch_key(m, d));
+    const int r = g_plugins[kp].fn(STEP ? 1 : 0, g_plugins[kp].plan, m, d, gate, stream, g_pos_reuse ? 1 : 0,
+                                   launch_key(m, d));
     if (r != 0) {
       g_err = "specialised plugin launch failed (code " + std::to_string(r) + ")";
       return 2;
@@ -5123,11 +5124,18 @@ int mjh_plugin_plan(int* out, int cap) {
   return kPlanInts;
 }
 
-int mjh_plugin_step(int step, const mjh_model* m, const mjh_data* d, const unsigned char* gate, void* stream, int reuse,
-                    unsigned long long key) {
+int mjh_plugin_step(int step, const int* plan, const mjh_model* m, const mjh_data* d, const unsigned char* gate,
+                    void* stream, int reuse, unsigned long long key) {
   if constexpr (MJH_NSPEC == 1) {
-    const Plan p = make_plan(m);
-    if (find_spec(p, m) != 0 || !data_is_slab(m, d)) return 3;  // not this plugin's plan
+    // the plan the caller matched (its own build state, e.g. a test's LDS row
+    // cap, entered it) must be this plugin's; the launch geometry follows from it
+    if (!plan || std::memcmp(plan, kSpecPlan[0], sizeof(int) * kPlanInts) != 0 || !data_is_slab(m, d)) return 3;
+    Plan p;
+    std::memcpy(&p.lo, plan + 1 + kSizeInts, sizeof(Layout));
+    std::memcpy(&p.io, plan + 1 + kSizeInts + kLayoutInts, sizeof(ImgOff));
+    constexpr int WPB = wpb_of_nvp(kSpecNvp[0]);
+    p.shmem = (size_t)((img_global(WPB) ? 0 : p.io.img_words) + WPB * p.lo.total) * 4;
+    p.shmem_pos = (size_t)((img_global(kPosWorldsPerBlock) ? 0 : p.io.img_words) + kPosWorldsPerBlock * p.lo.ptotal) * 4;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     constexpr int NVP = kSpecNvp[0];
     if (step)

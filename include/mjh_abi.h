@@ -179,9 +179,11 @@ int mjh_spec_index(const mjh_model* m);
  * table, mjlab_amd/sim/jit.py) export:
  *   int mjh_plugin_abi(void);                    MJH_ABI_VERSION it was built at
  *   int mjh_plugin_plan(int* out, int cap);      the plan it was built for
- *   int mjh_plugin_step(int step, const mjh_model*, const mjh_data*,
- *                       const unsigned char* gate, void* stream, int reuse,
- *                       unsigned long long key); 0 on success */
+ *   int mjh_plugin_step(int step, const int* plan, const mjh_model*,
+ *                       const mjh_data*, const unsigned char* gate,
+ *                       void* stream, int reuse, unsigned long long key);
+ *       0 on success, 3 if plan is not the plugin's (this library passes the
+ *       plan it matched, so the plugin never recomputes it) */
 int mjh_register_spec_plugin(void* fn, const int* plan, int nplan);
 
 /* Index of the registered plugin the launches of model m use (-1: none; a
