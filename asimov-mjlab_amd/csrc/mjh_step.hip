@@ -84,6 +84,16 @@ constexpr int kSolverPGS = 0, kSolverCG = 1;  // mjtSolver: mjSOL_PGS 0, mjSOL_C
 #ifndef MJH_PRESET
 #define MJH_PRESET 5
 #endif
+// the Newton direction after a Hessian rebuild: factor with the forward
+// substitution fused into its sweep (1) or factor, then solve (0)
+#ifndef MJH_FUSED_FWD
+#define MJH_FUSED_FWD 0
+#endif
+// collision pairs read from per-pair records the pack launch writes (1) or
+// through the pair and geom arrays (0): see make_imgoff
+#ifndef MJH_PAIR_REC
+#define MJH_PAIR_REC 1
+#endif
 // sensor-phase variants (contact sensors: metadata preload, match test from
 // registers, LDS-only fences): A/B switches, see the sensor phase. Measured
 // (profiles/r06f_sensor_ab.log, G1 4096 kernel_bench, two passes): preload packed
@@ -236,6 +246,7 @@ struct ImgOff {
 #define X_IOW(type, name, count) int w_##name;
   MJH_MODEL_WARRAYS(X_IOW)
 #undef X_IOW
+  int pair_rec;  // the collision pairs' records (pack_kernel; MJH_PAIR_REC)
   int img_words;
   int nfields;
 };
@@ -769,6 +780,69 @@ __device__ MJH_SOLVER_INLINE void ldl_factor_reg(float* A, int n, int ld) {
   wsync();
   load_row_lower<NVP, PK>(A, n, ld, a);
   ldl_factor_rows<NVP, PK>(a, A, n, ld);
+}
+
+// The factor of the rows in A (as ldl_factor_reg) with the forward substitution
+// of b (x, in LDS) carried through the same column sweep, then the backward
+// substitution: x = (L D L^T)^-1 b in place. The same operations in the same
+// order as ldl_factor_reg + ldl_solve_reg (bit-identical): the forward update
+// of column k uses the multipliers the factor computes at step k, and y_k is
+// final once the sweep reaches column k. Saves the solve's reload of the rows
+// and its separate forward sweep (MJH_FUSED_FWD).
+template <int NVP, bool PK>
+__device__ MJH_SOLVER_INLINE void ldl_factor_solve_reg(float* A, int n, int ld, float* x) {
+  const int lane = threadIdx.x & 63;
+  float a[NVP];
+  wsync();
+  load_row_lower<NVP, PK>(A, n, ld, a);
+  float xi = lane < n ? x[lane] : 0.f, di = 1.f;
+  typedef float v2f __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int k = 0; k < NVP; k++) {
+    const float ak = a[k];
+    float piv = rdlane_f(ak, k);
+    piv = piv < MJH_MINVAL ? MJH_MINVAL : piv;
+    const float lik = ak * __builtin_amdgcn_rcpf(piv);
+    const float xk = rdlane_f(xi, k);
+    xi -= (lane > k ? lik : 0.f) * xk;
+    di = lane == k ? piv : di;
+#if MJH_PK_FACTOR
+    const v2f l2 = {lik, lik};
+#pragma unroll
+    for (int j = (k + 1) & ~1; j < NVP; j += 2) {
+      const v2f r = {rdlane_f(ak, j), rdlane_f(ak, j + 1)};
+      v2f y = {a[j], a[j + 1]};
+      y -= l2 * r;
+      a[j] = y.x;
+      a[j + 1] = y.y;
+    }
+#else
+#pragma unroll
+    for (int j = k + 1; j < NVP; j++) a[j] -= lik * rdlane_f(ak, j);
+#endif
+    a[k] = lane > k ? lik : (lane == k ? piv : a[k]);
+  }
+  if (lane < n) {
+    float* r = A + lofs<PK>(lane, ld);
+    const int len = lspan<PK>(lane, ld);
+#pragma unroll
+    for (int k = 0; k < NVP; k += 4)
+      if (k < len) *reinterpret_cast<float4*>(r + k) = make_float4(a[k], a[k + 1], a[k + 2], a[k + 3]);
+  }
+  wsync();
+  int cl = lane < n ? lane : 0;
+  asm volatile("" : "+v"(cl));  // the column loads wait until the rows are dead
+  float c[NVP];
+#pragma unroll
+  for (int k = 0; k < NVP; k++) c[k] = A[lofs<PK>(k < n ? k : 0, ld) + cl];
+  xi = lane < n ? xi / di : 0.f;
+#pragma unroll
+  for (int k = NVP - 1; k > 0; k--) {
+    const float xk = rdlane_f(xi, k);
+    xi -= (lane < k && k < n ? c[k] : 0.f) * xk;
+  }
+  if (lane < n) x[lane] = xi;
+  wsync();
 }
 
 // (L D L^T) x = b with the factor from ldl_factor_reg; x in LDS (in place).
@@ -2533,22 +2607,32 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       Con cc[4];
       int n = 0, g1 = 0, g2 = 0;
       if (p < npair) {
+#if MJH_PAIR_REC
+        const int4* rec = reinterpret_cast<const int4*>(IMGB + Io.pair_rec) + 2 * p;
+        const int4 ra = rec[0], rb = rec[1];
+        g1 = ra.x;
+        g2 = ra.y;
+        const int s1 = ra.z, s2 = ra.w, t1 = rb.x, t2 = rb.y;
+        const float margin = __int_as_float(rb.z), reach = __int_as_float(rb.w);
+#else
         g1 = IMG_I(pair_geom1)[p];
         g2 = IMG_I(pair_geom2)[p];
         const int s1 = IMG_I(geom_colslot)[g1], s2 = IMG_I(geom_colslot)[g2];
+        const float margin = fmaxf(IMG_F(geom_margin)[g1], IMG_F(geom_margin)[g2]);
+        const int t1 = IMG_I(geom_type)[g1], t2 = IMG_I(geom_type)[g2];
+        const float reach = t1 == 0 ? margin + IMG_F(geom_rbound)[g2] : margin + IMG_F(geom_rbound)[g1] + IMG_F(geom_rbound)[g2];
+#endif
         const float* p1 = cgpos + 3 * s1;
         const float* p2 = cgpos + 3 * s2;
         const float* m1 = cgmat + 9 * s1;
         const float* m2 = cgmat + 9 * s2;
-        const float margin = fmaxf(IMG_F(geom_margin)[g1], IMG_F(geom_margin)[g2]);
-        const int t1 = IMG_I(geom_type)[g1], t2 = IMG_I(geom_type)[g2];
         float dif[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
         bool near;
         if (t1 == 0) {
           float nrm[3] = {m1[2], m1[5], m1[8]};
-          near = dot3(dif, nrm) <= margin + IMG_F(geom_rbound)[g2];
+          near = dot3(dif, nrm) <= reach;
         } else {
-          near = sqrtf(dot3(dif, dif)) <= margin + IMG_F(geom_rbound)[g1] + IMG_F(geom_rbound)[g2];
+          near = sqrtf(dot3(dif, dif)) <= reach;
         }
         if (near)
           n = narrowphase(t1, t2, p1, m1, IMG_F(geom_size) + 3 * g1, p2, m2, IMG_F(geom_size) + 3 * g2, margin, cc,
@@ -3405,7 +3489,12 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
 #endif
         PROF_ACC(15, th);
         unsigned long long tf = PROF_NOW();
+#if MJH_FUSED_FWD
+        for (int i = tid; i < nv; i += NT) search[i] = grad[i];
+        ldl_factor_solve_reg<NVP, PKL>(Lm, nv, ldm, search);
+#else
         ldl_factor_reg<NVP, PKL>(Lm, nv, ldm);
+#endif
         PROF_ACC(16, tf);
 #pragma unroll
         for (int q = 0; q < kMaskWords; q++) act_prev[q] = act[q];
@@ -3414,9 +3503,11 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         nfactor++;
         nfactor_total++;
       }
-      for (int i = tid; i < nv; i += NT) search[i] = grad[i];
       unsigned long long ts = PROF_NOW();
-      ldl_solve_reg<NVP, PKL>(Lm, nv, ldm, search);
+      if (!MJH_FUSED_FWD || diff == 0.f) {  // a kept factor: the plain solve
+        for (int i = tid; i < nv; i += NT) search[i] = grad[i];
+        ldl_solve_reg<NVP, PKL>(Lm, nv, ldm, search);
+      }
       PROF_ACC(17, ts);
       for (int i = tid; i < nv; i += NT) search[i] = -search[i];
       wsync();
@@ -3849,14 +3940,15 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     }
     auto sq = [&](int v, const int* p, int s) -> int { return s < NT ? __builtin_amdgcn_readlane(v, s) : p[s]; };
 #elif MJH_SENS_PRELOAD == 2
-    // [type | objtype << 8 | reftype << 12 | bits << 16 | reduce << 24], adr,
-    // [objid | (refid + 1) << 16], [nslot | dim << 16] (field ranges checked by the compiler)
+    // [type | objtype << 8 | reftype << 14 | bits << 20 | reduce << 27], adr,
+    // [(objid + 1) | (refid + 1) << 16], [nslot | dim << 16] (field ranges checked by
+    // the compiler, spec/compiler.py)
     int q_a = -1, q_b = 0, q_c = 0, q_d = 0;
     if (tid < Z.nsensor) {
-      q_a = IMG_I(sensor_type)[tid] | IMG_I(sensor_objtype)[tid] << 8 | IMG_I(sensor_reftype)[tid] << 12 |
-            IMG_I(sensor_intprm)[3 * tid] << 16 | IMG_I(sensor_intprm)[3 * tid + 1] << 24;
+      q_a = IMG_I(sensor_type)[tid] | IMG_I(sensor_objtype)[tid] << 8 | IMG_I(sensor_reftype)[tid] << 14 |
+            IMG_I(sensor_intprm)[3 * tid] << 20 | IMG_I(sensor_intprm)[3 * tid + 1] << 27;
       q_b = IMG_I(sensor_adr)[tid];
-      q_c = IMG_I(sensor_objid)[tid] | (IMG_I(sensor_refid)[tid] + 1) << 16;
+      q_c = (IMG_I(sensor_objid)[tid] + 1) | (IMG_I(sensor_refid)[tid] + 1) << 16;
       q_d = IMG_I(sensor_intprm)[3 * tid + 2] | IMG_I(sensor_dim)[tid] << 16;
     }
 #endif
@@ -3888,7 +3980,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       const bool qr = s < NT;
       const int qa = qr ? __builtin_amdgcn_readlane(q_a, s) : 0, qc = qr ? __builtin_amdgcn_readlane(q_c, s) : 0;
       const int type = qr ? (qa & 255) : IMG_I(sensor_type)[s];
-      const int id = qr ? (qc & 0xffff) : IMG_I(sensor_objid)[s];
+      const int id = qr ? (qc & 0xffff) - 1 : IMG_I(sensor_objid)[s];
       const int adr = qr ? __builtin_amdgcn_readlane(q_b, s) : IMG_I(sensor_adr)[s];
 #else
       const int type = IMG_I(sensor_type)[s], id = IMG_I(sensor_objid)[s], adr = IMG_I(sensor_adr)[s];
@@ -3907,10 +3999,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         const int dim = sq(q_dim, IMG_I(sensor_dim), s);
 #elif MJH_SENS_PRELOAD == 2
         const int qd = qr ? __builtin_amdgcn_readlane(q_d, s) : 0;
-        const int bits = qr ? (qa >> 16) & 255 : ip[3 * s];
-        const int reduce = qr ? (qa >> 24) & 255 : ip[3 * s + 1];
+        const int bits = qr ? (qa >> 20) & 127 : ip[3 * s];
+        const int reduce = qr ? (qa >> 27) & 7 : ip[3 * s + 1];
         const int nslot = qr ? (qd & 0xffff) : ip[3 * s + 2];
-        const int otype = qr ? (qa >> 8) & 15 : IMG_I(sensor_objtype)[s], rtype = qr ? (qa >> 12) & 15 : IMG_I(sensor_reftype)[s];
+        const int otype = qr ? (qa >> 8) & 63 : IMG_I(sensor_objtype)[s], rtype = qr ? (qa >> 14) & 63 : IMG_I(sensor_reftype)[s];
         const int rid = qr ? (qc >> 16) - 1 : IMG_I(sensor_refid)[s];
         const int dim = qr ? (qd >> 16) : IMG_I(sensor_dim)[s];
 #else
@@ -4745,7 +4837,23 @@ __device__ void order_worlds_block(const int* __restrict__ niter, const int* __r
 
 __global__ __launch_bounds__(1024) void pack_kernel(const mjh_model m, const ImgOff io, const int* niter, const int* nefc_w,
                                                    long long* order, long long nworld) {
-  if ((int)blockIdx.x == io.nfields) {  // the extra workgroup: world order
+  if ((int)blockIdx.x == io.nfields) {  // extra workgroup 1: the collision pairs' records
+    if (MJH_PAIR_REC) {
+      int* rec = reinterpret_cast<int*>(m.image) + io.pair_rec;
+      for (int p = threadIdx.x; p < m.npair; p += blockDim.x) {
+        const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+        const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+        const float mg = fmaxf(m.geom_margin[g1], m.geom_margin[g2]);
+        // the same float operations, in the same order, as the test it replaces
+        const float reach = t1 == 0 ? mg + m.geom_rbound[g2] : mg + m.geom_rbound[g1] + m.geom_rbound[g2];
+        int* r = rec + 8 * p;
+        r[0] = g1; r[1] = g2; r[2] = m.geom_colslot[g1]; r[3] = m.geom_colslot[g2];
+        r[4] = t1; r[5] = t2; r[6] = __float_as_int(mg); r[7] = __float_as_int(reach);
+      }
+    }
+    return;
+  }
+  if ((int)blockIdx.x == io.nfields + 1) {  // extra workgroup 2: world order
     order_worlds_block(niter, nefc_w, order, nworld);
     return;
   }
@@ -4802,6 +4910,12 @@ ImgOff make_imgoff(const mjh_model* m) {
   MJH_MODEL_ARRAYS(X_OFF)
   MJH_MODEL_WARRAYS(X_OFF)
 #undef X_OFF
+  // per collision pair, 8 words written by the pack launch from the geom arrays:
+  // [geom1, geom2, colslot1, colslot2 | type1, type2, margin, reach] (reach: the
+  // bounding-sphere test's right-hand side), two 16-byte loads per lane in the
+  // collision pass instead of three dependent rounds of loads
+  io.pair_rec = (off + 3) & ~3;
+  off = io.pair_rec + (MJH_PAIR_REC ? 8 * m->npair : 0);
   io.img_words = (off + 3) & ~3;
   io.nfields = nf;
 #define X_W(type, name, count) io.w_##name = -1;
@@ -5080,7 +5194,7 @@ int launch(const mjh_model* m, const mjh_data* d, const unsigned char* gate, voi
   const bool order = g_auto_order && d->world_order != nullptr && d->nworld > 1;
   // 1024 threads: the order workgroup's counting sort is the launch's long pole
   if (!g_keep_image)
-    hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields + (order ? 1 : 0)), dim3(1024), 0, s, *m, p.io, d->solver_niter,
+    hipLaunchKernelGGL(pack_kernel, dim3(p.io.nfields + 1 + (order ? 1 : 0)), dim3(1024), 0, s, *m, p.io, d->solver_niter,
                        d->nefc, const_cast<long long*>(d->world_order), (long long)d->nworld);
   // specialised instances assume the slab data layout (data_is_slab)
   const bool slab = !g_disable_spec && data_is_slab(m, d);

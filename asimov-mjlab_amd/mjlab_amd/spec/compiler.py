@@ -675,9 +675,10 @@ def _compile_sensors(m: Model, spec: Spec) -> None:
   # the step kernel keeps each sensor's metadata packed in four lane registers
   # (mjh_step.hip MJH_SENS_PRELOAD 2): the fields must fit their bit ranges
   for i in range(ns):
-    ok = (0 <= int(m.sensor_objtype[i]) < 16 and 0 <= int(m.sensor_reftype[i]) < 16 and 0 <= int(m.sensor_objid[i]) < 65536
+    ip = np.asarray(m.sensor_intprm).reshape(-1, 3)[i]
+    ok = (0 <= int(m.sensor_objtype[i]) < 64 and 0 <= int(m.sensor_reftype[i]) < 64 and -1 <= int(m.sensor_objid[i]) < 65535
           and -1 <= int(m.sensor_refid[i]) < 65535 and 0 <= int(m.sensor_dim[i]) < 65536 and 0 <= int(m.sensor_type[i]) < 256
-          and all(0 <= int(v) < (65536 if k == 2 else 256) for k, v in enumerate(np.asarray(m.sensor_intprm).reshape(-1, 3)[i])))
+          and 0 <= int(ip[0]) < 128 and 0 <= int(ip[1]) < 8 and 0 <= int(ip[2]) < 65536)
     if not ok:
       raise NotImplementedError(f"sensor {i}: metadata outside the device's packed ranges")
   # sensors outside the benchmark tasks' set (a size, so it is part of the
