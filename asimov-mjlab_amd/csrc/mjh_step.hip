@@ -774,6 +774,28 @@ __device__ __forceinline__ void ldl_factor_rows(float (&a)[NVP], float* A, int n
   wsync();
 }
 
+// M's rows (full rows of stride ldm >= NVP, 16-byte aligned, in global scratch) into
+// A's rows: lane i issues all of row i's 16-byte loads before its stores. The
+// element-strided copy this replaces (i += NT over n ldm entries) waited one global
+// round trip per iteration: 21 in a row for G1's implicitfast integration.
+template <int NVP, bool PK>
+__device__ __forceinline__ void mass_rows_to(const float* M, float* A, int n, int ld) {
+  const int lane = threadIdx.x & 63;
+  wsync();
+  if (lane < n) {
+    float4 v[NVP / 4];
+    const float* s = M + lane * ld;
+#pragma unroll
+    for (int k = 0; k < NVP; k += 4) v[k >> 2] = *reinterpret_cast<const float4*>(s + k);
+    float* r = A + lofs<PK>(lane, ld);
+    const int len = lspan<PK>(lane, ld);
+#pragma unroll
+    for (int k = 0; k < NVP; k += 4)
+      if (k < len) *reinterpret_cast<float4*>(r + k) = v[k >> 2];
+  }
+  wsync();
+}
+
 template <int NVP, bool PK>
 __device__ MJH_SOLVER_INLINE void ldl_factor_reg(float* A, int n, int ld) {
   float a[NVP];
@@ -2890,6 +2912,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       for (int base = 0; base < ncon; base += NT) {
         const int cl = base + tid;
         int r0 = -1, b1 = 0, b2 = 0, dim = 1;
+        unsigned long long m1 = 0ull, m2 = 0ull;  // the bodies' dof masks (no image load in the row loop below)
         float cp[3] = {0.f, 0.f, 0.f}, fr[9], fk[5], c1[3] = {0.f, 0.f, 0.f}, c2[3] = {0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < 9; k++) fr[k] = 0.f;
@@ -2900,6 +2923,8 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
           b1 = IMG_I(geom_bodyid)[con_geom[2 * cl]];
           b2 = IMG_I(geom_bodyid)[con_geom[2 * cl + 1]];
           dim = con_dim[cl];
+          m1 = IMG_L(body_dofmask)[b1];
+          m2 = IMG_L(body_dofmask)[b2];
 #pragma unroll
           for (int k = 0; k < 3; k++) cp[k] = con_pos[3 * cl + k];
 #pragma unroll
@@ -2915,11 +2940,11 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         for (int k = 0; k < cnt; k++) {
           const int r0k = __builtin_amdgcn_readlane(r0, k);
           if (r0k < 0) continue;
-          const int b1k = __builtin_amdgcn_readlane(b1, k), b2k = __builtin_amdgcn_readlane(b2, k);
+          const unsigned long long m1k = rl64(m1, k), m2k = rl64(m2, k);
           const int dimk = __builtin_amdgcn_readlane(dim, k);
           const int nr = dimk == 1 ? 1 : 2 * (dimk - 1);  // pyramidal (elliptic: dimk rows)
-          const bool in1 = tid < nv && (((unsigned long long)IMG_L(body_dofmask)[b1k] >> tid) & 1ull);
-          const bool in2 = tid < nv && (((unsigned long long)IMG_L(body_dofmask)[b2k] >> tid) & 1ull);
+          const bool in1 = tid < nv && ((m1k >> tid) & 1ull);
+          const bool in2 = tid < nv && ((m2k >> tid) & 1ull);
           // not in either chain, or in both (relative motion cancels): zero column
           const bool use = in1 != in2;
           const float sg = in2 ? 1.f : -1.f;
@@ -2962,7 +2987,10 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         }
       }
     }
-    // contact row parameters
+    // contact rows' type, mask and parameters: lane = contact, every input loaded
+    // before the first row store (a load behind a store waits for it). The rows of
+    // a frictionless or pyramidal contact share one set of parameters (MuJoCo
+    // Warp's per-row evaluation computes the same values from the same inputs).
     for (int ci = tid; ci < ncon; ci += NT) {
       const int r0 = con_efcadr[ci];
       if (r0 < 0) continue;
@@ -2972,46 +3000,46 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       const int nr = dim == 1 ? 1 : (ell ? dim : 2 * (dim - 1));
       const unsigned long long msk =
           (unsigned long long)IMG_L(body_dofmask)[b1] ^ (unsigned long long)IMG_L(body_dofmask)[b2];
+      const float dist = con_dist[ci], imarg = con_imargin[ci], f0 = con_fric[5 * ci];
+      const float pos = dist - imarg;
+      const float invw0 = IMG_F(body_invweight0)[2 * b1] + IMG_F(body_invweight0)[2 * b2];
+      float pD = 0.f, pR = 0.f, paref = 0.f, pb = 0.f;
+      if (!ell) {
+        float invw = invw0;
+        if (dim > 1) {
+          invw = invw + f0 * f0 * invw;
+          invw = invw * 2.f * f0 * f0 / m.impratio;
+        }
+        row_params_pos(m.timestep, pos, pos, invw, con_solref + 2 * ci, con_solimp + 5 * ci, &pD, &pR, &paref, &pb);
+      }
       for (int e = 0; e < nr; e++) {
         const int r = r0 + e;
         if (!MJH_BOK(r, tcap)) break;
         efc_type[r] = dim == 1 ? MJH_CNSTR_CONTACT_FRICTIONLESS
                                : (ell ? MJH_CNSTR_CONTACT_ELLIPTIC : MJH_CNSTR_CONTACT_PYRAMIDAL);
         efc_id[r] = ci;
-        // elliptic: the cone's row scales (mu = friction0 / sqrt(impratio), then friction_{e-1})
-        efc_fl[r] = !ell ? 0.f : (e == 0 ? con_fric[5 * ci] / sqrtf(m.impratio) : con_fric[5 * ci + e - 1]);
         efc_mask[r] = msk;
-        // elliptic friction rows: no position term (efc_pos = margin, as MuJoCo Warp)
-        efc_pos[r] = ell && e > 0 ? con_imargin[ci] : con_dist[ci];
-      }
-    }
-    wsync();
-    for (int r = tid; r < nefc; r += NT) {
-      const int ty = efc_type[r];
-      if (ty != MJH_CNSTR_CONTACT_FRICTIONLESS && ty != MJH_CNSTR_CONTACT_PYRAMIDAL && ty != MJH_CNSTR_CONTACT_ELLIPTIC)
-        continue;
-      const int ci = efc_id[r];
-      const int b1 = IMG_I(geom_bodyid)[con_geom[2 * ci]], b2 = IMG_I(geom_bodyid)[con_geom[2 * ci + 1]];
-      float invw = IMG_F(body_invweight0)[2 * b1] + IMG_F(body_invweight0)[2 * b2];
-      const float pos = con_dist[ci] - con_imargin[ci];
-      float pos_aref = pos;
-      if (ELL && ty == MJH_CNSTR_CONTACT_ELLIPTIC) {
-        // MuJoCo Warp constraint.py _efc_contact_elliptic: friction rows without
-        // a position term, invweight / impratio (times f0^2 / f_{e-1}^2 beyond the first)
-        const int e = r - con_efcadr[ci];
+        if (!ell) {
+          efc_fl[r] = 0.f;
+          efc_pos[r] = dist;
+          efc_D[r] = pD; efc_R[r] = pR; efc_aref[r] = paref; efc_b[r] = pb;
+          continue;
+        }
+        // elliptic: the cone's row scales (mu = friction0 / sqrt(impratio), then
+        // friction_{e-1}); friction rows have no position term (efc_pos = margin,
+        // as MuJoCo Warp), invweight / impratio, times f0^2 / f_{e-1}^2 beyond the
+        // first (constraint.py _efc_contact_elliptic)
+        const float fe = e > 0 ? con_fric[5 * ci + e - 1] : f0;
+        efc_fl[r] = e == 0 ? f0 / sqrtf(m.impratio) : fe;
+        efc_pos[r] = e > 0 ? imarg : dist;
+        float invw = invw0;
         if (e > 0) {
-          const float f0 = con_fric[5 * ci], fe = con_fric[5 * ci + e - 1];
-          pos_aref = 0.f;
           invw = invw / m.impratio;
           if (e > 1) invw *= f0 * f0 / (fe * fe);
         }
-      } else if (con_dim[ci] > 1) {
-        const float f0 = con_fric[5 * ci];
-        invw = invw + f0 * f0 * invw;
-        invw = invw * 2.f * f0 * f0 / m.impratio;
+        row_params_pos(m.timestep, e > 0 ? 0.f : pos, pos, invw, con_solref + 2 * ci, con_solimp + 5 * ci, efc_D + r,
+                       efc_R + r, efc_aref + r, efc_b + r);
       }
-      row_params_pos(m.timestep, pos_aref, pos, invw, con_solref + 2 * ci, con_solimp + 5 * ci, efc_D + r, efc_R + r,
-                     efc_aref + r, efc_b + r);
     }
     if (tid == 0) ints[I_NEFC] = nefc;
     wsync();
@@ -3143,7 +3171,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) kend = max(kend, __shfl_xor(kend, o, 64));
     for (int k = 0; k < kend; k++) {
-      const int jk = IMG_I(dof_jntid)[k];
+      const int jk = __builtin_amdgcn_readlane(jnt, k);  // dof k's joint (lane k < nv loaded it)
       const bool use = k >= d0 && k < i && !(jk == jnt && !(freej && k - da < 3));
       const float q = use ? rl(r_qv, k) : 0.f;  // adds exactly 0 when unused
 #pragma unroll
@@ -4676,11 +4704,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     const float dt = m.timestep;
     float* qa_int = tmp;
     if (m.integrator == MJH_INT_IMPLICITFAST) {
-      for (int i = tid; i < nv * ldm; i += NT) {
-        const int row = i / ldm, col = i - row * ldm;
-        if (col < lspan<PKL>(row, ldm)) Lm[lofs<PKL>(row, ldm) + col] = Mm[i];
-      }
-      wsync();
+      mass_rows_to<NVP, PKL>(Mm, Lm, nv, ldm);
       for (int i = tid; i < nv; i += NT) Lm[lofs<PKL>(i, ldm) + i] += dt * dof_damping[i];
       wsync();
       for (int i = tid; i < nu; i += NT) {
@@ -4700,11 +4724,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       for (int i = tid; i < nv; i += NT) anyd += dof_damping[i] > 0.f ? 1.f : 0.f;
       anyd = bsum<NT>(anyd, red);
       if (anyd > 0.f) {
-        for (int i = tid; i < nv * ldm; i += NT) {
-          const int row = i / ldm, col = i - row * ldm;
-          if (col < lspan<PKL>(row, ldm)) Lm[lofs<PKL>(row, ldm) + col] = Mm[i];
-        }
-        wsync();
+        mass_rows_to<NVP, PKL>(Mm, Lm, nv, ldm);
         for (int i = tid; i < nv; i += NT) Lm[lofs<PKL>(i, ldm) + i] += dt * dof_damping[i];
         symv_u<NT, NVP>(Mm, nv, ldm, qacc, qa_int);
         ldl_factor_reg<NVP, PKL>(Lm, nv, ldm);
