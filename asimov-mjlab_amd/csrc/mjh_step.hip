@@ -556,6 +556,15 @@ __host__ __device__ constexpr bool pack_l(int wpb) { return cu_worlds(wpb); }
 #ifndef MJH_HESS_PF
 #define MJH_HESS_PF(nvp) ((nvp) <= 20 ? 6 : 4)
 #endif
+// rows of J in flight per round of the solver's J^T f (a multiple of 4)
+#ifndef MJH_JTF_B
+#define MJH_JTF_B 16
+#endif
+// the Hessian's accumulators start from M's tiles with one 16-byte load per tile
+// (M's symmetric rows, read transposed) instead of four scattered dword loads
+#ifndef MJH_HESS_MROW
+#define MJH_HESS_MROW 1
+#endif
 // H (lower triangle of Hout, packed rows) = M + sum_k ash[k]^2 J[arow[k]] J[arow[k]]^T over the
 // nact compacted active rows, on the f32 matrix cores (v_mfma_f32_16x16x4_f32:
 // exact fp32 FMA chains). Tiles of 16x16 on the lower block triangle; at most
@@ -576,12 +585,24 @@ __device__ MJH_SOLVER_INLINE void hessian_mfma(const float* M, int ldm, const fl
 #pragma unroll
     for (int I = 0; I < NB; I++)
 #pragma unroll
-      for (int Jb = 0; Jb <= I; Jb++, t++)
+      for (int Jb = 0; Jb <= I; Jb++, t++) {
+#if MJH_HESS_MROW
+        // lane (ci, kq)'s entries (rows I*16+kq*4+q, column j = Jb*16+ci) are, M
+        // being stored as whole symmetric rows, 4 consecutive entries of row j: one
+        // 16-byte load. Entries never stored (right of the diagonal, rows or
+        // columns >= n: padding zeros or row n-1's values) only pass through.
+        const int j = Jb * 16 + ci, i0 = I * 16 + kq * 4;
+        const float4 mv = i0 < n ? *reinterpret_cast<const float4*>(M + (j < n ? j : n - 1) * ldm + i0)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        acc[t][0] = mv.x; acc[t][1] = mv.y; acc[t][2] = mv.z; acc[t][3] = mv.w;
+#else
 #pragma unroll
         for (int q = 0; q < 4; q++) {
           const int i = I * 16 + kq * 4 + q, j = Jb * 16 + ci;
           acc[t][q] = (i < n && j <= i) ? M[i * ldm + j] : 0.f;
         }
+#endif
+      }
   }
   // software pipeline: the next k-step's J values are loaded (J may live in
   // L2) while this step's MFMAs run
@@ -3366,16 +3387,16 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       wsync();
       for (int i = tid; i < nv; i += NT) {
         // J^T f: entries outside a row's dof mask are exact zeros, so no test.
-        // 16 rows of J loads in flight per round; accumulator k takes rows r = k
+        // MJH_JTF_B rows of J loads in flight per round; accumulator k takes rows r = k
         // mod 4 in increasing order (as a plain 4-way unrolled loop)
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
         int r = 0;
-        for (; r + 16 <= nefc; r += 16) {
-          float jj[16];
+        for (; r + MJH_JTF_B <= nefc; r += MJH_JTF_B) {
+          float jj[MJH_JTF_B];
 #pragma unroll
-          for (int q = 0; q < 16; q++) jj[q] = J[(r + q) * ldj + i];
+          for (int q = 0; q < MJH_JTF_B; q++) jj[q] = J[(r + q) * ldj + i];
 #pragma unroll
-          for (int q = 0; q < 16; q += 4) {
+          for (int q = 0; q < MJH_JTF_B; q += 4) {
             s0 += jj[q] * efc_force[r + q];
             s1 += jj[q + 1] * efc_force[r + q + 1];
             s2 += jj[q + 2] * efc_force[r + q + 2];
