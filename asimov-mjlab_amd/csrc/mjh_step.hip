@@ -109,6 +109,19 @@ constexpr int kSolverPGS = 0, kSolverCG = 1;  // mjtSolver: mjSOL_PGS 0, mjSOL_C
 #ifndef MJH_SENS_LSYNC
 #define MJH_SENS_LSYNC 0
 #endif
+// cacc's chain sum over lane-formed per-dof terms (6 readlanes per dof instead of
+// 14). Measured (profiles/r06p_cacc_ab_kb.log): Go1 0.415 -> 0.409 ms per launch, G1 flat
+#ifndef MJH_CACC_W
+#define MJH_CACC_W 1
+#endif
+// every contact sensor's matches computed in one pass before the first sensor
+// output is stored (ballots per sensor in the solver's dead ash array): the match
+// test's dependent image loads run once, not once per contact sensor behind the
+// previous sensors' stores. Measured (profiles/r06o_prematch_ab_kb.log): G1 0.471 ->
+// 0.478 ms per launch (VGPR spills 119 -> 192), Go1 flat: off
+#ifndef MJH_SENS_PREMATCH
+#define MJH_SENS_PREMATCH 0
+#endif
 #define MJH_REGIONS(X)                                                                              \
   X(qpos, 0) X(qvel, 0) X(qacc, 0) X(qacc_smooth, 0) X(qfrc_smooth, 0) X(qfrc_bias, 1) X(qfrc_con, 0)  \
   X(qfrc_passive, 1) X(qfrc_act, 1) X(grad, 0) X(search, 0) X(Ma, 0) X(Mv, 0) X(tmp, 0) X(tmp2, 0)    \
@@ -3946,6 +3959,21 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     }
     const unsigned long long dm = bl ? dmk[tid] : 0ull;
     float a[6] = {0.f, 0.f, 0.f, g0, g1, g2};
+#if MJH_CACC_W
+    // lane j forms its own term cdof_dot_j qvel_j + cdof_j qacc_j; the chain sum
+    // then reads 6 values per dof instead of 14
+    float wv[6];
+#pragma unroll
+    for (int c = 0; c < 6; c++) wv[c] = cdd[c] * qv_l + cd[c] * qa_l;
+    for (int j = 0; j < nv; j++) {
+      const bool in = (dm >> j) & 1ull;
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        const float t = rl(wv[c], j);
+        a[c] += in ? t : 0.f;
+      }
+    }
+#else
     for (int j = 0; j < nv; j++) {
       const bool in = (dm >> j) & 1ull;
       const float qv = in ? rl(qv_l, j) : 0.f, qa = in ? rl(qa_l, j) : 0.f;
@@ -3955,6 +3983,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         a[c] += x * qv + y * qa;
       }
     }
+#endif
     if (bl) {
 #pragma unroll
       for (int c = 0; c < 6; c++) cacc[6 * tid + c] = a[c];
@@ -3999,6 +4028,52 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       q_b = IMG_I(sensor_adr)[tid];
       q_c = (IMG_I(sensor_objid)[tid] + 1) | (IMG_I(sensor_refid)[tid] + 1) << 16;
       q_d = IMG_I(sensor_intprm)[3 * tid + 2] | IMG_I(sensor_dim)[tid] << 16;
+    }
+#endif
+    // geom g (body gb, subtree mask tm) matches object (ty, oid)
+    auto om_match = [](int ty, int oid, int g, int gb, unsigned long long tm) -> bool {
+      if (oid < 0) return true;
+      if (ty == 5) return g == oid;
+      if (ty == 1) return gb == oid;
+      if (ty == 2) return oid == 0 || ((tm >> oid) & 1ull);
+      return false;
+    };
+    // match / flip ballots of contact sensor s at pmb[2 s], pmb[2 s + 1] (contacts in
+    // lanes: ncon <= 64; sensor metadata in lanes: nsensor <= 64)
+    unsigned long long* const pmb = reinterpret_cast<unsigned long long*>(ash);
+    bool pm = MJH_SENS_PREMATCH && MJH_SENS_PRELOAD == 2 && !MJH_SENS_OMREG && creg && Z.nsensor <= NT &&
+              4 * Z.nsensor <= acap + 4;
+#if MJH_SENS_PRELOAD == 2
+    pm = pm && __ballot((q_a & 255) == 40) != 0ull;  // a contact sensor at all (q_a is -1 past nsensor)
+    if (pm) {
+      int g1 = 0, g2 = 0, b1 = 0, b2 = 0;
+      unsigned long long t1 = 0ull, t2 = 0ull;
+      const bool cl = tid < ncon;
+      if (cl) {
+        g1 = con_geom[2 * tid];
+        g2 = con_geom[2 * tid + 1];
+        b1 = IMG_I(geom_bodyid)[g1];
+        b2 = IMG_I(geom_bodyid)[g2];
+        t1 = (unsigned long long)IMG_L(body_treemask)[b1];
+        t2 = (unsigned long long)IMG_L(body_treemask)[b2];
+      }
+      for (int s = 0; s < Z.nsensor; s++) {
+        const int qa = __builtin_amdgcn_readlane(q_a, s);
+        if ((qa & 255) != 40) continue;
+        const int qc = __builtin_amdgcn_readlane(q_c, s);
+        const int otype = (qa >> 8) & 63, rtype = (qa >> 14) & 63, id = (qc & 0xffff) - 1, rid = (qc >> 16) - 1;
+        bool match = false, flip = false;
+        if (cl) {
+          if (om_match(otype, id, g1, b1, t1) && om_match(rtype, rid, g2, b2, t2)) match = true;
+          else if (om_match(otype, id, g2, b2, t2) && om_match(rtype, rid, g1, b1, t1)) { match = true; flip = true; }
+        }
+        const unsigned long long mb = __ballot(match), fb = __ballot(flip);
+        if (tid == 0) {
+          pmb[2 * s] = mb;
+          pmb[2 * s + 1] = fb;
+        }
+      }
+      wsync();
     }
 #endif
     auto contact_force = [&](int ci, float (&F)[6]) {
@@ -4111,6 +4186,16 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         int cnt = 0;
         if (otype == p_ot && id == p_id && rtype == p_rt && rid == p_rid) {
           cnt = p_cnt;  // same matches as the previous contact sensor (sx unchanged)
+        } else if (pm) {
+          // the pre-pass's ballots: the same list, in contact order, as the scan below
+          const unsigned long long mb = pmb[2 * s], fb = pmb[2 * s + 1];
+          cnt = __popcll(mb);
+          if ((mb >> tid) & 1ull) {
+            const int off = __popcll(mb & ((1ull << tid) - 1ull));
+            if (off < cap) sx[off] = ((fb >> tid) & 1ull) ? ~tid : tid;
+          }
+          sx_fence();
+          p_ot = otype; p_id = id; p_rt = rtype; p_rid = rid; p_cnt = cnt;
         } else {
           for (int base = 0; base < ncon; base += NT) {
             const int ci = base + tid;
