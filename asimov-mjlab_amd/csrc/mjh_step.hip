@@ -573,6 +573,23 @@ __host__ __device__ constexpr bool pack_l(int wpb) { return cu_worlds(wpb); }
 #ifndef MJH_JTF_B
 #define MJH_JTF_B 16
 #endif
+// kinematics by pointer jumping over the body tree (A/B switch). Measured
+// (profiles/r06r_jtfpf_cdof_kinjump_ab_kb.log): G1 0.466 -> 0.459, Go1 0.409 -> 0.402 ms per
+// launch, but the 40-step rollout parity test met a line-search choice beyond float32
+// noise in one world (profiles/r06r_gputests_kinjump.log): off until that is explained
+#ifndef MJH_KIN_JUMP
+#define MJH_KIN_JUMP 0
+#endif
+// cdof rows built by dof lanes and kept in registers for the crb pass (A/B switch).
+// Measured (same log): G1 0.466 -> 0.470, Go1 0.409 -> 0.407: off
+#ifndef MJH_CDOF_LANE
+#define MJH_CDOF_LANE 0
+#endif
+// J^T f's first round of loads issued ahead of the constraint-row pass (A/B switch).
+// Measured (same log): flat on G1 and Go1: off
+#ifndef MJH_JTF_PF
+#define MJH_JTF_PF 0
+#endif
 // the Hessian's accumulators start from M's tiles with one 16-byte load per tile
 // (M's symmetric rows, read transposed) instead of four scattered dword loads
 #ifndef MJH_HESS_MROW
@@ -2312,6 +2329,139 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       }
       quat_normalize(q);
     }
+#elif MJH_KIN_JUMP
+  // Pointer jumping over the body tree: log2(depth) rounds instead of one round
+  // per level. Each lane forms its body's transform relative to its parent (the
+  // body offset, then its joints about their anchors: the chain walk's
+  // operations in the parent's frame); round r composes it with the transform of
+  // the ancestor 2^r levels up (ds_bpermute). The same poses as the level sweep
+  // with the composition reassociated (float32 rounding differs).
+  if (bl) {
+    const int b = tid;
+    float p[3] = {0.f, 0.f, 0.f}, q[4] = {1.f, 0.f, 0.f, 0.f};
+    const int cn = b == 0 ? 0 : IMG_I(body_chainnum)[b];
+    const int par = cn > 0 ? IMG_I(body_parentid)[b] : 0;
+    const int ja = cn > 0 ? IMG_I(body_jntadr)[b] : 0, jn = cn > 0 ? IMG_I(body_jntnum)[b] : 0;
+    const int mid = (cn > 0 && Z.nmocap > 0) ? IMG_I(body_mocapid)[b] : -1;
+    const int jt0 = jn > 0 ? IMG_I(jnt_type)[ja] : -1, qa0 = jn > 0 ? IMG_I(jnt_qposadr)[ja] : 0;
+    int anc = -1;  // the body whose frame (p, q) is expressed in (-1: the world)
+    // joint j of the body applied to (p, q); anchor / axis in that frame
+    auto apply_joint = [&](int j, float (&ax)[3], float (&an)[3]) {
+      float jax[3], jp[3], Rq[9];
+#pragma unroll
+      for (int k = 0; k < 3; k++) { jax[k] = IMG_F(jnt_axis)[3 * j + k]; jp[k] = IMG_F(jnt_pos)[3 * j + k]; }
+      const int jt = IMG_I(jnt_type)[j], qa = IMG_I(jnt_qposadr)[j];
+      quat2mat(Rq, q);
+      mat_vec(ax, Rq, jax);
+      mat_vec(an, Rq, jp);
+      an[0] += p[0]; an[1] += p[1]; an[2] += p[2];
+      if (jt == 2) {
+        const float dd = qpos[qa] - qpos0[qa];
+        p[0] += ax[0] * dd; p[1] += ax[1] * dd; p[2] += ax[2] * dd;
+      } else if (jt == 3 || jt == 1) {
+        float ql[4], v[3];
+        if (jt == 3) {
+          axis_angle(ql, jax, qpos[qa] - qpos0[qa]);
+        } else {
+          ql[0] = qpos[qa]; ql[1] = qpos[qa + 1]; ql[2] = qpos[qa + 2]; ql[3] = qpos[qa + 3];
+          quat_normalize(ql);
+        }
+        quat_mul(q, q, ql);
+        quat2mat(Rq, q);
+        mat_vec(v, Rq, jp);
+        p[0] = an[0] - v[0]; p[1] = an[1] - v[1]; p[2] = an[2] - v[2];
+      }
+    };
+    if (cn > 0) {
+      if (mid >= 0) {  // mocap body (a child of the world): pose from mocap_pos / mocap_quat
+        const float* mp = DP(mocap_pos) + (W * Z.nmocap + mid) * 3;
+        const float* mq = DP(mocap_quat) + (W * Z.nmocap + mid) * 4;
+        p[0] = mp[0]; p[1] = mp[1]; p[2] = mp[2];
+        q[0] = mq[0]; q[1] = mq[1]; q[2] = mq[2]; q[3] = mq[3];
+        quat_normalize(q);
+      } else if (jn == 1 && jt0 == 0) {  // free joint: the pose is the joint's coordinates
+        p[0] = qpos[qa0]; p[1] = qpos[qa0 + 1]; p[2] = qpos[qa0 + 2];
+        q[0] = qpos[qa0 + 3]; q[1] = qpos[qa0 + 4]; q[2] = qpos[qa0 + 5]; q[3] = qpos[qa0 + 6];
+        quat_normalize(q);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++) p[k] = body_pos[3 * b + k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) q[k] = body_quat[4 * b + k];
+        for (int j = ja; j < ja + jn; j++) {
+          float ax[3], an[3];
+          apply_joint(j, ax, an);
+        }
+        anc = par == 0 ? -1 : par;
+      }
+    }
+    for (int r = 0; r < 6 && __any(anc >= 0); r++) {  // 2^6 levels >= any tree of <= 64 bodies
+      const int src = anc >= 0 ? anc : b;
+      float ap[3], aq[4];
+#pragma unroll
+      for (int k = 0; k < 3; k++) ap[k] = shfl(p[k], src);
+#pragma unroll
+      for (int k = 0; k < 4; k++) aq[k] = shfl(q[k], src);
+      const int aa = __shfl(anc, src, 64);
+      if (anc >= 0) {
+        float Ra[9], t[3];
+        quat2mat(Ra, aq);
+        mat_vec(t, Ra, p);
+        p[0] = ap[0] + t[0]; p[1] = ap[1] + t[1]; p[2] = ap[2] + t[2];
+        quat_mul(q, aq, q);
+        anc = aa;
+      }
+    }
+    quat_normalize(q);
+    // joint anchors and axes. A hinge's anchor and axis, and a slide's axis, are
+    // fixed by the joint's own motion, so the body's final frame gives them; a
+    // free joint's are its position and z axis. Ball joints and bodies with
+    // several joints replay their joints from the parent's final pose.
+    const bool replay = cn > 0 && mid < 0 && jn > 0 && !(jn == 1 && jt0 != 1);
+    if (cn > 0 && mid < 0 && jn == 1 && jt0 != 1) {
+      float R[9], ax[3], an[3], jax[3], jp[3];
+      quat2mat(R, q);
+      if (jt0 == 0) {
+        an[0] = p[0]; an[1] = p[1]; an[2] = p[2];
+        ax[0] = R[2]; ax[1] = R[5]; ax[2] = R[8];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++) { jax[k] = IMG_F(jnt_axis)[3 * ja + k]; jp[k] = IMG_F(jnt_pos)[3 * ja + k]; }
+        mat_vec(ax, R, jax);
+        mat_vec(an, R, jp);
+        const float dd = jt0 == 2 ? qpos[qa0] - qpos0[qa0] : 0.f;
+        an[0] += p[0] - ax[0] * dd; an[1] += p[1] - ax[1] * dd; an[2] += p[2] - ax[2] * dd;
+      }
+      xanchor[3 * ja] = an[0]; xanchor[3 * ja + 1] = an[1]; xanchor[3 * ja + 2] = an[2];
+      xaxis[3 * ja] = ax[0]; xaxis[3 * ja + 1] = ax[1]; xaxis[3 * ja + 2] = ax[2];
+    }
+    if (__any(replay)) {
+      float pp[3], pq[4];
+#pragma unroll
+      for (int k = 0; k < 3; k++) pp[k] = shfl(p[k], par);
+#pragma unroll
+      for (int k = 0; k < 4; k++) pq[k] = shfl(q[k], par);
+      if (replay) {
+        const float fp[3] = {p[0], p[1], p[2]}, fq[4] = {q[0], q[1], q[2], q[3]};
+        float R[9], t[3], bp[3], bq[4];
+#pragma unroll
+        for (int k = 0; k < 3; k++) bp[k] = body_pos[3 * b + k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) bq[k] = body_quat[4 * b + k];
+        quat2mat(R, pq);
+        mat_vec(t, R, bp);
+        p[0] = pp[0] + t[0]; p[1] = pp[1] + t[1]; p[2] = pp[2] + t[2];
+        quat_mul(q, pq, bq);
+        for (int j = ja; j < ja + jn; j++) {
+          float ax[3], an[3];
+          apply_joint(j, ax, an);
+          xanchor[3 * j] = an[0]; xanchor[3 * j + 1] = an[1]; xanchor[3 * j + 2] = an[2];
+          xaxis[3 * j] = ax[0]; xaxis[3 * j + 1] = ax[1]; xaxis[3 * j + 2] = ax[2];
+        }
+        p[0] = fp[0]; p[1] = fp[1]; p[2] = fp[2];
+        q[0] = fq[0]; q[1] = fq[1]; q[2] = fq[2]; q[3] = fq[3];
+      }
+    }
 #else
   // Level-synchronous sweep: at level d the lanes of the bodies at depth d take
   // their parent's final pose from its lane (ds_bpermute) and apply their own
@@ -2539,6 +2689,43 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   }
   PROF(18);
   wsync();  // subtree_com visible to the per-joint lanes
+#if MJH_CDOF_LANE
+  // lane i = dof i builds its own cdof row (the per-joint rows below, row by
+  // row: the same operations), kept in registers for the crb pass instead of
+  // stored and reloaded through global scratch
+  if (tid < nv) {
+    const int i = tid;
+    const int jn = IMG_I(dof_jntid)[i], b = IMG_I(dof_bodyid)[i];
+    const int da = IMG_I(jnt_dofadr)[jn], t = IMG_I(jnt_type)[jn];
+    const float* c = subtree_com + 3 * IMG_I(body_rootid)[b];
+    const float off[3] = {c[0] - xanchor[3 * jn], c[1] - xanchor[3 * jn + 1], c[2] - xanchor[3 * jn + 2]};
+    const int k = i - da;
+    float row[6];
+    if (t == 0 && k < 3) {  // free joint translation k
+      row[0] = row[1] = row[2] = 0.f;
+      row[3] = k == 0 ? 1.f : 0.f; row[4] = k == 1 ? 1.f : 0.f; row[5] = k == 2 ? 1.f : 0.f;
+    } else if (t == 2) {  // slide
+      row[0] = row[1] = row[2] = 0.f;
+      row[3] = xaxis[3 * jn]; row[4] = xaxis[3 * jn + 1]; row[5] = xaxis[3 * jn + 2];
+    } else {  // rotation: free joint rotation k-3 / ball k (the body's axes), hinge (its axis)
+      float ax[3];
+      if (t == 0 || t == 1) {
+        const int kk = t == 0 ? k - 3 : k;
+        ax[0] = xmat[9 * b + kk]; ax[1] = xmat[9 * b + 3 + kk]; ax[2] = xmat[9 * b + 6 + kk];
+      } else {
+        ax[0] = xaxis[3 * jn]; ax[1] = xaxis[3 * jn + 1]; ax[2] = xaxis[3 * jn + 2];
+      }
+      row[0] = ax[0]; row[1] = ax[1]; row[2] = ax[2];
+      cross3(&row[3], ax, off);
+    }
+#pragma unroll
+    for (int e = 0; e < 6; e++) {
+      cdof[6 * i + e] = row[e];
+      r_cdof[e] = row[e];
+    }
+  }
+  if (false)
+#endif
   for (int j = tid; j < nj; j += NT) {
     // every input is loaded before the first cdof store (a load behind a store
     // waits for it)
@@ -2592,7 +2779,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   PROF(19);
   // ---------------------------------------------------------------- crb + M
   // lane i's cdof row in registers
-  if (tid < nv) {
+  if (!MJH_CDOF_LANE && tid < nv) {
 #pragma unroll
     for (int c = 0; c < 6; c++) r_cdof[c] = cdof[6 * tid + c];
   }
@@ -3372,6 +3559,17 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     };
     auto update_constraint = [&]() -> float {
       float c = 0.f;
+#if MJH_JTF_PF
+      // J^T f's first round of J loads issued before the row pass (they do not
+      // depend on it): one global round trip off the update's chain
+      float jpf[MJH_JTF_B];
+      const bool pf = nefc >= MJH_JTF_B;
+      if (pf) {
+        const int ic = tid < nv ? tid : 0;
+#pragma unroll
+        for (int q = 0; q < MJH_JTF_B; q++) jpf[q] = J[q * ldj + ic];
+      }
+#endif
       for (int r = tid; r < nefc; r += NT) {
         float f, cr;
         if (ELL && efc_type[r] == MJH_CNSTR_CONTACT_ELLIPTIC) {
@@ -3404,6 +3602,18 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
         // mod 4 in increasing order (as a plain 4-way unrolled loop)
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
         int r = 0;
+#if MJH_JTF_PF
+        if (pf) {
+#pragma unroll
+          for (int q = 0; q < MJH_JTF_B; q += 4) {
+            s0 += jpf[q] * efc_force[q];
+            s1 += jpf[q + 1] * efc_force[q + 1];
+            s2 += jpf[q + 2] * efc_force[q + 2];
+            s3 += jpf[q + 3] * efc_force[q + 3];
+          }
+          r = MJH_JTF_B;
+        }
+#endif
         for (; r + MJH_JTF_B <= nefc; r += MJH_JTF_B) {
           float jj[MJH_JTF_B];
 #pragma unroll
