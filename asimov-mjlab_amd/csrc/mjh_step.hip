@@ -573,6 +573,19 @@ __host__ __device__ constexpr bool pack_l(int wpb) { return cu_worlds(wpb); }
 #ifndef MJH_JTF_B
 #define MJH_JTF_B 16
 #endif
+// body / joint outputs computed in place in the data arrays (slab layout) instead of
+// global scratch copied out at the end. Measured (profiles/r06y_out_direct_ab.log): G1
+// 0.468 -> 0.454 ms, Go1 0.410 -> 0.405 ms per launch, env bench 1.707M -> 1.749M
+#ifndef MJH_OUT_DIRECT
+#define MJH_OUT_DIRECT 1
+#endif
+// contacts and sites computed in place in the data arrays too (A/B switch). Measured
+// (gpurun_out r06z): G1 flat, Go1 0.405 -> 0.400 ms, 156 GPU tests green, but Go1's
+// outputs are not bit-identical to the copy-out build (tools/lib_diff.py; G1's are): off
+// until that difference is explained
+#ifndef MJH_OUT_DIRECT2
+#define MJH_OUT_DIRECT2 0
+#endif
 // kinematics by pointer jumping over the body tree (A/B switch). Measured
 // (profiles/r06r_jtfpf_cdof_kinjump_ab_kb.log): G1 0.466 -> 0.459, Go1 0.409 -> 0.402 ms per
 // launch, but the 40-step rollout parity test met a line-search choice beyond float32
@@ -2111,38 +2124,49 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   float* Mv = SP(Mv);
   float* tmp = SP(tmp);
   float* tmp2 = SP(tmp2);
-  float* xpos = SP(xpos);
-  float* xquat = SP(xquat);
-  float* xmat = SP(xmat);
-  float* xipos = SP(xipos);
-  float* ximat = SP(ximat);
-  float* subtree_com = SP(subtree_com);
+  // slab data: the body and joint arrays the step outputs are computed in place in
+  // the data arrays (this world's rows), not in global scratch copied out at the end
+  constexpr bool kOutDirect = SLAB && MJH_OUT_DIRECT && Rg::xpos && Rg::xquat && Rg::xmat && Rg::xipos && Rg::ximat &&
+                              Rg::subtree_com && Rg::cvel && Rg::cacc && Rg::xanchor && Rg::xaxis;
+  const long long wb = W * Z.nbody, wj = W * Z.njnt;
+  float* xpos = kOutDirect ? DP(xpos) + 3 * wb : SP(xpos);
+  float* xquat = kOutDirect ? DP(xquat) + 4 * wb : SP(xquat);
+  float* xmat = kOutDirect ? DP(xmat) + 9 * wb : SP(xmat);
+  float* xipos = kOutDirect ? DP(xipos) + 3 * wb : SP(xipos);
+  float* ximat = kOutDirect ? DP(ximat) + 9 * wb : SP(ximat);
+  float* subtree_com = kOutDirect ? DP(subtree_com) + 3 * wb : SP(subtree_com);
   float* cinert = SP(cinert);
   float* crb = SP(crb);
-  float* cvel = SP(cvel);
-  float* cacc = SP(cacc);
+  float* cvel = kOutDirect ? DP(cvel) + 6 * wb : SP(cvel);
+  float* cacc = kOutDirect ? DP(cacc) + 6 * wb : SP(cacc);
   float* cfrc = SP(cfrc);
-  float* xanchor = SP(xanchor);
-  float* xaxis = SP(xaxis);
+  float* xanchor = kOutDirect ? DP(xanchor) + 3 * wj : SP(xanchor);
+  float* xaxis = kOutDirect ? DP(xaxis) + 3 * wj : SP(xaxis);
   float* cdof = SP(cdof);
   float* cdof_dot = SP(cdof_dot);
   float* cgpos = SP(cgpos);
   float* cgmat = SP(cgmat);
-  float* sxpos = SP(sxpos);
-  float* sxmat = SP(sxmat);
+  // contacts and sites computed in place in the data arrays as well (slab layout)
+  constexpr bool kOutDirect2 = kOutDirect && MJH_OUT_DIRECT2 && Rg::sxpos && Rg::sxmat && Rg::con_pos &&
+                               Rg::con_frame && Rg::con_dist && Rg::con_fric && Rg::con_imargin && Rg::con_dim &&
+                               Rg::con_geom && Rg::con_efcadr;
+  const long long s_row0 = d.site_wstride ? W * d.site_wstride + d.site_off : W * Z.nsite;
+  float* sxpos = kOutDirect2 ? (d.site_wstride ? d.site_xpos : DP(site_xpos)) + 3 * s_row0 : SP(sxpos);
+  float* sxmat = kOutDirect2 ? (d.site_wstride ? d.site_xmat : DP(site_xmat)) + 9 * s_row0 : SP(sxmat);
   float* Mm = SP(M);
   float* Lm = HO ? G + Lo.h_L : SP(L);
   float* act_force = SP(act_force);
-  float* con_pos = SP(con_pos);
-  float* con_frame = SP(con_frame);
-  float* con_dist = SP(con_dist);
-  float* con_fric = SP(con_fric);
+  const long long wc = W * Z.nconmax;
+  float* con_pos = kOutDirect2 ? DP(contact_pos) + 3 * wc : SP(con_pos);
+  float* con_frame = kOutDirect2 ? DP(contact_frame) + 9 * wc : SP(con_frame);
+  float* con_dist = kOutDirect2 ? DP(contact_dist) + wc : SP(con_dist);
+  float* con_fric = kOutDirect2 ? DP(contact_friction) + 5 * wc : SP(con_fric);
   float* con_solref = SP(con_solref);
   float* con_solimp = SP(con_solimp);
-  float* con_imargin = SP(con_imargin);
-  int* con_dim = SPI(con_dim);
-  int* con_geom = SPI(con_geom);
-  int* con_efcadr = SPI(con_efcadr);
+  float* con_imargin = kOutDirect2 ? DP(contact_includemargin) + wc : SP(con_imargin);
+  int* con_dim = kOutDirect2 ? DP(contact_dim) + wc : SPI(con_dim);
+  int* con_geom = kOutDirect2 ? DP(contact_geom) + 2 * wc : SPI(con_geom);
+  int* con_efcadr = kOutDirect2 ? DP(contact_efc_address) + wc : SPI(con_efcadr);
   float* J = SP(J);
   float* efc_pos = SP(efc_pos);
   int* efc_id = SPI(efc_id);
@@ -4892,7 +4916,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   // arrays may alias the scratch as far as the compiler knows, and a load
   // issued after a store waits for the store too (one memory latency per
   // array otherwise). Lane = body / joint / site / dof / contact / row.
-  if (tid < nb) {
+  if (!kOutDirect && tid < nb) {
     const int b = tid;
     float v[43];
 #pragma unroll
@@ -4926,11 +4950,11 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
   {
     float vj[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, vs[12], vd[8];
     const bool jl = tid < nj, sl = tid < Z.nsite, dl = tid < nv;  // nj <= nv < 64
-    if (jl) {
+    if (!kOutDirect && jl) {
 #pragma unroll
       for (int k = 0; k < 3; k++) { vj[k] = xanchor[3 * tid + k]; vj[3 + k] = xaxis[3 * tid + k]; }
     }
-    if (sl) {
+    if (!kOutDirect2 && sl) {
 #pragma unroll
       for (int k = 0; k < 3; k++) vs[k] = sxpos[3 * tid + k];
 #pragma unroll
@@ -4940,7 +4964,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       vd[0] = qfrc_bias[tid]; vd[1] = qfrc_passive[tid]; vd[2] = qfrc_act[tid]; vd[3] = qfrc_smooth[tid];
       vd[4] = qfrc_con[tid]; vd[5] = qacc_smooth[tid]; vd[6] = qacc[tid];
     }
-    if (jl) {
+    if (!kOutDirect && jl) {
       const long long o = (long long)W * nj + tid;
 #pragma unroll
       for (int k = 0; k < 3; k++) { DP(xanchor)[3 * o + k] = vj[k]; DP(xaxis)[3 * o + k] = vj[3 + k]; }
@@ -4950,7 +4974,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
     float* const o_sxpos = d.site_wstride ? d.site_xpos : DP(site_xpos);
     float* const o_sxmat = d.site_wstride ? d.site_xmat : DP(site_xmat);
     const long long s_row = d.site_wstride ? (long long)W * d.site_wstride + d.site_off : (long long)W * Z.nsite;
-    for (int st = tid; sl; st += NT) {  // sites beyond the first 64: one more round each
+    for (int st = tid; sl && !kOutDirect2; st += NT) {  // sites beyond the first 64: one more round each
       const long long o = s_row + st;
 #pragma unroll
       for (int k = 0; k < 3; k++) o_sxpos[3 * o + k] = vs[k];
@@ -4968,7 +4992,7 @@ __global__ __launch_bounds__(64 * WPB, MODE == 1 ? MJH_PMINWAVES : MJH_MINWAVES(
       DP(qfrc_constraint)[o] = vd[4]; DP(qacc_smooth)[o] = vd[5]; DP(qacc)[o] = vd[6]; DP(qacc_warmstart)[o] = vd[6];
     }
   }
-  for (int ci = tid; ci < ncon; ci += NT) {
+  for (int ci = tid; !kOutDirect2 && ci < ncon; ci += NT) {
     float c[22];
     int ic[4];
     c[0] = con_dist[ci];
